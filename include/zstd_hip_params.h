@@ -1,0 +1,31 @@
+/*
+ * zstd_hip_params.h — constants that define the compressed bit stream of the
+ * gfx950 path.  Shared by the HIP kernels (custom-nvcomp-with-zstd_amd/csrc)
+ * and the CPU restatement used as the test oracle (oracle/zstd_oracle.c), so
+ * that both run the same algorithm.  Changing any value changes the output
+ * bytes (but never their decodability).
+ *
+ * Level-3 parameters follow the reference's level table
+ * (src/cuda_zstd_types.cpp:158-164: DFAST, min_match 3, search depth 2) mapped
+ * onto a deterministic, LDS-resident double-hash match finder.
+ */
+#ifndef ZSTD_HIP_PARAMS_H_
+#define ZSTD_HIP_PARAMS_H_
+
+#define ZH_BLOCK_MAX 65536          /* bytes per device block (one workgroup) */
+#define ZH_TILE 256                 /* hash insertion granularity (positions) */
+#define ZH_WINDOW 4096              /* parse window (positions) */
+#define ZH_SEG 16                   /* positions per thread in the parse */
+#define ZH_HASH_LOG_LONG 13         /* 8-byte hash table: 2^13 u32 entries */
+#define ZH_HASH_LOG_SHORT 13        /* 5-byte hash table: 2^13 u32 entries */
+#define ZH_HASH_READ 8              /* bytes read per hashed position */
+#define ZH_MIN_MATCH_LONG 8
+#define ZH_MIN_MATCH_SHORT 5
+#define ZH_MAX_MATCH 255            /* per-position length cap; continuations are merged */
+#define ZH_PRIME_LONG 0xCF1BBCDCB7A56463ull
+#define ZH_PRIME_SHORT 0x9E3779B185EBCA87ull
+#define ZH_COMPRESS_LITERALS_SIZE_MIN 63
+#define ZH_LONGNBSEQ 0x7F00
+#define ZH_MAGIC 0xFD2FB528u
+
+#endif
