@@ -1,0 +1,197 @@
+"""Benchmark: BASELINE.json metric "compress GB/s + ratio, 1 GB @ level 3, 64 KB chunks;
+libzstd round-trip OK" on MI355X.
+
+Workload (config C3): every rank compresses 16384 x 64 KiB chunks
+(1 GiB, Silesia-like synthetic mix, seed 0x5EED0003) that are already resident in
+HBM, through the stream-ordered C-ABI entry nvcomp_zstd_batched_compress_async_v5
+(K1 zh_lz_kernel -> K2 zh_entropy_kernel).  Multi-GPU (C4): one process per GPU,
+chunks sharded by rank with no data-path collective (weak scaling); the only
+collective is the RCCL all-gather of per-chunk compressed sizes that gives every
+rank the global output offsets, inside the timed step.
+
+Prints one JSON line (driver contract).  Roofline = the dominant kernel's
+algorithmic bytes (input + compressed output) per launch / its
+average HIP-event duration on the launch stream.  cpu_baseline = libzstd level 3
+(the reference's own CPU route for <1 MiB items, src/cuda_zstd_manager.cu:1604-1668)
+over a bounded sample of the same chunks on the host cores.
+"""
+import argparse
+import ctypes
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "custom-nvcomp-with-zstd_amd"))
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+
+CHUNK = 64 * 1024
+CHUNKS_PER_GPU = 16384
+HBM_PEAK_GBS = 8000.0
+METRIC = "compress GB/s + ratio, 1 GB @ level 3, 64 KB chunks; libzstd round-trip OK"
+SEEDS = {"mix": 0x5EED0003, "random": 0x5EED0004}
+
+
+def gen_chunks(kind, n, first):
+    import zh_testlib as T
+
+    return T.gen(T.KINDS[kind], n, SEEDS[kind], CHUNK, first=first)
+
+
+def cpu_baseline(data, threads, seconds=1.5):
+    """libzstd ZSTD_compress(level 3) over the rank-0 chunks, one CCtx per call,
+    `threads` host threads, bounded wall time."""
+    import concurrent.futures as cf
+
+    import zh_testlib as T
+
+    z = T.zstd()
+    if z is None:
+        return None
+    n = len(data) // CHUNK
+    cap = 80000
+
+    def work(lo, hi, out):
+        tot = 0
+        vp = ctypes.c_void_p
+        for i in range(lo, hi):
+            tot += z.ZSTD_compress(out.ctypes.data_as(vp), ctypes.c_size_t(cap), ctypes.c_void_p(data.ctypes.data + i * CHUNK), ctypes.c_size_t(CHUNK), 3)
+        return tot
+
+    bufs = [np.zeros(cap, np.uint8) for _ in range(threads)]
+    per = 64  # chunks per task
+    done_bytes, comp_bytes, t0 = 0, 0, time.perf_counter()
+    with cf.ThreadPoolExecutor(threads) as ex:
+        nxt = 0
+        while time.perf_counter() - t0 < seconds:
+            futs = []
+            for t in range(threads):
+                lo = nxt % n
+                hi = min(lo + per, n)
+                futs.append(ex.submit(work, lo, hi, bufs[t]))
+                done_bytes += (hi - lo) * CHUNK
+                nxt = hi
+            comp_bytes += sum(f.result() for f in futs)
+    el = time.perf_counter() - t0
+    return {"value": round(done_bytes / el / 1e9, 3), "unit": "GB/s", "cores": threads, "kind": "reference",
+            "sample": f"libzstd {z.ZSTD_versionNumber()} ZSTD_compress level 3 (the reference's CPU route) on {done_bytes >> 20} MiB "
+                      f"of the same 64 KiB chunks, {threads} threads, {el:.2f} s wall; ratio {done_bytes / max(comp_bytes, 1):.3f}"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--dataset", default="mix", choices=sorted(SEEDS))
+    ap.add_argument("--chunks", type=int, default=CHUNKS_PER_GPU, help="chunks per GPU")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--verify", action="store_true", help="libzstd-decode every rank-0 frame after timing")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
+
+    import cuda_zstd
+
+    n = args.chunks
+    host = gen_chunks(args.dataset, n, first=rank * n)
+    d_in = torch.from_numpy(host).to(dev)
+    bc = cuda_zstd.BatchedCompressor(3, CHUNK)
+    slot = (bc.max_out(CHUNK) + 255) // 256 * 256
+    d_out = torch.empty(n * slot, dtype=torch.uint8, device=dev)
+    ar = torch.arange(n, dtype=torch.int64, device=dev)
+    in_ptrs = d_in.data_ptr() + ar * CHUNK
+    out_ptrs = d_out.data_ptr() + ar * slot
+    in_sizes = torch.full((n,), CHUNK, dtype=torch.int64, device=dev)
+    out_sizes = torch.zeros(n, dtype=torch.int64, device=dev)
+    status = torch.zeros(n, dtype=torch.int32, device=dev)
+    temp = torch.empty(bc.temp_size(n, CHUNK), dtype=torch.uint8, device=dev)
+    all_sizes = torch.zeros(world * n, dtype=torch.int64, device=dev)
+    stream = torch.cuda.current_stream(dev)
+
+    def step():
+        bc.compress_async(in_ptrs, in_sizes, CHUNK, out_ptrs, out_sizes, status, temp, stream)
+        if world > 1:
+            dist.all_gather_into_tensor(all_sizes, out_sizes)  # RCCL: global per-chunk sizes -> offsets
+            return torch.cumsum(all_sizes, 0)
+        return torch.cumsum(out_sizes, 0)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    cuda_zstd.profile_enable(True)
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    cuda_zstd.profile_enable(False)
+    launches, kms = cuda_zstd.profile_collect()
+
+    assert int((status != 0).sum().item()) == 0, "compression failed on some chunks"
+    comp = int(out_sizes.sum().item())
+    stats = torch.tensor([el, float(comp), kms[0] / max(launches, 1), kms[1] / max(launches, 1)], dtype=torch.float64, device=dev)
+    if world > 1:
+        mx = stats.clone()
+        dist.all_reduce(mx, op=dist.ReduceOp.MAX)
+        tot = stats.clone()
+        dist.all_reduce(tot, op=dist.ReduceOp.SUM)
+        el, comp_all = mx[0].item(), tot[1].item()
+        k1, k2 = mx[2].item(), mx[3].item()
+    else:
+        comp_all, k1, k2 = float(comp), stats[2].item(), stats[3].item()
+
+    verified = None
+    if args.verify and rank == 0:
+        import zh_testlib as T
+
+        sizes = out_sizes.cpu().numpy()
+        hb = d_out.cpu().numpy()
+        verified = all(T.zstd_decompress(hb[i * slot:i * slot + sizes[i]].tobytes(), CHUNK) == host[i * CHUNK:(i + 1) * CHUNK].tobytes() for i in range(n))
+
+    if rank == 0:
+        total_in = float(world * n * CHUNK)
+        gbs = total_in * args.steps / el / 1e9
+        # dominant kernel roofline: algorithmic bytes per launch = sum over its chunks of (input + compressed)
+        per_launch_bytes = n * CHUNK + comp_all / world
+        dom, dom_ms = ("zh_lz_kernel", k1) if k1 >= k2 else ("zh_entropy_kernel", k2)
+        achieved = per_launch_bytes / (dom_ms / 1e3) / 1e9 if dom_ms > 0 else 0.0
+        line = {
+            "metric": METRIC, "value": round(gbs, 3), "unit": "GB/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": round(el / args.steps * 1e3, 3), "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+            "dtype": "u8", "data": f"synthetic {args.dataset} corpus (tools/datagen.c, seed {SEEDS[args.dataset]:#x}), device-resident",
+            "config": {"workload": f"C3: {n} x 64 KiB chunks ({n * CHUNK / 2**30:.2f} GiB) per GPU, level 3, independent frames",
+                       "chunk_bytes": CHUNK, "chunks_per_gpu": n, "level": 3, "ratio": round(total_in / comp_all, 4),
+                       "kernel_ms": {"zh_lz_kernel": round(k1, 3), "zh_entropy_kernel": round(k2, 3)},
+                       "parallelism": f"dp{world} (chunk shards, RCCL all-gather of sizes)", "libzstd_verified": verified},
+            "roofline": {"kernel": dom, "bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": None},
+        }
+        if not args.no_cpu_baseline:
+            threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
+            line["cpu_baseline"] = cpu_baseline(host, threads)
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

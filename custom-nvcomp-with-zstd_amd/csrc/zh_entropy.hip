@@ -1,0 +1,937 @@
+// zh_entropy.hip — K2: entropy coding + block/frame assembly, one wave64 per block.
+//
+// Replaces the reference's compress_literals (Raw only, src/cuda_zstd_manager.cu:4406-4484),
+// encode_sequences_with_predefined_fse / k_build_ctable / k_encode_fse_interleaved
+// (src/cuda_zstd_manager.cu:4493-4661, src/cuda_zstd_fse_encoding_kernel.cu:32-325),
+// write_block (:4227-4286) and write_frame_header (:3998-4106).
+// Bit-for-bit the same stream as oracle/zstd_oracle.c (orc_compress_block), whose
+// entropy stage is pinned byte-identical to libzstd 1.4.9.
+//
+// Work split: everything data-parallel (histograms, code computation, sequence
+// merge, Huffman stream packing, FSE bit packing) runs on the 64 lanes; the
+// inherently serial parts (repcode history, table builds, FSE state chain)
+// run as wave-uniform loops.  Many blocks are resident per CU (small LDS), so
+// one block's serial chain overlaps other blocks' parallel phases.
+#include "zh_common.h"
+
+namespace {
+
+constexpr u32 K2_THREADS = 64;
+constexpr u32 SW_WORDS = 168;
+
+// ---------------- LDS layout (bytes) ----------------
+constexpr u32 OFF_SW = 0;                          // bit sink words
+constexpr u32 OFF_MISC = OFF_SW + 4 * SW_WORDS;    // 64 u32 scalars / broadcast
+constexpr u32 OFF_HIST = OFF_MISC + 4 * 64;        // 256 u32 literal histogram; later 121 code counts
+constexpr u32 OFF_HVAL = OFF_HIST + 4 * 256;       // u16[256] Huffman code values
+constexpr u32 OFF_HNB = OFF_HVAL + 2 * 256;        // u8[256] Huffman code lengths
+constexpr u32 OFF_HBUF = OFF_HNB + 256;            // u8[768] header scratch (weights / NCount)
+constexpr u32 OFF_U = OFF_HBUF + 768;              // union: Huffman nodes | FSE tables
+// Huffman build view
+constexpr u32 OFF_NODES = OFF_U;                   // 514 nodes x 8 B
+constexpr u32 U_HUF_END = OFF_NODES + 8 * 516;
+// FSE view
+constexpr u32 OFF_ST_LL = OFF_U;                   // u16[512]
+constexpr u32 OFF_ST_OF = OFF_ST_LL + 1024;        // u16[256]
+constexpr u32 OFF_ST_ML = OFF_ST_OF + 512;         // u16[512]
+constexpr u32 OFF_SYM = OFF_ST_ML + 1024;          // 3 x 64 x (u32 dNb, s32 dFS)
+constexpr u32 OFF_TSYM = OFF_SYM + 3 * 64 * 8;     // u8[512] spread scratch
+constexpr u32 OFF_NORM = OFF_TSYM + 512;           // s16[64]
+constexpr u32 OFF_WTS = OFF_NORM + 128;            // u8[256] Huffman weights (used during Huffman header)
+constexpr u32 U_FSE_END = OFF_WTS + 256;
+constexpr u32 K2_LDS = (U_HUF_END > U_FSE_END ? U_HUF_END : U_FSE_END);
+static_assert(K2_LDS < 16384, "K2 LDS budget");
+
+__constant__ u8 c_LL_bits[36] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 1, 1, 1, 1, 2, 2, 3, 3, 4, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16};
+__constant__ u8 c_ML_bits[53] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0,
+                                 1, 1, 1, 1, 2, 2, 3, 3, 4, 4, 5, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16};
+__constant__ s16 c_LL_def[36] = {4, 3, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 1, 1, 1, 2, 2, 2, 2, 2, 2, 2, 2, 2, 3, 2, 1, 1, 1, 1, 1, -1, -1, -1, -1};
+__constant__ s16 c_ML_def[53] = {1, 4, 3, 2, 2, 2, 2, 2, 2, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1,
+                                 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, -1, -1, -1, -1, -1, -1, -1};
+__constant__ s16 c_OF_def[29] = {1, 1, 1, 1, 1, 1, 2, 2, 2, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, -1, -1, -1, -1, -1};
+__constant__ u8 c_LL_code[64] = {0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16, 16, 17, 17, 18, 18, 19, 19,
+                                 20, 20, 20, 20, 21, 21, 21, 21, 22, 22, 22, 22, 22, 22, 22, 22, 23, 23, 23, 23, 23, 23, 23, 23,
+                                 24, 24, 24, 24, 24, 24, 24, 24, 24, 24, 24, 24, 24, 24, 24, 24};
+__constant__ u8 c_ML_code[128] = {0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16, 17, 18, 19, 20, 21, 22, 23, 24, 25, 26, 27, 28, 29, 30, 31,
+                                  32, 32, 33, 33, 34, 34, 35, 35, 36, 36, 36, 36, 37, 37, 37, 37, 38, 38, 38, 38, 38, 38, 38, 38, 39, 39, 39, 39, 39, 39, 39, 39,
+                                  40, 40, 40, 40, 40, 40, 40, 40, 40, 40, 40, 40, 40, 40, 40, 40, 41, 41, 41, 41, 41, 41, 41, 41, 41, 41, 41, 41, 41, 41, 41, 41,
+                                  42, 42, 42, 42, 42, 42, 42, 42, 42, 42, 42, 42, 42, 42, 42, 42, 42, 42, 42, 42, 42, 42, 42, 42, 42, 42, 42, 42, 42, 42, 42, 42};
+
+__device__ __forceinline__ u32 highbit32(u32 v) { return 31u - (u32)__builtin_clz(v); }
+__device__ __forceinline__ u32 ll_code(u32 ll) { return ll > 63 ? highbit32(ll) + 19 : c_LL_code[ll]; }
+__device__ __forceinline__ u32 ml_code(u32 mlBase) { return mlBase > 127 ? highbit32(mlBase) + 36 : c_ML_code[mlBase]; }
+__device__ __forceinline__ u32 lane_id() { return threadIdx.x; }
+__device__ __forceinline__ void wave_sync() { __syncthreads(); }  // one wave per workgroup
+// write a wave-uniform value into lane j of a per-lane vector
+__device__ __forceinline__ u32 setlane(u32 acc, u32 v, u32 j) { return lane_id() == j ? v : acc; }
+
+__device__ __forceinline__ u32 wave_excl_scan(u32 v, u32 &total) {
+  u32 const lane = lane_id();
+  u32 incl = v;
+#pragma unroll
+  for (u32 d = 1; d < 64; d <<= 1) {
+    u32 t = __shfl_up(incl, d, 64);
+    if (lane >= d) incl += t;
+  }
+  total = __shfl(incl, 63, 64);
+  return incl - v;
+}
+__device__ __forceinline__ u32 wave_sum(u32 v) {
+#pragma unroll
+  for (u32 d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d, 64);
+  return v;
+}
+__device__ __forceinline__ u32 wave_max(u32 v) {
+#pragma unroll
+  for (u32 d = 32; d >= 1; d >>= 1) v = max(v, (u32)__shfl_xor(v, d, 64));
+  return v;
+}
+
+// ---------------- output: bytes at dst[pos..] guarded by cap ----------------
+struct Out {
+  u8 *dst;
+  u32 cap;
+  __device__ __forceinline__ void put(u32 pos, u8 v) const { if (pos < cap) dst[pos] = v; }
+};
+
+// ---------------- bit sink: LSB-first fields, little-endian bytes (BIT_CStream) ----------------
+// Wave-uniform state; sw[] holds the pending partial byte in sw[0] bits [0, pend).
+struct BitSink {
+  u32 pos;   // next byte to write in Out
+  u32 pend;  // pending bits in sw[0] (0..7)
+};
+
+template <int K>
+__device__ __forceinline__ void sink_append(BitSink &bs, const Out &o, u32 *sw, const u32 (&val)[K], const u32 (&nb)[K]) {
+  u32 const lane = lane_id();
+  u32 tot = 0;
+#pragma unroll
+  for (int k = 0; k < K; k++) tot += nb[k];
+  u32 all;
+  u32 bit = wave_excl_scan(tot, all) + bs.pend;
+  u32 const end = bs.pend + all;
+  u32 const nwords = (end + 31) >> 5;
+  for (u32 w = 1 + lane; w < nwords + 1; w += 64) sw[w] = 0;
+  wave_sync();
+#pragma unroll
+  for (int k = 0; k < K; k++) {
+    if (nb[k]) {
+      u32 const v = val[k] & ((nb[k] >= 32) ? 0xFFFFFFFFu : ((1u << nb[k]) - 1u));
+      u32 const w = bit >> 5, sh = bit & 31;
+      atomicOr(&sw[w], v << sh);
+      if (sh + nb[k] > 32) atomicOr(&sw[w + 1], v >> (32 - sh));
+      bit += nb[k];
+    }
+  }
+  wave_sync();
+  u32 const full = end >> 3;
+  const u8 *sb = (const u8 *)sw;
+  for (u32 i = lane; i < full; i += 64) o.put(bs.pos + i, sb[i]);
+  u8 const part = sb[full];
+  wave_sync();
+  if (lane == 0) sw[0] = (end & 7) ? part : 0;
+  bs.pos += full;
+  bs.pend = end & 7;
+  wave_sync();
+}
+
+// BIT_closeCStream: end mark + flush of the partial byte
+__device__ __forceinline__ void sink_close(BitSink &bs, const Out &o, u32 *sw) {
+  u32 v[1] = {1u}, nb[1] = {lane_id() == 0 ? 1u : 0u};
+  sink_append<1>(bs, o, sw, v, nb);
+  if (bs.pend) {
+    if (lane_id() == 0) o.put(bs.pos, (u8)sw[0]);
+    bs.pos += 1;
+    bs.pend = 0;
+  }
+  if (lane_id() == 0) sw[0] = 0;
+  wave_sync();
+}
+
+// ---------------- FSE (libzstd v1.4.9 algorithms; lane-0 serial) ----------------
+__device__ u32 fse_min_table_log(u32 srcSize, u32 maxSV) {
+  u32 a = highbit32(srcSize) + 1, b = highbit32(maxSV) + 2;
+  return a < b ? a : b;
+}
+__device__ u32 fse_optimal_table_log(u32 maxTableLog, u32 srcSize, u32 maxSV, u32 minus) {
+  u32 maxBitsSrc = highbit32(srcSize - 1) - minus;
+  u32 tableLog = maxTableLog;
+  u32 minBits = fse_min_table_log(srcSize, maxSV);
+  if (maxBitsSrc < tableLog) tableLog = maxBitsSrc;
+  if (minBits > tableLog) tableLog = minBits;
+  if (tableLog < 5) tableLog = 5;
+  if (tableLog > 12) tableLog = 12;
+  return tableLog;
+}
+
+__device__ bool fse_normalize_m2(s16 *norm, u32 tableLog, const u32 *count, u32 total, u32 maxSV, s16 lowProbCount) {
+  const s16 NOT_YET = -2;
+  u32 distributed = 0, toDistribute;
+  u32 lowThreshold = total >> tableLog;
+  u32 lowOne = (u32)(((u64)total * 3) >> (tableLog + 1));
+  for (u32 s = 0; s <= maxSV; s++) {
+    if (count[s] == 0) { norm[s] = 0; continue; }
+    if (count[s] <= lowThreshold) { norm[s] = lowProbCount; distributed++; total -= count[s]; continue; }
+    if (count[s] <= lowOne) { norm[s] = 1; distributed++; total -= count[s]; continue; }
+    norm[s] = NOT_YET;
+  }
+  toDistribute = (1u << tableLog) - distributed;
+  if (toDistribute == 0) return true;
+  if ((total / toDistribute) > lowOne) {
+    lowOne = (u32)(((u64)total * 3) / (toDistribute * 2));
+    for (u32 s = 0; s <= maxSV; s++)
+      if (norm[s] == NOT_YET && count[s] <= lowOne) { norm[s] = 1; distributed++; total -= count[s]; }
+    toDistribute = (1u << tableLog) - distributed;
+  }
+  if (distributed == maxSV + 1) {
+    u32 maxV = 0, maxC = 0;
+    for (u32 s = 0; s <= maxSV; s++) if (count[s] > maxC) { maxV = s; maxC = count[s]; }
+    norm[maxV] += (s16)toDistribute;
+    return true;
+  }
+  if (total == 0) {
+    for (u32 s = 0; toDistribute > 0; s = (s + 1) % (maxSV + 1)) if (norm[s] > 0) { toDistribute--; norm[s]++; }
+    return true;
+  }
+  u64 const vStepLog = 62 - tableLog;
+  u64 const mid = (1ull << (vStepLog - 1)) - 1;
+  u64 const rStep = (((1ull << vStepLog) * toDistribute) + mid) / (u64)total;
+  u64 tmpTotal = mid;
+  for (u32 s = 0; s <= maxSV; s++) {
+    if (norm[s] == NOT_YET) {
+      u64 const end = tmpTotal + (count[s] * rStep);
+      u32 const weight = (u32)(end >> vStepLog) - (u32)(tmpTotal >> vStepLog);
+      if (weight < 1) return false;
+      norm[s] = (s16)weight;
+      tmpTotal = end;
+    }
+  }
+  return true;
+}
+
+__device__ bool fse_normalize(s16 *norm, u32 tableLog, const u32 *count, u32 total, u32 maxSV, bool useLowProbCount) {
+  const u32 rtbTable[8] = {0, 473195, 504333, 520860, 550000, 700000, 750000, 830000};
+  if (tableLog < fse_min_table_log(total, maxSV)) return false;
+  s16 const lowProbCount = useLowProbCount ? -1 : 1;
+  u64 const scale = 62 - tableLog;
+  u64 const step = (1ull << 62) / total;
+  u64 const vStep = 1ull << (scale - 20);
+  int stillToDistribute = 1 << tableLog;
+  u32 largest = 0;
+  s16 largestP = 0;
+  u32 const lowThreshold = total >> tableLog;
+  for (u32 s = 0; s <= maxSV; s++) {
+    if (count[s] == total) return true;  // never reached: RLE handled by the caller
+    if (count[s] == 0) { norm[s] = 0; continue; }
+    if (count[s] <= lowThreshold) { norm[s] = lowProbCount; stillToDistribute--; }
+    else {
+      s16 proba = (s16)((count[s] * step) >> scale);
+      if (proba < 8) {
+        u64 const restToBeat = vStep * rtbTable[proba];
+        proba += (count[s] * step) - ((u64)proba << scale) > restToBeat;
+      }
+      if (proba > largestP) { largestP = proba; largest = s; }
+      norm[s] = proba;
+      stillToDistribute -= proba;
+    }
+  }
+  if (-stillToDistribute >= (norm[largest] >> 1)) return fse_normalize_m2(norm, tableLog, count, total, maxSV, lowProbCount);
+  norm[largest] += (s16)stillToDistribute;
+  return true;
+}
+
+// FSE_writeNCount into out[] (LDS); returns size (0 on error)
+__device__ u32 fse_write_ncount(u8 *out, const s16 *norm, u32 maxSV, u32 tableLog) {
+  u8 *const ostart = out;
+  int const tableSize = 1 << tableLog;
+  int remaining = tableSize + 1, threshold = tableSize, nbBits = (int)tableLog + 1;
+  u32 bitStream = (tableLog - 5);
+  int bitCount = 4;
+  u32 symbol = 0;
+  u32 const alphabetSize = maxSV + 1;
+  bool previousIs0 = false;
+  while (symbol < alphabetSize && remaining > 1) {
+    if (previousIs0) {
+      u32 start = symbol;
+      while (symbol < alphabetSize && !norm[symbol]) symbol++;
+      if (symbol == alphabetSize) break;
+      while (symbol >= start + 24) {
+        start += 24;
+        bitStream += 0xFFFFu << bitCount;
+        out[0] = (u8)bitStream; out[1] = (u8)(bitStream >> 8); out += 2; bitStream >>= 16;
+      }
+      while (symbol >= start + 3) { start += 3; bitStream += 3u << bitCount; bitCount += 2; }
+      bitStream += (symbol - start) << bitCount;
+      bitCount += 2;
+      if (bitCount > 16) { out[0] = (u8)bitStream; out[1] = (u8)(bitStream >> 8); out += 2; bitStream >>= 16; bitCount -= 16; }
+    }
+    int count = norm[symbol++];
+    int const max = (2 * threshold - 1) - remaining;
+    remaining -= count < 0 ? -count : count;
+    count++;
+    if (count >= threshold) count += max;
+    bitStream += (u32)count << bitCount;
+    bitCount += nbBits;
+    bitCount -= (count < max);
+    previousIs0 = (count == 1);
+    if (remaining < 1) return 0;
+    while (remaining < threshold) { nbBits--; threshold >>= 1; }
+    if (bitCount > 16) { out[0] = (u8)bitStream; out[1] = (u8)(bitStream >> 8); out += 2; bitStream >>= 16; bitCount -= 16; }
+  }
+  if (remaining != 1) return 0;
+  out[0] = (u8)bitStream;
+  out[1] = (u8)(bitStream >> 8);
+  out += (bitCount + 7) / 8;
+  return (u32)(out - ostart);
+}
+
+struct FseSym { u32 dNb; s32 dFS; };
+
+// FSE_buildCTable_wksp into LDS (stateTable + symbol transforms)
+__device__ void fse_build_ctable(u16 *st, FseSym *sym, u8 *tableSymbol, const s16 *norm, u32 maxSV, u32 tableLog) {
+  u32 const tableSize = 1u << tableLog, tableMask = tableSize - 1;
+  u32 const step = (tableSize >> 1) + (tableSize >> 3) + 3;
+  u32 cumul[54];
+  u32 highThreshold = tableSize - 1;
+  cumul[0] = 0;
+  for (u32 u = 1; u <= maxSV + 1; u++) {
+    if (norm[u - 1] == -1) { cumul[u] = cumul[u - 1] + 1; tableSymbol[highThreshold--] = (u8)(u - 1); }
+    else cumul[u] = cumul[u - 1] + (u32)norm[u - 1];
+  }
+  u32 position = 0;
+  for (u32 s = 0; s <= maxSV; s++)
+    for (int k = 0; k < norm[s]; k++) {
+      tableSymbol[position] = (u8)s;
+      position = (position + step) & tableMask;
+      while (position > highThreshold) position = (position + step) & tableMask;
+    }
+  for (u32 u = 0; u < tableSize; u++) { u8 s = tableSymbol[u]; st[cumul[s]++] = (u16)(tableSize + u); }
+  u32 total = 0;
+  for (u32 s = 0; s <= maxSV; s++) {
+    int const nv = norm[s];
+    if (nv == 0) { sym[s].dNb = ((tableLog + 1) << 16) - (1u << tableLog); sym[s].dFS = 0; }
+    else if (nv == -1 || nv == 1) { sym[s].dNb = (tableLog << 16) - (1u << tableLog); sym[s].dFS = (s32)total - 1; total++; }
+    else {
+      u32 const maxBitsOut = tableLog - highbit32((u32)nv - 1);
+      u32 const minStatePlus = (u32)nv << maxBitsOut;
+      sym[s].dNb = (maxBitsOut << 16) - minStatePlus;
+      sym[s].dFS = (s32)total - nv;
+      total += (u32)nv;
+    }
+  }
+}
+
+__device__ __forceinline__ u32 fse_init_state(const u16 *st, const FseSym *sym, u32 s) {
+  FseSym const tt = sym[s];
+  u32 const nbBitsOut = (tt.dNb + (1u << 15)) >> 16;
+  u32 const v = (nbBitsOut << 16) - tt.dNb;
+  return st[(v >> nbBitsOut) + tt.dFS];
+}
+__device__ __forceinline__ u32 fse_step(const u16 *st, const FseSym *sym, u32 &state, u32 s, u32 &nbOut) {
+  FseSym const tt = sym[s];
+  u32 const nb = (state + tt.dNb) >> 16;
+  u32 const v = state & ((1u << nb) - 1u);
+  state = st[(state >> nb) + tt.dFS];
+  nbOut = nb;
+  return v;
+}
+
+// ---------------- Huffman (libzstd v1.4.9 HUF_buildCTable; lane-0 serial) ----------------
+struct HufNode { u32 count; u16 parent; u8 byte; u8 nbBits; };
+
+__device__ u32 huf_set_max_height(HufNode *huffNode, u32 lastNonNull, u32 maxNbBits) {
+  u32 const largestBits = huffNode[lastNonNull].nbBits;
+  if (largestBits <= maxNbBits) return largestBits;
+  int totalCost = 0;
+  u32 const baseCost = 1u << (largestBits - maxNbBits);
+  int n = (int)lastNonNull;
+  while (huffNode[n].nbBits > maxNbBits) {
+    totalCost += (int)(baseCost - (1u << (largestBits - huffNode[n].nbBits)));
+    huffNode[n].nbBits = (u8)maxNbBits;
+    n--;
+  }
+  while (huffNode[n].nbBits == maxNbBits) n--;
+  totalCost >>= (largestBits - maxNbBits);
+  u32 const noSymbol = 0xF0F0F0F0u;
+  u32 rankLast[14];
+  for (int i = 0; i < 14; i++) rankLast[i] = noSymbol;
+  {
+    u32 currentNbBits = maxNbBits;
+    for (int pos = n; pos >= 0; pos--) {
+      if (huffNode[pos].nbBits >= currentNbBits) continue;
+      currentNbBits = huffNode[pos].nbBits;
+      rankLast[maxNbBits - currentNbBits] = (u32)pos;
+    }
+  }
+  while (totalCost > 0) {
+    u32 nBitsToDecrease = highbit32((u32)totalCost) + 1;
+    for (; nBitsToDecrease > 1; nBitsToDecrease--) {
+      u32 const highPos = rankLast[nBitsToDecrease];
+      u32 const lowPos = rankLast[nBitsToDecrease - 1];
+      if (highPos == noSymbol) continue;
+      if (lowPos == noSymbol) break;
+      if (huffNode[highPos].count <= 2 * huffNode[lowPos].count) break;
+    }
+    while ((nBitsToDecrease <= 12) && (rankLast[nBitsToDecrease] == noSymbol)) nBitsToDecrease++;
+    totalCost -= 1 << (nBitsToDecrease - 1);
+    if (rankLast[nBitsToDecrease - 1] == noSymbol) rankLast[nBitsToDecrease - 1] = rankLast[nBitsToDecrease];
+    huffNode[rankLast[nBitsToDecrease]].nbBits++;
+    if (rankLast[nBitsToDecrease] == 0) rankLast[nBitsToDecrease] = noSymbol;
+    else {
+      rankLast[nBitsToDecrease]--;
+      if (huffNode[rankLast[nBitsToDecrease]].nbBits != maxNbBits - nBitsToDecrease) rankLast[nBitsToDecrease] = noSymbol;
+    }
+  }
+  while (totalCost < 0) {
+    if (rankLast[1] == noSymbol) {
+      while (huffNode[n].nbBits == maxNbBits) n--;
+      huffNode[n + 1].nbBits--;
+      rankLast[1] = (u32)(n + 1);
+      totalCost++;
+      continue;
+    }
+    huffNode[rankLast[1] + 1].nbBits--;
+    rankLast[1]++;
+    totalCost++;
+  }
+  return maxNbBits;
+}
+
+// returns maxNbBits (0 on error); fills hval/hnb for symbols 0..maxSV
+__device__ u32 huf_build_ctable(HufNode *huffNode0, u16 *hval, u8 *hnb, const u32 *count, u32 maxSV, u32 maxNbBits) {
+  HufNode *const huffNode = huffNode0 + 1;
+  int const STARTNODE = 256;
+  for (int i = 0; i < 2 * 256 + 2; i++) { huffNode0[i].count = 0; huffNode0[i].parent = 0; huffNode0[i].byte = 0; huffNode0[i].nbBits = 0; }
+  // HUF_sort
+  {
+    u32 base[32], curr[32];
+    for (int r = 0; r < 32; r++) base[r] = 0;
+    for (u32 n = 0; n <= maxSV; n++) base[highbit32(count[n] + 1)]++;
+    for (u32 n = 30; n > 0; n--) base[n - 1] += base[n];
+    for (int r = 0; r < 32; r++) curr[r] = base[r];
+    for (u32 n = 0; n <= maxSV; n++) {
+      u32 const c = count[n];
+      u32 const r = highbit32(c + 1) + 1;
+      u32 pos = curr[r]++;
+      while ((pos > base[r]) && (c > huffNode[pos - 1].count)) { huffNode[pos] = huffNode[pos - 1]; pos--; }
+      huffNode[pos].count = c;
+      huffNode[pos].byte = (u8)n;
+    }
+  }
+  int nonNullRank = (int)maxSV;
+  while (huffNode[nonNullRank].count == 0) nonNullRank--;
+  int lowS = nonNullRank, nodeNb = STARTNODE;
+  int const nodeRoot = nodeNb + lowS - 1;
+  int lowN = nodeNb;
+  huffNode[nodeNb].count = huffNode[lowS].count + huffNode[lowS - 1].count;
+  huffNode[lowS].parent = huffNode[lowS - 1].parent = (u16)nodeNb;
+  nodeNb++;
+  lowS -= 2;
+  for (int n = nodeNb; n <= nodeRoot; n++) huffNode[n].count = 1u << 30;
+  huffNode0[0].count = 1u << 31;
+  while (nodeNb <= nodeRoot) {
+    int const n1 = (huffNode[lowS].count < huffNode[lowN].count) ? lowS-- : lowN++;
+    int const n2 = (huffNode[lowS].count < huffNode[lowN].count) ? lowS-- : lowN++;
+    huffNode[nodeNb].count = huffNode[n1].count + huffNode[n2].count;
+    huffNode[n1].parent = huffNode[n2].parent = (u16)nodeNb;
+    nodeNb++;
+  }
+  huffNode[nodeRoot].nbBits = 0;
+  for (int n = nodeRoot - 1; n >= STARTNODE; n--) huffNode[n].nbBits = huffNode[huffNode[n].parent].nbBits + 1;
+  for (int n = 0; n <= nonNullRank; n++) huffNode[n].nbBits = huffNode[huffNode[n].parent].nbBits + 1;
+  maxNbBits = huf_set_max_height(huffNode, (u32)nonNullRank, maxNbBits);
+  if (maxNbBits > 12) return 0;
+  u16 nbPerRank[13], valPerRank[13];
+  for (int i = 0; i < 13; i++) { nbPerRank[i] = 0; valPerRank[i] = 0; }
+  for (int n = 0; n <= nonNullRank; n++) nbPerRank[huffNode[n].nbBits]++;
+  {
+    u16 mn = 0;
+    for (int n = (int)maxNbBits; n > 0; n--) { valPerRank[n] = mn; mn += nbPerRank[n]; mn >>= 1; }
+  }
+  for (u32 n = 0; n <= maxSV; n++) hnb[huffNode[n].byte] = huffNode[n].nbBits;
+  for (u32 n = 0; n <= maxSV; n++) hval[n] = valPerRank[hnb[n]]++;
+  return maxNbBits;
+}
+
+// serial FSE_compress_usingCTable of Huffman weights into out[] (LDS), two states
+__device__ u32 fse_compress_weights_stream(u8 *out, const u8 *src, u32 n, const u16 *st, const FseSym *sym, u32 tableLog) {
+  u64 acc = 0;
+  u32 nbits = 0, o = 0;
+#define ZH_ADD(v, nb)                                           \
+  do {                                                          \
+    acc |= ((u64)(v) & ((1ull << (nb)) - 1)) << nbits;          \
+    nbits += (nb);                                              \
+    while (nbits >= 8) { out[o++] = (u8)acc; acc >>= 8; nbits -= 8; } \
+  } while (0)
+  u32 s1, s2, nb;
+  int ip = (int)n;
+  if (n & 1) {
+    s1 = fse_init_state(st, sym, src[--ip]);
+    s2 = fse_init_state(st, sym, src[--ip]);
+    u32 v = fse_step(st, sym, s1, src[--ip], nb);
+    ZH_ADD(v, nb);
+  } else {
+    s2 = fse_init_state(st, sym, src[--ip]);
+    s1 = fse_init_state(st, sym, src[--ip]);
+  }
+  while (ip > 0) {
+    u32 v = fse_step(st, sym, s2, src[--ip], nb);
+    ZH_ADD(v, nb);
+    v = fse_step(st, sym, s1, src[--ip], nb);
+    ZH_ADD(v, nb);
+  }
+  ZH_ADD(s2, tableLog);
+  ZH_ADD(s1, tableLog);
+  ZH_ADD(1, 1);
+  if (nbits) out[o++] = (u8)acc;
+#undef ZH_ADD
+  return o;
+}
+
+// HUF_writeCTable into hbuf; returns size (0 = error -> raw literals)
+__device__ u32 huf_write_ctable(u8 *hbuf, u8 *w, const u8 *hnb, u32 maxSV, u32 huffLog, u16 *st, FseSym *sym, u8 *tsym, s16 *norm) {
+  for (u32 n = 0; n < maxSV; n++) w[n] = hnb[n] ? (u8)(huffLog + 1 - hnb[n]) : 0;
+  // HUF_compressWeights
+  u32 h = 0;
+  if (maxSV > 1) {
+    u32 count[13];
+    for (int i = 0; i < 13; i++) count[i] = 0;
+    for (u32 i = 0; i < maxSV; i++) count[w[i]]++;
+    u32 mx = 12;
+    while (!count[mx]) mx--;
+    u32 maxCount = 0;
+    for (u32 s = 0; s <= mx; s++) if (count[s] > maxCount) maxCount = count[s];
+    if (maxCount == maxSV) h = 1;
+    else if (maxCount == 1) h = 0;
+    else {
+      u32 tableLog = fse_optimal_table_log(6, maxSV, mx, 2);
+      if (fse_normalize(norm, tableLog, count, maxSV, mx, false)) {
+        u32 hs = fse_write_ncount(hbuf + 1, norm, mx, tableLog);
+        if (hs) {
+          fse_build_ctable(st, sym, tsym, norm, mx, tableLog);
+          u32 cs = maxSV > 2 ? fse_compress_weights_stream(hbuf + 1 + hs, w, maxSV, st, sym, tableLog) : 0;
+          h = cs ? hs + cs : 0;
+        }
+      }
+    }
+  }
+  if ((h > 1) & (h < maxSV / 2)) { hbuf[0] = (u8)h; return h + 1; }
+  if (maxSV > 128) return 0;
+  hbuf[0] = (u8)(128 + (maxSV - 1));
+  w[maxSV] = 0;
+  for (u32 n = 0; n < maxSV; n += 2) hbuf[(n / 2) + 1] = (u8)((w[n] << 4) + w[n + 1]);
+  return ((maxSV + 1) / 2) + 1;
+}
+
+// byte copy global -> Out (wave-parallel)
+__device__ __forceinline__ void copy_bytes(const Out &o, u32 pos, const u8 *src, u32 n) {
+  for (u32 i = lane_id(); i < n; i += 64) o.put(pos + i, src[i]);
+}
+
+}  // namespace
+
+// ============================================================================
+extern "C" __global__ __launch_bounds__(K2_THREADS) void zh_entropy_kernel(const ZhBlockDesc *__restrict__ blocks, ZhWorkspace ws, u32 window_log,
+                                                                             u32 cfg_block_size, u64 *__restrict__ item_size,
+                                                                             u32 *__restrict__ item_status, u32 *__restrict__ blk_size) {
+  extern __shared__ __attribute__((aligned(16))) u8 smem[];
+  u32 *sw = (u32 *)(smem + OFF_SW);
+  u32 *misc = (u32 *)(smem + OFF_MISC);
+  u32 *hist = (u32 *)(smem + OFF_HIST);
+  u16 *hval = (u16 *)(smem + OFF_HVAL);
+  u8 *hnb = smem + OFF_HNB;
+  u8 *hbuf = smem + OFF_HBUF;
+  HufNode *nodes = (HufNode *)(smem + OFF_NODES);
+  u16 *stLL = (u16 *)(smem + OFF_ST_LL), *stOF = (u16 *)(smem + OFF_ST_OF), *stML = (u16 *)(smem + OFF_ST_ML);
+  FseSym *symLL = (FseSym *)(smem + OFF_SYM), *symOF = symLL + 64, *symML = symLL + 128;
+  u8 *tsym = smem + OFF_TSYM;
+  s16 *norm = (s16 *)(smem + OFF_NORM);
+  u8 *wts = smem + OFF_WTS;
+
+  u32 const b = blockIdx.x, lane = lane_id();
+  ZhBlockDesc const d = blocks[b];
+  u32 const n = d.n;
+  if (n == 0) return;
+  const u32 *meta = ws.meta(b);
+  u32 const nseq_raw = meta[0], nlit = meta[1], rle = meta[2];
+  Out const o{d.dst, d.dst_cap};
+  if (lane == 0) sw[0] = 0;
+
+  // ---- frame header (reference write_frame_header choices, no dict / checksum)
+  u32 pos = 0;
+  if (d.flags & ZH_F_FIRST) {
+    u64 const content = d.frame_size;
+    bool const ss = content <= cfg_block_size;
+    u32 fcs_flag, fcs_size;
+    if (ss) {
+      if (content < 256) { fcs_flag = 0; fcs_size = 1; }
+      else if (content < 65536 + 256) { fcs_flag = 1; fcs_size = 2; }
+      else if (content <= 0xFFFFFFFFull) { fcs_flag = 2; fcs_size = 4; }
+      else { fcs_flag = 3; fcs_size = 8; }
+    } else {
+      if (content >= 256 && content < 65536 + 256) { fcs_flag = 1; fcs_size = 2; }
+      else if (content <= 0xFFFFFFFFull) { fcs_flag = 2; fcs_size = 4; }
+      else { fcs_flag = 3; fcs_size = 8; }
+    }
+    if (lane == 0) {
+      u32 p = 0;
+      o.put(p++, 0x28); o.put(p++, 0xB5); o.put(p++, 0x2F); o.put(p++, 0xFD);
+      o.put(p++, (u8)((fcs_flag << 6) | (ss ? 0x20 : 0)));
+      if (!ss) o.put(p++, (u8)((window_log - 10) << 3));
+      u64 v = fcs_size == 2 ? content - 256 : content;
+      for (u32 k = 0; k < fcs_size; k++) o.put(p++, (u8)(v >> (8 * k)));
+    }
+    pos = 5 + (ss ? 0 : 1) + fcs_size;
+  }
+  u32 const blk = pos;
+  u32 const body0 = blk + 3;
+  u32 const last = (d.flags & ZH_F_LAST) ? 1u : 0u;
+  u32 total;
+  bool raw = false;
+
+  if (rle) {
+    u32 const hdr = last + (1u << 1) + (n << 3);
+    if (lane == 0) { o.put(blk, (u8)hdr); o.put(blk + 1, (u8)(hdr >> 8)); o.put(blk + 2, (u8)(hdr >> 16)); o.put(blk + 3, d.src[0]); }
+    total = blk + 4;
+  } else {
+    const u8 *lits = ws.lits(b);
+    u64 *seq = ws.seq(b);
+    u32 op = body0;
+    // ======================= literals section (ZSTD_compressLiterals) =======================
+    {
+      u32 const nl = nlit;
+      u32 const minGain = (nl >> 6) + 2;
+      u32 const lhSize = 3 + (nl >= 1024) + (nl >= 16384);
+      bool const single = nl < 256;
+      u32 cLit = 0, hsz = 0, huffLog = 0;
+      u32 ssz[4] = {0, 0, 0, 0};
+      if (nl > ZH_COMPRESS_LITERALS_SIZE_MIN) {
+        for (u32 i = lane; i < 256; i += 64) hist[i] = 0;
+        wave_sync();
+        for (u32 i = lane; i < nl; i += 64) atomicAdd(&hist[lits[i]], 1u);
+        wave_sync();
+        u32 mx = 0, lg = 0;
+        for (u32 i = lane; i < 256; i += 64) { u32 c = hist[i]; if (c) mx = max(mx, i); lg = max(lg, c); }
+        u32 const maxSV = wave_max(mx), largest = wave_max(lg);
+        if (largest == nl) cLit = 1;
+        else if (largest <= (nl >> 7) + 4) cLit = 0;
+        else {
+          if (lane == 0) {
+            for (u32 i = 0; i < 256; i++) hnb[i] = 0;
+            u32 hl = fse_optimal_table_log(11, nl, maxSV, 1);
+            hl = huf_build_ctable(nodes, hval, hnb, hist, maxSV, hl);
+            u32 h = hl ? huf_write_ctable(hbuf, wts, hnb, maxSV, hl, stLL, symLL, tsym, norm) : 0;
+            misc[0] = hl;
+            misc[1] = h;
+          }
+          wave_sync();
+          huffLog = misc[0];
+          hsz = misc[1];
+          if (hsz && hsz + 12 < nl) {
+            // stream sizes: sum of code lengths per stream (+ end mark)
+            u32 const seg = (nl + 3) / 4;
+            u32 ns = single ? 1 : 4;
+            if (!single && nl < 12) ns = 0;
+            u32 cs = single ? 0 : 6;
+            for (u32 k = 0; k < ns; k++) {
+              u32 a = single ? 0 : k * seg, e = single ? nl : (k < 3 ? (k + 1) * seg : nl);
+              u32 bits = 0;
+              for (u32 i = a + lane; i < e; i += 64) bits += hnb[lits[i]];
+              bits = wave_sum(bits);
+              ssz[k] = (bits + 1 + 7) >> 3;
+              cs += ssz[k];
+            }
+            if (ns) {
+              u32 const tot = hsz + cs;
+              cLit = (tot >= nl - 1) ? 0 : tot;
+            }
+          }
+        }
+      }
+      if (cLit == 0 || cLit >= nl - minGain) {
+        // raw literals
+        u32 const fl = 1 + (nl > 31) + (nl > 4095);
+        u32 v = fl == 1 ? (nl << 3) : fl == 2 ? ((1u << 2) + (nl << 4)) : ((3u << 2) + (nl << 4));
+        if (lane < fl) o.put(op + lane, (u8)(v >> (8 * lane)));
+        copy_bytes(o, op + fl, lits, nl);
+        op += fl + nl;
+      } else if (cLit == 1) {
+        u32 const fl = 1 + (nl > 31) + (nl > 4095);
+        u32 v = fl == 1 ? (1 + (nl << 3)) : fl == 2 ? (1 + (1u << 2) + (nl << 4)) : (1 + (3u << 2) + (nl << 4));
+        if (lane < fl) o.put(op + lane, (u8)(v >> (8 * lane)));
+        if (lane == 0) o.put(op + fl, lits[0]);
+        op += fl + 1;
+      } else {
+        u64 lhc;
+        if (lhSize == 3) lhc = 2 + ((u64)(!single) << 2) + ((u64)nl << 4) + ((u64)cLit << 14);
+        else if (lhSize == 4) lhc = 2 + (2u << 2) + ((u64)nl << 4) + ((u64)cLit << 18);
+        else lhc = 2 + (3u << 2) + ((u64)nl << 4) + ((u64)cLit << 22);
+        if (lane < lhSize) o.put(op + lane, (u8)(lhc >> (8 * lane)));
+        op += lhSize;
+        for (u32 i = lane; i < hsz; i += 64) o.put(op + i, hbuf[i]);
+        op += hsz;
+        u32 const seg = (nl + 3) / 4;
+        u32 const ns = single ? 1 : 4;
+        if (!single) {
+          if (lane < 6) { u32 k = lane >> 1; o.put(op + lane, (u8)(ssz[k] >> (8 * (lane & 1)))); }
+          op += 6;
+        }
+        for (u32 k = 0; k < ns; k++) {
+          u32 a = single ? 0 : k * seg, e = single ? nl : (k < 3 ? (k + 1) * seg : nl);
+          BitSink bs{op, 0};
+          // symbols from e-1 down to a
+          for (u32 base = 0; base < e - a; base += 64) {
+            u32 const j = base + lane;
+            u32 v[1] = {0}, nb[1] = {0};
+            if (j < e - a) { u8 const c = lits[e - 1 - j]; v[0] = hval[c]; nb[0] = hnb[c]; }
+            sink_append<1>(bs, o, sw, v, nb);
+          }
+          sink_close(bs, o, sw);
+          op = bs.pos;
+        }
+      }
+      (void)huffLog;
+    }
+
+    // ======================= sequences section =======================
+    // pass A: literal lengths from cumulative counts, merge same-offset continuations (in place)
+    u32 nbSeq = 0;
+    {
+      u32 carryCum = 0, carryOff = 0, openIdx = 0, openLL = 0, openMl = 0, openOff = 0;
+      bool open = false;
+      for (u32 base = 0; base < nseq_raw; base += 64) {
+        u32 const i = base + lane;
+        bool const valid = i < nseq_raw;
+        u64 const rec = valid ? seq[i] : 0;
+        u32 const cum = (u32)(rec & 0x1FFFFu), ml = (u32)((rec >> 17) & 255u), off = (u32)((rec >> 25) & 0xFFFFu);
+        u32 pc = __shfl_up(cum, 1, 64), po = __shfl_up(off, 1, 64);
+        if (lane == 0) { pc = carryCum; po = carryOff; }
+        u32 const ll = cum - pc;
+        bool const flag = valid && i > 0 && ll == 0 && off == po;
+        bool const head = valid && !flag;
+        u64 const hm = __ballot(head);
+        // ml accumulation into the run head (in-batch) or into the open head (carried)
+        if (lane == 0) misc[64 - 1] = 0;
+        for (u32 k = lane; k < 64; k += 64) misc[k] = 0;  // misc[0..63] per-head sums
+        wave_sync();
+        u64 const below = hm & ((lane == 63) ? ~0ull : ((2ull << lane) - 1));
+        int const h = below ? 63 - __builtin_clzll(below) : -1;
+        u32 carryAdd = 0;
+        if (valid) {
+          if (h >= 0) atomicAdd(&misc[h], ml);
+          else carryAdd = ml;
+        }
+        carryAdd = wave_sum(carryAdd);
+        wave_sync();
+        u32 const hcount = (u32)__popcll(hm);
+        u32 const rank = (u32)__popcll(hm & ((1ull << lane) - 1));
+        u64 const headBitsAfter = hm & ~((lane == 63) ? ~0ull : ((2ull << lane) - 1));
+        // finalize the carried open head: closed if this batch has any head, or at the very end
+        openMl += carryAdd;
+        if (open && hcount) {
+          if (lane == 0) seq[openIdx] = (u64)openLL | ((u64)openMl << 17) | ((u64)openOff << 34);
+          open = false;
+        }
+        if (head) {
+          u32 const myMl = misc[lane];
+          u32 const idx = nbSeq + rank;
+          if (headBitsAfter) seq[idx] = (u64)ll | ((u64)myMl << 17) | ((u64)off << 34);
+        }
+        if (hcount) {
+          int const lastH = 63 - __builtin_clzll(hm);
+          openIdx = nbSeq + hcount - 1;
+          openLL = __shfl(ll, lastH, 64);
+          openOff = __shfl(off, lastH, 64);
+          openMl = __shfl(misc[lane], lastH, 64);
+          open = true;
+        }
+        nbSeq += hcount;
+        u32 const lastLane = min(63u, nseq_raw - 1 - base);
+        carryCum = __shfl(cum, lastLane, 64);
+        carryOff = __shfl(off, lastLane, 64);
+        wave_sync();
+      }
+      if (open && lane == 0) seq[openIdx] = (u64)openLL | ((u64)openMl << 17) | ((u64)openOff << 34);
+      wave_sync();
+    }
+
+    // nbSeq header
+    if (nbSeq < 128) { if (lane == 0) o.put(op, (u8)nbSeq); op += 1; }
+    else if (nbSeq < ZH_LONGNBSEQ) { if (lane == 0) { o.put(op, (u8)((nbSeq >> 8) + 0x80)); o.put(op + 1, (u8)nbSeq); } op += 2; }
+    else { if (lane == 0) { o.put(op, 0xFF); o.put(op + 1, (u8)(nbSeq - ZH_LONGNBSEQ)); o.put(op + 2, (u8)((nbSeq - ZH_LONGNBSEQ) >> 8)); } op += 3; }
+
+    if (nbSeq > 0) {
+      // pass B: repcodes (serial, wave-uniform) + codes + histograms; record = ll | mlBase<<17 | offBase<<34
+      u32 *hLL = hist, *hOF = hist + 64, *hML = hist + 128;
+      for (u32 i = lane; i < 192; i += 64) hist[i] = 0;
+      wave_sync();
+      u32 r0 = 1, r1 = 4, r2 = 8;
+      if (!(d.flags & ZH_F_FIRST)) { r0 = r1 = r2 = 0; }
+      for (u32 base = 0; base < nbSeq; base += 64) {
+        u32 const i = base + lane;
+        bool const valid = i < nbSeq;
+        u64 const rec = valid ? seq[i] : 0;
+        u32 const ll = (u32)(rec & 0x1FFFFu), ml = (u32)((rec >> 17) & 0x1FFFFu), off = (u32)(rec >> 34);
+        u32 obv = 0;
+        u32 const cnt = min(64u, nbSeq - base);
+        for (u32 j = 0; j < cnt; j++) {
+          u32 const o_ = __builtin_amdgcn_readlane(off, j);
+          u32 const l_ = __builtin_amdgcn_readlane(ll, j);
+          u32 const ll0 = l_ == 0;
+          u32 ob;
+          if (!ll0) ob = (o_ == r0 && r0) ? 1 : (o_ == r1 && r1) ? 2 : (o_ == r2 && r2) ? 3 : o_ + 3;
+          else ob = (o_ == r1 && r1) ? 1 : (o_ == r2 && r2) ? 2 : (r0 > 1 && o_ == r0 - 1) ? 3 : o_ + 3;
+          if (ob > 3) { r2 = r1; r1 = r0; r0 = o_; }
+          else {
+            u32 const idx = ob - 1 + ll0;
+            if (idx == 1) { u32 t = r1; r1 = r0; r0 = t; }
+            else if (idx == 2) { u32 t = r2; r2 = r1; r1 = r0; r0 = t; }
+            else if (idx == 3) { r2 = r1; r1 = r0; r0 = o_; }
+          }
+          obv = setlane(obv, ob, j);
+        }
+        if (valid) {
+          u32 const mlb = ml - 3;
+          atomicAdd(&hLL[ll_code(ll)], 1u);
+          atomicAdd(&hML[ml_code(mlb)], 1u);
+          atomicAdd(&hOF[highbit32(obv)], 1u);
+          seq[i] = (u64)ll | ((u64)mlb << 17) | ((u64)obv << 34);
+        }
+      }
+      wave_sync();
+      // tables: LL, OF, ML (ZSTD_selectEncodingType for strategy dfast + ZSTD_buildCTable)
+      u32 const seqHead = op;
+      op += 1;
+      u64 const rec0 = seq[0], recL = seq[nbSeq - 1];
+      u32 const first_code[3] = {ll_code((u32)(rec0 & 0x1FFFFu)), highbit32((u32)(rec0 >> 34)), ml_code((u32)((rec0 >> 17) & 0x1FFFFu))};
+      u32 const last_code[3] = {ll_code((u32)(recL & 0x1FFFFu)), highbit32((u32)(recL >> 34)), ml_code((u32)((recL >> 17) & 0x1FFFFu))};
+      u32 types[3], logs[3];
+      if (lane == 0) {
+        u32 hpos = 0;
+        for (int t = 0; t < 3; t++) {
+          u32 *cnt = hist + 64 * t;
+          u32 const maxSym = t == 0 ? 35 : t == 1 ? 31 : 52;
+          u32 const fseLog = t == 1 ? 8 : 9, defLog = t == 1 ? 5 : 6, defMax = t == 0 ? 35 : t == 1 ? 28 : 52;
+          const s16 *defNorm = t == 0 ? c_LL_def : t == 1 ? c_OF_def : c_ML_def;
+          u16 *st = t == 0 ? stLL : t == 1 ? stOF : stML;
+          FseSym *sy = t == 0 ? symLL : t == 1 ? symOF : symML;
+          u32 mx = maxSym;
+          while (mx && !cnt[mx]) mx--;
+          u32 mostFrequent = 0;
+          for (u32 s = 0; s <= mx; s++) mostFrequent = max(mostFrequent, cnt[s]);
+          bool const defAllowed = (t == 1) ? (mx <= 28) : true;
+          u32 type;
+          if (mostFrequent == nbSeq) type = (defAllowed && nbSeq <= 2) ? 0 : 1;
+          else if (defAllowed && ((nbSeq < (1u << defLog)) || (mostFrequent < (nbSeq >> (defLog - 1))))) type = 0;
+          else type = 2;
+          if (type == 1) {
+            st[0] = 0; st[1] = 0;
+            u32 const c = first_code[t];
+            sy[c].dNb = 0; sy[c].dFS = 0;
+            hbuf[hpos++] = (u8)c;
+            logs[t] = 0;
+          } else if (type == 0) {
+            for (u32 s = 0; s <= defMax; s++) norm[s] = defNorm[s];
+            fse_build_ctable(st, sy, tsym, norm, defMax, defLog);
+            logs[t] = defLog;
+          } else {
+            u32 nb1 = nbSeq;
+            u32 const tl = fse_optimal_table_log(fseLog, nbSeq, mx, 2);
+            if (cnt[last_code[t]] > 1) { cnt[last_code[t]]--; nb1--; }
+            fse_normalize(norm, tl, cnt, nb1, mx, nb1 >= 2048);
+            u32 h = fse_write_ncount(hbuf + hpos, norm, mx, tl);
+            hpos += h;
+            fse_build_ctable(st, sy, tsym, norm, mx, tl);
+            logs[t] = tl;
+          }
+          types[t] = type;
+        }
+        misc[0] = hpos;
+        misc[1] = (types[0] << 6) + (types[1] << 4) + (types[2] << 2);
+        misc[2] = logs[0]; misc[3] = logs[1]; misc[4] = logs[2];
+      }
+      wave_sync();
+      u32 const hpos = misc[0];
+      if (lane == 0) o.put(seqHead, (u8)misc[1]);
+      for (u32 i = lane; i < hpos; i += 64) o.put(op + i, hbuf[i]);
+      op += hpos;
+      u32 const logLL = misc[2], logOF = misc[3], logML = misc[4];
+
+      // pass C: FSE state chain (wave-uniform) + parallel bit packing, encode order nbSeq-1 .. 0
+      BitSink bs{op, 0};
+      u32 sLL = 0, sOF = 0, sML = 0;
+      for (u32 e0 = 0; e0 < nbSeq; e0 += 64) {
+        u32 const e = e0 + lane;
+        bool const valid = e < nbSeq;
+        u32 const i = nbSeq - 1 - e;
+        u64 const rec = valid ? seq[i] : 0;
+        u32 const ll = (u32)(rec & 0x1FFFFu), mlb = (u32)((rec >> 17) & 0x1FFFFu), ob = (u32)(rec >> 34);
+        u32 const llc = valid ? ll_code(ll) : 0, mlc = valid ? ml_code(mlb) : 0, ofc = valid ? highbit32(ob) : 0;
+        u32 vOF = 0, nOF = 0, vML = 0, nML = 0, vLL = 0, nLL = 0;
+        u32 const cnt = min(64u, nbSeq - e0);
+        for (u32 j = 0; j < cnt; j++) {
+          u32 const cl = __builtin_amdgcn_readlane(llc, j), cm = __builtin_amdgcn_readlane(mlc, j), co = __builtin_amdgcn_readlane(ofc, j);
+          if (e0 + j == 0) {
+            sML = fse_init_state(stML, symML, cm);
+            sOF = fse_init_state(stOF, symOF, co);
+            sLL = fse_init_state(stLL, symLL, cl);
+          } else {
+            u32 nb;
+            u32 v = fse_step(stOF, symOF, sOF, co, nb);
+            vOF = setlane(vOF, v, j); nOF = setlane(nOF, nb, j);
+            v = fse_step(stML, symML, sML, cm, nb);
+            vML = setlane(vML, v, j); nML = setlane(nML, nb, j);
+            v = fse_step(stLL, symLL, sLL, cl, nb);
+            vLL = setlane(vLL, v, j); nLL = setlane(nLL, nb, j);
+          }
+        }
+        u32 v6[6] = {vOF, vML, vLL, ll, mlb, ob};
+        u32 n6[6] = {nOF, nML, nLL, valid ? (u32)c_LL_bits[llc] : 0u, valid ? (u32)c_ML_bits[mlc] : 0u, ofc};
+        if (!valid) { n6[0] = n6[1] = n6[2] = 0; }
+        sink_append<6>(bs, o, sw, v6, n6);
+      }
+      {
+        u32 v3[3] = {sML, sOF, sLL};
+        u32 n3[3] = {lane == 0 ? logML : 0u, lane == 0 ? logOF : 0u, lane == 0 ? logLL : 0u};
+        sink_append<3>(bs, o, sw, v3, n3);
+      }
+      sink_close(bs, o, sw);
+      op = bs.pos;
+    }
+
+    u32 const body = op - body0;
+    u32 const minGain = (n >> 6) + 2;
+    u32 const maxC = n > minGain ? n - minGain : 0;
+    raw = body >= maxC;
+    if (!raw) {
+      u32 const hdr = last + (2u << 1) + (body << 3);
+      if (lane == 0) { o.put(blk, (u8)hdr); o.put(blk + 1, (u8)(hdr >> 8)); o.put(blk + 2, (u8)(hdr >> 16)); }
+      total = op;
+    } else {
+      u32 const hdr = last + (n << 3);
+      wave_sync();
+      if (lane == 0) { o.put(blk, (u8)hdr); o.put(blk + 1, (u8)(hdr >> 8)); o.put(blk + 2, (u8)(hdr >> 16)); }
+      copy_bytes(o, body0, d.src, n);
+      total = body0 + n;
+    }
+  }
+  if (lane == 0) {
+    if (d.flags & ZH_F_DIRECT) {
+      item_size[d.item] = total;
+      item_status[d.item] = total <= d.dst_cap ? ZH_ST_OK : ZH_ST_TOO_SMALL;
+    } else {
+      blk_size[b] = total <= d.dst_cap ? total : 0xFFFFFFFFu;
+    }
+  }
+}
+
+extern "C" u32 zh_entropy_lds_bytes() { return K2_LDS; }
+
+namespace zh {
+hipError_t entropy_init() { return hipFuncSetAttribute((const void *)zh_entropy_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)K2_LDS); }
+void entropy_launch(const ZhBlockDesc *d_descs, u32 nblocks, ZhWorkspace ws, u32 window_log, u32 cfg_block_size, u64 *d_item_size,
+                    u32 *d_item_status, u32 *d_blk_size, hipStream_t stream) {
+  hipLaunchKernelGGL(zh_entropy_kernel, dim3(nblocks), dim3(K2_THREADS), K2_LDS, stream, d_descs, ws, window_log, cfg_block_size, d_item_size,
+                     d_item_status, d_blk_size);
+}
+}  // namespace zh

@@ -1,0 +1,179 @@
+// zh_plan.hip — batch planning, multi-block frame gather, and launch wrappers.
+//
+// zh_plan_kernel : builds one ZhBlockDesc per (item, 64 KiB sub-block) from device
+//                  pointer/size arrays, for the stream-ordered batched entry point
+//                  (no host round trip, unlike the reference's compress_async,
+//                  src/cuda_zstd_nvcomp.cpp:319-437).
+// zh_gather_kernel: concatenates the staged blocks of multi-block frames (the
+//                  reference assembles them on the host with blocking copies,
+//                  src/cuda_zstd_manager.cu:2765-3027).
+#include "zh_common.h"
+#include "zh_launch.h"
+
+#include <mutex>
+#include <vector>
+
+extern "C" u32 zh_lz_lds_bytes();
+extern "C" u32 zh_entropy_lds_bytes();
+namespace zh {
+hipError_t lz_init();
+void lz_launch(const ZhBlockDesc *d_descs, u32 nblocks, ZhWorkspace ws, hipStream_t stream);
+hipError_t entropy_init();
+void entropy_launch(const ZhBlockDesc *d_descs, u32 nblocks, ZhWorkspace ws, u32 window_log, u32 cfg_block_size, u64 *d_item_size,
+                    u32 *d_item_status, u32 *d_blk_size, hipStream_t stream);
+}  // namespace zh
+
+extern "C" __global__ void zh_plan_kernel(const void *const *__restrict__ in_ptrs, const size_t *__restrict__ in_sizes, u32 nitems,
+                                          u32 bpi, void *const *__restrict__ out_ptrs, u64 out_cap, u8 *staging, ZhBlockDesc *descs,
+                                          ZhItemDesc *items, u64 *item_size, u32 *item_status) {
+  u32 const b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= nitems * bpi) return;
+  u32 const it = b / bpi, k = b % bpi;
+  u64 const size = in_sizes[it];
+  u64 const nb = (size + ZH_BLOCK_MAX - 1) / ZH_BLOCK_MAX;
+  ZhBlockDesc d;
+  d.src = (const u8 *)in_ptrs[it] + (u64)k * ZH_BLOCK_MAX;
+  d.frame_size = size;
+  d.item = it;
+  d.n = (k < nb) ? (u32)min((u64)ZH_BLOCK_MAX, size - (u64)k * ZH_BLOCK_MAX) : 0u;
+  d.flags = (k == 0 ? ZH_F_FIRST : 0u) | (k + 1 == nb ? ZH_F_LAST : 0u) | (nb == 1 ? ZH_F_DIRECT : 0u);
+  if (nb == 1) {
+    d.dst = (u8 *)out_ptrs[it];
+    d.dst_cap = (u32)min(out_cap, (u64)0xFFFFFFFFu);
+  } else {
+    d.dst = staging + (size_t)b * ZH_STAGE_SLOT;
+    d.dst_cap = ZH_STAGE_SLOT;
+  }
+  descs[b] = d;
+  if (k == 0) {
+    ZhItemDesc id;
+    id.dst = (u8 *)out_ptrs[it];
+    id.cap = out_cap;
+    id.first_block = b;
+    id.nblocks = (u32)nb;
+    items[it] = id;
+    if (size == 0) { item_size[it] = 0; item_status[it] = ZH_ST_INVALID; }
+  }
+}
+
+// one workgroup per item; only items with more than one block do work
+extern "C" __global__ __launch_bounds__(256) void zh_gather_kernel(const ZhItemDesc *__restrict__ items, const ZhBlockDesc *__restrict__ descs,
+                                                                    const u32 *__restrict__ blk_size, u64 *item_size, u32 *item_status) {
+  ZhItemDesc const id = items[blockIdx.x];
+  if (id.nblocks <= 1) return;
+  __shared__ u64 total_s;
+  __shared__ u32 bad_s;
+  if (threadIdx.x == 0) {
+    u64 t = 0;
+    u32 bad = 0;
+    for (u32 k = 0; k < id.nblocks; k++) {
+      u32 const s = blk_size[id.first_block + k];
+      if (s == 0xFFFFFFFFu) bad = 1; else t += s;
+    }
+    total_s = t;
+    bad_s = bad || t > id.cap;
+    item_size[blockIdx.x] = t;
+    item_status[blockIdx.x] = (bad || t > id.cap) ? ZH_ST_TOO_SMALL : ZH_ST_OK;
+  }
+  __syncthreads();
+  if (bad_s) return;
+  u64 off = 0;
+  for (u32 k = 0; k < id.nblocks; k++) {
+    u32 const s = blk_size[id.first_block + k];
+    const u8 *src = descs[id.first_block + k].dst;
+    u8 *dst = id.dst + off;
+    for (u32 i = threadIdx.x; i < s; i += blockDim.x) dst[i] = src[i];
+    off += s;
+  }
+  (void)total_s;
+}
+
+namespace zh {
+
+hipError_t init_kernels() {
+  hipError_t e = lz_init();
+  if (e != hipSuccess) return e;
+  return entropy_init();
+}
+
+u32 lz_lds_bytes() { return zh_lz_lds_bytes(); }
+u32 entropy_lds_bytes() { return zh_entropy_lds_bytes(); }
+
+// ---- optional per-kernel event timing (bench.py roofline): events recorded on the launch stream
+namespace {
+struct ProfState {
+  std::mutex mu;
+  bool on = false;
+  std::vector<hipEvent_t> pool;           // free events
+  std::vector<std::vector<hipEvent_t>> pending;  // per launch: e0 (pre-K1), e1 (K1 done), e2 (K2 done), e3 (K3 done)
+};
+ProfState &prof() {
+  static ProfState p;
+  return p;
+}
+hipEvent_t prof_event() {
+  ProfState &p = prof();
+  if (!p.pool.empty()) { hipEvent_t e = p.pool.back(); p.pool.pop_back(); return e; }
+  hipEvent_t e = nullptr;
+  (void)hipEventCreate(&e);
+  return e;
+}
+}  // namespace
+
+void profile_enable(bool on) {
+  std::lock_guard<std::mutex> g(prof().mu);
+  prof().on = on;
+}
+
+// totals[0..2] = summed ms of K1, K2, K3 over the recorded launches; returns launch count
+int profile_collect(double *totals) {
+  ProfState &p = prof();
+  std::lock_guard<std::mutex> g(p.mu);
+  totals[0] = totals[1] = totals[2] = 0;
+  int n = 0;
+  for (auto &ev : p.pending) {
+    (void)hipEventSynchronize(ev[3]);
+    float a = 0, b = 0, c = 0;
+    (void)hipEventElapsedTime(&a, ev[0], ev[1]);
+    (void)hipEventElapsedTime(&b, ev[1], ev[2]);
+    (void)hipEventElapsedTime(&c, ev[2], ev[3]);
+    totals[0] += a; totals[1] += b; totals[2] += c;
+    for (auto e : ev) p.pool.push_back(e);
+    n++;
+  }
+  p.pending.clear();
+  return n;
+}
+
+hipError_t launch_compress(const ZhBlockDesc *d_descs, u32 nblocks, ZhWorkspace ws, u32 window_log, u32 cfg_block_size, u64 *d_item_size,
+                           u32 *d_item_status, u32 *d_blk_size, const ZhItemDesc *d_items, u32 nitems, bool gather, hipStream_t stream) {
+  if (nblocks == 0) return hipSuccess;
+  std::vector<hipEvent_t> ev;
+  {
+    std::lock_guard<std::mutex> g(prof().mu);
+    if (prof().on) for (int k = 0; k < 4; k++) ev.push_back(prof_event());
+  }
+  if (!ev.empty()) (void)hipEventRecord(ev[0], stream);
+  lz_launch(d_descs, nblocks, ws, stream);
+  if (!ev.empty()) (void)hipEventRecord(ev[1], stream);
+  entropy_launch(d_descs, nblocks, ws, window_log, cfg_block_size, d_item_size, d_item_status, d_blk_size, stream);
+  if (!ev.empty()) (void)hipEventRecord(ev[2], stream);
+  if (gather && nitems) hipLaunchKernelGGL(zh_gather_kernel, dim3(nitems), dim3(256), 0, stream, d_items, d_descs, d_blk_size, d_item_size, d_item_status);
+  if (!ev.empty()) {
+    (void)hipEventRecord(ev[3], stream);
+    std::lock_guard<std::mutex> g(prof().mu);
+    prof().pending.push_back(ev);
+  }
+  return hipGetLastError();
+}
+
+hipError_t launch_plan(const void *const *d_in_ptrs, const size_t *d_in_sizes, u32 nitems, u32 bpi, void *const *d_out_ptrs, u64 out_cap,
+                       u8 *staging, ZhBlockDesc *d_descs, ZhItemDesc *d_items, u64 *d_item_size, u32 *d_item_status, hipStream_t stream) {
+  u32 const total = nitems * bpi;
+  if (!total) return hipSuccess;
+  hipLaunchKernelGGL(zh_plan_kernel, dim3((total + 255) / 256), dim3(256), 0, stream, d_in_ptrs, d_in_sizes, nitems, bpi, d_out_ptrs, out_cap,
+                     staging, d_descs, d_items, d_item_size, d_item_status);
+  return hipGetLastError();
+}
+
+}  // namespace zh

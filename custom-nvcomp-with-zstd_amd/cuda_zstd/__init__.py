@@ -1,0 +1,214 @@
+"""Python binding of libcuda_zstd_hip.so (gfx950 Zstandard compressor).
+
+Mirrors the reference's Python package (python/cuda_zstd/__init__.py:90-120,
+python/src/binding.cpp:151-330): ``compress``, ``decompress``,
+``compress_batch`` and a ``Manager`` class, here over torch device tensors and
+the library's C ABI (include/cuda_zstd_capi.h).  PyTorch is only used for
+device memory and streams.
+
+The product path never falls back to a CPU implementation: if the shared
+library or a GPU is missing, every call raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from typing import List, Sequence
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(os.path.dirname(_HERE), "libcuda_zstd_hip.so")
+
+# nvcomp-style return codes (reference src/cuda_zstd_nvcomp.cpp:75-96)
+OK, INVALID, OOM, DEVICE_ERROR, CORRUPT, TOO_SMALL, CHECKSUM, COMPRESSION = 0, 2, 3, 4, 6, 7, 10, 12
+
+_lib = None
+
+
+class ZstdError(RuntimeError):
+    def __init__(self, code: int, what: str = ""):
+        self.code = code
+        super().__init__(f"{what}: {error_string(code)} (code {code})")
+
+
+def lib() -> ctypes.CDLL:
+    """Load the HIP library (raises if it was not built)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise ImportError(f"{LIB_PATH} not found: build it with __graft_entry__.build() (make -C custom-nvcomp-with-zstd_amd)")
+        L = ctypes.CDLL(LIB_PATH)
+        vp, sz, i = ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int
+        psz, pvp, pi = ctypes.POINTER(sz), ctypes.POINTER(vp), ctypes.POINTER(i)
+        sig = {
+            "cuda_zstd_create_manager": (vp, [i]),
+            "cuda_zstd_destroy_manager": (None, [vp]),
+            "cuda_zstd_compress": (i, [vp, vp, sz, vp, psz, vp, sz, vp]),
+            "cuda_zstd_decompress": (i, [vp, vp, sz, vp, psz, vp, sz, vp]),
+            "cuda_zstd_get_compress_workspace_size": (sz, [vp, sz]),
+            "cuda_zstd_get_decompress_workspace_size": (sz, [vp, sz]),
+            "cuda_zstd_get_max_compressed_size": (sz, [vp, sz]),
+            "cuda_zstd_get_batch_compress_workspace_size": (sz, [vp, psz, sz]),
+            "cuda_zstd_compress_batch": (i, [vp, pvp, psz, sz, pvp, psz, pi, vp, sz, vp]),
+            "cuda_zstd_get_error_string": (ctypes.c_char_p, [i]),
+            "cuda_zstd_is_error": (i, [i]),
+            "nvcomp_zstd_batch_create_v5": (vp, [i, ctypes.c_uint, i]),
+            "nvcomp_zstd_batch_destroy_v5": (None, [vp]),
+            "nvcomp_zstd_batch_get_compress_temp_size_v5": (sz, [vp, psz, sz]),
+            "nvcomp_zstd_batch_get_max_compressed_chunk_size_v5": (sz, [vp, sz]),
+            "nvcomp_zstd_batch_compress_async_v5": (i, [vp, vp, vp, sz, vp, vp, vp, sz, vp]),
+            "nvcomp_zstd_batched_compress_get_temp_size_v5": (sz, [sz, sz]),
+            "nvcomp_zstd_batched_compress_async_v5": (i, [vp, vp, vp, sz, sz, vp, vp, vp, vp, sz, vp]),
+            "cuda_zstd_hip_version": (ctypes.c_char_p, []),
+            "cuda_zstd_hip_profile_enable": (None, [i]),
+            "cuda_zstd_hip_profile_collect": (i, [ctypes.POINTER(ctypes.c_double)]),
+            "cuda_zstd_hip_kernel_lds_bytes": (ctypes.c_uint, [i]),
+        }
+        for name, (res, args) in sig.items():
+            f = getattr(L, name)
+            f.restype = res
+            f.argtypes = args
+        _lib = L
+    return _lib
+
+
+def error_string(code: int) -> str:
+    return lib().cuda_zstd_get_error_string(code).decode()
+
+
+def _torch():
+    import torch
+
+    if not torch.cuda.is_available():
+        raise RuntimeError("cuda_zstd: no GPU visible (the gfx950 path has no CPU fallback)")
+    return torch
+
+
+def _stream_ptr(stream) -> int:
+    torch = _torch()
+    s = stream if stream is not None else torch.cuda.current_stream()
+    return s.cuda_stream
+
+
+def max_compressed_size(n: int) -> int:
+    """reference estimate_compressed_size (src/cuda_zstd_types.cpp:831-853)."""
+    nb = max(1, (n + 128 * 1024 - 1) // (128 * 1024))
+    return n + n // 255 + nb * 3 + 512
+
+
+class Manager:
+    """C-ABI manager handle (reference PyManager, python/src/binding.cpp:272-329)."""
+
+    def __init__(self, level: int = 3):
+        self.level = level
+        self._h = lib().cuda_zstd_create_manager(level)
+        if not self._h:
+            raise ZstdError(INVALID, "cuda_zstd_create_manager")
+        self._ws = None
+
+    def close(self):
+        if self._h:
+            lib().cuda_zstd_destroy_manager(self._h)
+            self._h = None
+
+    __del__ = close
+
+    def _workspace(self, nbytes: int):
+        torch = _torch()
+        if self._ws is None or self._ws.numel() < nbytes:
+            self._ws = torch.empty(max(nbytes, 256), dtype=torch.uint8, device="cuda")
+        return self._ws
+
+    def compress(self, data, stream=None):
+        """Compress a contiguous uint8 device tensor into one zstd frame (device tensor)."""
+        torch = _torch()
+        data = data.contiguous().view(torch.uint8)
+        n = data.numel()
+        out = torch.empty(max_compressed_size(n), dtype=torch.uint8, device=data.device)
+        ws_n = lib().cuda_zstd_get_compress_workspace_size(self._h, n)
+        ws = self._workspace(ws_n)
+        size = ctypes.c_size_t(out.numel())
+        rc = lib().cuda_zstd_compress(self._h, data.data_ptr(), n, out.data_ptr(), ctypes.byref(size), ws.data_ptr(), ws.numel(), _stream_ptr(stream))
+        if rc:
+            raise ZstdError(rc, "cuda_zstd_compress")
+        return out[: size.value]
+
+    def compress_batch(self, chunks: Sequence, stream=None) -> List:
+        """ZstdBatchManager::compress_batch over a list of uint8 device tensors."""
+        torch = _torch()
+        n = len(chunks)
+        ins = [c.contiguous().view(torch.uint8) for c in chunks]
+        sizes = [t.numel() for t in ins]
+        caps = [max_compressed_size(s) for s in sizes]
+        offs = [0]
+        for c in caps:
+            offs.append(offs[-1] + ((c + 255) // 256) * 256)
+        out = torch.empty(offs[-1], dtype=torch.uint8, device="cuda")
+        in_ptrs = (ctypes.c_void_p * n)(*[t.data_ptr() for t in ins])
+        out_ptrs = (ctypes.c_void_p * n)(*[out.data_ptr() + o for o in offs[:-1]])
+        in_sz = (ctypes.c_size_t * n)(*sizes)
+        out_sz = (ctypes.c_size_t * n)(*caps)
+        st = (ctypes.c_int * n)()
+        ws_n = lib().cuda_zstd_get_batch_compress_workspace_size(self._h, in_sz, n)
+        ws = self._workspace(ws_n)
+        rc = lib().cuda_zstd_compress_batch(self._h, in_ptrs, in_sz, n, out_ptrs, out_sz, st, ws.data_ptr(), ws.numel(), _stream_ptr(stream))
+        if rc and all(s == OK for s in st):
+            raise ZstdError(rc, "cuda_zstd_compress_batch")
+        res = []
+        for k in range(n):
+            if st[k] != OK:
+                raise ZstdError(st[k], f"cuda_zstd_compress_batch item {k}")
+            res.append(out[offs[k] : offs[k] + out_sz[k]])
+        return res
+
+
+class BatchedCompressor:
+    """Stream-ordered batched compression of equal-capacity chunk slots
+    (nvcomp_zstd_batched_compress_async_v5).  Used by bench.py."""
+
+    def __init__(self, level: int = 3, chunk_size: int = 64 * 1024):
+        self._h = lib().nvcomp_zstd_batch_create_v5(level, chunk_size, 0)
+        if not self._h:
+            raise ZstdError(INVALID, "nvcomp_zstd_batch_create_v5")
+        self.chunk_size = chunk_size
+
+    def close(self):
+        if self._h:
+            lib().nvcomp_zstd_batch_destroy_v5(self._h)
+            self._h = None
+
+    __del__ = close
+
+    @staticmethod
+    def temp_size(num_chunks: int, max_chunk: int) -> int:
+        return lib().nvcomp_zstd_batched_compress_get_temp_size_v5(num_chunks, max_chunk)
+
+    def max_out(self, max_chunk: int) -> int:
+        return lib().nvcomp_zstd_batch_get_max_compressed_chunk_size_v5(self._h, max_chunk)
+
+    def compress_async(self, d_in_ptrs, d_in_sizes, max_chunk, d_out_ptrs, d_out_sizes, d_status, temp, stream=None):
+        n = d_in_ptrs.numel()
+        rc = lib().nvcomp_zstd_batched_compress_async_v5(
+            self._h, d_in_ptrs.data_ptr(), d_in_sizes.data_ptr(), max_chunk, n, d_out_ptrs.data_ptr(), d_out_sizes.data_ptr(),
+            d_status.data_ptr() if d_status is not None else None, temp.data_ptr(), temp.numel(), _stream_ptr(stream))
+        if rc:
+            raise ZstdError(rc, "nvcomp_zstd_batched_compress_async_v5")
+
+
+def compress(data, level: int = 3, stream=None):
+    return Manager(level).compress(data, stream)
+
+
+def compress_batch(chunks, level: int = 3, stream=None):
+    return Manager(level).compress_batch(chunks, stream)
+
+
+def profile_enable(on: bool = True) -> None:
+    """Record HIP events around each kernel of every launch (on the launch stream)."""
+    lib().cuda_zstd_hip_profile_enable(1 if on else 0)
+
+
+def profile_collect():
+    """-> (launches, [ms_lz, ms_entropy, ms_gather] summed over them)."""
+    ms = (ctypes.c_double * 3)()
+    n = lib().cuda_zstd_hip_profile_collect(ms)
+    return n, list(ms)

@@ -1,0 +1,55 @@
+// cuda_zstd_hybrid.h — CPU/GPU routing engine (reference include/cuda_zstd_hybrid.h:73-240).
+//
+// Routing here is explicit: FORCE_CPU runs host libzstd (the reference's
+// cpu_compress, src/cuda_zstd_hybrid.cu:402-458); FORCE_GPU / PREFER_GPU run the
+// gfx950 kernels; AUTO / PREFER_CPU / ADAPTIVE follow the reference's simple
+// size/location rules (decide_route, :196-328) without its profiling heuristics.
+// The C ABI (:292-363) lives in cuda_zstd_capi.h.
+#ifndef CUDA_ZSTD_HYBRID_H_
+#define CUDA_ZSTD_HYBRID_H_
+
+#include "cuda_zstd_manager.h"
+
+#ifdef __cplusplus
+namespace cuda_zstd {
+
+class HybridEngine {
+ public:
+  HybridEngine();
+  explicit HybridEngine(const HybridConfig &config);
+  ~HybridEngine();
+  HybridEngine(const HybridEngine &) = delete;
+  HybridEngine &operator=(const HybridEngine &) = delete;
+
+  Status configure(const HybridConfig &config);
+  HybridConfig get_config() const;
+  Status set_compression_level(int level);
+
+  Status compress(const void *input, size_t input_size, void *output, size_t *output_size, DataLocation input_loc = DataLocation::HOST,
+                  DataLocation output_loc = DataLocation::HOST, HybridResult *result = nullptr, hipStream_t stream = 0);
+  Status decompress(const void *input, size_t input_size, void *output, size_t *output_size, DataLocation input_loc = DataLocation::HOST,
+                    DataLocation output_loc = DataLocation::HOST, HybridResult *result = nullptr, hipStream_t stream = 0);
+  Status compress_batch(const void *const *inputs, const size_t *input_sizes, void **outputs, size_t *output_sizes, size_t count,
+                        DataLocation input_loc = DataLocation::HOST, DataLocation output_loc = DataLocation::HOST,
+                        BatchRoutingResult *results = nullptr, hipStream_t stream = 0);
+
+  size_t get_max_compressed_size(size_t input_size) const;
+  ExecutionBackend query_routing(size_t data_size, DataLocation input_loc, DataLocation output_loc, bool is_compression) const;
+  CompressionStats get_stats() const;
+  void reset_stats();
+  static DataLocation detect_location(const void *ptr);
+
+ private:
+  class Impl;
+  std::unique_ptr<Impl> pimpl_;
+};
+
+Status hybrid_compress(const void *input, size_t input_size, void *output, size_t *output_size, DataLocation input_loc = DataLocation::HOST,
+                       DataLocation output_loc = DataLocation::HOST, int compression_level = 3, HybridResult *result = nullptr,
+                       hipStream_t stream = 0);
+std::unique_ptr<HybridEngine> create_hybrid_engine(const HybridConfig &config = HybridConfig{});
+std::unique_ptr<HybridEngine> create_hybrid_engine(int compression_level);
+
+}  // namespace cuda_zstd
+#endif  // __cplusplus
+#endif  // CUDA_ZSTD_HYBRID_H_

@@ -1,0 +1,164 @@
+// cuda_zstd_manager.h — manager interface of the gfx950 Zstandard compressor.
+//
+// Same class names, virtual signatures and semantics as the reference's
+// include/cuda_zstd_manager.h:
+//   ZstdManager          :45-100   (pure-virtual interface)
+//   ZstdBatchManager     :113-278  (compress_batch, inference decompress API)
+//   ZstdStreamingManager :300-352  (each chunk an independent frame, as in the reference)
+//   factories            :358-363, convenience :369-386, utilities :392-419
+// The C ABI of the same header (:433-479) lives in cuda_zstd_capi.h.
+#ifndef CUDA_ZSTD_MANAGER_H_
+#define CUDA_ZSTD_MANAGER_H_
+
+#include "cuda_zstd_types.h"
+#include "cuda_zstd_capi.h"
+
+#ifdef __cplusplus
+#include <memory>
+#include <vector>
+
+namespace cuda_zstd {
+
+namespace dictionary {
+// Raw-content dictionary (reference include/cuda_zstd_dictionary.h).  Dictionary
+// compression is a "next" row: set_dictionary() reports
+// ERROR_NOT_IMPLEMENTED until then, instead of emitting frames libzstd cannot decode.
+struct Dictionary {
+  std::vector<u8> raw_content;
+  u32 dict_id = 0;
+  size_t size() const { return raw_content.size(); }
+};
+}  // namespace dictionary
+
+class ZstdManager {
+ public:
+  virtual ~ZstdManager() = default;
+  virtual Status configure(const CompressionConfig &config) = 0;
+  virtual CompressionConfig get_config() const = 0;
+  virtual size_t get_compress_temp_size(size_t uncompressed_size) const = 0;
+  virtual size_t get_decompress_temp_size(size_t compressed_size) const = 0;
+  virtual size_t get_max_compressed_size(size_t uncompressed_size) const = 0;
+  virtual Status compress(const void *uncompressed_data, size_t uncompressed_size, void *compressed_data, size_t *compressed_size,
+                          void *temp_workspace, size_t temp_size, const void *dict_buffer, size_t dict_size, hipStream_t stream,
+                          void *streaming_context = nullptr) = 0;
+  virtual Status decompress(const void *compressed_data, size_t compressed_size, void *uncompressed_data, size_t *uncompressed_size,
+                            void *temp_workspace, size_t temp_size, hipStream_t stream = 0) = 0;
+  virtual Status set_dictionary(const dictionary::Dictionary &dict) = 0;
+  virtual Status get_dictionary(dictionary::Dictionary &dict) const = 0;
+  virtual Status clear_dictionary() = 0;
+  virtual const CompressionStats &get_stats() const = 0;
+  virtual Status set_compression_level(int level) = 0;
+  virtual int get_compression_level() const = 0;
+  virtual void reset_stats() = 0;
+
+  enum class ExecutionPath { CPU, GPU_BATCH, GPU_CHUNK };
+  // reference src/cuda_zstd_manager.cu:6465-6471: size < threshold -> CPU
+  static ExecutionPath select_execution_path(size_t size, int cpu_threshold = 0);
+  virtual Status preallocate_tables(hipStream_t stream = 0) { (void)stream; return Status::SUCCESS; }
+  virtual Status free_tables(hipStream_t stream = 0) { (void)stream; return Status::SUCCESS; }
+};
+
+class ZstdBatchManager : public ZstdManager {
+ public:
+  ZstdBatchManager();
+  explicit ZstdBatchManager(const CompressionConfig &config);
+  ~ZstdBatchManager() override;
+
+  Status configure(const CompressionConfig &config) override;
+  CompressionConfig get_config() const override;
+  size_t get_compress_temp_size(size_t uncompressed_size) const override;
+  size_t get_decompress_temp_size(size_t compressed_size) const override;
+  size_t get_max_compressed_size(size_t uncompressed_size) const override;
+  Status compress(const void *uncompressed_data, size_t uncompressed_size, void *compressed_data, size_t *compressed_size,
+                  void *temp_workspace, size_t temp_size, const void *dict_buffer, size_t dict_size, hipStream_t stream = 0,
+                  void *streaming_context = nullptr) override;
+  Status decompress(const void *compressed_data, size_t compressed_size, void *uncompressed_data, size_t *uncompressed_size,
+                    void *temp_workspace, size_t temp_size, hipStream_t stream = 0) override;
+  Status set_dictionary(const dictionary::Dictionary &dict) override;
+  Status get_dictionary(dictionary::Dictionary &dict) const override;
+  Status clear_dictionary() override;
+  const CompressionStats &get_stats() const override;
+  Status set_compression_level(int level) override;
+  int get_compression_level() const override;
+  void reset_stats() override;
+
+  Status compress_batch(const std::vector<BatchItem> &items, void *temp_workspace, size_t temp_size, hipStream_t stream = 0);
+  Status decompress_batch(const std::vector<BatchItem> &items, void *temp_workspace, size_t temp_size, hipStream_t stream = 0);
+  size_t get_batch_compress_temp_size(const std::vector<size_t> &uncompressed_sizes) const;
+  size_t get_batch_decompress_temp_size(const std::vector<size_t> &compressed_sizes) const;
+
+  Status decompress_to_preallocated(const void *compressed_data, size_t compressed_size, void *preallocated_output,
+                                    size_t output_capacity, size_t *actual_output_size, void *temp_workspace, size_t temp_size,
+                                    hipStream_t stream = 0);
+  Status decompress_batch_preallocated(std::vector<BatchItem> &items, void *temp_workspace, size_t temp_size, hipStream_t stream = 0);
+  Status decompress_async_no_sync(const void *compressed_data, size_t compressed_size, void *preallocated_output,
+                                  size_t output_capacity, size_t *d_actual_size, void *temp_workspace, size_t temp_size,
+                                  hipStream_t stream);
+  size_t get_inference_workspace_size(size_t max_compressed_size, size_t max_output_size) const;
+  Status allocate_inference_workspace(size_t max_compressed_size, size_t max_output_size, void **workspace_ptr, size_t *workspace_size);
+  Status free_inference_workspace(void *workspace_ptr);
+
+  // Stream-ordered batched compression over device arrays (no host sync); used by the
+  // nvcomp_zstd_batched_compress_async_v5 C entry.
+  Status compress_batch_device(const void *const *d_in_ptrs, const size_t *d_in_sizes, size_t max_chunk_bytes, size_t count,
+                               void *const *d_out_ptrs, size_t *d_out_sizes, int *d_statuses, void *temp_workspace, size_t temp_size,
+                               hipStream_t stream);
+  static size_t get_batch_device_temp_size(size_t count, size_t max_chunk_bytes);
+
+ private:
+  class Impl;
+  std::unique_ptr<Impl> pimpl_;
+};
+
+class ZstdStreamingManager {
+ public:
+  ZstdStreamingManager();
+  explicit ZstdStreamingManager(const CompressionConfig &config);
+  ~ZstdStreamingManager();
+  Status init_compression(hipStream_t stream = 0, size_t max_chunk_size = 0);
+  Status init_compression_with_history(hipStream_t stream = 0, size_t max_chunk_size = 0);
+  Status init_decompression(hipStream_t stream = 0);
+  Status compress_chunk(const void *input, size_t input_size, void *output, size_t *output_size, bool is_last_chunk, hipStream_t stream = 0);
+  Status compress_chunk_with_history(const void *input, size_t input_size, void *output, size_t *output_size, bool is_last_chunk,
+                                     hipStream_t stream = 0);
+  Status decompress_chunk(const void *input, size_t input_size, void *output, size_t *output_size, bool *is_last_chunk,
+                          hipStream_t stream = 0);
+  Status reset();
+  Status reset_streaming();
+  Status flush(hipStream_t stream = 0);
+  Status flush_streaming(hipStream_t stream = 0);
+  Status set_config(const CompressionConfig &config);
+  Status set_dictionary(const dictionary::Dictionary &dict);
+  CompressionConfig get_config() const;
+  size_t get_temp_size() const;
+  bool is_compression_initialized() const;
+  bool is_decompression_initialized() const;
+
+ private:
+  class Impl;
+  std::unique_ptr<Impl> pimpl_;
+};
+
+std::unique_ptr<ZstdManager> create_manager(int compression_level = 3);
+std::unique_ptr<ZstdManager> create_manager(const CompressionConfig &config);
+std::unique_ptr<ZstdBatchManager> create_batch_manager(int compression_level = 3);
+std::unique_ptr<ZstdStreamingManager> create_streaming_manager(int compression_level = 3);
+
+Status compress_simple(const void *uncompressed_data, size_t uncompressed_size, void *compressed_data, size_t *compressed_size,
+                       int compression_level = 3, hipStream_t stream = 0);
+Status decompress_simple(const void *compressed_data, size_t compressed_size, void *uncompressed_data, size_t *uncompressed_size,
+                         hipStream_t stream = 0);
+
+Status get_decompressed_size(const void *compressed_data, size_t compressed_size, size_t *decompressed_size);
+Status validate_compressed_data(const void *compressed_data, size_t compressed_size, bool check_checksum = true);
+size_t estimate_compressed_size(size_t uncompressed_size, int compression_level);
+Status validate_config(const CompressionConfig &config);
+void apply_level_parameters(CompressionConfig &config);
+u32 get_optimal_block_size(u32 input_size, u32 compression_level);
+
+constexpr const char *get_format_name() { return "cuda_zstd"; }
+constexpr u32 get_format_version() { return 0x00010000; }
+
+}  // namespace cuda_zstd
+#endif  // __cplusplus
+#endif  // CUDA_ZSTD_MANAGER_H_

@@ -1,0 +1,80 @@
+"""C ABI surface (no GPU needed): the library loads, exports every entry point
+include/cuda_zstd_capi.h declares, and the host-only calls behave like the
+reference's C API (src/cuda_zstd_c_api.cpp:10-209, src/cuda_zstd_nvcomp.cpp:75-119)."""
+import ctypes
+import os
+import re
+
+import pytest
+
+import zh_testlib as T
+
+HDR = os.path.join(T.ROOT, "include", "cuda_zstd_capi.h")
+
+
+def declared_functions():
+    txt = open(HDR).read()
+    txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
+    names = re.findall(r"\b([a-z_0-9]+)\s*\(", txt)
+    return sorted({n for n in names if n.startswith(("cuda_zstd_", "nvcomp_zstd_"))})
+
+
+@pytest.fixture(scope="module")
+def L():
+    import cuda_zstd
+
+    return cuda_zstd.lib()
+
+
+def test_exports_every_declared_symbol(L):
+    names = declared_functions()
+    assert len(names) >= 35
+    missing = [n for n in names if not hasattr(L, n)]
+    assert not missing, missing
+
+
+def test_error_strings_and_codes(L):
+    import cuda_zstd
+
+    assert L.cuda_zstd_is_error(0) == 0 and L.cuda_zstd_is_error(7) == 1
+    assert cuda_zstd.error_string(0) == "Success"
+    assert cuda_zstd.error_string(7) == "Buffer too small"
+    assert cuda_zstd.error_string(99) == "Generic error"
+
+
+def test_manager_lifecycle_and_invalid_args(L):
+    assert not L.cuda_zstd_create_manager(0) and not L.cuda_zstd_create_manager(23)
+    m = L.cuda_zstd_create_manager(3)
+    assert m
+    sz = ctypes.c_size_t(100)
+    # null manager / null pointers -> 2 (invalid parameter), like the reference
+    assert L.cuda_zstd_compress(None, None, 10, None, ctypes.byref(sz), None, 0, None) == 2
+    assert L.cuda_zstd_compress(m, None, 10, None, ctypes.byref(sz), None, 0, None) == 2
+    assert L.cuda_zstd_get_compress_workspace_size(None, 65536) == 0
+    ws = L.cuda_zstd_get_compress_workspace_size(m, 65536)
+    assert 0 < ws < 1 << 20  # reference asked for 13 MiB per 64 KiB item
+    assert L.cuda_zstd_get_max_compressed_size(m, 65536) == 65536 + 65536 // 255 + 3 + 512
+    L.cuda_zstd_destroy_manager(m)
+
+
+def test_batch_workspace_is_linear_and_small(L):
+    m = L.cuda_zstd_create_manager(3)
+    n = 1024
+    sizes = (ctypes.c_size_t * n)(*([65536] * n))
+    ws = L.cuda_zstd_get_batch_compress_workspace_size(m, sizes, n)
+    assert ws < n * 200 * 1024
+    assert L.nvcomp_zstd_batched_compress_get_temp_size_v5(n, 65536) <= ws + 4096
+    L.cuda_zstd_destroy_manager(m)
+
+
+def test_nvcomp_batch_manager_handle(L):
+    h = L.nvcomp_zstd_batch_create_v5(3, 65536, 0)
+    assert h
+    assert L.nvcomp_zstd_batch_get_max_compressed_chunk_size_v5(h, 65536) == 65536 + 257 + 3 + 512
+    L.nvcomp_zstd_batch_destroy_v5(h)
+    assert not L.nvcomp_zstd_batch_create_v5(40, 65536, 0)
+
+
+def test_kernel_lds_budget(L):
+    assert 150 * 1024 < L.cuda_zstd_hip_kernel_lds_bytes(0) <= 160 * 1024
+    assert L.cuda_zstd_hip_kernel_lds_bytes(1) <= 16 * 1024

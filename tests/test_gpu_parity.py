@@ -1,0 +1,161 @@
+"""GPU parity: frames produced by the gfx950 kernels through the C ABI are
+byte-identical to the oracle (oracle/zstd_oracle.c) on the same inputs, and stock
+libzstd decodes them to the original bytes.  Sizes cover the reference's edge
+cases (tests/test_compressible_data.cu, tests/test_c_api_edge_cases.cu) and the
+BASELINE.json configs (C2: 64 MiB single buffer, C3: 16384 x 64 KiB)."""
+import ctypes
+
+import numpy as np
+import pytest
+
+import zh_testlib as T
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def torch_cuda():
+    import torch
+
+    assert torch.cuda.is_available(), "gpu tests need a GPU"
+    return torch
+
+
+@pytest.fixture(scope="module")
+def mgr(torch_cuda):
+    import cuda_zstd
+
+    return cuda_zstd.Manager(3)
+
+
+def _check(frames, datas, decode=True):
+    for k, (f, d) in enumerate(zip(frames, datas)):
+        got = f.cpu().numpy().tobytes() if not isinstance(f, (bytes, bytearray)) else bytes(f)
+        want = T.oracle_frame(d)
+        assert got == want, f"item {k}: GPU frame ({len(got)} B) != oracle ({len(want)} B)"
+        if decode and T.zstd() is not None:
+            assert T.zstd_decompress(got, len(d)) == np.ascontiguousarray(d).tobytes(), f"item {k}: libzstd round trip"
+
+
+def test_special_inputs(torch_cuda, mgr):
+    items = T.special_inputs()
+    names = sorted(items)
+    datas = [items[k] for k in names]
+    outs = mgr.compress_batch([torch_cuda.from_numpy(d.copy()).cuda() for d in datas])
+    _check(outs, datas)
+
+
+@pytest.mark.parametrize("kind", sorted(T.KINDS))
+def test_corpora_batch(torch_cuda, mgr, kind):
+    data = T.gen(T.KINDS[kind], 48, 0x5EED0003)
+    datas = [data[i * 65536:(i + 1) * 65536] for i in range(48)]
+    dev = torch_cuda.from_numpy(data).cuda()
+    outs = mgr.compress_batch([dev[i * 65536:(i + 1) * 65536] for i in range(48)])
+    _check(outs, datas)
+
+
+def test_ragged_sizes(torch_cuda, mgr):
+    rng = np.random.default_rng(5)
+    sizes = [int(s) for s in rng.integers(1, 65537, 40)] + [65536, 65535, 4096, 4097, 8, 9, 16, 17, 255, 256, 257]
+    datas = [T.gen(T.DG_MIX, 1, 100 + i, s) for i, s in enumerate(sizes)]
+    outs = mgr.compress_batch([torch_cuda.from_numpy(d).cuda() for d in datas])
+    _check(outs, datas)
+
+
+def test_single_buffer_multiblock(torch_cuda, mgr):
+    data = np.concatenate([T.gen(T.DG_TEXT, 3, 5, 65536), T.gen(T.DG_CSV, 1, 6, 50000), T.gen(T.DG_RANDOM, 1, 7, 9000), np.zeros(70000, np.uint8)])
+    out = mgr.compress(torch_cuda.from_numpy(data).cuda())
+    _check([out], [data])
+
+
+def test_c2_64mib_single_buffer(torch_cuda, mgr):
+    """BASELINE config 2: 64 MiB of iid bytes over a 16-symbol alphabet, one frame."""
+    data = T.gen(T.DG_SYM16, 1024, 0x5EED0002)
+    out = mgr.compress(torch_cuda.from_numpy(data).cuda()).cpu().numpy().tobytes()
+    assert out == T.oracle_frame(data)
+    if T.zstd() is not None:
+        assert T.zstd_decompress(out, len(data)) == data.tobytes()
+    assert len(data) / len(out) > 1.9
+
+
+def test_errors_per_item(torch_cuda):
+    import cuda_zstd
+
+    L = cuda_zstd.lib()
+    m = L.cuda_zstd_create_manager(3)
+    src = torch_cuda.from_numpy(T.gen(T.DG_RANDOM, 1, 9, 65536)).cuda()
+    dst = torch_cuda.empty(70000, dtype=torch_cuda.uint8, device="cuda")
+    n = 3
+    ins = (ctypes.c_void_p * n)(src.data_ptr(), src.data_ptr(), src.data_ptr())
+    outs = (ctypes.c_void_p * n)(dst.data_ptr(), dst.data_ptr() + 35000, dst.data_ptr())
+    isz = (ctypes.c_size_t * n)(65536, 0, 1000)
+    osz = (ctypes.c_size_t * n)(100, 35000, 35000)  # item0: capacity too small; item1: empty input
+    st = (ctypes.c_int * n)()
+    ws = torch_cuda.empty(L.cuda_zstd_get_batch_compress_workspace_size(m, isz, n), dtype=torch_cuda.uint8, device="cuda")
+    rc = L.cuda_zstd_compress_batch(m, ins, isz, n, outs, osz, st, ws.data_ptr(), ws.numel(), None)
+    assert rc == 1  # ERROR_GENERIC when any item failed (reference :5795)
+    assert list(st) == [7, 2, 0]
+    L.cuda_zstd_destroy_manager(m)
+
+
+def test_batched_device_api_matches(torch_cuda):
+    """nvcomp_zstd_batched_compress_async_v5: device pointer/size arrays, stream-ordered."""
+    import cuda_zstd
+
+    n, cs = 64, 65536
+    data = T.gen(T.DG_MIX, n, 0x5EED0003, cs, first=1000)
+    dev = torch_cuda.from_numpy(data).cuda()
+    bc = cuda_zstd.BatchedCompressor(3, cs)
+    slot = (bc.max_out(cs) + 255) // 256 * 256
+    out = torch_cuda.empty(n * slot, dtype=torch_cuda.uint8, device="cuda")
+    in_ptrs = torch_cuda.tensor([dev.data_ptr() + i * cs for i in range(n)], dtype=torch_cuda.int64, device="cuda")
+    out_ptrs = torch_cuda.tensor([out.data_ptr() + i * slot for i in range(n)], dtype=torch_cuda.int64, device="cuda")
+    in_sizes = torch_cuda.full((n,), cs, dtype=torch_cuda.int64, device="cuda")
+    out_sizes = torch_cuda.zeros(n, dtype=torch_cuda.int64, device="cuda")
+    status = torch_cuda.full((n,), -1, dtype=torch_cuda.int32, device="cuda")
+    temp = torch_cuda.empty(bc.temp_size(n, cs), dtype=torch_cuda.uint8, device="cuda")
+    bc.compress_async(in_ptrs, in_sizes, cs, out_ptrs, out_sizes, status, temp)
+    torch_cuda.cuda.synchronize()
+    assert status.cpu().tolist() == [0] * n
+    sizes = out_sizes.cpu().tolist()
+    host = out.cpu().numpy()
+    frames = [host[i * slot:i * slot + sizes[i]].tobytes() for i in range(n)]
+    _check(frames, [data[i * cs:(i + 1) * cs] for i in range(n)])
+
+
+def test_c3_full_batch_roundtrip(torch_cuda):
+    """BASELINE config 3 at full size (16384 x 64 KiB = 1 GiB): every frame decodes
+    with libzstd to its chunk (size-independent property); a sample is checked
+    byte-for-byte against the oracle."""
+    import cuda_zstd
+
+    n, cs = 16384, 65536
+    data = T.gen(T.DG_MIX, n, 0x5EED0003, cs)
+    dev = torch_cuda.from_numpy(data).cuda()
+    bc = cuda_zstd.BatchedCompressor(3, cs)
+    slot = (bc.max_out(cs) + 255) // 256 * 256
+    out = torch_cuda.empty(n * slot, dtype=torch_cuda.uint8, device="cuda")
+    base_in, base_out = dev.data_ptr(), out.data_ptr()
+    ar = torch_cuda.arange(n, dtype=torch_cuda.int64, device="cuda")
+    in_ptrs, out_ptrs = base_in + ar * cs, base_out + ar * slot
+    in_sizes = torch_cuda.full((n,), cs, dtype=torch_cuda.int64, device="cuda")
+    out_sizes = torch_cuda.zeros(n, dtype=torch_cuda.int64, device="cuda")
+    status = torch_cuda.full((n,), -1, dtype=torch_cuda.int32, device="cuda")
+    temp = torch_cuda.empty(bc.temp_size(n, cs), dtype=torch_cuda.uint8, device="cuda")
+    bc.compress_async(in_ptrs, in_sizes, cs, out_ptrs, out_sizes, status, temp)
+    torch_cuda.cuda.synchronize()
+    assert (status == 0).all().item()
+    sizes = out_sizes.cpu().numpy()
+    host = out.cpu().numpy()
+    del out, temp
+    z = T.zstd()
+    if z is not None:
+        dst = np.zeros(cs, np.uint8)
+        for i in range(n):
+            f = host[i * slot:i * slot + sizes[i]]
+            r = z.ZSTD_decompress(dst.ctypes.data_as(ctypes.c_void_p), ctypes.c_size_t(cs), f.ctypes.data_as(ctypes.c_void_p), ctypes.c_size_t(len(f)))
+            assert r == cs and (dst == data[i * cs:(i + 1) * cs]).all(), f"chunk {i}"
+    for i in range(0, n, 257):
+        assert host[i * slot:i * slot + sizes[i]].tobytes() == T.oracle_frame(data[i * cs:(i + 1) * cs]), f"chunk {i}"
+    ratio = n * cs / sizes.sum()
+    assert ratio > 2.3

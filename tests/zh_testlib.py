@@ -1,0 +1,124 @@
+"""Test helpers: ctypes access to the oracle (CPU restatement), libzstd (the
+reference's own dependency, used as the decoder / stage oracle) and the seeded
+synthetic-data generator.  Test infrastructure only."""
+import ctypes
+import os
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PKG = os.path.join(ROOT, "custom-nvcomp-with-zstd_amd")
+ORACLE_SO = os.path.join(ROOT, "oracle", "liboracle.so")
+DATAGEN_SO = os.path.join(ROOT, "tools", "libdatagen.so")
+GOLDEN = os.path.join(ROOT, "tests", "golden")
+
+DG_MIX, DG_RANDOM, DG_SYM16, DG_TEXT, DG_JSON, DG_SOURCE, DG_CSV, DG_EXE, DG_SENSOR = range(9)
+KINDS = {"mix": DG_MIX, "random": DG_RANDOM, "sym16": DG_SYM16, "text": DG_TEXT, "json": DG_JSON, "source": DG_SOURCE,
+         "csv": DG_CSV, "exe": DG_EXE, "sensor": DG_SENSOR}
+
+vp = ctypes.c_void_p
+_o = _d = _z = None
+
+
+def oracle():
+    global _o
+    if _o is None:
+        L = ctypes.CDLL(ORACLE_SO)
+        L.orc_compress_frame.restype = ctypes.c_size_t
+        L.orc_compress_frame.argtypes = [vp, ctypes.c_size_t, vp, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32]
+        L.orc_fse_normalize.restype = ctypes.c_int
+        L.orc_fse_write_ncount.restype = ctypes.c_size_t
+        L.orc_huf_build_ctable.restype = ctypes.c_uint32
+        L.orc_huf_write_ctable.restype = ctypes.c_size_t
+        L.orc_compress_literals.restype = ctypes.c_size_t
+        L.orc_lz_parse.restype = ctypes.c_size_t
+        L.orc_compress_block.restype = ctypes.c_size_t
+        L.orc_max_compressed_size.restype = ctypes.c_size_t
+        L.orc_fse_optimal_table_log.restype = ctypes.c_uint32
+        _o = L
+    return _o
+
+
+def datagen():
+    global _d
+    if _d is None:
+        _d = ctypes.CDLL(DATAGEN_SO)
+    return _d
+
+
+def find_libzstd():
+    for p in ("/opt/conda/lib/libzstd.so.1", "libzstd.so.1", "/usr/lib/x86_64-linux-gnu/libzstd.so.1"):
+        try:
+            return ctypes.CDLL(p)
+        except OSError:
+            continue
+    return None
+
+
+def zstd():
+    global _z
+    if _z is None:
+        L = find_libzstd()
+        if L is None:
+            return None
+        L.ZSTD_decompress.restype = ctypes.c_size_t
+        L.ZSTD_compress.restype = ctypes.c_size_t
+        L.ZSTD_isError.restype = ctypes.c_uint
+        L.ZSTD_getErrorName.restype = ctypes.c_char_p
+        L.ZSTD_versionNumber.restype = ctypes.c_uint
+        _z = L
+    return _z
+
+
+def gen(kind, nchunks, seed, chunk_size=65536, first=0):
+    a = np.zeros(nchunks * chunk_size, np.uint8)
+    datagen().dg_fill(a.ctypes.data_as(vp), ctypes.c_size_t(nchunks), ctypes.c_size_t(chunk_size), ctypes.c_uint64(seed),
+                      ctypes.c_int(kind), ctypes.c_uint64(first))
+    return a
+
+
+def oracle_frame(data, block_size=128 * 1024, window_log=19):
+    data = np.ascontiguousarray(np.frombuffer(bytes(data), np.uint8) if not isinstance(data, np.ndarray) else data)
+    cap = int(oracle().orc_max_compressed_size(ctypes.c_uint64(len(data)))) + 64
+    out = np.zeros(cap, np.uint8)
+    n = oracle().orc_compress_frame(out.ctypes.data_as(vp), cap, data.ctypes.data_as(vp), len(data), block_size, window_log)
+    assert n > 0
+    return out[:n].tobytes()
+
+
+def zstd_decompress(frame, size):
+    z = zstd()
+    assert z is not None, "libzstd not available"
+    src = np.frombuffer(frame, np.uint8).copy()
+    dst = np.zeros(max(size, 1), np.uint8)
+    r = z.ZSTD_decompress(dst.ctypes.data_as(vp), ctypes.c_size_t(len(dst)), src.ctypes.data_as(vp), ctypes.c_size_t(len(src)))
+    if z.ZSTD_isError(r):
+        raise AssertionError("libzstd: " + z.ZSTD_getErrorName(r).decode())
+    return dst[:r].tobytes()
+
+
+def special_inputs():
+    """Edge cases the reference tests exercise (tests/test_compressible_data.cu:22-101,
+    tests/test_c_api_edge_cases.cu): tiny, ragged, zeros, 0xFF, periodic, random."""
+    rng = np.random.default_rng(42)
+    out = {
+        "one": np.array([7], np.uint8),
+        "seven": np.frombuffer(b"abcdefg", np.uint8).copy(),
+        "nine": np.frombuffer(b"abcdefghi", np.uint8).copy(),
+        "two_same": np.array([5, 5], np.uint8),
+        "zeros_64k": np.zeros(65536, np.uint8),
+        "ff_64k": np.full(65536, 255, np.uint8),
+        "period8_64k": np.tile(np.arange(8, dtype=np.uint8), 8192),
+        "iota_4k": (np.arange(4097) % 256).astype(np.uint8),
+        "random_64k": rng.integers(0, 256, 65536, dtype=np.uint8),
+        "random_300": rng.integers(0, 256, 300, dtype=np.uint8),
+        "text_ragged": gen(DG_TEXT, 1, 11, 40001),
+        "json_4095": gen(DG_JSON, 1, 12, 4095),
+        "csv_65535": gen(DG_CSV, 1, 13, 65535),
+        "exe_777": gen(DG_EXE, 1, 14, 777),
+        "sensor_64k": gen(DG_SENSOR, 1, 15, 65536),
+        "sym16_64k": gen(DG_SYM16, 1, 0x5EED0002, 65536),
+        "long_repeat": np.tile(rng.integers(0, 256, 1000, dtype=np.uint8), 66)[:65536].copy(),
+        "runs": np.repeat(rng.integers(0, 4, 700, dtype=np.uint8), 97)[:65536].copy(),
+    }
+    return out
