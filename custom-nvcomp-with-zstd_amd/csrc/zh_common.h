@@ -35,7 +35,7 @@ enum : u32 {
 #define ZH_SEQ_CAP 13120u
 #define ZH_SEQ_BYTES (ZH_SEQ_CAP * 8u)
 #define ZH_LIT_BYTES ((u32)ZH_BLOCK_MAX)
-#define ZH_META_BYTES 16u
+#define ZH_META_BYTES 128u  // u32[4] counters + u32[28] diagnostic stamps
 #define ZH_WS_BLOCK_BYTES (ZH_SEQ_BYTES + ZH_LIT_BYTES + ZH_META_BYTES)
 
 struct ZhWorkspace {
@@ -43,6 +43,7 @@ struct ZhWorkspace {
   __device__ u64 *seq(u32 b) const { return (u64 *)(base + (size_t)b * ZH_WS_BLOCK_BYTES); }
   __device__ u8 *lits(u32 b) const { return base + (size_t)b * ZH_WS_BLOCK_BYTES + ZH_SEQ_BYTES; }
   __device__ u32 *meta(u32 b) const { return (u32 *)(base + (size_t)b * ZH_WS_BLOCK_BYTES + ZH_SEQ_BYTES + ZH_LIT_BYTES); }
+  __device__ u32 *dbg(u32 b) const { return meta(b) + 4; }
 };
 
 // Status codes written per item (values of cuda_zstd::Status).

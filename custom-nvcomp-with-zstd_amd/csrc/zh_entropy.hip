@@ -26,7 +26,8 @@ constexpr u32 OFF_HIST = OFF_MISC + 4 * 64;        // 256 u32 literal histogram;
 constexpr u32 OFF_HVAL = OFF_HIST + 4 * 256;       // u16[256] Huffman code values
 constexpr u32 OFF_HNB = OFF_HVAL + 2 * 256;        // u8[256] Huffman code lengths
 constexpr u32 OFF_HBUF = OFF_HNB + 256;            // u8[768] header scratch (weights / NCount)
-constexpr u32 OFF_U = OFF_HBUF + 768;              // union: Huffman nodes | FSE tables
+constexpr u32 OFF_SCR = OFF_HBUF + 768;            // serial-helper scratch (lane 0)
+constexpr u32 OFF_U = OFF_SCR + 1024;              // union: Huffman nodes | FSE tables
 // Huffman build view
 constexpr u32 OFF_NODES = OFF_U;                   // 514 nodes x 8 B
 constexpr u32 U_HUF_END = OFF_NODES + 8 * 516;
@@ -56,6 +57,20 @@ __constant__ u8 c_ML_code[128] = {0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 
                                   32, 32, 33, 33, 34, 34, 35, 35, 36, 36, 36, 36, 37, 37, 37, 37, 38, 38, 38, 38, 38, 38, 38, 38, 39, 39, 39, 39, 39, 39, 39, 39,
                                   40, 40, 40, 40, 40, 40, 40, 40, 40, 40, 40, 40, 40, 40, 40, 40, 41, 41, 41, 41, 41, 41, 41, 41, 41, 41, 41, 41, 41, 41, 41, 41,
                                   42, 42, 42, 42, 42, 42, 42, 42, 42, 42, 42, 42, 42, 42, 42, 42, 42, 42, 42, 42, 42, 42, 42, 42, 42, 42, 42, 42, 42, 42, 42, 42};
+
+__constant__ u32 c_rtb[8] = {0, 473195, 504333, 520860, 550000, 700000, 750000, 830000};
+
+// LDS scratch for the lane-0 serial helpers (keeps them out of scratch memory)
+struct SerialScratch {
+  u32 cumul[64];
+  u32 rankLast[16];
+  u32 base[32];
+  u32 curr[32];
+  u32 wcount[16];
+  u16 nbPerRank[16];
+  u16 valPerRank[16];
+};
+static_assert(sizeof(SerialScratch) <= 1024, "scratch");
 
 __device__ __forceinline__ u32 highbit32(u32 v) { return 31u - (u32)__builtin_clz(v); }
 __device__ __forceinline__ u32 ll_code(u32 ll) { return ll > 63 ? highbit32(ll) + 19 : c_LL_code[ll]; }
@@ -210,7 +225,7 @@ __device__ bool fse_normalize_m2(s16 *norm, u32 tableLog, const u32 *count, u32 
 }
 
 __device__ bool fse_normalize(s16 *norm, u32 tableLog, const u32 *count, u32 total, u32 maxSV, bool useLowProbCount) {
-  const u32 rtbTable[8] = {0, 473195, 504333, 520860, 550000, 700000, 750000, 830000};
+  const u32 *rtbTable = c_rtb;
   if (tableLog < fse_min_table_log(total, maxSV)) return false;
   s16 const lowProbCount = useLowProbCount ? -1 : 1;
   u64 const scale = 62 - tableLog;
@@ -288,10 +303,10 @@ __device__ u32 fse_write_ncount(u8 *out, const s16 *norm, u32 maxSV, u32 tableLo
 struct FseSym { u32 dNb; s32 dFS; };
 
 // FSE_buildCTable_wksp into LDS (stateTable + symbol transforms)
-__device__ void fse_build_ctable(u16 *st, FseSym *sym, u8 *tableSymbol, const s16 *norm, u32 maxSV, u32 tableLog) {
+__device__ void fse_build_ctable(u16 *st, FseSym *sym, u8 *tableSymbol, const s16 *norm, u32 maxSV, u32 tableLog, SerialScratch *scr) {
   u32 const tableSize = 1u << tableLog, tableMask = tableSize - 1;
   u32 const step = (tableSize >> 1) + (tableSize >> 3) + 3;
-  u32 cumul[54];
+  u32 *cumul = scr->cumul;
   u32 highThreshold = tableSize - 1;
   cumul[0] = 0;
   for (u32 u = 1; u <= maxSV + 1; u++) {
@@ -339,7 +354,7 @@ __device__ __forceinline__ u32 fse_step(const u16 *st, const FseSym *sym, u32 &s
 // ---------------- Huffman (libzstd v1.4.9 HUF_buildCTable; lane-0 serial) ----------------
 struct HufNode { u32 count; u16 parent; u8 byte; u8 nbBits; };
 
-__device__ u32 huf_set_max_height(HufNode *huffNode, u32 lastNonNull, u32 maxNbBits) {
+__device__ u32 huf_set_max_height(HufNode *huffNode, u32 lastNonNull, u32 maxNbBits, SerialScratch *scr) {
   u32 const largestBits = huffNode[lastNonNull].nbBits;
   if (largestBits <= maxNbBits) return largestBits;
   int totalCost = 0;
@@ -353,7 +368,7 @@ __device__ u32 huf_set_max_height(HufNode *huffNode, u32 lastNonNull, u32 maxNbB
   while (huffNode[n].nbBits == maxNbBits) n--;
   totalCost >>= (largestBits - maxNbBits);
   u32 const noSymbol = 0xF0F0F0F0u;
-  u32 rankLast[14];
+  u32 *rankLast = scr->rankLast;
   for (int i = 0; i < 14; i++) rankLast[i] = noSymbol;
   {
     u32 currentNbBits = maxNbBits;
@@ -398,13 +413,13 @@ __device__ u32 huf_set_max_height(HufNode *huffNode, u32 lastNonNull, u32 maxNbB
 }
 
 // returns maxNbBits (0 on error); fills hval/hnb for symbols 0..maxSV
-__device__ u32 huf_build_ctable(HufNode *huffNode0, u16 *hval, u8 *hnb, const u32 *count, u32 maxSV, u32 maxNbBits) {
+__device__ u32 huf_build_ctable(HufNode *huffNode0, u16 *hval, u8 *hnb, const u32 *count, u32 maxSV, u32 maxNbBits, SerialScratch *scr) {
   HufNode *const huffNode = huffNode0 + 1;
   int const STARTNODE = 256;
   for (int i = 0; i < 2 * 256 + 2; i++) { huffNode0[i].count = 0; huffNode0[i].parent = 0; huffNode0[i].byte = 0; huffNode0[i].nbBits = 0; }
   // HUF_sort
   {
-    u32 base[32], curr[32];
+    u32 *base = scr->base, *curr = scr->curr;
     for (int r = 0; r < 32; r++) base[r] = 0;
     for (u32 n = 0; n <= maxSV; n++) base[highbit32(count[n] + 1)]++;
     for (u32 n = 30; n > 0; n--) base[n - 1] += base[n];
@@ -439,9 +454,9 @@ __device__ u32 huf_build_ctable(HufNode *huffNode0, u16 *hval, u8 *hnb, const u3
   huffNode[nodeRoot].nbBits = 0;
   for (int n = nodeRoot - 1; n >= STARTNODE; n--) huffNode[n].nbBits = huffNode[huffNode[n].parent].nbBits + 1;
   for (int n = 0; n <= nonNullRank; n++) huffNode[n].nbBits = huffNode[huffNode[n].parent].nbBits + 1;
-  maxNbBits = huf_set_max_height(huffNode, (u32)nonNullRank, maxNbBits);
+  maxNbBits = huf_set_max_height(huffNode, (u32)nonNullRank, maxNbBits, scr);
   if (maxNbBits > 12) return 0;
-  u16 nbPerRank[13], valPerRank[13];
+  u16 *nbPerRank = scr->nbPerRank, *valPerRank = scr->valPerRank;
   for (int i = 0; i < 13; i++) { nbPerRank[i] = 0; valPerRank[i] = 0; }
   for (int n = 0; n <= nonNullRank; n++) nbPerRank[huffNode[n].nbBits]++;
   {
@@ -489,12 +504,13 @@ __device__ u32 fse_compress_weights_stream(u8 *out, const u8 *src, u32 n, const 
 }
 
 // HUF_writeCTable into hbuf; returns size (0 = error -> raw literals)
-__device__ u32 huf_write_ctable(u8 *hbuf, u8 *w, const u8 *hnb, u32 maxSV, u32 huffLog, u16 *st, FseSym *sym, u8 *tsym, s16 *norm) {
+__device__ u32 huf_write_ctable(u8 *hbuf, u8 *w, const u8 *hnb, u32 maxSV, u32 huffLog, u16 *st, FseSym *sym, u8 *tsym, s16 *norm,
+                                SerialScratch *scr) {
   for (u32 n = 0; n < maxSV; n++) w[n] = hnb[n] ? (u8)(huffLog + 1 - hnb[n]) : 0;
   // HUF_compressWeights
   u32 h = 0;
   if (maxSV > 1) {
-    u32 count[13];
+    u32 *count = scr->wcount;
     for (int i = 0; i < 13; i++) count[i] = 0;
     for (u32 i = 0; i < maxSV; i++) count[w[i]]++;
     u32 mx = 12;
@@ -508,7 +524,7 @@ __device__ u32 huf_write_ctable(u8 *hbuf, u8 *w, const u8 *hnb, u32 maxSV, u32 h
       if (fse_normalize(norm, tableLog, count, maxSV, mx, false)) {
         u32 hs = fse_write_ncount(hbuf + 1, norm, mx, tableLog);
         if (hs) {
-          fse_build_ctable(st, sym, tsym, norm, mx, tableLog);
+          fse_build_ctable(st, sym, tsym, norm, mx, tableLog, scr);
           u32 cs = maxSV > 2 ? fse_compress_weights_stream(hbuf + 1 + hs, w, maxSV, st, sym, tableLog) : 0;
           h = cs ? hs + cs : 0;
         }
@@ -530,6 +546,17 @@ __device__ __forceinline__ void copy_bytes(const Out &o, u32 pos, const u8 *src,
 
 }  // namespace
 
+#ifdef ZH_STAMPS
+#define ZH_STAMP(k)                                     \
+  do {                                                  \
+    u64 _t = __builtin_amdgcn_s_memtime();              \
+    st[k] += (u32)(_t - stamp_prev);                    \
+    stamp_prev = _t;                                    \
+  } while (0)
+#else
+#define ZH_STAMP(k) do { } while (0)
+#endif
+
 // ============================================================================
 extern "C" __global__ __launch_bounds__(K2_THREADS) void zh_entropy_kernel(const ZhBlockDesc *__restrict__ blocks, ZhWorkspace ws, u32 window_log,
                                                                              u32 cfg_block_size, u64 *__restrict__ item_size,
@@ -547,6 +574,7 @@ extern "C" __global__ __launch_bounds__(K2_THREADS) void zh_entropy_kernel(const
   u8 *tsym = smem + OFF_TSYM;
   s16 *norm = (s16 *)(smem + OFF_NORM);
   u8 *wts = smem + OFF_WTS;
+  SerialScratch *scr = (SerialScratch *)(smem + OFF_SCR);
 
   u32 const b = blockIdx.x, lane = lane_id();
   ZhBlockDesc const d = blocks[b];
@@ -556,6 +584,10 @@ extern "C" __global__ __launch_bounds__(K2_THREADS) void zh_entropy_kernel(const
   u32 const nseq_raw = meta[0], nlit = meta[1], rle = meta[2];
   Out const o{d.dst, d.dst_cap};
   if (lane == 0) sw[0] = 0;
+#ifdef ZH_STAMPS
+  u64 stamp_prev = __builtin_amdgcn_s_memtime();
+  u32 st[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+#endif
 
   // ---- frame header (reference write_frame_header choices, no dict / checksum)
   u32 pos = 0;
@@ -604,7 +636,7 @@ extern "C" __global__ __launch_bounds__(K2_THREADS) void zh_entropy_kernel(const
       u32 const lhSize = 3 + (nl >= 1024) + (nl >= 16384);
       bool const single = nl < 256;
       u32 cLit = 0, hsz = 0, huffLog = 0;
-      u32 ssz[4] = {0, 0, 0, 0};
+      u32 *ssz = misc + 8;  // per-stream byte sizes (LDS, wave-uniform)
       if (nl > ZH_COMPRESS_LITERALS_SIZE_MIN) {
         for (u32 i = lane; i < 256; i += 64) hist[i] = 0;
         wave_sync();
@@ -616,17 +648,19 @@ extern "C" __global__ __launch_bounds__(K2_THREADS) void zh_entropy_kernel(const
         if (largest == nl) cLit = 1;
         else if (largest <= (nl >> 7) + 4) cLit = 0;
         else {
+          ZH_STAMP(0);  // literal histogram
           if (lane == 0) {
             for (u32 i = 0; i < 256; i++) hnb[i] = 0;
             u32 hl = fse_optimal_table_log(11, nl, maxSV, 1);
-            hl = huf_build_ctable(nodes, hval, hnb, hist, maxSV, hl);
-            u32 h = hl ? huf_write_ctable(hbuf, wts, hnb, maxSV, hl, stLL, symLL, tsym, norm) : 0;
+            hl = huf_build_ctable(nodes, hval, hnb, hist, maxSV, hl, scr);
+            u32 h = hl ? huf_write_ctable(hbuf, wts, hnb, maxSV, hl, stLL, symLL, tsym, norm, scr) : 0;
             misc[0] = hl;
             misc[1] = h;
           }
           wave_sync();
           huffLog = misc[0];
           hsz = misc[1];
+          ZH_STAMP(1);  // Huffman tree + header (serial)
           if (hsz && hsz + 12 < nl) {
             // stream sizes: sum of code lengths per stream (+ end mark)
             u32 const seg = (nl + 3) / 4;
@@ -648,6 +682,7 @@ extern "C" __global__ __launch_bounds__(K2_THREADS) void zh_entropy_kernel(const
           }
         }
       }
+      ZH_STAMP(2);  // stream sizes
       if (cLit == 0 || cLit >= nl - minGain) {
         // raw literals
         u32 const fl = 1 + (nl > 31) + (nl > 4095);
@@ -691,6 +726,7 @@ extern "C" __global__ __launch_bounds__(K2_THREADS) void zh_entropy_kernel(const
         }
       }
       (void)huffLog;
+      ZH_STAMP(3);  // literal streams
     }
 
     // ======================= sequences section =======================
@@ -755,6 +791,7 @@ extern "C" __global__ __launch_bounds__(K2_THREADS) void zh_entropy_kernel(const
       wave_sync();
     }
 
+    ZH_STAMP(4);  // merge pass
     // nbSeq header
     if (nbSeq < 128) { if (lane == 0) o.put(op, (u8)nbSeq); op += 1; }
     else if (nbSeq < ZH_LONGNBSEQ) { if (lane == 0) { o.put(op, (u8)((nbSeq >> 8) + 0x80)); o.put(op + 1, (u8)nbSeq); } op += 2; }
@@ -799,14 +836,15 @@ extern "C" __global__ __launch_bounds__(K2_THREADS) void zh_entropy_kernel(const
         }
       }
       wave_sync();
+      ZH_STAMP(5);  // repcodes + codes + histograms
       // tables: LL, OF, ML (ZSTD_selectEncodingType for strategy dfast + ZSTD_buildCTable)
       u32 const seqHead = op;
       op += 1;
       u64 const rec0 = seq[0], recL = seq[nbSeq - 1];
-      u32 const first_code[3] = {ll_code((u32)(rec0 & 0x1FFFFu)), highbit32((u32)(rec0 >> 34)), ml_code((u32)((rec0 >> 17) & 0x1FFFFu))};
-      u32 const last_code[3] = {ll_code((u32)(recL & 0x1FFFFu)), highbit32((u32)(recL >> 34)), ml_code((u32)((recL >> 17) & 0x1FFFFu))};
-      u32 types[3], logs[3];
       if (lane == 0) {
+        u32 *first_code = scr->wcount, *last_code = scr->wcount + 4, *types = scr->wcount + 8, *logs = scr->wcount + 12;
+        first_code[0] = ll_code((u32)(rec0 & 0x1FFFFu)); first_code[1] = highbit32((u32)(rec0 >> 34)); first_code[2] = ml_code((u32)((rec0 >> 17) & 0x1FFFFu));
+        last_code[0] = ll_code((u32)(recL & 0x1FFFFu)); last_code[1] = highbit32((u32)(recL >> 34)); last_code[2] = ml_code((u32)((recL >> 17) & 0x1FFFFu));
         u32 hpos = 0;
         for (int t = 0; t < 3; t++) {
           u32 *cnt = hist + 64 * t;
@@ -832,7 +870,7 @@ extern "C" __global__ __launch_bounds__(K2_THREADS) void zh_entropy_kernel(const
             logs[t] = 0;
           } else if (type == 0) {
             for (u32 s = 0; s <= defMax; s++) norm[s] = defNorm[s];
-            fse_build_ctable(st, sy, tsym, norm, defMax, defLog);
+            fse_build_ctable(st, sy, tsym, norm, defMax, defLog, scr);
             logs[t] = defLog;
           } else {
             u32 nb1 = nbSeq;
@@ -841,7 +879,7 @@ extern "C" __global__ __launch_bounds__(K2_THREADS) void zh_entropy_kernel(const
             fse_normalize(norm, tl, cnt, nb1, mx, nb1 >= 2048);
             u32 h = fse_write_ncount(hbuf + hpos, norm, mx, tl);
             hpos += h;
-            fse_build_ctable(st, sy, tsym, norm, mx, tl);
+            fse_build_ctable(st, sy, tsym, norm, mx, tl, scr);
             logs[t] = tl;
           }
           types[t] = type;
@@ -856,6 +894,7 @@ extern "C" __global__ __launch_bounds__(K2_THREADS) void zh_entropy_kernel(const
       for (u32 i = lane; i < hpos; i += 64) o.put(op + i, hbuf[i]);
       op += hpos;
       u32 const logLL = misc[2], logOF = misc[3], logML = misc[4];
+      ZH_STAMP(6);  // FSE tables (serial)
 
       // pass C: FSE state chain (wave-uniform) + parallel bit packing, encode order nbSeq-1 .. 0
       BitSink bs{op, 0};
@@ -868,21 +907,28 @@ extern "C" __global__ __launch_bounds__(K2_THREADS) void zh_entropy_kernel(const
         u32 const ll = (u32)(rec & 0x1FFFFu), mlb = (u32)((rec >> 17) & 0x1FFFFu), ob = (u32)(rec >> 34);
         u32 const llc = valid ? ll_code(ll) : 0, mlc = valid ? ml_code(mlb) : 0, ofc = valid ? highbit32(ob) : 0;
         u32 vOF = 0, nOF = 0, vML = 0, nML = 0, vLL = 0, nLL = 0;
+        // per-lane symbol transforms, so the serial chain only waits on state-table reads
+        FseSym const tO = symOF[ofc], tM = symML[mlc], tL = symLL[llc];
         u32 const cnt = min(64u, nbSeq - e0);
         for (u32 j = 0; j < cnt; j++) {
-          u32 const cl = __builtin_amdgcn_readlane(llc, j), cm = __builtin_amdgcn_readlane(mlc, j), co = __builtin_amdgcn_readlane(ofc, j);
+          u32 const dnO = __builtin_amdgcn_readlane(tO.dNb, j), dnM = __builtin_amdgcn_readlane(tM.dNb, j), dnL = __builtin_amdgcn_readlane(tL.dNb, j);
+          s32 const dfO = __builtin_amdgcn_readlane(tO.dFS, j), dfM = __builtin_amdgcn_readlane(tM.dFS, j), dfL = __builtin_amdgcn_readlane(tL.dFS, j);
           if (e0 + j == 0) {
-            sML = fse_init_state(stML, symML, cm);
-            sOF = fse_init_state(stOF, symOF, co);
-            sLL = fse_init_state(stLL, symLL, cl);
+            u32 nb = (dnM + (1u << 15)) >> 16;
+            sML = stML[((((nb << 16) - dnM)) >> nb) + dfM];
+            nb = (dnO + (1u << 15)) >> 16;
+            sOF = stOF[((((nb << 16) - dnO)) >> nb) + dfO];
+            nb = (dnL + (1u << 15)) >> 16;
+            sLL = stLL[((((nb << 16) - dnL)) >> nb) + dfL];
           } else {
-            u32 nb;
-            u32 v = fse_step(stOF, symOF, sOF, co, nb);
-            vOF = setlane(vOF, v, j); nOF = setlane(nOF, nb, j);
-            v = fse_step(stML, symML, sML, cm, nb);
-            vML = setlane(vML, v, j); nML = setlane(nML, nb, j);
-            v = fse_step(stLL, symLL, sLL, cl, nb);
-            vLL = setlane(vLL, v, j); nLL = setlane(nLL, nb, j);
+            u32 const bO = (sOF + dnO) >> 16, bM = (sML + dnM) >> 16, bL = (sLL + dnL) >> 16;
+            u32 const oO = sOF & ((1u << bO) - 1u), oM = sML & ((1u << bM) - 1u), oL = sLL & ((1u << bL) - 1u);
+            sOF = stOF[(sOF >> bO) + dfO];
+            sML = stML[(sML >> bM) + dfM];
+            sLL = stLL[(sLL >> bL) + dfL];
+            vOF = setlane(vOF, oO, j); nOF = setlane(nOF, bO, j);
+            vML = setlane(vML, oM, j); nML = setlane(nML, bM, j);
+            vLL = setlane(vLL, oL, j); nLL = setlane(nLL, bL, j);
           }
         }
         u32 v6[6] = {vOF, vML, vLL, ll, mlb, ob};
@@ -897,6 +943,7 @@ extern "C" __global__ __launch_bounds__(K2_THREADS) void zh_entropy_kernel(const
       }
       sink_close(bs, o, sw);
       op = bs.pos;
+      ZH_STAMP(7);  // FSE chain + packing
     }
 
     u32 const body = op - body0;
@@ -915,6 +962,10 @@ extern "C" __global__ __launch_bounds__(K2_THREADS) void zh_entropy_kernel(const
       total = body0 + n;
     }
   }
+  ZH_STAMP(8);  // tail (raw copy etc.)
+#ifdef ZH_STAMPS
+  if (lane == 0) { u32 *dbg = ws.dbg(b); for (int k = 0; k < 9; k++) dbg[6 + k] = st[k]; }
+#endif
   if (lane == 0) {
     if (d.flags & ZH_F_DIRECT) {
       item_size[d.item] = total;

@@ -16,7 +16,7 @@ import os
 from typing import List, Sequence
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(os.path.dirname(_HERE), "libcuda_zstd_hip.so")
+LIB_PATH = os.environ.get("CUDA_ZSTD_HIP_LIB") or os.path.join(os.path.dirname(_HERE), "libcuda_zstd_hip.so")
 
 # nvcomp-style return codes (reference src/cuda_zstd_nvcomp.cpp:75-96)
 OK, INVALID, OOM, DEVICE_ERROR, CORRUPT, TOO_SMALL, CHECKSUM, COMPRESSION = 0, 2, 3, 4, 6, 7, 10, 12
@@ -110,7 +110,11 @@ class Manager:
             lib().cuda_zstd_destroy_manager(self._h)
             self._h = None
 
-    __del__ = close
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:  # interpreter shutdown: module globals may already be gone
+            pass
 
     def _workspace(self, nbytes: int):
         torch = _torch()
@@ -176,7 +180,11 @@ class BatchedCompressor:
             lib().nvcomp_zstd_batch_destroy_v5(self._h)
             self._h = None
 
-    __del__ = close
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
 
     @staticmethod
     def temp_size(num_chunks: int, max_chunk: int) -> int:

@@ -21,7 +21,7 @@
 #define ZH_HASH_READ 8              /* bytes read per hashed position */
 #define ZH_MIN_MATCH_LONG 8
 #define ZH_MIN_MATCH_SHORT 5
-#define ZH_MAX_MATCH 255            /* per-position length cap; continuations are merged */
+#define ZH_MAX_MATCH 64             /* per-position length cap; continuations are merged */
 #define ZH_PRIME_LONG 0xCF1BBCDCB7A56463ull
 #define ZH_PRIME_SHORT 0x9E3779B185EBCA87ull
 #define ZH_COMPRESS_LITERALS_SIZE_MIN 63

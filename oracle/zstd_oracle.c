@@ -36,7 +36,7 @@
  *      - insertion in tiles of 256 positions: a lookup sees every position of
  *        earlier tiles (latest wins), none of its own tile,
  *      - per-position best = longer of the two candidates (long needs >= 8,
- *        short >= 5), lengths capped at 255,
+ *        short >= 5), lengths capped at 64,
  *      - greedy parse with one-step lazy deferral (take p unless len[p+1] > len[p]),
  *      - a match directly followed (LL = 0) by one with the same offset is merged.
  *    Output of this stage is pinned by libzstd round-trip of every frame.

@@ -1,0 +1,54 @@
+"""Diagnostic: per-phase cycle breakdown of zh_lz_kernel (wave 0 of each block),
+from the -DZH_STAMPS build (tools/libcuda_zstd_hip_stamps.so).  Not a benchmark."""
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+os.environ["CUDA_ZSTD_HIP_LIB"] = os.path.join(ROOT, "tools", "libcuda_zstd_hip_stamps.so")
+sys.path.insert(0, os.path.join(ROOT, "custom-nvcomp-with-zstd_amd"))
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+import numpy as np
+import torch
+
+import cuda_zstd
+import zh_testlib as T
+
+kind = sys.argv[1] if len(sys.argv) > 1 else "mix"
+n, cs = 2048, 65536
+data = T.gen(T.KINDS[kind], n, 0x5EED0003, cs)
+dev = torch.from_numpy(data).cuda()
+bc = cuda_zstd.BatchedCompressor(3, cs)
+slot = (bc.max_out(cs) + 255) // 256 * 256
+out = torch.empty(n * slot, dtype=torch.uint8, device="cuda")
+ar = torch.arange(n, dtype=torch.int64, device="cuda")
+args = (dev.data_ptr() + ar * cs, torch.full((n,), cs, dtype=torch.int64, device="cuda"), cs, out.data_ptr() + ar * slot,
+        torch.zeros(n, dtype=torch.int64, device="cuda"), torch.zeros(n, dtype=torch.int32, device="cuda"))
+temp = torch.empty(bc.temp_size(n, cs), dtype=torch.uint8, device="cuda")
+bc.compress_async(*args, temp)
+torch.cuda.synchronize()
+a256 = lambda v: (v + 255) // 256 * 256
+base = a256(temp.data_ptr()) - temp.data_ptr()
+off = a256(n * 40)
+off = a256(off + n * 24)
+off = a256(off + n * 4)
+off = a256(off + n * 8)
+off = a256(off + n * 4)
+off = a256(off + 0)
+blocks = base + off
+WS = 13120 * 8 + 65536 + 128
+h = temp.cpu().numpy()
+raw = np.array([h[blocks + b * WS + 13120 * 8 + 65536 + 16: blocks + b * WS + 13120 * 8 + 65536 + 16 + 17 * 4].view(np.uint32) for b in range(n)])
+st = raw[:, :6]
+k2 = raw[:, 6:15].astype(np.float64)
+names = ["stage", "A(insert)", "B(lengths+exit)", "J(jacobi)", "E(emit)", "rounds"]
+tot = st[:, :5].sum(1).mean()
+print(kind, "mean cycles/block (s_memtime units)", int(tot))
+for k, nm in enumerate(names):
+    print(f"  {nm:16s} mean {st[:, k].mean():12.0f}  share {st[:, k].mean() / tot * 100 if k < 5 else 0:5.1f}%")
+print(f"    of B: loads+prefix8 {raw[:, 16].mean():12.0f}")
+
+k2n = ["lit_hist", "huf_build(serial)", "stream_sizes", "lit_streams", "merge", "repcode+codes", "fse_tables(serial)", "fse_chain+pack", "tail"]
+t2 = k2.sum(1).mean()
+print(kind, "K2 mean cycles/block", int(t2))
+for k, nm in enumerate(k2n):
+    print(f"  {nm:20s} mean {k2[:, k].mean():12.0f}  share {k2[:, k].mean() / t2 * 100:5.1f}%")
