@@ -35,7 +35,7 @@ enum : u32 {
 #define ZH_SEQ_CAP 13120u
 #define ZH_SEQ_BYTES (ZH_SEQ_CAP * 8u)
 #define ZH_LIT_BYTES ((u32)ZH_BLOCK_MAX)
-#define ZH_META_BYTES 128u  // u32[4] counters + u32[28] diagnostic stamps
+#define ZH_META_BYTES 256u  // u32[4] counters + u32[60] diagnostic stamps (-DZH_STAMPS builds)
 #define ZH_WS_BLOCK_BYTES (ZH_SEQ_BYTES + ZH_LIT_BYTES + ZH_META_BYTES)
 
 struct ZhWorkspace {

@@ -77,8 +77,6 @@ __device__ __forceinline__ u32 ll_code(u32 ll) { return ll > 63 ? highbit32(ll) 
 __device__ __forceinline__ u32 ml_code(u32 mlBase) { return mlBase > 127 ? highbit32(mlBase) + 36 : c_ML_code[mlBase]; }
 __device__ __forceinline__ u32 lane_id() { return threadIdx.x; }
 __device__ __forceinline__ void wave_sync() { __syncthreads(); }  // one wave per workgroup
-// write a wave-uniform value into lane j of a per-lane vector
-__device__ __forceinline__ u32 setlane(u32 acc, u32 v, u32 j) { return lane_id() == j ? v : acc; }
 
 __device__ __forceinline__ u32 wave_excl_scan(u32 v, u32 &total) {
   u32 const lane = lane_id();
@@ -586,7 +584,7 @@ extern "C" __global__ __launch_bounds__(K2_THREADS) void zh_entropy_kernel(const
   if (lane == 0) sw[0] = 0;
 #ifdef ZH_STAMPS
   u64 stamp_prev = __builtin_amdgcn_s_memtime();
-  u32 st[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+  u32 st[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
 #endif
 
   // ---- frame header (reference write_frame_header choices, no dict / checksum)
@@ -802,37 +800,50 @@ extern "C" __global__ __launch_bounds__(K2_THREADS) void zh_entropy_kernel(const
       u32 *hLL = hist, *hOF = hist + 64, *hML = hist + 128;
       for (u32 i = lane; i < 192; i += 64) hist[i] = 0;
       wave_sync();
-      u32 r0 = 1, r1 = 4, r2 = 8;
-      if (!(d.flags & ZH_F_FIRST)) { r0 = r1 = r2 = 0; }
+      // Repcode resolution, lane-parallel.  With o_i the offset of sequence i:
+      //  - r0 before i is o_{i-1} (every zstd repcode update leaves the used offset in rep[0]);
+      //  - rep[1] survives sequence j only when j repeats rep[0] with LL > 0, otherwise it
+      //    becomes rep[0]-before-j: r1_i = r0_m for the last such m < i;
+      //  - rep[2] survives j when j used rep[0] (LL > 0) or rep[1], otherwise it becomes
+      //    rep[1]-before-j: r2_i = r1_m for the last such m < i.
+      // (oracle/zstd_oracle.c orc_resolve_repcodes is the serial form.)
+      u32 cr0 = 1, cr1 = 4, cr2 = 8;  // reps before the batch's first sequence
+      if (!(d.flags & ZH_F_FIRST)) { cr0 = cr1 = cr2 = 0; }
+      u64 const below = (1ull << lane) - 1ull;
       for (u32 base = 0; base < nbSeq; base += 64) {
         u32 const i = base + lane;
         bool const valid = i < nbSeq;
         u64 const rec = valid ? seq[i] : 0;
         u32 const ll = (u32)(rec & 0x1FFFFu), ml = (u32)((rec >> 17) & 0x1FFFFu), off = (u32)(rec >> 34);
-        u32 obv = 0;
-        u32 const cnt = min(64u, nbSeq - base);
-        for (u32 j = 0; j < cnt; j++) {
-          u32 const o_ = __builtin_amdgcn_readlane(off, j);
-          u32 const l_ = __builtin_amdgcn_readlane(ll, j);
-          u32 const ll0 = l_ == 0;
-          u32 ob;
-          if (!ll0) ob = (o_ == r0 && r0) ? 1 : (o_ == r1 && r1) ? 2 : (o_ == r2 && r2) ? 3 : o_ + 3;
-          else ob = (o_ == r1 && r1) ? 1 : (o_ == r2 && r2) ? 2 : (r0 > 1 && o_ == r0 - 1) ? 3 : o_ + 3;
-          if (ob > 3) { r2 = r1; r1 = r0; r0 = o_; }
-          else {
-            u32 const idx = ob - 1 + ll0;
-            if (idx == 1) { u32 t = r1; r1 = r0; r0 = t; }
-            else if (idx == 2) { u32 t = r2; r2 = r1; r1 = r0; r0 = t; }
-            else if (idx == 3) { r2 = r1; r1 = r0; r0 = o_; }
-          }
-          obv = setlane(obv, ob, j);
-        }
+        u32 r0 = __shfl_up(off, 1, 64);
+        if (lane == 0) r0 = cr0;
+        bool const keep1 = ll > 0 && off == r0;
+        u64 const nk1 = __ballot(valid && !keep1);
+        u64 const m1 = nk1 & below;
+        u32 const src1 = m1 ? 63u - (u32)__builtin_clzll(m1) : 0u;
+        u32 const t1 = __shfl(r0, src1, 64);
+        u32 const r1 = m1 ? t1 : cr1;
+        bool const keep2 = (ll > 0 && off == r0) || off == r1;
+        u64 const nk2 = __ballot(valid && !keep2);
+        u64 const m2 = nk2 & below;
+        u32 const src2 = m2 ? 63u - (u32)__builtin_clzll(m2) : 0u;
+        u32 const t2 = __shfl(r1, src2, 64);
+        u32 const r2 = m2 ? t2 : cr2;
+        u32 ob;
+        if (ll) ob = off == r0 ? 1u : off == r1 ? 2u : off == r2 ? 3u : off + 3;
+        else ob = off == r1 ? 1u : off == r2 ? 2u : (r0 > 1 && off == r0 - 1) ? 3u : off + 3;
+        // reps after the batch's last sequence
+        u32 const lastLane = min(63u, nbSeq - 1 - base);
+        u32 const n1 = keep1 ? r1 : r0, n2 = keep2 ? r2 : r1;
+        cr0 = __shfl(off, lastLane, 64);
+        cr1 = __shfl(n1, lastLane, 64);
+        cr2 = __shfl(n2, lastLane, 64);
         if (valid) {
           u32 const mlb = ml - 3;
           atomicAdd(&hLL[ll_code(ll)], 1u);
           atomicAdd(&hML[ml_code(mlb)], 1u);
-          atomicAdd(&hOF[highbit32(obv)], 1u);
-          seq[i] = (u64)ll | ((u64)mlb << 17) | ((u64)obv << 34);
+          atomicAdd(&hOF[highbit32(ob)], 1u);
+          seq[i] = (u64)ll | ((u64)mlb << 17) | ((u64)ob << 34);
         }
       }
       wave_sync();
@@ -896,9 +907,76 @@ extern "C" __global__ __launch_bounds__(K2_THREADS) void zh_entropy_kernel(const
       u32 const logLL = misc[2], logOF = misc[3], logML = misc[4];
       ZH_STAMP(6);  // FSE tables (serial)
 
-      // pass C: FSE state chain (wave-uniform) + parallel bit packing, encode order nbSeq-1 .. 0
+      // pass C1: the three FSE state chains, lane-parallel by speculation.  Encode step e
+      // (e = 0 .. nbSeq-1, sequence nbSeq-1-e) is split into chunks of C steps, one per
+      // lane.  Lane c first runs the C steps of chunk c-1 from an arbitrary state (tANS
+      // states synchronise quickly), then its own chunk from that guess, storing the
+      // state word before every step.  A lane whose guess differs from its predecessor's
+      // true end state re-runs its chunk from the right one until nothing changes, so the
+      // stored states equal the serial chain's exactly.
+      u32 *stw = (u32 *)ws.lits(b);  // literals are consumed; one u32 of states per step
+      u32 const C = max((nbSeq + 63) >> 6, 16u);
+      u32 const nch = (nbSeq + C - 1) / C;
+      u32 const cb = lane * C, ce = min(cb + C, nbSeq);
+      bool const act = lane < nch;
+      auto codes_at = [&](u32 e, u32 &lc, u32 &oc, u32 &mc) {
+        u64 const rec = seq[nbSeq - 1 - e];
+        lc = ll_code((u32)(rec & 0x1FFFFu));
+        mc = ml_code((u32)((rec >> 17) & 0x1FFFFu));
+        oc = highbit32((u32)(rec >> 34));
+      };
+      auto step = [&](u32 &sL_, u32 &sO_, u32 &sM_, u32 lc, u32 oc, u32 mc) {
+        FseSym const tO = symOF[oc], tM = symML[mc], tL = symLL[lc];
+        u32 const bO = (sO_ + tO.dNb) >> 16, bM = (sM_ + tM.dNb) >> 16, bL = (sL_ + tL.dNb) >> 16;
+        sO_ = stOF[(sO_ >> bO) + tO.dFS];
+        sM_ = stML[(sM_ >> bM) + tM.dFS];
+        sL_ = stLL[(sL_ >> bL) + tL.dFS];
+      };
+      u32 gL = 0, gO = 0, gM = 0;  // state at the start of the own chunk
+      if (act) {
+        u32 lc, oc, mc;
+        if (lane == 0) {
+          codes_at(0, lc, oc, mc);
+          FseSym const tO = symOF[oc], tM = symML[mc], tL = symLL[lc];
+          u32 nb = (tM.dNb + (1u << 15)) >> 16;
+          gM = stML[(((nb << 16) - tM.dNb) >> nb) + tM.dFS];
+          nb = (tO.dNb + (1u << 15)) >> 16;
+          gO = stOF[(((nb << 16) - tO.dNb) >> nb) + tO.dFS];
+          nb = (tL.dNb + (1u << 15)) >> 16;
+          gL = stLL[(((nb << 16) - tL.dNb) >> nb) + tL.dFS];
+        } else {
+          gL = 1u << logLL; gO = 1u << logOF; gM = 1u << logML;  // any valid state
+          for (u32 e = cb - C; e < cb; e++) { codes_at(e, lc, oc, mc); step(gL, gO, gM, lc, oc, mc); }
+        }
+      }
+      u32 fL = 0, fO = 0, fM = 0;  // state after the own chunk
+      bool redo = act;
+      for (;;) {
+        if (redo) {
+          u32 sL_ = gL, sO_ = gO, sM_ = gM;
+          for (u32 e = max(cb, 1u); e < ce; e++) {
+            u32 lc, oc, mc;
+            codes_at(e, lc, oc, mc);
+            stw[e] = sL_ | (sO_ << 10) | (sM_ << 20);
+            step(sL_, sO_, sM_, lc, oc, mc);
+          }
+          fL = sL_; fO = sO_; fM = sM_;
+        }
+        u32 const pL = __shfl_up(fL, 1, 64), pO = __shfl_up(fO, 1, 64), pM = __shfl_up(fM, 1, 64);
+        redo = act && lane > 0 && (pL != gL || pO != gO || pM != gM);
+        if (redo) { gL = pL; gO = pO; gM = pM; }
+#ifdef ZH_STAMPS
+        st[10]++;
+#endif
+        if (!__ballot(redo)) break;
+      }
+      u32 const sLL = __shfl(fL, nch - 1, 64), sOF = __shfl(fO, nch - 1, 64), sML = __shfl(fM, nch - 1, 64);
+      __threadfence_block();
+      wave_sync();
+
+      ZH_STAMP(9);  // FSE chains
+      // pass C2: bit packing, lane-parallel over encode steps
       BitSink bs{op, 0};
-      u32 sLL = 0, sOF = 0, sML = 0;
       for (u32 e0 = 0; e0 < nbSeq; e0 += 64) {
         u32 const e = e0 + lane;
         bool const valid = e < nbSeq;
@@ -907,33 +985,15 @@ extern "C" __global__ __launch_bounds__(K2_THREADS) void zh_entropy_kernel(const
         u32 const ll = (u32)(rec & 0x1FFFFu), mlb = (u32)((rec >> 17) & 0x1FFFFu), ob = (u32)(rec >> 34);
         u32 const llc = valid ? ll_code(ll) : 0, mlc = valid ? ml_code(mlb) : 0, ofc = valid ? highbit32(ob) : 0;
         u32 vOF = 0, nOF = 0, vML = 0, nML = 0, vLL = 0, nLL = 0;
-        // per-lane symbol transforms, so the serial chain only waits on state-table reads
-        FseSym const tO = symOF[ofc], tM = symML[mlc], tL = symLL[llc];
-        u32 const cnt = min(64u, nbSeq - e0);
-        for (u32 j = 0; j < cnt; j++) {
-          u32 const dnO = __builtin_amdgcn_readlane(tO.dNb, j), dnM = __builtin_amdgcn_readlane(tM.dNb, j), dnL = __builtin_amdgcn_readlane(tL.dNb, j);
-          s32 const dfO = __builtin_amdgcn_readlane(tO.dFS, j), dfM = __builtin_amdgcn_readlane(tM.dFS, j), dfL = __builtin_amdgcn_readlane(tL.dFS, j);
-          if (e0 + j == 0) {
-            u32 nb = (dnM + (1u << 15)) >> 16;
-            sML = stML[((((nb << 16) - dnM)) >> nb) + dfM];
-            nb = (dnO + (1u << 15)) >> 16;
-            sOF = stOF[((((nb << 16) - dnO)) >> nb) + dfO];
-            nb = (dnL + (1u << 15)) >> 16;
-            sLL = stLL[((((nb << 16) - dnL)) >> nb) + dfL];
-          } else {
-            u32 const bO = (sOF + dnO) >> 16, bM = (sML + dnM) >> 16, bL = (sLL + dnL) >> 16;
-            u32 const oO = sOF & ((1u << bO) - 1u), oM = sML & ((1u << bM) - 1u), oL = sLL & ((1u << bL) - 1u);
-            sOF = stOF[(sOF >> bO) + dfO];
-            sML = stML[(sML >> bM) + dfM];
-            sLL = stLL[(sLL >> bL) + dfL];
-            vOF = setlane(vOF, oO, j); nOF = setlane(nOF, bO, j);
-            vML = setlane(vML, oM, j); nML = setlane(nML, bM, j);
-            vLL = setlane(vLL, oL, j); nLL = setlane(nLL, bL, j);
-          }
+        if (valid && e > 0) {
+          u32 const w = stw[e];
+          u32 const s_L = w & 1023u, s_O = (w >> 10) & 1023u, s_M = w >> 20;
+          nOF = (s_O + symOF[ofc].dNb) >> 16; vOF = s_O;
+          nML = (s_M + symML[mlc].dNb) >> 16; vML = s_M;
+          nLL = (s_L + symLL[llc].dNb) >> 16; vLL = s_L;
         }
         u32 v6[6] = {vOF, vML, vLL, ll, mlb, ob};
         u32 n6[6] = {nOF, nML, nLL, valid ? (u32)c_LL_bits[llc] : 0u, valid ? (u32)c_ML_bits[mlc] : 0u, ofc};
-        if (!valid) { n6[0] = n6[1] = n6[2] = 0; }
         sink_append<6>(bs, o, sw, v6, n6);
       }
       {
@@ -964,7 +1024,7 @@ extern "C" __global__ __launch_bounds__(K2_THREADS) void zh_entropy_kernel(const
   }
   ZH_STAMP(8);  // tail (raw copy etc.)
 #ifdef ZH_STAMPS
-  if (lane == 0) { u32 *dbg = ws.dbg(b); for (int k = 0; k < 9; k++) dbg[6 + k] = st[k]; }
+  if (lane == 0) { u32 *dbg = ws.dbg(b); for (int k = 0; k < 9; k++) dbg[6 + k] = st[k]; dbg[17] = st[9]; dbg[18] = st[10]; dbg[19] = nseq_raw; }
 #endif
   if (lane == 0) {
     if (d.flags & ZH_F_DIRECT) {

@@ -3,45 +3,60 @@
 // Replaces the reference's find_matches_kernel / greedy_parse_kernel /
 // build_sequences_gpu_kernel<<<1,1>>> (src/lz77_parallel.cu:26-70, 177-268)
 // and the literal gather kernels (src/cuda_zstd_manager.cu:602-723).
+// Output is identical to oracle/zstd_oracle.c orc_lz_parse (tile-lagged hash
+// insertion, longer of long/short candidate, greedy + lazy-1 parse).
 //
-// Layout (all LDS, 256 threads = 4 wave64, one workgroup per CU):
+// One workgroup of 1024 threads (16 wave64, one workgroup per CU) per block,
+// everything in LDS:
 //   in[]   the block, staged once with 16-B loads (64 KiB)
-//   TL/TS  2 x 2^13 u32 hash tables (value = position+1, 0 = empty), updated
-//          with ds_max so insertion order inside a tile never matters
-//   info[] per-position best match (off<<8 | len) for one 4096-position window
-//   lstage one window's literals, staged for coalesced global writes
-//   (per-position parse exits live in registers)
-// The parse is the serial greedy/lazy-1 parse of oracle/zstd_oracle.c
-// (orc_lz_parse) computed as a Jacobi fixed point over 256 segments.
+//   TL/TS  2 x 2^13 u32 hash tables, entry = (position+1) << 16 | content tag
+//   cinfo  one 4096-position window: candidates -> match info (off<<8|len) in place
+//   exb    per-position exits of the 16-position parse segments
+// Wave roles (wave specialisation, all synchronised with workgroup barriers):
+//   waves 14, 15  inserters: one wave per hash table walks the next window's
+//                 tiles of 256 positions (4 per lane).  A single wave needs no
+//                 barrier between a tile's lookups and its inserts because LDS
+//                 executes one wave's operations in order.  Candidates are held
+//                 in registers and dumped into cinfo at the window switch, so
+//                 the next window's insertion overlaps this window's lengths.
+//   waves 0..13   match lengths of the window, 5 positions per thread, with
+//                 same-offset chains resolved in registers.
+//   waves 0..3    the serial greedy/lazy-1 parse as a Jacobi fixed point over
+//                 256 segments of 16 positions, then emission.
 #include "zh_common.h"
 
 namespace {
 
-constexpr u32 K1_THREADS = 256;
-constexpr u32 NSEG = ZH_WINDOW / ZH_SEG;  // 256 segments per window, one per thread
-static_assert(NSEG == K1_THREADS, "one parse segment per thread");
-static_assert(ZH_WINDOW % ZH_TILE == 0 && ZH_TILE == K1_THREADS, "tiles tile windows");
+constexpr u32 K1_THREADS = 1024;
+constexpr u32 NSEG = ZH_WINDOW / ZH_SEG;    // parse segments per window (one per parse thread)
+constexpr u32 INS_TID = 896;                // first inserter thread (waves 14, 15)
+constexpr u32 SB = 5;                       // positions per thread in the length phase
+constexpr u32 NB = (ZH_WINDOW + SB - 1) / SB;  // length-phase threads (thread NB takes position `we`)
+constexpr u32 TILES = ZH_WINDOW / ZH_TILE;  // 16 tiles per window
+constexpr u32 TPL = ZH_TILE / 64;           // positions per inserter lane per tile
+static_assert(NSEG == 256 && NB + 1 <= INS_TID, "thread roles");
+static_assert(ZH_WINDOW % ZH_TILE == 0 && TPL == 4, "tiles tile windows");
 
 constexpr u32 HL_SIZE = 1u << ZH_HASH_LOG_LONG;
 constexpr u32 HS_SIZE = 1u << ZH_HASH_LOG_SHORT;
 constexpr u32 OFF_IN = 0;
 constexpr u32 OFF_TL = OFF_IN + ZH_BLOCK_MAX + 16;
 constexpr u32 OFF_TS = OFF_TL + 4 * HL_SIZE;
-constexpr u32 OFF_INFO = OFF_TS + 4 * HS_SIZE;
-// candidates per window position, one pad word per 16 so that a thread's 17-entry
-// segment slice (stride 17 words across lanes) is free of bank conflicts
-constexpr u32 CAND_WORDS = ZH_WINDOW + ZH_WINDOW / 16 + 8;
-__device__ __forceinline__ u32 cidx(u32 i) { return i + (i >> 4); }
-constexpr u32 OFF_LSTAGE = OFF_INFO + 4 * CAND_WORDS;
-// per-thread results of the chain-head extensions (34 bytes used of 36)
-constexpr u32 RES_STRIDE = 36;
-constexpr u32 OFF_RES = OFF_LSTAGE + ZH_WINDOW;
-constexpr u32 OFF_SEG = OFF_RES + RES_STRIDE * K1_THREADS;
-constexpr u32 OFF_SCAN = OFF_SEG + 4 * NSEG;
-constexpr u32 OFF_MISC = OFF_SCAN + 4 * 16;
+constexpr u32 OFF_CI = OFF_TS + 4 * HS_SIZE;
+constexpr u32 CI_WORDS = ZH_WINDOW + 8;  // + the lookahead slot of position `we`
+__device__ __forceinline__ u32 cidx(u32 i) { return i; }
+constexpr u32 OFF_EXB = OFF_CI + 4 * CI_WORDS;      // u8 per position: its parse segment exit (relative)
+constexpr u32 OFF_SEG = OFF_EXB + ZH_WINDOW;
+constexpr u32 NWW = INS_TID / 64;                   // worker waves
+constexpr u32 PR = (ZH_WINDOW + INS_TID - 1) / INS_TID;  // lane-per-position rounds over a window
+constexpr u32 WP_OFF = 80, WP_TOT = 160;
+static_assert(PR * NWW <= WP_OFF, "emission scan slots");
+constexpr u32 OFF_WP = OFF_SEG + 4 * 2 * NSEG;      // emission scan: wave counts, offsets, total
+constexpr u32 OFF_HB = OFF_WP + 4 * 164;            // per worker wave: 64 head-extension slots
+constexpr u32 OFF_MISC = OFF_HB + 4 * 64 * (INS_TID / 64);  // [0..3] scan partials, [4..6] barrier-or words
 constexpr u32 K1_LDS = OFF_MISC + 4 * 16;
-static_assert(K1_LDS <= 163840, "K1 LDS budget");
-static_assert(OFF_TL % 16 == 0 && OFF_INFO % 16 == 0 && OFF_SEG % 16 == 0, "alignment");
+static_assert(K1_LDS <= 163840 - 256, "K1 LDS budget");
+static_assert(OFF_TL % 16 == 0 && OFF_CI % 16 == 0 && OFF_SEG % 16 == 0, "alignment");
 
 __device__ __forceinline__ u32 hash_long(u64 v) {
   return (u32)((v * ZH_PRIME_LONG) >> (64 - ZH_HASH_LOG_LONG));
@@ -58,8 +73,7 @@ __device__ __forceinline__ void ld64u(const u32 *in32, u32 p, u32 &lo, u32 &hi) 
   hi = __builtin_amdgcn_alignbyte(w2, w1, sh);
 }
 
-
-// common prefix (0..8) of the 8 own bytes (olo, ohi) with in[b..b+8)
+// common prefix (0..8) of the 8 bytes (olo, ohi) with in[b..b+8)
 __device__ __forceinline__ u32 prefix8(const u32 *in32, u32 b, u32 olo, u32 ohi) {
   u32 blo, bhi;
   ld64u(in32, b, blo, bhi);
@@ -68,23 +82,32 @@ __device__ __forceinline__ u32 prefix8(const u32 *in32, u32 b, u32 olo, u32 ohi)
 }
 
 // Extension of a chain head (p, q) whose first 8 bytes match: E = min(common prefix,
-// 80, n - p).  80 = cap 64 + 16, so every later position of the segment continuing the
-// same offset gets its exact capped length as min(E - i, cap) without touching the
-// input again.  Bytes 8..79 are compared as 18 dwords with every load issued up front;
-// bytes past the block end read LDS padding/tables and are cut off by n - p.
-constexpr u32 EXT_SPAN = ZH_MAX_MATCH + ZH_SEG;
+// EXT_SPAN, n - p).  EXT_SPAN = cap 64 + SB - 1, so every later position of the
+// thread's run continuing the same offset gets its exact capped length as
+// min(E - i, cap) without touching the input again.  Bytes 8.. are compared as
+// dwords with every load issued up front; bytes past the block end read LDS
+// padding/tables and are cut off by n - p.
+constexpr u32 EXT_SPAN = ZH_MAX_MATCH + SB - 1;
+static_assert((EXT_SPAN - 8) % 4 == 0, "dword span");
 __device__ __forceinline__ u32 ext_head(const u32 *in32, u32 p, u32 q, u32 n) {
-  constexpr u32 NW = (EXT_SPAN - 8) / 4;
+  constexpr u32 NW = (EXT_SPAN - 8) / 4;  // dwords compared
+  constexpr u32 H = (NW + 1) / 2;         // in two halves (bounded register use)
   u32 const pa = p + 8, qa = q + 8;
   u32 const wp = pa >> 2, sp = pa & 3, wq = qa >> 2, sq = qa & 3;
-  u32 A[NW + 1], B[NW + 1];
-#pragma unroll
-  for (u32 k = 0; k <= NW; k++) { A[k] = in32[wp + k]; B[k] = in32[wq + k]; }
   u32 l = EXT_SPAN;
 #pragma unroll
-  for (int k = (int)NW - 1; k >= 0; k--) {
-    u32 const x = __builtin_amdgcn_alignbyte(A[k + 1], A[k], sp) ^ __builtin_amdgcn_alignbyte(B[k + 1], B[k], sq);
-    if (x) l = 8 + 4 * (u32)k + (__builtin_ctz(x) >> 3);
+  for (u32 h0 = 0; h0 < NW; h0 += H) {
+    u32 A[H + 1], B[H + 1];
+#pragma unroll
+    for (u32 k = 0; k <= H; k++) { A[k] = in32[wp + h0 + k]; B[k] = in32[wq + h0 + k]; }
+    u32 lh = EXT_SPAN;
+#pragma unroll
+    for (int k = (int)H - 1; k >= 0; k--) {
+      if (h0 + (u32)k >= NW) continue;
+      u32 const x = __builtin_amdgcn_alignbyte(A[k + 1], A[k], sp) ^ __builtin_amdgcn_alignbyte(B[k + 1], B[k], sq);
+      if (x) lh = 8 + 4 * (h0 + (u32)k) + (__builtin_ctz(x) >> 3);
+    }
+    l = l == EXT_SPAN ? lh : l;
   }
   return min(l, n - p);
 }
@@ -96,38 +119,153 @@ __device__ __forceinline__ u32 ext_head(const u32 *in32, u32 p, u32 q, u32 n) {
 __device__ __forceinline__ u32 tag_long(u32 lo, u32 hi) { (void)lo; return hi >> 16; }               // bytes 6..7
 __device__ __forceinline__ u32 tag_short(u32 lo, u32 hi) { return (lo >> 24) | ((hi & 0xFFu) << 8); }  // bytes 3..4
 
-
-// candidates of p against the current tables (tag-filtered), packed cL | cS << 16
-__device__ __forceinline__ u32 lookup(const u32 *TL, const u32 *TS, u32 lo, u32 hi, u32 &hL, u32 &hS, u32 &eLnew, u32 &eSnew, u32 p) {
+template <bool LONG>
+__device__ __forceinline__ void hash_tag(u32 lo, u32 hi, u32 &h, u32 &tag) {
   u64 const v = ((u64)hi << 32) | lo;
-  hL = hash_long(v);
-  hS = hash_short(v);
-  u32 const tL = tag_long(lo, hi), tS = tag_short(lo, hi);
-  u32 const eL = TL[hL], eS = TS[hS];
-  eLnew = ((p + 1) << 16) | tL;
-  eSnew = ((p + 1) << 16) | tS;
-  u32 const cL = (eL && (eL & 0xFFFFu) == tL) ? (eL >> 16) : 0u;
-  u32 const cS = (eS && (eS & 0xFFFFu) == tS) ? (eS >> 16) : 0u;
-  return cL | (cS << 16);
+  if (LONG) { h = hash_long(v); tag = tag_long(lo, hi); }
+  else { h = hash_short(v); tag = tag_short(lo, hi); }
 }
 
-// Exclusive scan of one u32 per thread over the 256-thread workgroup.
-__device__ __forceinline__ u32 wg_excl_scan(u32 v, u32 *scratch, u32 &total) {
-  u32 const lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  u32 incl = v;
+// Inserter wave: the 16 tiles of window [wsb, we) against one table.  Lane l handles
+// positions tb + l + 64k of each tile; all lookups of a tile are issued before its
+// inserts and after the previous tile's inserts (program order = LDS order within a
+// wave).  Candidates (position+1, tag-filtered, 0 = none) go to creg as u16 pairs.
+template <bool LONG>
+__device__ __forceinline__ void insert_window(const u32 *in32, u32 *T, u32 wsb, u32 we, u32 lim, u32 lane, u32 (&creg)[TILES * TPL / 2], u32 &cwe) {
 #pragma unroll
-  for (u32 d = 1; d < 64; d <<= 1) {
-    u32 t = __shfl_up(incl, d, 64);
-    if (lane >= d) incl += t;
+  for (u32 t = 0; t < TILES; t++) {
+    // opaque per-tile copy of lim: keeps the compiler from hoisting every tile's
+    // bounds checks (64 masks) to the top of the unrolled loop
+    u32 lim_t;
+    __asm__ volatile("v_mov_b32 %0, %1" : "=v"(lim_t) : "v"(lim));
+    u32 const tb = wsb + t * ZH_TILE;
+    u32 h[TPL], tg[TPL], e[TPL];
+#pragma unroll
+    for (u32 k = 0; k < TPL; k++) {
+      u32 const p = tb + 64 * k + lane;
+      u32 lo, hi;
+      ld64u(in32, min(p, lim_t), lo, hi);
+      hash_tag<LONG>(lo, hi, h[k], tg[k]);
+      e[k] = T[h[k]];
+    }
+#pragma unroll
+    for (u32 k = 0; k < TPL; k++) {
+      u32 const p = tb + 64 * k + lane;
+      atomicMax(&T[h[k]], p < lim_t ? (((p + 1) << 16) | tg[k]) : 0u);  // max with 0: no-op
+    }
+    u32 c[TPL];
+#pragma unroll
+    for (u32 k = 0; k < TPL; k++) {
+      u32 const p = tb + 64 * k + lane;
+      c[k] = (p < lim_t && e[k] && (e[k] & 0xFFFFu) == tg[k]) ? (e[k] >> 16) : 0u;
+    }
+    creg[2 * t] = c[0] | (c[1] << 16);
+    creg[2 * t + 1] = c[2] | (c[3] << 16);
+    // materialise this tile's candidates now (otherwise the compiler sinks their
+    // computation to the dump and keeps every tile's temporaries alive)
+    __asm__ volatile("" : "+v"(creg[2 * t]), "+v"(creg[2 * t + 1]) :: "memory");
   }
-  if (lane == 63) scratch[wave] = incl;
-  __syncthreads();
-  u32 woff = 0, tot = 0;
+  // the next window's first position (lazy rule at this window's end): looked up
+  // after all of this window's tiles, before any of the next window's
+  cwe = 0;
+  if (lane == 0 && we < lim) {
+    u32 lo, hi, hh, tt;
+    ld64u(in32, we, lo, hi);
+    hash_tag<LONG>(lo, hi, hh, tt);
+    u32 const ee = T[hh];
+    cwe = (ee && (ee & 0xFFFFu) == tt) ? (ee >> 16) : 0u;
+  }
+  __asm__ volatile("" ::: "memory");
+}
+
+// Dump an inserter's candidates into its half of the cinfo words (LONG: low half).
+template <bool LONG>
+__device__ __forceinline__ void dump_window(u8 *ci8, u32 lane_, const u32 (&creg)[TILES * TPL / 2], u32 cwe) {
+  // opaque lane copy: stops the 64 addresses from being hoisted out of the window loop
+  u32 lane;
+  __asm__ volatile("v_mov_b32 %0, %1" : "=v"(lane) : "v"(lane_));
 #pragma unroll
-  for (u32 w = 0; w < K1_THREADS / 64; w++) { u32 s = scratch[w]; woff += (w < wave) ? s : 0; tot += s; }
-  total = tot;
+  for (u32 t = 0; t < TILES; t++) {
+#pragma unroll
+    for (u32 k = 0; k < TPL; k++) {
+      u32 const i = t * ZH_TILE + 64 * k + lane;
+      u16 const v = (u16)(creg[2 * t + (k >> 1)] >> (16 * (k & 1)));
+      *(u16 *)(ci8 + 4 * cidx(i) + (LONG ? 0 : 2)) = v;
+    }
+  }
+  if (lane == 0) *(u16 *)(ci8 + 4 * cidx(ZH_WINDOW) + (LONG ? 0 : 2)) = (u16)cwe;
+}
+
+// Lane-per-position parse step for window index i (lanes of a wave = 4 parse segments
+// of 16 positions): X[k] = position reached after 2^k parse steps from i, relative to
+// the segment start (values >= the segment length mean "left the segment").
+// Returns the match info of i if the parse takes a match there, else 0.
+__device__ __forceinline__ u32 parse_steps(const u32 *ci, u32 i, u32 wn, u32 la, u32 lane, u32 (&X)[5]) {
+  u32 const sb = i & ~15u, sl = i & 15u;
+  u32 const slen = wn > sb ? min(16u, wn - sb) : 0u;
+  u32 const inf = i < wn ? ci[i] : 0u;
+  u32 const inf1 = i + 1 < wn ? ci[i + 1] : la;
+  u32 const l = inf & 255u;
+  bool const tk = l != 0 && (inf1 & 255u) <= l;
+  u32 x = sl + (tk ? l : 1u);
+#pragma unroll
+  for (u32 k = 0; k < 4; k++) {
+    X[k] = x;
+    u32 const y = __shfl(x, (lane & ~15u) + min(x, 15u), 64);
+    x = x < slen ? y : x;
+  }
+  X[4] = x;
+  return tk ? inf : 0u;
+}
+
+// Workgroup barrier returning the OR of `pred` over all threads, one s_barrier.
+// Three rotating LDS words: word r%3 is set before barrier r, read after it, and
+// cleared by thread 0 after barrier r+1 (its next use is round r+3).
+__device__ __forceinline__ bool barrier_or(bool pred, u32 *orw, u32 &round) {
+  u32 const r = round++;
+  if (__ballot(pred) && (threadIdx.x & 63) == 0) orw[r % 3] = 1;
   __syncthreads();
-  return woff + incl - v;
+  bool const res = orw[r % 3] != 0;
+  if (threadIdx.x == 0) orw[(r + 2) % 3] = 0;
+  return res;
+}
+
+// Inserter wave main loop: mirrors the workers' barrier sequence window by window
+// (P, R, X, the parse's Jacobi rounds, E1, E2) and runs at raised priority, since the
+// next window's insertion is the longest chain of the window step.
+template <bool LONG>
+__device__ __forceinline__ void inserter_loop(const u32 *in32, u32 *T, u8 *ci8, u32 *orw, u32 *misc_, u32 n, u32 lim, u32 lane, u32 *dbg) {
+  // (no priority boost: measured slower)
+
+  u32 creg[TILES * TPL / 2];
+  u32 cwe = 0, bround = 0;
+  insert_window<LONG>(in32, T, 0, min((u32)ZH_WINDOW, n), lim, lane, creg, cwe);
+#ifdef ZH_STAMPS
+  u32 st_ins = 0;
+#endif
+  for (u32 wsb = 0; wsb < n; wsb += ZH_WINDOW) {
+    u32 const we = min(wsb + ZH_WINDOW, n);
+    dump_window<LONG>(ci8, lane, creg, cwe);
+    __syncthreads();  // P: candidates of this window in cinfo
+#ifdef ZH_STAMPS
+    u64 const ti0 = __builtin_amdgcn_s_memtime();
+#endif
+    if (we < n) insert_window<LONG>(in32, T, we, min(we + ZH_WINDOW, n), lim, lane, creg, cwe);
+#ifdef ZH_STAMPS
+    u32 const dti = (u32)(__builtin_amdgcn_s_memtime() - ti0);
+    st_ins += dti;
+    if (lane == 0) atomicMax(&misc_[9], dti);
+#endif
+    __syncthreads();  // R: match info of this window in cinfo
+    __syncthreads();  // X: segment exits
+    while (barrier_or(false, orw, bround)) {}  // the parse's Jacobi rounds
+    __syncthreads();  // E1: the parse has read this window's info; cinfo is free
+    __syncthreads();  // E2: emission offsets
+  }
+#ifdef ZH_STAMPS
+  if (LONG && lane == 0) dbg[16] = st_ins;
+#endif
+  (void)dbg; (void)misc_;
 }
 
 }  // namespace
@@ -149,20 +287,25 @@ extern "C" __global__ __launch_bounds__(K1_THREADS) void zh_lz_kernel(const ZhBl
   u8 *in = smem + OFF_IN;
   u32 *in32 = (u32 *)in;
   u32 *TL = (u32 *)(smem + OFF_TL), *TS = (u32 *)(smem + OFF_TS);
-  u32 *info = (u32 *)(smem + OFF_INFO);
-  u8 *lstage = smem + OFF_LSTAGE;
+  u32 *ci = (u32 *)(smem + OFF_CI);
+  u8 *ci8 = smem + OFF_CI;
+  u8 *exb = smem + OFF_EXB;
+  u32 *wpart = (u32 *)(smem + OFF_WP);
+  u32 *hbuf = (u32 *)(smem + OFF_HB);
   u32 *segx = (u32 *)(smem + OFF_SEG);
-  u32 *scan = (u32 *)(smem + OFF_SCAN);
   u32 *misc = (u32 *)(smem + OFF_MISC);
+  u32 *orw = misc + 4;
 
-  u32 const b = blockIdx.x, tid = threadIdx.x;
+  u32 const b = blockIdx.x, tid = threadIdx.x, lane = tid & 63;
   ZhBlockDesc const d = blocks[b];
   u32 const n = d.n;
   if (n == 0) return;
   u32 *meta = ws.meta(b);
 #ifdef ZH_STAMPS
+  u64 const rt0 = __builtin_amdgcn_s_memrealtime();
   u64 stamp_prev = __builtin_amdgcn_s_memtime();
-  u32 st_stage = 0, st_A = 0, st_B1 = 0, st_B = 0, st_J = 0, st_E = 0, st_rounds = 0;
+  u64 const mt0 = stamp_prev;
+  u32 st_stage = 0, st_A = 0, st_X = 0, st_E1 = 0, st_Bmax = 0, st_Imax = 0, st_Bw = 0, st_B = 0, st_J = 0, st_E = 0, st_rounds = 0;
 #endif
 
   // ---- stage the block into LDS (16 B per lane when the source allows it) and probe RLE
@@ -185,6 +328,8 @@ extern "C" __global__ __launch_bounds__(K1_THREADS) void zh_lz_kernel(const ZhBl
   if (tid < 16) in[n + tid] = 0;
   for (u32 i = tid; i < HL_SIZE; i += K1_THREADS) TL[i] = 0;
   for (u32 i = tid; i < HS_SIZE; i += K1_THREADS) TS[i] = 0;
+  if (tid < 3) orw[tid] = 0;
+  if (tid < 2) misc[8 + tid] = 0;
   bool const rle = __syncthreads_and(same) && n >= 2;
   if (rle) {
     if (tid == 0) { meta[0] = 0; meta[1] = 0; meta[2] = 1; }
@@ -195,126 +340,126 @@ extern "C" __global__ __launch_bounds__(K1_THREADS) void zh_lz_kernel(const ZhBl
   u64 *seq_out = ws.seq(b);
   u8 *lit_out = ws.lits(b);
   u32 const lim = n > ZH_HASH_READ ? n - ZH_HASH_READ : 0;
-  u32 nseq_tot = 0, nlit_tot = 0, e_in = 0;
+  u32 nseq_tot = 0, nlit_tot = 0, e_in = 0, bround = 0;
+  // ---- inserter waves: their own loop with the same barrier sequence as the workers'
+  // (separate code, so their registers never add to the workers' pressure)
+  if (tid >= INS_TID) {
+    if (tid < INS_TID + 64) inserter_loop<true>(in32, TL, ci8, orw, misc, n, lim, lane, ws.dbg(b));
+    else inserter_loop<false>(in32, TS, ci8, orw, misc, n, lim, lane, ws.dbg(b));
+    return;
+  }
 
   for (u32 wsb = 0; wsb < n; wsb += ZH_WINDOW) {
     u32 const we = min(wsb + ZH_WINDOW, n);
-
-    // ---- phase A: insertion in tiles of 256 positions; lookups see earlier tiles only.
-    // The next tile's bytes and hashes are computed between the two barriers (software pipeline).
-    u32 *cand = info;  // candidates live in info[] until phase B overwrites them
-    u32 a_lo = 0, a_hi = 0;
-    if (wsb + tid < lim) ld64u(in32, wsb + tid, a_lo, a_hi);
-    for (u32 tb = wsb; tb < we; tb += ZH_TILE) {
-      u32 const p = tb + tid;
-      bool const act = p < lim;
-      u32 hL = 0, hS = 0, nL = 0, nS = 0, c = 0;
-      if (act) c = lookup(TL, TS, a_lo, a_hi, hL, hS, nL, nS, p);
-      if (p < we) cand[cidx(p - wsb)] = c;
-      __syncthreads();
-      if (act) {
-        atomicMax(&TL[hL], nL);
-        atomicMax(&TS[hS], nS);
-      }
-      u32 const pn = p + ZH_TILE;
-      if (pn < lim && tb + ZH_TILE < we) ld64u(in32, pn, a_lo, a_hi);
-      __syncthreads();
-    }
-    if (tid == 0) {  // first position of the next window (lazy check at the window end)
-      u32 c = 0, hL, hS, nL, nS;
-      if (we < lim) { u32 lo, hi; ld64u(in32, we, lo, hi); c = lookup(TL, TS, lo, hi, hL, hS, nL, nS, we); }
-      cand[cidx(we - wsb)] = c;
-    }
-    __syncthreads();
-
+    __syncthreads();  // P
     ZH_STAMP(st_A);
-    // ---- phase B (no barriers): match lengths of the thread's own segment (+ the
-    // next segment's first position, for the lazy rule), then per-position exits
-    u32 const s = wsb + tid * ZH_SEG;
-    u32 const se = min(s + ZH_SEG, we);
-    u32 inf[ZH_SEG + 1];
-    u32 own[ZH_SEG / 4];
+#ifdef ZH_STAMPS
+    u64 const tP = __builtin_amdgcn_s_memtime();
+#endif
+
+    // ---- match lengths (threads 0..NB), while the inserter waves build the next window
     {
-      // (1) candidates of the 16 own positions + the next segment's first position,
-      //     own bytes, and the first-8-byte prefix of every candidate: all loads
-      //     unconditional so they issue back to back
-      u32 cv[ZH_SEG + 1];
+      // thread tid < NB: positions [s, se) of the window; thread NB: position `we`;
+      // threads above NB take part in the wave-level steps with no positions
+      u32 const s = tid < NB ? wsb + SB * tid : we;
+      u32 const se = tid < NB ? min(s + SB, we) : (tid == NB ? min(we + 1, n) : s);
+      u32 const cbase = tid < NB ? SB * tid : ZH_WINDOW;  // window index of position s
+      // (1) candidates, own bytes and first-8-byte prefixes; loads unconditional
+      u32 cv[SB], plp = 0, psp = 0;  // prefixes packed 4 bits per position
 #pragma unroll
-      for (u32 j = 0; j <= ZH_SEG; j++) {
+      for (u32 j = 0; j < SB; j++) {
         u32 const p = s + j;
-        cv[j] = (p <= se && p < lim) ? cand[cidx(p - wsb)] : 0u;
-      }
-      u32 ow[ZH_SEG / 4 + 4];
-      {
-        uint4 const v0 = ((const uint4 *)in)[s >> 4], v1 = ((const uint4 *)in)[(s >> 4) + 1];
-        ow[0] = v0.x; ow[1] = v0.y; ow[2] = v0.z; ow[3] = v0.w;
-        ow[4] = v1.x; ow[5] = v1.y; ow[6] = v1.z; ow[7] = v1.w;
-      }
-      u32 pl[ZH_SEG + 1], ps[ZH_SEG + 1];
-#pragma unroll
-      for (u32 j = 0; j <= ZH_SEG; j++) {
-        u32 const olo = __builtin_amdgcn_alignbyte(ow[(j >> 2) + 1], ow[j >> 2], j & 3);
-        u32 const ohi = __builtin_amdgcn_alignbyte(ow[(j >> 2) + 2], ow[(j >> 2) + 1], j & 3);
+        bool const v = p < se && p < lim;
+        cv[j] = v ? ci[cidx(cbase + j)] : 0u;
+        u32 olo, ohi;
+        ld64u(in32, min(p, lim), olo, ohi);
         u32 const cL = cv[j] & 0xFFFFu, cS = cv[j] >> 16;
         u32 const xL = prefix8(in32, cL ? cL - 1 : 0u, olo, ohi);
         u32 const xS = prefix8(in32, cS ? cS - 1 : 0u, olo, ohi);
-        pl[j] = cL ? xL : 0u;
-        ps[j] = (cS && cS != cL) ? xS : 0u;
+        plp |= (cL ? xL : 0u) << (4 * j);
+        psp |= ((cS && cS != cL) ? xS : 0u) << (4 * j);
       }
-      ZH_STAMP(st_B1);
-      // (2) chains: a candidate whose first 8 bytes match and that continues a
-      //     previous-position candidate with the same offset (which also had 8
-      //     matching bytes) is a follower; the others with 8 matching bytes are heads
-      u32 dL = 0, dS = 0;       // follower bits
-      u32 fromSL = 0, fromSS = 0;  // follower whose predecessor is the previous position's S pair
-      u64 heads = 0;        // bit j = L head, bit 32 + j = S head
+#define PL(j) ((plp >> (4 * (j))) & 15u)
+#define PS(j) ((psp >> (4 * (j))) & 15u)
+      // (2) chains: a candidate with 8 matching bytes that continues a previous-position
+      //     candidate with the same offset (also 8 matching) is a follower; else a head
+      u32 dL = 0, dS = 0, fromSL = 0, fromSS = 0, heads = 0;  // heads: bit j = L, bit 8 + j = S
 #pragma unroll
-      for (u32 j = 0; j <= ZH_SEG; j++) {
+      for (u32 j = 0; j < SB; j++) {
         u32 const cL = cv[j] & 0xFFFFu, cS = cv[j] >> 16;
-        bool const eL = cL && pl[j] == 8, eS = cS && cS != cL && ps[j] == 8;
+        bool const eL = cL && PL(j) == 8, eS = cS && cS != cL && PS(j) == 8;
         u32 const pcL = j ? (cv[j - 1] & 0xFFFFu) : 0u, pcS = j ? (cv[j - 1] >> 16) : 0u;
-        bool const peL = j && pcL && pl[j - 1] == 8;
-        bool const peS = j && pcS && pcS != pcL && ps[j - 1] == 8;
+        bool const peL = j && pcL && PL(j - 1) == 8;
+        bool const peS = j && pcS && pcS != pcL && PS(j - 1) == 8;
         if (eL) {
           if (peL && cL == pcL + 1) dL |= 1u << j;
           else if (peS && cL == pcS + 1) { dL |= 1u << j; fromSL |= 1u << j; }
-          else heads |= 1ull << j;
+          else heads |= 1u << j;
         }
         if (eS) {
           if (peL && cS == pcL + 1) dS |= 1u << j;
           else if (peS && cS == pcS + 1) { dS |= 1u << j; fromSS |= 1u << j; }
-          else heads |= 1ull << (32 + j);
+          else heads |= 1u << (8 + j);
         }
       }
-      // (3) extend the heads, one per lane per iteration (compacted across positions)
-      u8 *res = smem + OFF_RES + tid * RES_STRIDE;
-      for (u64 hm = heads; hm; hm &= hm - 1) {
-        u32 const k = (u32)__builtin_ctzll(hm);
-        u32 const j = k & 31u;
-        u32 const cw = cand[cidx(s + j - wsb)];
-        u32 const c = k >= 32 ? (cw >> 16) : (cw & 0xFFFFu);
-        res[k >= 32 ? ZH_SEG + 1 + j : j] = (u8)ext_head(in32, s + j, c - 1, n);
-      }
-      // (4) lengths in position order: E = exact prefix below 8, the head's extension,
-      //     or the predecessor's E - 1; capped length = min(E, 64, n - p)
-      u32 rw[(2 * (ZH_SEG + 1) + 3) / 4];
+      // (3) extend the heads, compacted across the wave: heads are ranked in (lane, bit)
+      //     order and handed out 64 at a time, one per lane (wave-private LDS slots;
+      //     a wave's LDS operations execute in order, so no barrier is needed)
+      u32 hr[(2 * SB + 3) / 4] = {};  // head extensions packed as bytes, slot k = L_j (k=j) / S_j (k=SB+j)
+      {
+        u32 const nh = __builtin_popcount(heads);
+        u32 inc = nh;
 #pragma unroll
-      for (u32 k = 0; k < (2 * (ZH_SEG + 1) + 3) / 4; k++) rw[k] = ((const u32 *)res)[k];
+        for (u32 dd = 1; dd < 64; dd <<= 1) {
+          u32 const t = __shfl_up(inc, dd, 64);
+          if (lane >= dd) inc += t;
+        }
+        u32 const hbase = inc - nh, htot = __shfl(inc, 63, 64);
+        u32 *hb = hbuf + (tid >> 6) * 64;
+        for (u32 c0 = 0; c0 < htot; c0 += 64) {
+          u32 r = hbase;
+#pragma unroll
+          for (u32 k = 0; k < 2 * SB; k++) {
+            u32 const bit = k < SB ? k : 8 + (k - SB);
+            if ((heads >> bit) & 1u) {
+              u32 const c = k < SB ? (cv[k] & 0xFFFFu) : (cv[k - SB] >> 16);
+              u32 const j = k < SB ? k : k - SB;
+              if (r >= c0 && r < c0 + 64) hb[r - c0] = (s + j) | ((c - 1) << 16);
+              r++;
+            }
+          }
+          __asm__ volatile("" ::: "memory");
+          if (c0 + lane < htot) {
+            u32 const e = hb[lane];
+            hb[lane] = ext_head(in32, e & 0xFFFFu, e >> 16, n);
+          }
+          __asm__ volatile("" ::: "memory");
+          r = hbase;
+#pragma unroll
+          for (u32 k = 0; k < 2 * SB; k++) {
+            u32 const bit = k < SB ? k : 8 + (k - SB);
+            if ((heads >> bit) & 1u) {
+              if (r >= c0 && r < c0 + 64) hr[k >> 2] |= hb[r - c0] << (8 * (k & 3));
+              r++;
+            }
+          }
+          __asm__ volatile("" ::: "memory");
+        }
+      }
+      // (4) lengths in position order; E = exact prefix below 8, the head's extension,
+      //     or the predecessor's E - 1; capped length = min(E, 64, n - p)
       u32 EL = 0, ES = 0;
 #pragma unroll
-      for (u32 j = 0; j <= ZH_SEG; j++) {
+      for (u32 j = 0; j < SB; j++) {
         u32 const p = s + j;
         u32 const cL = cv[j] & 0xFFFFu, cS = cv[j] >> 16;
-        u32 const capj = min((u32)ZH_MAX_MATCH, n - p);
-        u32 const hLr = (rw[j >> 2] >> (8 * (j & 3))) & 255u;
-        u32 const jS = ZH_SEG + 1 + j;
-        u32 const hSr = (rw[jS >> 2] >> (8 * (jS & 3))) & 255u;
-        u32 nL = pl[j];
+        u32 const capj = min((u32)ZH_MAX_MATCH, n - min(p, n));
+        u32 nL = PL(j);
         if (dL & (1u << j)) nL = ((fromSL >> j) & 1u ? ES : EL) - 1;
-        else if ((heads >> j) & 1u) nL = hLr;
-        u32 nS = ps[j];
+        else if ((heads >> j) & 1u) nL = (hr[j >> 2] >> (8 * (j & 3))) & 255u;
+        u32 nS = PS(j);
         if (dS & (1u << j)) nS = ((fromSS >> j) & 1u ? ES : EL) - 1;
-        else if ((heads >> (32 + j)) & 1u) nS = hSr;
+        else if ((heads >> (8 + j)) & 1u) nS = (hr[(SB + j) >> 2] >> (8 * ((SB + j) & 3))) & 255u;
         if (cS && cS == cL) nS = nL;
         EL = nL; ES = nS;
         u32 const rL = min(nL, capj), rS = min(nS, capj);
@@ -323,88 +468,136 @@ extern "C" __global__ __launch_bounds__(K1_THREADS) void zh_lz_kernel(const ZhBl
         u32 v = 0;
         if (lL && lL >= lS) v = ((p - (cL - 1)) << 8) | lL;
         else if (lS) v = ((p - (cS - 1)) << 8) | lS;
-        inf[j] = v;
+        if (p < se) ci[cidx(cbase + j)] = v;
       }
-#pragma unroll
-      for (u32 k = 0; k < ZH_SEG / 4; k++) own[k] = ow[k];
+      if (tid == NB && we >= n) ci[cidx(ZH_WINDOW)] = 0;  // no position after the block
+#undef PL
+#undef PS
     }
-    // per-position exits of the own segment (relative to s), backward, in registers
-    u32 const slen = se > s ? se - s : 0u;
-    u32 ex0[ZH_SEG];
-#pragma unroll
-    for (int j = (int)ZH_SEG - 1; j >= 0; j--) {
-      u32 const l = inf[j] & 255u;
-      bool const tk = l != 0 && (inf[j + 1] & 255u) <= l;
-      u32 const x = tk ? (u32)j + l : (u32)j + 1;
-      u32 v = x;
-#pragma unroll
-      for (u32 k = j + 1; k < ZH_SEG; k++) v = (x == k && k < slen) ? ex0[k] : v;
-      ex0[j] = v;
-    }
+    ZH_STAMP(st_Bw);
+#ifdef ZH_STAMPS
+    if (lane == 0) atomicMax(&misc[8], (u32)(__builtin_amdgcn_s_memtime() - tP));
+#endif
+    __syncthreads();  // R
     ZH_STAMP(st_B);
-    u32 entry = max(s, e_in);
-    for (;;) {
-      u32 ex = entry;
+#ifdef ZH_STAMPS
+    if (tid == 0) { st_Bmax += misc[8]; st_Imax += misc[9]; misc[8] = 0; misc[9] = 0; }
+#endif
+    u32 const info_ahead = ci[cidx(ZH_WINDOW)];
+
+    // ---- parse.  Lanes = positions (PR rounds of the 896 worker lanes); a wave's 64 lanes are 4 parse
+    // segments of 16.  step(p) = next position the greedy/lazy-1 parse visits after p;
+    // pointer doubling inside the segment (ds_bpermute) gives X_k = 2^k steps, and the
+    // segment exit of every position after 4 doublings.
+    u32 const wn = we - wsb;
+    u32 const la = info_ahead;  // match info of position `we` (lazy rule at the window end)
 #pragma unroll
-      for (u32 k = 0; k < ZH_SEG; k++) ex = (entry == s + k && k < slen) ? s + ex0[k] : ex;
-      segx[tid] = ex;
-      __syncthreads();
-      u32 const ne = tid == 0 ? max(s, e_in) : max(segx[tid - 1], s);
-      bool const ch = ne != entry;
-      entry = ne;
+    for (u32 rr = 0; rr < PR; rr++) {
+      u32 const i = INS_TID * rr + tid;
+      u32 X[5];
+      parse_steps(ci, i, wn, la, lane, X);
+      if (i < wn) exb[i] = (u8)X[4];
+    }
+    __syncthreads();  // X: exits of all positions
+    ZH_STAMP(st_X);
+    // Jacobi fixed point of the segment entries (threads 0..255, one per segment;
+    // == the serial parse).  One barrier per round: round r writes exits into
+    // segx[r & 1] and reads the predecessor's exit of round r-1 from the other half.
+    bool const pt = tid < NSEG;
+    u32 const s = wsb + ZH_SEG * tid;
+    u32 const se = pt ? min(s + ZH_SEG, we) : 0u;
+    u32 entry = max(s, e_in), rfin = 0;
+    for (u32 r = 0;; r++) {
+      bool ch = r == 0;
+      if (pt && r) {
+        u32 const ne = tid == 0 ? max(s, e_in) : max(segx[((r - 1) & 1) * NSEG + tid - 1], s);
+        ch = ne != entry;
+        entry = ne;
+      }
+      if (pt) segx[(r & 1) * NSEG + tid] = (entry < se) ? s + exb[ZH_SEG * tid + (entry - s)] : entry;
 #ifdef ZH_STAMPS
       st_rounds++;
 #endif
-      if (!__syncthreads_or(ch)) break;
+      if (!barrier_or(ch, orw, bround)) { rfin = r; break; }
     }
     ZH_STAMP(st_J);
-    // segx[] now holds every segment's exit for the converged entries
-    u32 const e_out = segx[NSEG - 1];
+    u32 const *segf = segx + (rfin & 1) * NSEG;  // converged exits
+    u32 const e_out = segf[NSEG - 1];
 
-    // ---- emission: one walk records match starts / literals as bit masks; literals are
-    // staged in LDS and written out coalesced
-    u32 tmask = 0, lmask = 0;
-    {
-      u32 nxt = entry - s;  // >= ZH_SEG when the segment is skipped entirely
+    // ---- emission, lanes = positions: a position is on the parse path iff binary
+    // lifting from its segment's entry (X_8, X_4, X_2, X_1) lands on it; scans of the
+    // take/literal flags give each record's and literal's slot
+    u32 fl[PR];    // bit 0 literal, bit 1 match start
+    u32 infr[PR];  // match info of the match starts
 #pragma unroll
-      for (u32 j = 0; j < ZH_SEG; j++) {
-        if (j == nxt && s + j < se) {
-          u32 const l = inf[j] & 255u;
-          bool const tk = l != 0 && (inf[j + 1] & 255u) <= l;
-          if (tk) { tmask |= 1u << j; nxt = j + l; }
-          else { lmask |= 1u << j; nxt = j + 1; }
+    for (u32 rr = 0; rr < PR; rr++) {
+      u32 const i = INS_TID * rr + tid;
+      u32 X[5];
+      infr[rr] = parse_steps(ci, i, wn, la, lane, X);
+      u32 const sb = i & ~15u, sl = i & 15u, t = i >> 4;
+      u32 const ent = t == 0 ? max(wsb, e_in) : max(wsb + sb, segf[min(t, NSEG) - 1]);
+      u32 cur = ent - (wsb + sb);  // >= 16 when the segment is skipped
+#pragma unroll
+      for (int k = 3; k >= 0; k--) {
+        u32 const y = __shfl(X[k], (lane & ~15u) + min(cur, 15u), 64);
+        if (cur <= sl && y <= sl) cur = y;
+      }
+      bool const vis = i < wn && cur == sl;
+      fl[rr] = vis ? (infr[rr] ? 2u : 1u) : 0u;
+    }
+    u32 lcnt[PR], scnt[PR];
+#pragma unroll
+    for (u32 rr = 0; rr < PR; rr++) {
+      u64 const ml = __ballot(fl[rr] & 1u), ms = __ballot(fl[rr] & 2u);
+      lcnt[rr] = __builtin_amdgcn_mbcnt_hi((u32)(ml >> 32), __builtin_amdgcn_mbcnt_lo((u32)ml, 0u));
+      scnt[rr] = __builtin_amdgcn_mbcnt_hi((u32)(ms >> 32), __builtin_amdgcn_mbcnt_lo((u32)ms, 0u));
+      if (lane == 0) wpart[rr * NWW + (tid >> 6)] = (u32)__popcll(ml) | ((u32)__popcll(ms) << 16);
+    }
+    __syncthreads();  // E1: per-wave counts (cinfo is free for the inserters from here on)
+    ZH_STAMP(st_E1);
+    if (tid < 64) {   // exclusive scan of the PR*NWW (round, wave) counts, in position order
+      u32 carry = 0;
+#pragma unroll
+      for (u32 c0 = 0; c0 < PR * NWW; c0 += 64) {
+        u32 const v = c0 + lane < PR * NWW ? wpart[c0 + lane] : 0u;
+        u32 inc = v;
+#pragma unroll
+        for (u32 dd = 1; dd < 64; dd <<= 1) {
+          u32 const t = __shfl_up(inc, dd, 64);
+          if (lane >= dd) inc += t;
         }
+        if (c0 + lane < PR * NWW) wpart[WP_OFF + c0 + lane] = carry + inc - v;
+        carry += __shfl(inc, 63, 64);
       }
+      if (tid == 0) wpart[WP_TOT] = carry;
     }
-    u32 const c = __builtin_popcount(tmask), l = __builtin_popcount(lmask);
-    u32 total;
-    u32 const ex = wg_excl_scan((c << 16) | l, scan, total);
-    u32 lit_i = ex & 0xFFFFu, seq_i = nseq_tot + (ex >> 16);
+    __syncthreads();  // E2: offsets
 #pragma unroll
-    for (u32 j = 0; j < ZH_SEG; j++) {
-      if (tmask & (1u << j)) {
-        seq_out[seq_i++] = (u64)(nlit_tot + lit_i) | ((u64)(inf[j] & 255u) << 17) | ((u64)(inf[j] >> 8) << 25);
-      } else if (lmask & (1u << j)) {
-        lstage[lit_i++] = (u8)(own[j >> 2] >> (8 * (j & 3)));
-      }
+    for (u32 rr = 0; rr < PR; rr++) {
+      u32 const i = INS_TID * rr + tid;
+      u32 const off = wpart[WP_OFF + rr * NWW + (tid >> 6)];
+      u32 const li = (off & 0xFFFFu) + lcnt[rr], si = (off >> 16) + scnt[rr];
+      if (fl[rr] & 1u) lit_out[nlit_tot + li] = in[wsb + i];
+      if (fl[rr] & 2u) seq_out[nseq_tot + si] = (u64)(nlit_tot + li) | ((u64)(infr[rr] & 255u) << 17) | ((u64)(infr[rr] >> 8) << 25);
     }
-    __syncthreads();
-    u32 const ltot = total & 0xFFFFu;
-    for (u32 i = tid; i < ltot; i += K1_THREADS) lit_out[nlit_tot + i] = lstage[i];
+    u32 const total = wpart[WP_TOT];
     nseq_tot += total >> 16;
     nlit_tot += total & 0xFFFFu;
     e_in = e_out;
-    __syncthreads();
     ZH_STAMP(st_E);
   }
   if (tid == 0) { meta[0] = nseq_tot; meta[1] = nlit_tot; meta[2] = 0; }
 #ifdef ZH_STAMPS
   if (tid == 0) {
     u32 *dbg = ws.dbg(b);
-    dbg[0] = st_stage; dbg[1] = st_A; dbg[2] = st_B; dbg[3] = st_J; dbg[4] = st_E; dbg[5] = st_rounds; dbg[16] = st_B1;
+    dbg[23] = (u32)rt0; dbg[24] = (u32)__builtin_amdgcn_s_memrealtime();
+    dbg[25] = __builtin_amdgcn_s_getreg((31 << 11) | 4);   // HW_ID
+    dbg[26] = __builtin_amdgcn_s_getreg((31 << 11) | 20);  // XCC_ID
+    dbg[27] = (u32)(__builtin_amdgcn_s_memtime() - mt0);
+    dbg[40] = st_Bmax; dbg[41] = st_Imax;
+    dbg[0] = st_stage; dbg[1] = st_A; dbg[2] = st_B; dbg[3] = st_J; dbg[4] = st_E; dbg[5] = st_rounds; dbg[20] = st_Bw; dbg[21] = st_X; dbg[22] = st_E1;
   }
 #endif
-  (void)misc;
 }
 
 extern "C" u32 zh_lz_lds_bytes() { return K1_LDS; }

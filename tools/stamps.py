@@ -35,9 +35,9 @@ off = a256(off + n * 8)
 off = a256(off + n * 4)
 off = a256(off + 0)
 blocks = base + off
-WS = 13120 * 8 + 65536 + 128
+WS = 13120 * 8 + 65536 + 256
 h = temp.cpu().numpy()
-raw = np.array([h[blocks + b * WS + 13120 * 8 + 65536 + 16: blocks + b * WS + 13120 * 8 + 65536 + 16 + 17 * 4].view(np.uint32) for b in range(n)])
+raw = np.array([h[blocks + b * WS + 13120 * 8 + 65536 + 16: blocks + b * WS + 13120 * 8 + 65536 + 16 + 23 * 4].view(np.uint32) for b in range(n)])
 st = raw[:, :6]
 k2 = raw[:, 6:15].astype(np.float64)
 names = ["stage", "A(insert)", "B(lengths+exit)", "J(jacobi)", "E(emit)", "rounds"]
@@ -45,10 +45,26 @@ tot = st[:, :5].sum(1).mean()
 print(kind, "mean cycles/block (s_memtime units)", int(tot))
 for k, nm in enumerate(names):
     print(f"  {nm:16s} mean {st[:, k].mean():12.0f}  share {st[:, k].mean() / tot * 100 if k < 5 else 0:5.1f}%")
-print(f"    of B: loads+prefix8 {raw[:, 16].mean():12.0f}")
+print(f"  inserter busy (A of next window) {raw[:, 16].mean():12.0f}   worker B work (wave 0) {raw[:, 20].mean():12.0f}  exits {raw[:, 21].mean():12.0f}  emission-to-E1 {raw[:, 22].mean():12.0f}")
 
-k2n = ["lit_hist", "huf_build(serial)", "stream_sizes", "lit_streams", "merge", "repcode+codes", "fse_tables(serial)", "fse_chain+pack", "tail"]
+k2 = np.concatenate([k2, raw[:, 17:18].astype(np.float64)], 1)
+k2n = ["lit_hist", "huf_build(serial)", "stream_sizes", "lit_streams", "merge", "repcode+codes", "fse_tables(serial)", "fse_pack", "tail", "fse_chains"]
 t2 = k2.sum(1).mean()
 print(kind, "K2 mean cycles/block", int(t2))
 for k, nm in enumerate(k2n):
     print(f"  {nm:20s} mean {k2[:, k].mean():12.0f}  share {k2[:, k].mean() / t2 * 100:5.1f}%")
+print(f"  chain rounds mean {raw[:, 18].mean():.2f} max {raw[:, 18].max()}  raw seqs mean {raw[:, 19].mean():.0f}")
+# wall clock per block (s_memrealtime, 100 MHz) and placement
+rt = np.array([h[blocks + b * WS + 13120 * 8 + 65536 + 16 + 23 * 4: blocks + b * WS + 13120 * 8 + 65536 + 16 + 28 * 4].view(np.uint32) for b in range(n)]).astype(np.int64)
+dur = (rt[:, 1] - rt[:, 0]) & 0xFFFFFFFF
+print(f"  block wall (realtime 100MHz ticks) mean {dur.mean():.0f} = {dur.mean() * 10:.0f} ns; memtime mean {rt[:, 4].mean():.0f} -> clock {rt[:, 4].mean() / (dur.mean() * 10):.2f} GHz")
+cu = (rt[:, 3] & 0xFFFFFFFF).astype(np.int64) * 1000 + ((rt[:, 2] >> 8) & 0xF) + 16 * ((rt[:, 2] >> 12) & 0x1) + 32 * ((rt[:, 2] >> 13) & 0x7)
+t0 = rt[:, 0].min(); t1 = (rt[:, 0] + dur).max()
+print(f"  span {(t1 - t0) * 10 / 1e3:.1f} us, distinct CUs {len(set(cu.tolist()))}, blocks/CU max {np.bincount(np.unique(cu, return_inverse=True)[1]).max()}")
+busy = {}
+for c, d in zip(cu.tolist(), dur.tolist()):
+    busy[c] = busy.get(c, 0) + d
+print(f"  per-CU busy fraction of span: mean {np.mean(list(busy.values())) / (t1 - t0):.3f}")
+mx = np.array([h[blocks + b * WS + 13120 * 8 + 65536 + 16 + 40 * 4: blocks + b * WS + 13120 * 8 + 65536 + 16 + 42 * 4].view(np.uint32) for b in range(n)])
+if kind:
+    print(f"  B-work max over worker waves {mx[:, 0].mean():.0f}   inserter busy max {mx[:, 1].mean():.0f}  (per block)")
