@@ -69,6 +69,8 @@ struct SerialScratch {
   u32 wcount[16];
   u16 nbPerRank[16];
   u16 valPerRank[16];
+  u32 khigh[64];   // parallel FSE spread: step index of each high (low-probability) cell
+  u8 lowsym[64];   // ... and the symbol stored there
 };
 static_assert(sizeof(SerialScratch) <= 1024, "scratch");
 
@@ -334,6 +336,86 @@ __device__ void fse_build_ctable(u16 *st, FseSym *sym, u8 *tableSymbol, const s1
   }
 }
 
+// Wave-parallel FSE_buildCTable (same tables as fse_build_ctable).  Symbols <= 63.
+// Spread: the i-th positive-count cell in symbol order goes to the i-th position of
+// (k * step) & mask, k = 0, 1, ... skipping positions above highThreshold; with
+// step odd, position u is reached at k(u) = u * step^-1 mod tableSize, so its rank is
+// k(u) minus the number of skipped (high) positions reached earlier.
+__device__ void fse_build_ctable_par(u16 *st, FseSym *sym, u8 *tableSymbol, const s16 *norm, u32 maxSV, u32 tableLog, SerialScratch *scr) {
+  u32 const lane = lane_id();
+  u32 const T = 1u << tableLog, mask = T - 1;
+  u32 const step = (T >> 1) + (T >> 3) + 3;
+  u32 inv = step;
+#pragma unroll
+  for (int it = 0; it < 5; it++) inv *= 2u - step * inv;
+  inv &= mask;
+  int const nv = lane <= maxSV ? (int)norm[lane] : 0;
+  bool const isLow = nv == -1;
+  u32 tot;
+  u32 const cum = wave_excl_scan(isLow ? 1u : (u32)max(nv, 0), tot);   // first state slot of the symbol
+  u32 const pst = wave_excl_scan(nv > 0 ? (u32)nv : 0u, tot);           // first spread rank of the symbol
+  u64 const lowm = __ballot(isLow);
+  u32 const nLow = (u32)__popcll(lowm);
+  u32 const highThreshold = T - 1 - nLow;
+  if (isLow) {
+    u32 const i = (u32)__popcll(lowm & ((1ull << lane) - 1ull));  // low symbols fill the top, in symbol order
+    scr->lowsym[i] = (u8)lane;
+    scr->khigh[i] = ((T - 1 - i) * inv) & mask;
+  }
+  wave_sync();
+  u32 *pstart = scr->base;   // base[32] + curr[32] = 64 entries
+  pstart[lane] = lane <= maxSV ? pst : 0xFFFFFFFFu;
+  wave_sync();
+  for (u32 u = lane; u < T; u += 64) {
+    u32 sy;
+    if (u > highThreshold) {
+      sy = scr->lowsym[T - 1 - u];
+    } else {
+      u32 const k = (u * inv) & mask;
+      u32 before = 0;
+      for (u32 i = 0; i < nLow; i++) before += scr->khigh[i] < k ? 1u : 0u;
+      u32 const rank = k - before;
+      // last symbol whose first rank <= rank (symbols with no positive cells share a
+      // start with their successor and are skipped by the <=)
+      u32 lo = 0, hi = maxSV;
+      while (lo < hi) {
+        u32 const mid = (lo + hi + 1) >> 1;
+        if (pstart[mid] <= rank) lo = mid; else hi = mid - 1;
+      }
+      sy = lo;
+    }
+    tableSymbol[u] = (u8)sy;
+  }
+  wave_sync();
+  // state table: st[cum[s] + j] = T + (j-th smallest position holding s)
+  u32 run = 0;  // lane s: positions of symbol s placed so far
+  for (u32 u0 = 0; u0 < T; u0 += 64) {
+    u32 const u = u0 + lane;
+    u32 const sy = u < T ? tableSymbol[u] : 0xFFu;
+    u64 pend = __ballot(u < T);
+    while (pend) {
+      u32 const s0 = __builtin_amdgcn_readlane(sy, (u32)__builtin_ctzll(pend));
+      u64 const m = __ballot(sy == s0) & pend;
+      u32 const b0 = __builtin_amdgcn_readlane(run, s0) + __builtin_amdgcn_readlane(cum, s0);
+      if ((m >> lane) & 1ull) st[b0 + (u32)__popcll(m & ((1ull << lane) - 1ull))] = (u16)(T + u);
+      run += lane == s0 ? (u32)__popcll(m) : 0u;
+      pend &= ~m;
+    }
+  }
+  // symbol transforms
+  if (lane <= maxSV) {
+    if (nv == 0) { sym[lane].dNb = ((tableLog + 1) << 16) - T; sym[lane].dFS = 0; }
+    else if (nv == -1 || nv == 1) { sym[lane].dNb = (tableLog << 16) - T; sym[lane].dFS = (s32)cum - 1; }
+    else {
+      u32 const maxBitsOut = tableLog - highbit32((u32)nv - 1);
+      u32 const minStatePlus = (u32)nv << maxBitsOut;
+      sym[lane].dNb = (maxBitsOut << 16) - minStatePlus;
+      sym[lane].dFS = (s32)cum - nv;
+    }
+  }
+  wave_sync();
+}
+
 __device__ __forceinline__ u32 fse_init_state(const u16 *st, const FseSym *sym, u32 s) {
   FseSym const tt = sym[s];
   u32 const nbBitsOut = (tt.dNb + (1u << 15)) >> 16;
@@ -463,6 +545,165 @@ __device__ u32 huf_build_ctable(HufNode *huffNode0, u16 *hval, u8 *hnb, const u3
   }
   for (u32 n = 0; n <= maxSV; n++) hnb[huffNode[n].byte] = huffNode[n].nbBits;
   for (u32 n = 0; n <= maxSV; n++) hval[n] = valPerRank[hnb[n]]++;
+  return maxNbBits;
+}
+
+// --- wave-parallel HUF_buildCTable (same result as huf_build_ctable above) ---
+// element e of a 256-key array lives in lane e/4, slot e%4
+__device__ __forceinline__ void bitonic_sort_desc_256(u32 (&key)[4]) {
+  u32 const lane = lane_id();
+#pragma unroll
+  for (u32 size = 2; size <= 256; size <<= 1) {
+#pragma unroll
+    for (u32 d = size >> 1; d > 0; d >>= 1) {
+      u32 part[4];
+#pragma unroll
+      for (u32 k = 0; k < 4; k++) part[k] = d >= 4 ? (u32)__shfl_xor((int)key[k], (int)(d >> 2), 64) : key[k ^ d];
+#pragma unroll
+      for (u32 k = 0; k < 4; k++) {
+        u32 const e = 4 * lane + k;
+        bool const desc = (e & size) == 0;
+        bool const lo = (e & d) == 0;  // e is the lower index of its pair
+        u32 const mx = max(key[k], part[k]), mn = min(key[k], part[k]);
+        key[k] = (desc == lo) ? mx : mn;
+      }
+    }
+  }
+}
+
+// value of slot i (0..255) of a 4-register lane-major array (i = 64 r + lane), wave-uniform i
+__device__ __forceinline__ u32 wave_get(const u32 (&a)[4], u32 i) {
+  u32 const l = i & 63u, r = i >> 6;
+  u32 const v0 = __builtin_amdgcn_readlane(a[0], l), v1 = __builtin_amdgcn_readlane(a[1], l);
+  u32 const v2 = __builtin_amdgcn_readlane(a[2], l), v3 = __builtin_amdgcn_readlane(a[3], l);
+  return r == 0 ? v0 : r == 1 ? v1 : r == 2 ? v2 : v3;
+}
+__device__ __forceinline__ void wave_set(u32 (&a)[4], u32 i, u32 v) {
+  u32 const l = i & 63u, r = i >> 6;
+  bool const me = lane_id() == l;
+#pragma unroll
+  for (u32 k = 0; k < 4; k++) a[k] = (me && r == k) ? v : a[k];
+}
+
+__device__ u32 huf_build_ctable_par(HufNode *huffNode0, u16 *hval, u8 *hnb, const u32 *count, u32 maxSV, u32 maxNbBits, SerialScratch *scr) {
+  u32 const lane = lane_id();
+  HufNode *const huffNode = huffNode0 + 1;
+  u32 const STARTNODE = 256;
+  for (u32 i = lane; i < 2 * 256 + 2; i += 64) { huffNode0[i].count = 0; huffNode0[i].parent = 0; huffNode0[i].byte = 0; huffNode0[i].nbBits = 0; }
+  // HUF_sort order = count descending, symbol ascending among equal counts
+  u32 key[4];
+#pragma unroll
+  for (u32 k = 0; k < 4; k++) {
+    u32 const sym = 4 * lane + k;
+    key[k] = sym <= maxSV ? (count[sym] << 8) | (255u - sym) : 0u;
+  }
+  bitonic_sort_desc_256(key);
+  wave_sync();
+  u32 nz = 0;
+#pragma unroll
+  for (u32 k = 0; k < 4; k++) {
+    u32 const e = 4 * lane + k;
+    if (e <= maxSV) { huffNode[e].count = key[k] >> 8; huffNode[e].byte = (u8)(255u - (key[k] & 255u)); }
+    nz += (e <= maxSV && (key[k] >> 8) != 0) ? 1u : 0u;
+  }
+  int const nonNullRank = (int)wave_sum(nz) - 1;
+  wave_sync();
+  // two-queue merge with the counts in registers (leaf i / internal node m at lane i%64, reg i/64)
+  u32 L[4], I[4] = {0, 0, 0, 0};
+#pragma unroll
+  for (u32 r = 0; r < 4; r++) L[r] = huffNode[64 * r + lane].count;
+  int lowS = nonNullRank;
+  u32 const nodeRoot = STARTNODE + (u32)nonNullRank - 1;
+  u32 nodeNb = STARTNODE, lowN = STARTNODE;
+  {
+    u32 const c = wave_get(L, (u32)lowS) + wave_get(L, (u32)lowS - 1);
+    wave_set(I, 0, c);
+    if (lane == 0) { huffNode[lowS].parent = (u16)nodeNb; huffNode[lowS - 1].parent = (u16)nodeNb; }
+    nodeNb++;
+    lowS -= 2;
+  }
+  while (nodeNb <= nodeRoot) {
+    u32 n1, n2, c1, c2;
+    {
+      u32 const cs = lowS >= 0 ? wave_get(L, (u32)lowS) : (1u << 31);
+      u32 const cn = lowN < nodeNb ? wave_get(I, lowN - STARTNODE) : (1u << 30);
+      if (cs < cn) { n1 = (u32)lowS; c1 = cs; lowS--; } else { n1 = lowN; c1 = cn; lowN++; }
+    }
+    {
+      u32 const cs = lowS >= 0 ? wave_get(L, (u32)lowS) : (1u << 31);
+      u32 const cn = lowN < nodeNb ? wave_get(I, lowN - STARTNODE) : (1u << 30);
+      if (cs < cn) { n2 = (u32)lowS; c2 = cs; lowS--; } else { n2 = lowN; c2 = cn; lowN++; }
+    }
+    wave_set(I, nodeNb - STARTNODE, c1 + c2);
+    if (lane == 0) { huffNode[n1].parent = (u16)nodeNb; huffNode[n2].parent = (u16)nodeNb; }
+    nodeNb++;
+  }
+  wave_sync();
+  // depths by pointer doubling over leaves 0..nonNull and internal nodes 256..root:
+  // jump = parent (root: itself), dist = 1 (root: 0); nbBits of a leaf = its depth
+  u32 const nLeaf = (u32)nonNullRank + 1, nInt = (u32)nonNullRank;
+  for (u32 x = lane; x < nLeaf + nInt; x += 64) {
+    u32 const nd = x < nLeaf ? x : STARTNODE + (x - nLeaf);
+    huffNode[nd].nbBits = nd == nodeRoot ? 0 : 1;
+    if (nd == nodeRoot) huffNode[nd].parent = (u16)nodeRoot;
+  }
+  wave_sync();
+  for (u32 round = 0; (1u << round) < nLeaf; round++) {
+    u32 jd[8], jj[8];
+#pragma unroll
+    for (u32 k = 0; k < 8; k++) {
+      u32 const x = lane + 64 * k;
+      jd[k] = 0; jj[k] = 0;
+      if (x < nLeaf + nInt) {
+        u32 const nd = x < nLeaf ? x : STARTNODE + (x - nLeaf);
+        u32 const j = huffNode[nd].parent;
+        jd[k] = huffNode[j].nbBits;
+        jj[k] = huffNode[j].parent;
+      }
+    }
+    wave_sync();
+#pragma unroll
+    for (u32 k = 0; k < 8; k++) {
+      u32 const x = lane + 64 * k;
+      if (x < nLeaf + nInt) {
+        u32 const nd = x < nLeaf ? x : STARTNODE + (x - nLeaf);
+        huffNode[nd].nbBits = (u8)(huffNode[nd].nbBits + jd[k]);
+        huffNode[nd].parent = (u16)jj[k];
+      }
+    }
+    wave_sync();
+  }
+  if (lane == 0) maxNbBits = huf_set_max_height(huffNode, (u32)nonNullRank, maxNbBits, scr);
+  maxNbBits = __builtin_amdgcn_readfirstlane(maxNbBits);
+  if (maxNbBits > 12) return 0;
+  // nbPerRank / valPerRank, then codes in symbol order within each rank
+  u16 *nbPerRank = scr->nbPerRank, *valPerRank = scr->valPerRank;
+  if (lane < 16) { nbPerRank[lane] = 0; valPerRank[lane] = 0; }
+  for (u32 i = lane; i < 256; i += 64) hnb[i] = 0;
+  wave_sync();
+  for (u32 nn = lane; nn <= maxSV; nn += 64) hnb[huffNode[nn].byte] = huffNode[nn].nbBits;
+  wave_sync();
+  if (lane == 0) {
+    for (int nn = 0; nn <= nonNullRank; nn++) nbPerRank[huffNode[nn].nbBits]++;
+    u16 mn = 0;
+    for (int r = (int)maxNbBits; r > 0; r--) { valPerRank[r] = mn; mn += nbPerRank[r]; mn >>= 1; }
+  }
+  wave_sync();
+  u32 base = lane < 16 ? valPerRank[lane] : 0u;  // lane r holds the next code of rank r
+  for (u32 n0 = 0; n0 <= maxSV; n0 += 64) {
+    u32 const nn = n0 + lane;
+    u32 const v = nn <= maxSV ? hnb[nn] : 255u;
+    u32 code = 0;
+    for (u32 r = 0; r <= maxNbBits; r++) {
+      u64 const m = __ballot(v == r);
+      if (!m) continue;
+      u32 const b0 = __builtin_amdgcn_readlane(base, r);
+      if (v == r) code = b0 + (u32)__popcll(m & ((1ull << lane) - 1ull));
+      base += lane == r ? (u32)__popcll(m) : 0u;
+    }
+    if (nn <= maxSV) hval[nn] = (u16)code;
+  }
+  wave_sync();
   return maxNbBits;
 }
 
@@ -647,10 +888,10 @@ extern "C" __global__ __launch_bounds__(K2_THREADS) void zh_entropy_kernel(const
         else if (largest <= (nl >> 7) + 4) cLit = 0;
         else {
           ZH_STAMP(0);  // literal histogram
+          u32 hl = fse_optimal_table_log(11, nl, maxSV, 1);
+          hl = huf_build_ctable_par(nodes, hval, hnb, hist, maxSV, hl, scr);
+          ZH_STAMP(11);  // Huffman tree (parallel part)
           if (lane == 0) {
-            for (u32 i = 0; i < 256; i++) hnb[i] = 0;
-            u32 hl = fse_optimal_table_log(11, nl, maxSV, 1);
-            hl = huf_build_ctable(nodes, hval, hnb, hist, maxSV, hl, scr);
             u32 h = hl ? huf_write_ctable(hbuf, wts, hnb, maxSV, hl, stLL, symLL, tsym, norm, scr) : 0;
             misc[0] = hl;
             misc[1] = h;
@@ -852,52 +1093,64 @@ extern "C" __global__ __launch_bounds__(K2_THREADS) void zh_entropy_kernel(const
       u32 const seqHead = op;
       op += 1;
       u64 const rec0 = seq[0], recL = seq[nbSeq - 1];
-      if (lane == 0) {
+      {
         u32 *first_code = scr->wcount, *last_code = scr->wcount + 4, *types = scr->wcount + 8, *logs = scr->wcount + 12;
-        first_code[0] = ll_code((u32)(rec0 & 0x1FFFFu)); first_code[1] = highbit32((u32)(rec0 >> 34)); first_code[2] = ml_code((u32)((rec0 >> 17) & 0x1FFFFu));
-        last_code[0] = ll_code((u32)(recL & 0x1FFFFu)); last_code[1] = highbit32((u32)(recL >> 34)); last_code[2] = ml_code((u32)((recL >> 17) & 0x1FFFFu));
-        u32 hpos = 0;
+        if (lane == 0) {
+          first_code[0] = ll_code((u32)(rec0 & 0x1FFFFu)); first_code[1] = highbit32((u32)(rec0 >> 34)); first_code[2] = ml_code((u32)((rec0 >> 17) & 0x1FFFFu));
+          last_code[0] = ll_code((u32)(recL & 0x1FFFFu)); last_code[1] = highbit32((u32)(recL >> 34)); last_code[2] = ml_code((u32)((recL >> 17) & 0x1FFFFu));
+          misc[0] = 0;
+        }
         for (int t = 0; t < 3; t++) {
-          u32 *cnt = hist + 64 * t;
-          u32 const maxSym = t == 0 ? 35 : t == 1 ? 31 : 52;
-          u32 const fseLog = t == 1 ? 8 : 9, defLog = t == 1 ? 5 : 6, defMax = t == 0 ? 35 : t == 1 ? 28 : 52;
-          const s16 *defNorm = t == 0 ? c_LL_def : t == 1 ? c_OF_def : c_ML_def;
           u16 *st = t == 0 ? stLL : t == 1 ? stOF : stML;
           FseSym *sy = t == 0 ? symLL : t == 1 ? symOF : symML;
-          u32 mx = maxSym;
-          while (mx && !cnt[mx]) mx--;
-          u32 mostFrequent = 0;
-          for (u32 s = 0; s <= mx; s++) mostFrequent = max(mostFrequent, cnt[s]);
-          bool const defAllowed = (t == 1) ? (mx <= 28) : true;
-          u32 type;
-          if (mostFrequent == nbSeq) type = (defAllowed && nbSeq <= 2) ? 0 : 1;
-          else if (defAllowed && ((nbSeq < (1u << defLog)) || (mostFrequent < (nbSeq >> (defLog - 1))))) type = 0;
-          else type = 2;
-          if (type == 1) {
-            st[0] = 0; st[1] = 0;
-            u32 const c = first_code[t];
-            sy[c].dNb = 0; sy[c].dFS = 0;
-            hbuf[hpos++] = (u8)c;
-            logs[t] = 0;
-          } else if (type == 0) {
-            for (u32 s = 0; s <= defMax; s++) norm[s] = defNorm[s];
-            fse_build_ctable(st, sy, tsym, norm, defMax, defLog, scr);
-            logs[t] = defLog;
-          } else {
-            u32 nb1 = nbSeq;
-            u32 const tl = fse_optimal_table_log(fseLog, nbSeq, mx, 2);
-            if (cnt[last_code[t]] > 1) { cnt[last_code[t]]--; nb1--; }
-            fse_normalize(norm, tl, cnt, nb1, mx, nb1 >= 2048);
-            u32 h = fse_write_ncount(hbuf + hpos, norm, mx, tl);
-            hpos += h;
-            fse_build_ctable(st, sy, tsym, norm, mx, tl, scr);
-            logs[t] = tl;
+          if (lane == 0) {  // ZSTD_selectEncodingType (dfast) + normalisation + NCount header
+            u32 hpos = misc[0];
+            u32 *cnt = hist + 64 * t;
+            u32 const maxSym = t == 0 ? 35 : t == 1 ? 31 : 52;
+            u32 const fseLog = t == 1 ? 8 : 9, defLog = t == 1 ? 5 : 6, defMax = t == 0 ? 35 : t == 1 ? 28 : 52;
+            const s16 *defNorm = t == 0 ? c_LL_def : t == 1 ? c_OF_def : c_ML_def;
+            u32 mx = maxSym;
+            while (mx && !cnt[mx]) mx--;
+            u32 mostFrequent = 0;
+            for (u32 s = 0; s <= mx; s++) mostFrequent = max(mostFrequent, cnt[s]);
+            bool const defAllowed = (t == 1) ? (mx <= 28) : true;
+            u32 type;
+            if (mostFrequent == nbSeq) type = (defAllowed && nbSeq <= 2) ? 0 : 1;
+            else if (defAllowed && ((nbSeq < (1u << defLog)) || (mostFrequent < (nbSeq >> (defLog - 1))))) type = 0;
+            else type = 2;
+            u32 bmax = 0, blog = 0;
+            if (type == 1) {
+              st[0] = 0; st[1] = 0;
+              u32 const c = first_code[t];
+              sy[c].dNb = 0; sy[c].dFS = 0;
+              hbuf[hpos++] = (u8)c;
+              logs[t] = 0;
+            } else if (type == 0) {
+              for (u32 s = 0; s <= defMax; s++) norm[s] = defNorm[s];
+              bmax = defMax; blog = defLog;
+              logs[t] = defLog;
+            } else {
+              u32 nb1 = nbSeq;
+              u32 const tl = fse_optimal_table_log(fseLog, nbSeq, mx, 2);
+              if (cnt[last_code[t]] > 1) { cnt[last_code[t]]--; nb1--; }
+              fse_normalize(norm, tl, cnt, nb1, mx, nb1 >= 2048);
+              u32 h = fse_write_ncount(hbuf + hpos, norm, mx, tl);
+              hpos += h;
+              bmax = mx; blog = tl;
+              logs[t] = tl;
+            }
+            types[t] = type;
+            misc[0] = hpos;
+            misc[20] = type; misc[21] = bmax; misc[22] = blog;
           }
-          types[t] = type;
+          wave_sync();
+          if (misc[20] != 1) fse_build_ctable_par(st, sy, tsym, norm, misc[21], misc[22], scr);
+          wave_sync();
         }
-        misc[0] = hpos;
-        misc[1] = (types[0] << 6) + (types[1] << 4) + (types[2] << 2);
-        misc[2] = logs[0]; misc[3] = logs[1]; misc[4] = logs[2];
+        if (lane == 0) {
+          misc[1] = (types[0] << 6) + (types[1] << 4) + (types[2] << 2);
+          misc[2] = logs[0]; misc[3] = logs[1]; misc[4] = logs[2];
+        }
       }
       wave_sync();
       u32 const hpos = misc[0];
@@ -919,8 +1172,7 @@ extern "C" __global__ __launch_bounds__(K2_THREADS) void zh_entropy_kernel(const
       u32 const nch = (nbSeq + C - 1) / C;
       u32 const cb = lane * C, ce = min(cb + C, nbSeq);
       bool const act = lane < nch;
-      auto codes_at = [&](u32 e, u32 &lc, u32 &oc, u32 &mc) {
-        u64 const rec = seq[nbSeq - 1 - e];
+      auto codes_of = [&](u64 rec, u32 &lc, u32 &oc, u32 &mc) {
         lc = ll_code((u32)(rec & 0x1FFFFu));
         mc = ml_code((u32)((rec >> 17) & 0x1FFFFu));
         oc = highbit32((u32)(rec >> 34));
@@ -932,11 +1184,12 @@ extern "C" __global__ __launch_bounds__(K2_THREADS) void zh_entropy_kernel(const
         sM_ = stML[(sM_ >> bM) + tM.dFS];
         sL_ = stLL[(sL_ >> bL) + tL.dFS];
       };
+      constexpr u32 CB = 8;  // records fetched per batch (one global latency per CB steps)
       u32 gL = 0, gO = 0, gM = 0;  // state at the start of the own chunk
       if (act) {
-        u32 lc, oc, mc;
         if (lane == 0) {
-          codes_at(0, lc, oc, mc);
+          u32 lc, oc, mc;
+          codes_of(seq[nbSeq - 1], lc, oc, mc);
           FseSym const tO = symOF[oc], tM = symML[mc], tL = symLL[lc];
           u32 nb = (tM.dNb + (1u << 15)) >> 16;
           gM = stML[(((nb << 16) - tM.dNb) >> nb) + tM.dFS];
@@ -946,7 +1199,15 @@ extern "C" __global__ __launch_bounds__(K2_THREADS) void zh_entropy_kernel(const
           gL = stLL[(((nb << 16) - tL.dNb) >> nb) + tL.dFS];
         } else {
           gL = 1u << logLL; gO = 1u << logOF; gM = 1u << logML;  // any valid state
-          for (u32 e = cb - C; e < cb; e++) { codes_at(e, lc, oc, mc); step(gL, gO, gM, lc, oc, mc); }
+          for (u32 e0 = cb - C; e0 < cb; e0 += CB) {
+            u64 rec[CB];
+#pragma unroll
+            for (u32 k = 0; k < CB; k++) rec[k] = e0 + k < cb ? seq[nbSeq - 1 - (e0 + k)] : 0ull;
+#pragma unroll
+            for (u32 k = 0; k < CB; k++) {
+              if (e0 + k < cb) { u32 lc, oc, mc; codes_of(rec[k], lc, oc, mc); step(gL, gO, gM, lc, oc, mc); }
+            }
+          }
         }
       }
       u32 fL = 0, fO = 0, fM = 0;  // state after the own chunk
@@ -954,11 +1215,20 @@ extern "C" __global__ __launch_bounds__(K2_THREADS) void zh_entropy_kernel(const
       for (;;) {
         if (redo) {
           u32 sL_ = gL, sO_ = gO, sM_ = gM;
-          for (u32 e = max(cb, 1u); e < ce; e++) {
-            u32 lc, oc, mc;
-            codes_at(e, lc, oc, mc);
-            stw[e] = sL_ | (sO_ << 10) | (sM_ << 20);
-            step(sL_, sO_, sM_, lc, oc, mc);
+          for (u32 e0 = max(cb, 1u); e0 < ce; e0 += CB) {
+            u64 rec[CB];
+#pragma unroll
+            for (u32 k = 0; k < CB; k++) rec[k] = e0 + k < ce ? seq[nbSeq - 1 - (e0 + k)] : 0ull;
+#pragma unroll
+            for (u32 k = 0; k < CB; k++) {
+              u32 const e = e0 + k;
+              if (e < ce) {
+                u32 lc, oc, mc;
+                codes_of(rec[k], lc, oc, mc);
+                stw[e] = sL_ | (sO_ << 10) | (sM_ << 20);
+                step(sL_, sO_, sM_, lc, oc, mc);
+              }
+            }
           }
           fL = sL_; fO = sO_; fM = sM_;
         }
@@ -1024,7 +1294,7 @@ extern "C" __global__ __launch_bounds__(K2_THREADS) void zh_entropy_kernel(const
   }
   ZH_STAMP(8);  // tail (raw copy etc.)
 #ifdef ZH_STAMPS
-  if (lane == 0) { u32 *dbg = ws.dbg(b); for (int k = 0; k < 9; k++) dbg[6 + k] = st[k]; dbg[17] = st[9]; dbg[18] = st[10]; dbg[19] = nseq_raw; }
+  if (lane == 0) { u32 *dbg = ws.dbg(b); for (int k = 0; k < 9; k++) dbg[6 + k] = st[k]; dbg[17] = st[9]; dbg[18] = st[10]; dbg[19] = nseq_raw; dbg[42] = st[11]; }
 #endif
   if (lane == 0) {
     if (d.flags & ZH_F_DIRECT) {
