@@ -1160,104 +1160,55 @@ extern "C" __global__ __launch_bounds__(K2_THREADS) void zh_entropy_kernel(const
       u32 const logLL = misc[2], logOF = misc[3], logML = misc[4];
       ZH_STAMP(6);  // FSE tables (serial)
 
-      // pass C1: the three FSE state chains, lane-parallel by speculation.  Encode step e
-      // (e = 0 .. nbSeq-1, sequence nbSeq-1-e) is split into chunks of C steps, one per
-      // lane.  Lane c first runs the C steps of chunk c-1 from an arbitrary state (tANS
-      // states synchronise quickly), then its own chunk from that guess, storing the
-      // state word before every step.  A lane whose guess differs from its predecessor's
-      // true end state re-runs its chunk from the right one until nothing changes, so the
-      // stored states equal the serial chain's exactly.
-      u32 *stw = (u32 *)ws.lits(b);  // literals are consumed; one u32 of states per step
-      u32 const C = max((nbSeq + 63) >> 6, 16u);
-      u32 const nch = (nbSeq + C - 1) / C;
-      u32 const cb = lane * C, ce = min(cb + C, nbSeq);
-      bool const act = lane < nch;
-      auto codes_of = [&](u64 rec, u32 &lc, u32 &oc, u32 &mc) {
-        lc = ll_code((u32)(rec & 0x1FFFFu));
-        mc = ml_code((u32)((rec >> 17) & 0x1FFFFu));
-        oc = highbit32((u32)(rec >> 34));
-      };
-      auto step = [&](u32 &sL_, u32 &sO_, u32 &sM_, u32 lc, u32 oc, u32 mc) {
-        FseSym const tO = symOF[oc], tM = symML[mc], tL = symLL[lc];
-        u32 const bO = (sO_ + tO.dNb) >> 16, bM = (sM_ + tM.dNb) >> 16, bL = (sL_ + tL.dNb) >> 16;
-        sO_ = stOF[(sO_ >> bO) + tO.dFS];
-        sM_ = stML[(sM_ >> bM) + tM.dFS];
-        sL_ = stLL[(sL_ >> bL) + tL.dFS];
-      };
-      constexpr u32 CB = 8;  // records fetched per batch (one global latency per CB steps)
-      u32 gL = 0, gO = 0, gM = 0;  // state at the start of the own chunk
-      if (act) {
-        if (lane == 0) {
-          u32 lc, oc, mc;
-          codes_of(seq[nbSeq - 1], lc, oc, mc);
-          FseSym const tO = symOF[oc], tM = symML[mc], tL = symLL[lc];
-          u32 nb = (tM.dNb + (1u << 15)) >> 16;
-          gM = stML[(((nb << 16) - tM.dNb) >> nb) + tM.dFS];
-          nb = (tO.dNb + (1u << 15)) >> 16;
-          gO = stOF[(((nb << 16) - tO.dNb) >> nb) + tO.dFS];
-          nb = (tL.dNb + (1u << 15)) >> 16;
-          gL = stLL[(((nb << 16) - tL.dNb) >> nb) + tL.dFS];
-        } else {
-          gL = 1u << logLL; gO = 1u << logOF; gM = 1u << logML;  // any valid state
-          for (u32 e0 = cb - C; e0 < cb; e0 += CB) {
-            u64 rec[CB];
-#pragma unroll
-            for (u32 k = 0; k < CB; k++) rec[k] = e0 + k < cb ? seq[nbSeq - 1 - (e0 + k)] : 0ull;
-#pragma unroll
-            for (u32 k = 0; k < CB; k++) {
-              if (e0 + k < cb) { u32 lc, oc, mc; codes_of(rec[k], lc, oc, mc); step(gL, gO, gM, lc, oc, mc); }
-            }
-          }
-        }
-      }
-      u32 fL = 0, fO = 0, fM = 0;  // state after the own chunk
-      bool redo = act;
-      for (;;) {
-        if (redo) {
-          u32 sL_ = gL, sO_ = gO, sM_ = gM;
-          for (u32 e0 = max(cb, 1u); e0 < ce; e0 += CB) {
-            u64 rec[CB];
-#pragma unroll
-            for (u32 k = 0; k < CB; k++) rec[k] = e0 + k < ce ? seq[nbSeq - 1 - (e0 + k)] : 0ull;
-#pragma unroll
-            for (u32 k = 0; k < CB; k++) {
-              u32 const e = e0 + k;
-              if (e < ce) {
-                u32 lc, oc, mc;
-                codes_of(rec[k], lc, oc, mc);
-                stw[e] = sL_ | (sO_ << 10) | (sM_ << 20);
-                step(sL_, sO_, sM_, lc, oc, mc);
-              }
-            }
-          }
-          fL = sL_; fO = sO_; fM = sM_;
-        }
-        u32 const pL = __shfl_up(fL, 1, 64), pO = __shfl_up(fO, 1, 64), pM = __shfl_up(fM, 1, 64);
-        redo = act && lane > 0 && (pL != gL || pO != gO || pM != gM);
-        if (redo) { gL = pL; gO = pO; gM = pM; }
-#ifdef ZH_STAMPS
-        st[10]++;
-#endif
-        if (!__ballot(redo)) break;
-      }
-      u32 const sLL = __shfl(fL, nch - 1, 64), sOF = __shfl(fO, nch - 1, 64), sML = __shfl(fM, nch - 1, 64);
-      __threadfence_block();
-      wave_sync();
-
-      ZH_STAMP(9);  // FSE chains
-      // pass C2: bit packing, lane-parallel over encode steps
+      // pass C: FSE state chains + bit packing, 64 encode steps (sequence nbSeq-1-e)
+      // per chunk.  All lanes stage the chunk's codes in LDS; lanes 0, 1, 2 advance the
+      // LL / OF / ML state through it (the chain is serial by format: one LDS round trip
+      // per step, the three tables side by side); then all lanes pack the chunk's bits.
+      u32 *ccd = (u32 *)(smem + OFF_TSYM);          // 64 x (llc | ofc << 8 | mlc << 16)
+      u16 *cst = (u16 *)(smem + OFF_TSYM + 256);    // 64 x 3 states before each step
+      const u16 *stT = lane == 0 ? stLL : lane == 1 ? stOF : stML;
+      const FseSym *syT = lane == 0 ? symLL : lane == 1 ? symOF : symML;
+      u32 const csh = lane == 0 ? 0u : lane == 1 ? 8u : 16u;
+      u32 sreg = 0;
       BitSink bs{op, 0};
       for (u32 e0 = 0; e0 < nbSeq; e0 += 64) {
         u32 const e = e0 + lane;
         bool const valid = e < nbSeq;
-        u32 const i = nbSeq - 1 - e;
-        u64 const rec = valid ? seq[i] : 0;
+        u64 const rec = valid ? seq[nbSeq - 1 - e] : 0;
         u32 const ll = (u32)(rec & 0x1FFFFu), mlb = (u32)((rec >> 17) & 0x1FFFFu), ob = (u32)(rec >> 34);
         u32 const llc = valid ? ll_code(ll) : 0, mlc = valid ? ml_code(mlb) : 0, ofc = valid ? highbit32(ob) : 0;
+        ccd[lane] = llc | (ofc << 8) | (mlc << 16);
+        wave_sync();
+        if (lane < 3) {
+          u32 const cnt = min(64u, nbSeq - e0);
+          u32 k0 = 0;
+          if (e0 == 0) {  // FSE_initCState2 with the last sequence's symbol
+            FseSym const tr = syT[(ccd[0] >> csh) & 255u];
+            u32 const nb = (tr.dNb + (1u << 15)) >> 16;
+            sreg = stT[(((nb << 16) - tr.dNb) >> nb) + tr.dFS];
+            k0 = 1;
+          }
+          for (u32 k8 = k0; k8 < cnt; k8 += 8) {
+            FseSym tr[8];
+#pragma unroll
+            for (u32 k = 0; k < 8; k++) tr[k] = syT[(ccd[min(k8 + k, 63u)] >> csh) & 255u];
+            u32 sv[8];
+#pragma unroll
+            for (u32 k = 0; k < 8; k++) {
+              sv[k] = sreg;
+              if (k8 + k < cnt) {
+                u32 const nb = (sreg + tr[k].dNb) >> 16;
+                sreg = stT[(sreg >> nb) + tr[k].dFS];
+              }
+            }
+#pragma unroll
+            for (u32 k = 0; k < 8; k++) if (k8 + k < cnt) cst[3 * (k8 + k) + lane] = (u16)sv[k];
+          }
+        }
+        wave_sync();
         u32 vOF = 0, nOF = 0, vML = 0, nML = 0, vLL = 0, nLL = 0;
         if (valid && e > 0) {
-          u32 const w = stw[e];
-          u32 const s_L = w & 1023u, s_O = (w >> 10) & 1023u, s_M = w >> 20;
+          u32 const s_L = cst[3 * lane], s_O = cst[3 * lane + 1], s_M = cst[3 * lane + 2];
           nOF = (s_O + symOF[ofc].dNb) >> 16; vOF = s_O;
           nML = (s_M + symML[mlc].dNb) >> 16; vML = s_M;
           nLL = (s_L + symLL[llc].dNb) >> 16; vLL = s_L;
@@ -1266,6 +1217,8 @@ extern "C" __global__ __launch_bounds__(K2_THREADS) void zh_entropy_kernel(const
         u32 n6[6] = {nOF, nML, nLL, valid ? (u32)c_LL_bits[llc] : 0u, valid ? (u32)c_ML_bits[mlc] : 0u, ofc};
         sink_append<6>(bs, o, sw, v6, n6);
       }
+      u32 const sLL = __builtin_amdgcn_readlane(sreg, 0), sOF = __builtin_amdgcn_readlane(sreg, 1), sML = __builtin_amdgcn_readlane(sreg, 2);
+      ZH_STAMP(9);  // FSE chains + packing
       {
         u32 v3[3] = {sML, sOF, sLL};
         u32 n3[3] = {lane == 0 ? logML : 0u, lane == 0 ? logOF : 0u, lane == 0 ? logLL : 0u};
