@@ -11,7 +11,7 @@
 //   in[]   the block, staged once with 16-B loads (64 KiB)
 //   TL/TS  2 x 2^13 u32 hash tables, entry = (position+1) << 16 | content tag
 //   cinfo  one 4096-position window: candidates -> match info (off<<8|len) in place
-//   exb    per-position exits of the 16-position parse segments
+//   exb    per-position exits of the 64-position parse segments
 // Wave roles (wave specialisation, all synchronised with workgroup barriers):
 //   waves 14, 15  inserters: one wave per hash table walks the next window's
 //                 tiles of 256 positions (4 per lane).  A single wave needs no
@@ -21,20 +21,23 @@
 //                 the next window's insertion overlaps this window's lengths.
 //   waves 0..13   match lengths of the window, 5 positions per thread, with
 //                 same-offset chains resolved in registers.
-//   waves 0..3    the serial greedy/lazy-1 parse as a Jacobi fixed point over
-//                 256 segments of 16 positions, then emission.
+//   waves 0..13   the serial greedy/lazy-1 parse, lanes = positions: pointer
+//                 doubling gives every position's exit from its 64-position
+//                 segment, wave 0 finds the segment entries as a Jacobi fixed
+//                 point, binary lifting marks the visited positions, and scans of
+//                 the marks place literals and sequence records.
 #include "zh_common.h"
 
 namespace {
 
 constexpr u32 K1_THREADS = 1024;
-constexpr u32 NSEG = ZH_WINDOW / ZH_SEG;    // parse segments per window (one per parse thread)
+constexpr u32 NPSEG = ZH_WINDOW / 64;       // parse segments per window (64 positions = one wave)
 constexpr u32 INS_TID = 896;                // first inserter thread (waves 14, 15)
 constexpr u32 SB = 5;                       // positions per thread in the length phase
 constexpr u32 NB = (ZH_WINDOW + SB - 1) / SB;  // length-phase threads (thread NB takes position `we`)
 constexpr u32 TILES = ZH_WINDOW / ZH_TILE;  // 16 tiles per window
 constexpr u32 TPL = ZH_TILE / 64;           // positions per inserter lane per tile
-static_assert(NSEG == 256 && NB + 1 <= INS_TID, "thread roles");
+static_assert(NPSEG == 64 && NB + 1 <= INS_TID, "thread roles");
 static_assert(ZH_WINDOW % ZH_TILE == 0 && TPL == 4, "tiles tile windows");
 
 constexpr u32 HL_SIZE = 1u << ZH_HASH_LOG_LONG;
@@ -46,12 +49,12 @@ constexpr u32 OFF_CI = OFF_TS + 4 * HS_SIZE;
 constexpr u32 CI_WORDS = ZH_WINDOW + 8;  // + the lookahead slot of position `we`
 __device__ __forceinline__ u32 cidx(u32 i) { return i; }
 constexpr u32 OFF_EXB = OFF_CI + 4 * CI_WORDS;      // u8 per position: its parse segment exit (relative)
-constexpr u32 OFF_SEG = OFF_EXB + ZH_WINDOW;
+constexpr u32 OFF_SEG = OFF_EXB + ZH_WINDOW;        // parse segment entries + the window exit
 constexpr u32 NWW = INS_TID / 64;                   // worker waves
 constexpr u32 PR = (ZH_WINDOW + INS_TID - 1) / INS_TID;  // lane-per-position rounds over a window
 constexpr u32 WP_OFF = 80, WP_TOT = 160;
 static_assert(PR * NWW <= WP_OFF, "emission scan slots");
-constexpr u32 OFF_WP = OFF_SEG + 4 * 2 * NSEG;      // emission scan: wave counts, offsets, total
+constexpr u32 OFF_WP = OFF_SEG + 4 * (NPSEG + 4);     // emission scan: wave counts, offsets, total
 constexpr u32 OFF_HB = OFF_WP + 4 * 164;            // per worker wave: 64 head-extension slots
 constexpr u32 OFF_MISC = OFF_HB + 4 * 64 * (INS_TID / 64);  // [0..3] scan partials, [4..6] barrier-or words
 constexpr u32 K1_LDS = OFF_MISC + 4 * 16;
@@ -196,49 +199,38 @@ __device__ __forceinline__ void dump_window(u8 *ci8, u32 lane_, const u32 (&creg
   if (lane == 0) *(u16 *)(ci8 + 4 * cidx(ZH_WINDOW) + (LONG ? 0 : 2)) = (u16)cwe;
 }
 
-// Lane-per-position parse step for window index i (lanes of a wave = 4 parse segments
-// of 16 positions): X[k] = position reached after 2^k parse steps from i, relative to
-// the segment start (values >= the segment length mean "left the segment").
-// Returns the match info of i if the parse takes a match there, else 0.
-__device__ __forceinline__ u32 parse_steps(const u32 *ci, u32 i, u32 wn, u32 la, u32 lane, u32 (&X)[5]) {
-  u32 const sb = i & ~15u, sl = i & 15u;
-  u32 const slen = wn > sb ? min(16u, wn - sb) : 0u;
+// Lane-per-position parse steps for window index i (a wave's 64 lanes = one parse
+// segment of 64 positions): X[k] = position reached after 2^k parse steps from i, for
+// k < 6, and X[6] = the segment exit, relative to the segment start (values >= the
+// segment length mean "left the segment").  Returns the match info of i if the parse
+// takes a match there, else 0.
+__device__ __forceinline__ u32 parse_steps(const u32 *ci, u32 i, u32 wn, u32 la, u32 lane, u32 (&X)[7]) {
+  u32 const sb = i & ~63u;
+  u32 const slen = wn > sb ? min(64u, wn - sb) : 0u;
   u32 const inf = i < wn ? ci[i] : 0u;
   u32 const inf1 = i + 1 < wn ? ci[i + 1] : la;
   u32 const l = inf & 255u;
   bool const tk = l != 0 && (inf1 & 255u) <= l;
-  u32 x = sl + (tk ? l : 1u);
+  u32 x = lane + (tk ? l : 1u);
 #pragma unroll
-  for (u32 k = 0; k < 4; k++) {
+  for (u32 k = 0; k < 6; k++) {
     X[k] = x;
-    u32 const y = __shfl(x, (lane & ~15u) + min(x, 15u), 64);
+    u32 const y = __shfl(x, min(x, 63u), 64);
     x = x < slen ? y : x;
   }
-  X[4] = x;
+  X[6] = x;
   return tk ? inf : 0u;
 }
 
-// Workgroup barrier returning the OR of `pred` over all threads, one s_barrier.
-// Three rotating LDS words: word r%3 is set before barrier r, read after it, and
-// cleared by thread 0 after barrier r+1 (its next use is round r+3).
-__device__ __forceinline__ bool barrier_or(bool pred, u32 *orw, u32 &round) {
-  u32 const r = round++;
-  if (__ballot(pred) && (threadIdx.x & 63) == 0) orw[r % 3] = 1;
-  __syncthreads();
-  bool const res = orw[r % 3] != 0;
-  if (threadIdx.x == 0) orw[(r + 2) % 3] = 0;
-  return res;
-}
-
 // Inserter wave main loop: mirrors the workers' barrier sequence window by window
-// (P, R, X, the parse's Jacobi rounds, E1, E2) and runs at raised priority, since the
+// (P, R, X, J, E1, E2) and runs at raised priority, since the
 // next window's insertion is the longest chain of the window step.
 template <bool LONG>
-__device__ __forceinline__ void inserter_loop(const u32 *in32, u32 *T, u8 *ci8, u32 *orw, u32 *misc_, u32 n, u32 lim, u32 lane, u32 *dbg) {
+__device__ __forceinline__ void inserter_loop(const u32 *in32, u32 *T, u8 *ci8, u32 *misc_, u32 n, u32 lim, u32 lane, u32 *dbg) {
   // (no priority boost: measured slower)
 
   u32 creg[TILES * TPL / 2];
-  u32 cwe = 0, bround = 0;
+  u32 cwe = 0;
   insert_window<LONG>(in32, T, 0, min((u32)ZH_WINDOW, n), lim, lane, creg, cwe);
 #ifdef ZH_STAMPS
   u32 st_ins = 0;
@@ -258,7 +250,7 @@ __device__ __forceinline__ void inserter_loop(const u32 *in32, u32 *T, u8 *ci8, 
 #endif
     __syncthreads();  // R: match info of this window in cinfo
     __syncthreads();  // X: segment exits
-    while (barrier_or(false, orw, bround)) {}  // the parse's Jacobi rounds
+    __syncthreads();  // J: segment entries
     __syncthreads();  // E1: the parse has read this window's info; cinfo is free
     __syncthreads();  // E2: emission offsets
   }
@@ -294,7 +286,6 @@ extern "C" __global__ __launch_bounds__(K1_THREADS) void zh_lz_kernel(const ZhBl
   u32 *hbuf = (u32 *)(smem + OFF_HB);
   u32 *segx = (u32 *)(smem + OFF_SEG);
   u32 *misc = (u32 *)(smem + OFF_MISC);
-  u32 *orw = misc + 4;
 
   u32 const b = blockIdx.x, tid = threadIdx.x, lane = tid & 63;
   ZhBlockDesc const d = blocks[b];
@@ -328,7 +319,6 @@ extern "C" __global__ __launch_bounds__(K1_THREADS) void zh_lz_kernel(const ZhBl
   if (tid < 16) in[n + tid] = 0;
   for (u32 i = tid; i < HL_SIZE; i += K1_THREADS) TL[i] = 0;
   for (u32 i = tid; i < HS_SIZE; i += K1_THREADS) TS[i] = 0;
-  if (tid < 3) orw[tid] = 0;
   if (tid < 2) misc[8 + tid] = 0;
   bool const rle = __syncthreads_and(same) && n >= 2;
   if (rle) {
@@ -340,12 +330,12 @@ extern "C" __global__ __launch_bounds__(K1_THREADS) void zh_lz_kernel(const ZhBl
   u64 *seq_out = ws.seq(b);
   u8 *lit_out = ws.lits(b);
   u32 const lim = n > ZH_HASH_READ ? n - ZH_HASH_READ : 0;
-  u32 nseq_tot = 0, nlit_tot = 0, e_in = 0, bround = 0;
+  u32 nseq_tot = 0, nlit_tot = 0, e_in = 0;
   // ---- inserter waves: their own loop with the same barrier sequence as the workers'
   // (separate code, so their registers never add to the workers' pressure)
   if (tid >= INS_TID) {
-    if (tid < INS_TID + 64) inserter_loop<true>(in32, TL, ci8, orw, misc, n, lim, lane, ws.dbg(b));
-    else inserter_loop<false>(in32, TS, ci8, orw, misc, n, lim, lane, ws.dbg(b));
+    if (tid < INS_TID + 64) inserter_loop<true>(in32, TL, ci8, misc, n, lim, lane, ws.dbg(b));
+    else inserter_loop<false>(in32, TS, ci8, misc, n, lim, lane, ws.dbg(b));
     return;
   }
 
@@ -485,64 +475,66 @@ extern "C" __global__ __launch_bounds__(K1_THREADS) void zh_lz_kernel(const ZhBl
 #endif
     u32 const info_ahead = ci[cidx(ZH_WINDOW)];
 
-    // ---- parse.  Lanes = positions (PR rounds of the 896 worker lanes); a wave's 64 lanes are 4 parse
-    // segments of 16.  step(p) = next position the greedy/lazy-1 parse visits after p;
-    // pointer doubling inside the segment (ds_bpermute) gives X_k = 2^k steps, and the
-    // segment exit of every position after 4 doublings.
+    // ---- parse.  Lanes = positions (PR rounds of the 896 worker lanes); each wave's 64
+    // lanes are one parse segment of 64 positions.  step(p) = next position the greedy /
+    // lazy-1 parse visits after p; pointer doubling inside the segment (ds_bpermute)
+    // gives X_k = 2^k steps for k < 6 and the segment exit of every position.
     u32 const wn = we - wsb;
     u32 const la = info_ahead;  // match info of position `we` (lazy rule at the window end)
+    u32 xk[PR][6];              // [round][k]: X_{2^k}, relative to the segment start
+    u32 infr[PR];               // match info of positions where the parse takes a match
 #pragma unroll
     for (u32 rr = 0; rr < PR; rr++) {
       u32 const i = INS_TID * rr + tid;
-      u32 X[5];
-      parse_steps(ci, i, wn, la, lane, X);
-      if (i < wn) exb[i] = (u8)X[4];
+      u32 X[7];
+      infr[rr] = parse_steps(ci, i, wn, la, lane, X);
+#pragma unroll
+      for (u32 k = 0; k < 6; k++) xk[rr][k] = X[k];
+      if (i < wn) exb[i] = (u8)X[6];
     }
     __syncthreads();  // X: exits of all positions
     ZH_STAMP(st_X);
-    // Jacobi fixed point of the segment entries (threads 0..255, one per segment;
-    // == the serial parse).  One barrier per round: round r writes exits into
-    // segx[r & 1] and reads the predecessor's exit of round r-1 from the other half.
-    bool const pt = tid < NSEG;
-    u32 const s = wsb + ZH_SEG * tid;
-    u32 const se = pt ? min(s + ZH_SEG, we) : 0u;
-    u32 entry = max(s, e_in), rfin = 0;
-    for (u32 r = 0;; r++) {
-      bool ch = r == 0;
-      if (pt && r) {
-        u32 const ne = tid == 0 ? max(s, e_in) : max(segx[((r - 1) & 1) * NSEG + tid - 1], s);
-        ch = ne != entry;
+    // Jacobi fixed point of the 64 segment entries (wave 0, lane = segment, no barrier
+    // needed): entry(t) = max(start(t), exit of segment t-1 from its entry) == the
+    // serial parse once no entry changes
+    if (tid < 64) {
+      u32 const S = wsb + 64 * lane;
+      u32 const SE = min(S + 64, we);
+      u32 entry = lane == 0 ? max(wsb, e_in) : S;
+      u32 ex = entry;
+      for (;;) {
+        ex = entry < SE ? S + exb[64 * lane + (entry - S)] : entry;
+        u32 const pe = __shfl_up(ex, 1, 64);
+        u32 const ne = lane == 0 ? max(wsb, e_in) : max(S, pe);
+        bool const ch = ne != entry;
         entry = ne;
-      }
-      if (pt) segx[(r & 1) * NSEG + tid] = (entry < se) ? s + exb[ZH_SEG * tid + (entry - s)] : entry;
 #ifdef ZH_STAMPS
-      st_rounds++;
+        st_rounds++;
 #endif
-      if (!barrier_or(ch, orw, bround)) { rfin = r; break; }
+        if (!__ballot(ch)) break;
+      }
+      segx[lane] = entry;
+      if (lane == ((wn - 1) >> 6)) segx[64] = ex;  // the window's exit = next window's entry
     }
+    __syncthreads();  // J: converged segment entries
     ZH_STAMP(st_J);
-    u32 const *segf = segx + (rfin & 1) * NSEG;  // converged exits
-    u32 const e_out = segf[NSEG - 1];
+    u32 const e_out = segx[64];
 
     // ---- emission, lanes = positions: a position is on the parse path iff binary
-    // lifting from its segment's entry (X_8, X_4, X_2, X_1) lands on it; scans of the
+    // lifting from its segment's entry (X_32 .. X_1) lands on it; scans of the
     // take/literal flags give each record's and literal's slot
     u32 fl[PR];    // bit 0 literal, bit 1 match start
-    u32 infr[PR];  // match info of the match starts
 #pragma unroll
     for (u32 rr = 0; rr < PR; rr++) {
       u32 const i = INS_TID * rr + tid;
-      u32 X[5];
-      infr[rr] = parse_steps(ci, i, wn, la, lane, X);
-      u32 const sb = i & ~15u, sl = i & 15u, t = i >> 4;
-      u32 const ent = t == 0 ? max(wsb, e_in) : max(wsb + sb, segf[min(t, NSEG) - 1]);
-      u32 cur = ent - (wsb + sb);  // >= 16 when the segment is skipped
+      u32 const sb = i & ~63u;
+      u32 cur = segx[min(i >> 6, 63u)] - (wsb + sb);  // >= 64 when the segment is skipped
 #pragma unroll
-      for (int k = 3; k >= 0; k--) {
-        u32 const y = __shfl(X[k], (lane & ~15u) + min(cur, 15u), 64);
-        if (cur <= sl && y <= sl) cur = y;
+      for (int k = 5; k >= 0; k--) {
+        u32 const y = __shfl(xk[rr][k], min(cur, 63u), 64);
+        if (cur <= lane && y <= lane) cur = y;
       }
-      bool const vis = i < wn && cur == sl;
+      bool const vis = i < wn && cur == lane;
       fl[rr] = vis ? (infr[rr] ? 2u : 1u) : 0u;
     }
     u32 lcnt[PR], scnt[PR];
