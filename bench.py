@@ -83,6 +83,20 @@ def cpu_baseline(data, threads, seconds=1.5):
                       f"of the same 64 KiB chunks, {threads} threads, {el:.2f} s wall; ratio {done_bytes / max(comp_bytes, 1):.3f}"}
 
 
+def pmc_traffic(kernel):
+    """HBM bytes per launch of `kernel` from the newest committed rocprofv3 PMC summary
+    (profiles/*_rocprof_summary.json, written by tools/prof_summary.py: 2 x FETCH_SIZE +
+    WRITE_SIZE, the gfx950 correction of the microarchitecture guide)."""
+    import glob
+
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_rocprof_summary.json")))
+    if not files:
+        return None, None
+    k = json.load(open(files[-1])).get("kernels", {}).get(kernel, {})
+    b = k.get("hbm_bytes")
+    return (int(b) if b else None), os.path.relpath(files[-1], ROOT)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -107,7 +121,9 @@ def main():
     import cuda_zstd
 
     n = args.chunks
-    host = gen_chunks(args.dataset, n, first=rank * n)
+    from cuda_zstd import shard
+
+    host = gen_chunks(args.dataset, n, first=shard.weak_range(rank, n)[0])
     d_in = torch.from_numpy(host).to(dev)
     bc = cuda_zstd.BatchedCompressor(3, CHUNK)
     slot = (bc.max_out(CHUNK) + 255) // 256 * 256
@@ -119,15 +135,13 @@ def main():
     out_sizes = torch.zeros(n, dtype=torch.int64, device=dev)
     status = torch.zeros(n, dtype=torch.int32, device=dev)
     temp = torch.empty(bc.temp_size(n, CHUNK), dtype=torch.uint8, device=dev)
-    all_sizes = torch.zeros(world * n, dtype=torch.int64, device=dev)
     stream = torch.cuda.current_stream(dev)
+    from cuda_zstd import shard
 
     def step():
         bc.compress_async(in_ptrs, in_sizes, CHUNK, out_ptrs, out_sizes, status, temp, stream)
-        if world > 1:
-            dist.all_gather_into_tensor(all_sizes, out_sizes)  # RCCL: global per-chunk sizes -> offsets
-            return torch.cumsum(all_sizes, 0)
-        return torch.cumsum(out_sizes, 0)
+        # RCCL all-gather of the per-chunk sizes -> global frame offsets (the only exchange)
+        return shard.gather_offsets(out_sizes, world)[1]
 
     for _ in range(args.warmup):
         step()
@@ -174,6 +188,7 @@ def main():
         per_launch_bytes = n * CHUNK + comp_all / world
         dom, dom_ms = ("zh_lz_kernel", k1) if k1 >= k2 else ("zh_entropy_kernel", k2)
         achieved = per_launch_bytes / (dom_ms / 1e3) / 1e9 if dom_ms > 0 else 0.0
+        traffic, traffic_src = pmc_traffic(dom) if args.dataset == "mix" and n == CHUNKS_PER_GPU else (None, None)
         line = {
             "metric": METRIC, "value": round(gbs, 3), "unit": "GB/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": round(el / args.steps * 1e3, 3), "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
@@ -183,7 +198,8 @@ def main():
                        "kernel_ms": {"zh_lz_kernel": round(k1, 3), "zh_entropy_kernel": round(k2, 3)},
                        "parallelism": f"dp{world} (chunk shards, RCCL all-gather of sizes)", "libzstd_verified": verified},
             "roofline": {"kernel": dom, "bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": None},
+                         "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
+                         "algorithmic_bytes_per_launch": int(per_launch_bytes), "traffic_source": traffic_src},
         }
         if not args.no_cpu_baseline:
             threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
