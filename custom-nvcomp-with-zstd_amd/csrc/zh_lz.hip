@@ -58,6 +58,7 @@ constexpr u32 OFF_WP = OFF_SEG + 4 * (NPSEG + 4);     // emission scan: wave cou
 constexpr u32 OFF_HB = OFF_WP + 4 * 164;            // per worker wave: 64 head-extension slots
 constexpr u32 OFF_MISC = OFF_HB + 4 * 64 * (INS_TID / 64);  // [0..3] scan partials, [4..6] barrier-or words
 constexpr u32 K1_LDS = OFF_MISC + 4 * 16;
+constexpr u32 MISC_ARR = 12;  // misc[12]: worker-wave barrier arrivals (cumulative)
 static_assert(K1_LDS <= 163840 - 256, "K1 LDS budget");
 static_assert(OFF_TL % 16 == 0 && OFF_CI % 16 == 0 && OFF_SEG % 16 == 0, "alignment");
 
@@ -133,8 +134,9 @@ __device__ __forceinline__ void hash_tag(u32 lo, u32 hi, u32 &h, u32 &tag) {
 // positions tb + l + 64k of each tile; all lookups of a tile are issued before its
 // inserts and after the previous tile's inserts (program order = LDS order within a
 // wave).  Candidates (position+1, tag-filtered, 0 = none) go to creg as u16 pairs.
-template <bool LONG>
-__device__ __forceinline__ void insert_window(const u32 *in32, u32 *T, u32 wsb, u32 we, u32 lim, u32 lane, u32 (&creg)[TILES * TPL / 2], u32 &cwe) {
+template <bool LONG, typename Hook>
+__device__ __forceinline__ void insert_window(const u32 *in32, u32 *T, u32 wsb, u32 we, u32 lim, u32 lane, u32 (&creg)[TILES * TPL / 2], u32 &cwe,
+                                              Hook &&between_tiles) {
 #pragma unroll
   for (u32 t = 0; t < TILES; t++) {
     // opaque per-tile copy of lim: keeps the compiler from hoisting every tile's
@@ -167,6 +169,7 @@ __device__ __forceinline__ void insert_window(const u32 *in32, u32 *T, u32 wsb, 
     // materialise this tile's candidates now (otherwise the compiler sinks their
     // computation to the dump and keeps every tile's temporaries alive)
     __asm__ volatile("" : "+v"(creg[2 * t]), "+v"(creg[2 * t + 1]) :: "memory");
+    between_tiles();
   }
   // the next window's first position (lazy rule at this window's end): looked up
   // after all of this window's tiles, before any of the next window's
@@ -222,42 +225,46 @@ __device__ __forceinline__ u32 parse_steps(const u32 *ci, u32 i, u32 wn, u32 la,
   return tk ? inf : 0u;
 }
 
-// Inserter wave main loop: mirrors the workers' barrier sequence window by window
-// (P, R, X, J, E1, E2) and runs at raised priority, since the
-// next window's insertion is the longest chain of the window step.
+// Inserter wave main loop.  It mirrors the workers' barrier sequence window by window
+// (P, R, X, J, E1, E2) but fills the slack: between two tiles it takes the next
+// barrier only once all 14 worker waves have arrived there (an LDS arrival counter),
+// so the next window's insertion spreads over the whole window step.
+constexpr u32 WIN_BARRIERS = 5;  // R, X, J, E1, E2
 template <bool LONG>
 __device__ __forceinline__ void inserter_loop(const u32 *in32, u32 *T, u8 *ci8, u32 *misc_, u32 n, u32 lim, u32 lane, u32 *dbg) {
-  // (no priority boost: measured slower)
-
   u32 creg[TILES * TPL / 2];
   u32 cwe = 0;
-  insert_window<LONG>(in32, T, 0, min((u32)ZH_WINDOW, n), lim, lane, creg, cwe);
+  insert_window<LONG>(in32, T, 0, min((u32)ZH_WINDOW, n), lim, lane, creg, cwe, [] {});
 #ifdef ZH_STAMPS
   u32 st_ins = 0;
 #endif
+  u32 passed = 0;  // window barriers taken so far (all windows)
   for (u32 wsb = 0; wsb < n; wsb += ZH_WINDOW) {
     u32 const we = min(wsb + ZH_WINDOW, n);
     dump_window<LONG>(ci8, lane, creg, cwe);
     __syncthreads();  // P: candidates of this window in cinfo
+    u32 const done = passed + WIN_BARRIERS;
+    auto take_ready = [&] {
+      while (passed < done && __atomic_load_n(&misc_[MISC_ARR], __ATOMIC_RELAXED) >= (INS_TID / 64) * (passed + 1)) {
+        __syncthreads();
+        passed++;
+      }
+    };
 #ifdef ZH_STAMPS
     u64 const ti0 = __builtin_amdgcn_s_memtime();
 #endif
-    if (we < n) insert_window<LONG>(in32, T, we, min(we + ZH_WINDOW, n), lim, lane, creg, cwe);
+    if (we < n) insert_window<LONG>(in32, T, we, min(we + ZH_WINDOW, n), lim, lane, creg, cwe, take_ready);
 #ifdef ZH_STAMPS
     u32 const dti = (u32)(__builtin_amdgcn_s_memtime() - ti0);
     st_ins += dti;
     if (lane == 0) atomicMax(&misc_[9], dti);
 #endif
-    __syncthreads();  // R: match info of this window in cinfo
-    __syncthreads();  // X: segment exits
-    __syncthreads();  // J: segment entries
-    __syncthreads();  // E1: the parse has read this window's info; cinfo is free
-    __syncthreads();  // E2: emission offsets
+    while (passed < done) { __syncthreads(); passed++; }
   }
 #ifdef ZH_STAMPS
   if (LONG && lane == 0) dbg[16] = st_ins;
 #endif
-  (void)dbg; (void)misc_;
+  (void)dbg;
 }
 
 }  // namespace
@@ -320,6 +327,7 @@ extern "C" __global__ __launch_bounds__(K1_THREADS) void zh_lz_kernel(const ZhBl
   for (u32 i = tid; i < HL_SIZE; i += K1_THREADS) TL[i] = 0;
   for (u32 i = tid; i < HS_SIZE; i += K1_THREADS) TS[i] = 0;
   if (tid < 2) misc[8 + tid] = 0;
+  if (tid == 0) misc[MISC_ARR] = 0;
   bool const rle = __syncthreads_and(same) && n >= 2;
   if (rle) {
     if (tid == 0) { meta[0] = 0; meta[1] = 0; meta[2] = 1; }
@@ -468,6 +476,7 @@ extern "C" __global__ __launch_bounds__(K1_THREADS) void zh_lz_kernel(const ZhBl
 #ifdef ZH_STAMPS
     if (lane == 0) atomicMax(&misc[8], (u32)(__builtin_amdgcn_s_memtime() - tP));
 #endif
+    if (lane == 0) atomicAdd(&misc[MISC_ARR], 1u);
     __syncthreads();  // R
     ZH_STAMP(st_B);
 #ifdef ZH_STAMPS
@@ -492,6 +501,7 @@ extern "C" __global__ __launch_bounds__(K1_THREADS) void zh_lz_kernel(const ZhBl
       for (u32 k = 0; k < 6; k++) xk[rr][k] = X[k];
       if (i < wn) exb[i] = (u8)X[6];
     }
+    if (lane == 0) atomicAdd(&misc[MISC_ARR], 1u);
     __syncthreads();  // X: exits of all positions
     ZH_STAMP(st_X);
     // Jacobi fixed point of the 64 segment entries (wave 0, lane = segment, no barrier
@@ -516,6 +526,7 @@ extern "C" __global__ __launch_bounds__(K1_THREADS) void zh_lz_kernel(const ZhBl
       segx[lane] = entry;
       if (lane == ((wn - 1) >> 6)) segx[64] = ex;  // the window's exit = next window's entry
     }
+    if (lane == 0) atomicAdd(&misc[MISC_ARR], 1u);
     __syncthreads();  // J: converged segment entries
     ZH_STAMP(st_J);
     u32 const e_out = segx[64];
@@ -545,6 +556,7 @@ extern "C" __global__ __launch_bounds__(K1_THREADS) void zh_lz_kernel(const ZhBl
       scnt[rr] = __builtin_amdgcn_mbcnt_hi((u32)(ms >> 32), __builtin_amdgcn_mbcnt_lo((u32)ms, 0u));
       if (lane == 0) wpart[rr * NWW + (tid >> 6)] = (u32)__popcll(ml) | ((u32)__popcll(ms) << 16);
     }
+    if (lane == 0) atomicAdd(&misc[MISC_ARR], 1u);
     __syncthreads();  // E1: per-wave counts (cinfo is free for the inserters from here on)
     ZH_STAMP(st_E1);
     if (tid < 64) {   // exclusive scan of the PR*NWW (round, wave) counts, in position order
@@ -563,6 +575,7 @@ extern "C" __global__ __launch_bounds__(K1_THREADS) void zh_lz_kernel(const ZhBl
       }
       if (tid == 0) wpart[WP_TOT] = carry;
     }
+    if (lane == 0) atomicAdd(&misc[MISC_ARR], 1u);
     __syncthreads();  // E2: offsets
 #pragma unroll
     for (u32 rr = 0; rr < PR; rr++) {
