@@ -372,10 +372,12 @@ extern "C" __global__ __launch_bounds__(K1_THREADS) void zh_lz_kernel(const ZhBl
         u32 olo, ohi;
         ld64u(in32, min(p, lim), olo, ohi);
         u32 const cL = cv[j] & 0xFFFFu, cS = cv[j] >> 16;
-        u32 const xL = prefix8(in32, cL ? cL - 1 : 0u, olo, ohi);
-        u32 const xS = prefix8(in32, cS ? cS - 1 : 0u, olo, ohi);
-        plp |= (cL ? xL : 0u) << (4 * j);
-        psp |= ((cS && cS != cL) ? xS : 0u) << (4 * j);
+        // (skipped by the whole wave when no lane has a candidate here: rare matches)
+        u32 xL = 0, xS = 0;
+        if (cL) xL = prefix8(in32, cL - 1, olo, ohi);
+        if (cS && cS != cL) xS = prefix8(in32, cS - 1, olo, ohi);
+        plp |= xL << (4 * j);
+        psp |= xS << (4 * j);
       }
 #define PL(j) ((plp >> (4 * (j))) & 15u)
 #define PS(j) ((psp >> (4 * (j))) & 15u)
