@@ -215,11 +215,19 @@ __device__ __forceinline__ u32 parse_steps(const u32 *ci, u32 i, u32 wn, u32 la,
   u32 const l = inf & 255u;
   bool const tk = l != 0 && (inf1 & 255u) <= l;
   u32 x = lane + (tk ? l : 1u);
+  if (__ballot(tk)) {
 #pragma unroll
-  for (u32 k = 0; k < 6; k++) {
-    X[k] = x;
-    u32 const y = __shfl(x, min(x, 63u), 64);
-    x = x < slen ? y : x;
+    for (u32 k = 0; k < 6; k++) {
+      X[k] = x;
+      u32 const y = __shfl(x, min(x, 63u), 64);
+      x = x < slen ? y : x;
+    }
+  } else {  // all literals in this segment: 2^k steps are 2^k positions
+#pragma unroll
+    for (u32 k = 0; k < 6; k++) {
+      X[k] = x;
+      x = x < slen ? min(x + (1u << k), slen) : x;
+    }
   }
   X[6] = x;
   return tk ? inf : 0u;
@@ -542,10 +550,14 @@ extern "C" __global__ __launch_bounds__(K1_THREADS) void zh_lz_kernel(const ZhBl
       u32 const i = INS_TID * rr + tid;
       u32 const sb = i & ~63u;
       u32 cur = segx[min(i >> 6, 63u)] - (wsb + sb);  // >= 64 when the segment is skipped
+      if (__ballot(infr[rr] != 0)) {
 #pragma unroll
-      for (int k = 5; k >= 0; k--) {
-        u32 const y = __shfl(xk[rr][k], min(cur, 63u), 64);
-        if (cur <= lane && y <= lane) cur = y;
+        for (int k = 5; k >= 0; k--) {
+          u32 const y = __shfl(xk[rr][k], min(cur, 63u), 64);
+          if (cur <= lane && y <= lane) cur = y;
+        }
+      } else {  // all literals: every position from the entry on is visited
+        cur = cur <= lane ? lane : cur;
       }
       bool const vis = i < wn && cur == lane;
       fl[rr] = vis ? (infr[rr] ? 2u : 1u) : 0u;
