@@ -171,6 +171,10 @@ bool is_device_ptr(const void *p) {
 
 Status copy_any(void *dst, const void *src, size_t n, hipStream_t stream) {
   if (!n) return Status::SUCCESS;
+  if (!is_device_ptr(dst) && !is_device_ptr(src)) {  // host to host (FORCE_CPU on host buffers): no HIP call
+    memmove(dst, src, n);
+    return Status::SUCCESS;
+  }
   if (hipMemcpyAsync(dst, src, n, hipMemcpyDefault, stream) != hipSuccess) return Status::ERROR_CUDA_ERROR;
   if (hipStreamSynchronize(stream) != hipSuccess) return Status::ERROR_CUDA_ERROR;
   return Status::SUCCESS;
