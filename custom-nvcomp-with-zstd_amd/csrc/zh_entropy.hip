@@ -17,7 +17,7 @@
 namespace {
 
 constexpr u32 K2_THREADS = 64;
-constexpr u32 SW_WORDS = 168;
+constexpr u32 SW_WORDS = 184;  // >= 512 literal codes of <= 11 bits per append (+ pending bits)
 
 // ---------------- LDS layout (bytes) ----------------
 constexpr u32 OFF_SW = 0;                          // bit sink words
@@ -953,12 +953,19 @@ extern "C" __global__ __launch_bounds__(K2_THREADS) void zh_entropy_kernel(const
         for (u32 k = 0; k < ns; k++) {
           u32 a = single ? 0 : k * seg, e = single ? nl : (k < 3 ? (k + 1) * seg : nl);
           BitSink bs{op, 0};
-          // symbols from e-1 down to a
-          for (u32 base = 0; base < e - a; base += 64) {
-            u32 const j = base + lane;
-            u32 v[1] = {0}, nb[1] = {0};
-            if (j < e - a) { u8 const c = lits[e - 1 - j]; v[0] = hval[c]; nb[0] = hnb[c]; }
-            sink_append<1>(bs, o, sw, v, nb);
+          // symbols from e-1 down to a, 8 per lane per append (codes paired into <= 22-bit fields)
+          for (u32 base = 0; base < e - a; base += 512) {
+            u32 v[4], nb[4];
+#pragma unroll
+            for (u32 f = 0; f < 4; f++) {
+              u32 const j0 = base + 8 * lane + 2 * f, j1 = j0 + 1;
+              u32 c0 = 0, n0 = 0, c1 = 0, n1 = 0;
+              if (j0 < e - a) { u8 const c = lits[e - 1 - j0]; c0 = hval[c]; n0 = hnb[c]; }
+              if (j1 < e - a) { u8 const c = lits[e - 1 - j1]; c1 = hval[c]; n1 = hnb[c]; }
+              v[f] = c0 | (c1 << n0);
+              nb[f] = n0 + n1;
+            }
+            sink_append<4>(bs, o, sw, v, nb);
           }
           sink_close(bs, o, sw);
           op = bs.pos;
