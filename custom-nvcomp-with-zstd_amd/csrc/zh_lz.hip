@@ -355,8 +355,14 @@ extern "C" __global__ __launch_bounds__(K1_THREADS) void zh_lz_kernel(const ZhBl
     return;
   }
 
+  u32 const tid_ = tid;
   for (u32 wsb = 0; wsb < n; wsb += ZH_WINDOW) {
     u32 const we = min(wsb + ZH_WINDOW, n);
+    // opaque per-window thread index: keeps the compiler from hoisting every LDS address
+    // derived from it out of the window loop (they would be spilled to scratch)
+    u32 tid;
+    __asm__ volatile("v_mov_b32 %0, %1" : "=v"(tid) : "v"(tid_));
+    u32 const lane = tid & 63;
     __syncthreads();  // P
     ZH_STAMP(st_A);
 #ifdef ZH_STAMPS
@@ -492,7 +498,7 @@ extern "C" __global__ __launch_bounds__(K1_THREADS) void zh_lz_kernel(const ZhBl
 #ifdef ZH_STAMPS
     if (tid == 0) { st_Bmax += misc[8]; st_Imax += misc[9]; misc[8] = 0; misc[9] = 0; }
 #endif
-    u32 const info_ahead = ci[cidx(ZH_WINDOW)];
+    u32 const info_ahead = __builtin_amdgcn_readfirstlane(ci[cidx(ZH_WINDOW)]);
 
     // ---- parse.  Lanes = positions (PR rounds of the 896 worker lanes); each wave's 64
     // lanes are one parse segment of 64 positions.  step(p) = next position the greedy /
@@ -539,7 +545,7 @@ extern "C" __global__ __launch_bounds__(K1_THREADS) void zh_lz_kernel(const ZhBl
     if (lane == 0) atomicAdd(&misc[MISC_ARR], 1u);
     __syncthreads();  // J: converged segment entries
     ZH_STAMP(st_J);
-    u32 const e_out = segx[64];
+    u32 const e_out = __builtin_amdgcn_readfirstlane(segx[64]);
 
     // ---- emission, lanes = positions: a position is on the parse path iff binary
     // lifting from its segment's entry (X_32 .. X_1) lands on it; scans of the
@@ -599,7 +605,7 @@ extern "C" __global__ __launch_bounds__(K1_THREADS) void zh_lz_kernel(const ZhBl
       if (fl[rr] & 1u) lit_out[nlit_tot + li] = in[wsb + i];
       if (fl[rr] & 2u) seq_out[nseq_tot + si] = (u64)(nlit_tot + li) | ((u64)(infr[rr] & 255u) << 17) | ((u64)(infr[rr] >> 8) << 25);
     }
-    u32 const total = wpart[WP_TOT];
+    u32 const total = __builtin_amdgcn_readfirstlane(wpart[WP_TOT]);
     nseq_tot += total >> 16;
     nlit_tot += total & 0xFFFFu;
     e_in = e_out;
