@@ -418,8 +418,9 @@ extern "C" __global__ __launch_bounds__(K1_THREADS) void zh_lz_kernel(const ZhBl
       }
       // (3) extend the heads, compacted across the wave: heads are ranked in (lane, bit)
       //     order and handed out 64 at a time, one per lane (wave-private LDS slots;
-      //     a wave's LDS operations execute in order, so no barrier is needed)
-      u32 hr[(2 * SB + 3) / 4] = {};  // head extensions packed as bytes, slot k = L_j (k=j) / S_j (k=SB+j)
+      //     a wave's LDS operations execute in order, so no barrier is needed).  The
+      //     extension goes back into the head position's own cinfo word (byte 0 for L,
+      //     byte 2 for S: the half that was just consumed), read back in (4).
       {
         u32 const nh = __builtin_popcount(heads);
         u32 inc = nh;
@@ -438,24 +439,16 @@ extern "C" __global__ __launch_bounds__(K1_THREADS) void zh_lz_kernel(const ZhBl
             if ((heads >> bit) & 1u) {
               u32 const c = k < SB ? (cv[k] & 0xFFFFu) : (cv[k - SB] >> 16);
               u32 const j = k < SB ? k : k - SB;
-              if (r >= c0 && r < c0 + 64) hb[r - c0] = (s + j) | ((c - 1) << 16);
+              // window index (13 bits) | S flag (bit 15) | candidate position
+              if (r >= c0 && r < c0 + 64) hb[r - c0] = (cbase + j) | (k < SB ? 0u : 0x8000u) | ((c - 1) << 16);
               r++;
             }
           }
           __asm__ volatile("" ::: "memory");
           if (c0 + lane < htot) {
             u32 const e = hb[lane];
-            hb[lane] = ext_head(in32, e & 0xFFFFu, e >> 16, n);
-          }
-          __asm__ volatile("" ::: "memory");
-          r = hbase;
-#pragma unroll
-          for (u32 k = 0; k < 2 * SB; k++) {
-            u32 const bit = k < SB ? k : 8 + (k - SB);
-            if ((heads >> bit) & 1u) {
-              if (r >= c0 && r < c0 + 64) hr[k >> 2] |= hb[r - c0] << (8 * (k & 3));
-              r++;
-            }
+            u32 const w = e & 0x1FFFu;
+            ci8[4 * cidx(w) + ((e >> 14) & 2u)] = (u8)ext_head(in32, wsb + w, e >> 16, n);
           }
           __asm__ volatile("" ::: "memory");
         }
@@ -468,12 +461,13 @@ extern "C" __global__ __launch_bounds__(K1_THREADS) void zh_lz_kernel(const ZhBl
         u32 const p = s + j;
         u32 const cL = cv[j] & 0xFFFFu, cS = cv[j] >> 16;
         u32 const capj = min((u32)ZH_MAX_MATCH, n - min(p, n));
+        u32 const hx = ci[cidx(cbase + j)];  // head extensions from (3)
         u32 nL = PL(j);
         if (dL & (1u << j)) nL = ((fromSL >> j) & 1u ? ES : EL) - 1;
-        else if ((heads >> j) & 1u) nL = (hr[j >> 2] >> (8 * (j & 3))) & 255u;
+        else if ((heads >> j) & 1u) nL = hx & 255u;
         u32 nS = PS(j);
         if (dS & (1u << j)) nS = ((fromSS >> j) & 1u ? ES : EL) - 1;
-        else if ((heads >> (8 + j)) & 1u) nS = (hr[(SB + j) >> 2] >> (8 * ((SB + j) & 3))) & 255u;
+        else if ((heads >> (8 + j)) & 1u) nS = (hx >> 16) & 255u;
         if (cS && cS == cL) nS = nL;
         EL = nL; ES = nS;
         u32 const rL = min(nL, capj), rS = min(nS, capj);
