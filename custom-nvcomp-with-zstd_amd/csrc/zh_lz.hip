@@ -55,8 +55,9 @@ constexpr u32 PR = (ZH_WINDOW + INS_TID - 1) / INS_TID;  // lane-per-position ro
 constexpr u32 WP_OFF = 80, WP_TOT = 160;
 static_assert(PR * NWW <= WP_OFF, "emission scan slots");
 constexpr u32 OFF_WP = OFF_SEG + 4 * (NPSEG + 4);     // emission scan: wave counts, offsets, total
-constexpr u32 OFF_HB = OFF_WP + 4 * 164;            // per worker wave: 64 head-extension slots
-constexpr u32 OFF_MISC = OFF_HB + 4 * 64 * (INS_TID / 64);  // [0..3] scan partials, [4..6] barrier-or words
+constexpr u32 HB_STRIDE = 65;                        // per worker wave: 64 head slots + a junk slot
+constexpr u32 OFF_HB = OFF_WP + 4 * 164;
+constexpr u32 OFF_MISC = OFF_HB + 4 * HB_STRIDE * (INS_TID / 64);  // [0..3] scan partials, [4..6] barrier-or words
 constexpr u32 K1_LDS = OFF_MISC + 4 * 16;
 constexpr u32 MISC_ARR = 12;  // misc[12]: worker-wave barrier arrivals (cumulative)
 static_assert(K1_LDS <= 163840 - 256, "K1 LDS budget");
@@ -430,25 +431,24 @@ extern "C" __global__ __launch_bounds__(K1_THREADS) void zh_lz_kernel(const ZhBl
           if (lane >= dd) inc += t;
         }
         u32 const hbase = inc - nh, htot = __shfl(inc, 63, 64);
-        u32 *hb = hbuf + (tid >> 6) * 64;
+        u32 *hb = hbuf + (tid >> 6) * HB_STRIDE;
         for (u32 c0 = 0; c0 < htot; c0 += 64) {
-          u32 r = hbase;
+          // branch-free scatter: slots not in this pass (or not heads) write the junk slot
+          u32 r = hbase - c0;
 #pragma unroll
           for (u32 k = 0; k < 2 * SB; k++) {
             u32 const bit = k < SB ? k : 8 + (k - SB);
-            if ((heads >> bit) & 1u) {
-              u32 const c = k < SB ? (cv[k] & 0xFFFFu) : (cv[k - SB] >> 16);
-              u32 const j = k < SB ? k : k - SB;
-              // window index (13 bits) | S flag (bit 15) | candidate position
-              if (r >= c0 && r < c0 + 64) hb[r - c0] = (cbase + j) | (k < SB ? 0u : 0x8000u) | ((c - 1) << 16);
-              r++;
-            }
+            u32 const h = (heads >> bit) & 1u;
+            hb[h && r < 64u ? r : 64u] = (cbase + (k < SB ? k : k - SB)) | (k < SB ? 0u : 0x8000u);
+            r += h;
           }
           __asm__ volatile("" ::: "memory");
           if (c0 + lane < htot) {
-            u32 const e = hb[lane];
-            u32 const w = e & 0x1FFFu;
-            ci8[4 * cidx(w) + ((e >> 14) & 2u)] = (u8)ext_head(in32, wsb + w, e >> 16, n);
+            u32 const e = hb[lane];  // window index (13 bits) | S flag (bit 15)
+            u32 const w = e & 0x1FFFu, sf = e >> 15;
+            u32 const cw = ci[cidx(w)];
+            u32 const c = sf ? cw >> 16 : cw & 0xFFFFu;
+            ci8[4 * cidx(w) + 2 * sf] = (u8)ext_head(in32, wsb + w, c - 1, n);
           }
           __asm__ volatile("" ::: "memory");
         }
