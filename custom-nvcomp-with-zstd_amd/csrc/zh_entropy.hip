@@ -779,8 +779,40 @@ __device__ u32 huf_write_ctable(u8 *hbuf, u8 *w, const u8 *hnb, u32 maxSV, u32 h
 }
 
 // byte copy global -> Out (wave-parallel)
+// Wave copy of n bytes to o[pos..]: byte head up to a 4-B aligned destination, then
+// dword stores (source realigned with alignbyte, 8 independent loads per lane in
+// flight), byte tail; bytes at or past o.cap are dropped like Out::put does.
 __device__ __forceinline__ void copy_bytes(const Out &o, u32 pos, const u8 *src, u32 n) {
-  for (u32 i = lane_id(); i < n; i += 64) o.put(pos + i, src[i]);
+  u32 const lane = lane_id();
+  u8 *const d0 = o.dst + pos;
+  u32 const h = min((u32)((4u - ((uintptr_t)d0 & 3u)) & 3u), n);
+  u32 const nw = (n - h) >> 2;
+  u32 const capw = o.cap > pos + h ? (o.cap - pos - h) >> 2 : 0u;
+  u32 const lim = min(nw, capw);
+  const u8 *const s0 = src + h;
+  u32 const sa = (u32)((uintptr_t)s0 & 3u);
+  const u32 *const s32 = (const u32 *)(s0 - sa);
+  u32 *const d32 = (u32 *)(d0 + h);
+  constexpr u32 U = 8;
+  for (u32 w0 = 0; w0 < lim; w0 += 64 * U) {
+    u32 v[U];
+#pragma unroll
+    for (u32 u = 0; u < U; u++) {
+      u32 const w = w0 + 64 * u + lane;
+      if (w < lim) {
+        u32 const A = s32[w];
+        u32 const B = sa ? s32[w + 1] : A;  // word w+1 holds an in-range byte when sa != 0
+        v[u] = __builtin_amdgcn_alignbyte(B, A, sa);
+      }
+    }
+#pragma unroll
+    for (u32 u = 0; u < U; u++) {
+      u32 const w = w0 + 64 * u + lane;
+      if (w < lim) d32[w] = v[u];
+    }
+  }
+  if (lane < h) o.put(pos + lane, src[lane]);
+  for (u32 i = h + 4 * lim + lane; i < n; i += 64) o.put(pos + i, src[i]);
 }
 
 }  // namespace
@@ -879,7 +911,29 @@ extern "C" __global__ __launch_bounds__(K2_THREADS) void zh_entropy_kernel(const
       if (nl > ZH_COMPRESS_LITERALS_SIZE_MIN) {
         for (u32 i = lane; i < 256; i += 64) hist[i] = 0;
         wave_sync();
-        for (u32 i = lane; i < nl; i += 64) atomicAdd(&hist[lits[i]], 1u);
+        // 16 literals per lane per load (lits is 16-B aligned), two loads in flight
+        for (u32 i0 = 32 * lane; i0 < nl; i0 += 2048) {
+          uint4 q[2];
+#pragma unroll
+          for (u32 g = 0; g < 2; g++) {
+            u32 const i = i0 + 16 * g;
+            if (i + 16 <= nl) q[g] = *(const uint4 *)(lits + i);
+            else {
+              u32 t[4] = {0, 0, 0, 0};
+              for (u32 k = 0; i + k < nl && k < 16; k++) t[k >> 2] |= (u32)lits[i + k] << (8 * (k & 3));
+              q[g] = make_uint4(t[0], t[1], t[2], t[3]);
+            }
+          }
+#pragma unroll
+          for (u32 g = 0; g < 2; g++) {
+            u32 const i = i0 + 16 * g;
+            u32 const cnt = i < nl ? min(16u, nl - i) : 0u;
+            u32 const w[4] = {q[g].x, q[g].y, q[g].z, q[g].w};
+#pragma unroll
+            for (u32 k = 0; k < 16; k++)
+              if (k < cnt) atomicAdd(&hist[(w[k >> 2] >> (8 * (k & 3))) & 255u], 1u);
+          }
+        }
         wave_sync();
         u32 mx = 0, lg = 0;
         for (u32 i = lane; i < 256; i += 64) { u32 c = hist[i]; if (c) mx = max(mx, i); lg = max(lg, c); }

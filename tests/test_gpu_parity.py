@@ -62,6 +62,25 @@ def test_ragged_sizes(torch_cuda, mgr):
     _check(outs, datas)
 
 
+def test_unaligned_items(torch_cuda, mgr):
+    """Items starting at every byte alignment (raw-block and raw-literal copies realign
+    the source) and destinations at odd offsets inside one buffer."""
+    sizes = [65536, 65535, 40000, 65536, 3001, 65536, 777, 65533]
+    kinds = [T.DG_RANDOM, T.DG_TEXT, T.DG_RANDOM, T.DG_MIX, T.DG_RANDOM, T.DG_EXE, T.DG_RANDOM, T.DG_RANDOM]
+    datas = [T.gen(k, 1, 300 + i, s) for i, (k, s) in enumerate(zip(kinds, sizes))]
+    offs, pos = [], 0
+    for i, d in enumerate(datas):
+        pos += i % 4 + 1  # 1..4 bytes of padding: every start alignment
+        offs.append(pos)
+        pos += len(d)
+    buf = np.zeros(pos + 16, np.uint8)
+    for o, d in zip(offs, datas):
+        buf[o:o + len(d)] = d
+    dev = torch_cuda.from_numpy(buf).cuda()
+    outs = mgr.compress_batch([dev[o:o + len(d)] for o, d in zip(offs, datas)])
+    _check(outs, datas)
+
+
 def test_single_buffer_multiblock(torch_cuda, mgr):
     data = np.concatenate([T.gen(T.DG_TEXT, 3, 5, 65536), T.gen(T.DG_CSV, 1, 6, 50000), T.gen(T.DG_RANDOM, 1, 7, 9000), np.zeros(70000, np.uint8)])
     out = mgr.compress(torch_cuda.from_numpy(data).cuda())
