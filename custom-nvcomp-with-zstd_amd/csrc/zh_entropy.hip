@@ -890,7 +890,7 @@ extern "C" __global__ __launch_bounds__(K2_THREADS) void zh_entropy_kernel(const
   u32 const body0 = blk + 3;
   u32 const last = (d.flags & ZH_F_LAST) ? 1u : 0u;
   u32 total;
-  bool raw = false;
+  bool raw = false, early_raw = false;
 
   if (rle) {
     u32 const hdr = last + (1u << 1) + (n << 3);
@@ -980,8 +980,14 @@ extern "C" __global__ __launch_bounds__(K2_THREADS) void zh_entropy_kernel(const
         // raw literals
         u32 const fl = 1 + (nl > 31) + (nl > 4095);
         u32 v = fl == 1 ? (nl << 3) : fl == 2 ? ((1u << 2) + (nl << 4)) : ((3u << 2) + (nl << 4));
-        if (lane < fl) o.put(op + lane, (u8)(v >> (8 * lane)));
-        copy_bytes(o, op + fl, lits, nl);
+        // the sequences section adds >= 1 byte: past the block's minGain the block is
+        // emitted raw whatever the sequences cost, so skip writing this body at all
+        u32 const bmaxC = n > (n >> 6) + 2 ? n - ((n >> 6) + 2) : 0u;
+        early_raw = fl + nl + 1 >= bmaxC;
+        if (!early_raw) {
+          if (lane < fl) o.put(op + lane, (u8)(v >> (8 * lane)));
+          copy_bytes(o, op + fl, lits, nl);
+        }
         op += fl + nl;
       } else if (cLit == 1) {
         u32 const fl = 1 + (nl > 31) + (nl > 4095);
@@ -1030,6 +1036,7 @@ extern "C" __global__ __launch_bounds__(K2_THREADS) void zh_entropy_kernel(const
     }
 
     // ======================= sequences section =======================
+    if (!early_raw) {
     // pass A: literal lengths from cumulative counts, merge same-offset continuations (in place)
     u32 nbSeq = 0;
     {
@@ -1290,10 +1297,11 @@ extern "C" __global__ __launch_bounds__(K2_THREADS) void zh_entropy_kernel(const
       ZH_STAMP(7);  // FSE chain + packing
     }
 
+    }  // !early_raw
     u32 const body = op - body0;
     u32 const minGain = (n >> 6) + 2;
     u32 const maxC = n > minGain ? n - minGain : 0;
-    raw = body >= maxC;
+    raw = early_raw || body >= maxC;
     if (!raw) {
       u32 const hdr = last + (2u << 1) + (body << 3);
       if (lane == 0) { o.put(blk, (u8)hdr); o.put(blk + 1, (u8)(hdr >> 8)); o.put(blk + 2, (u8)(hdr >> 16)); }
