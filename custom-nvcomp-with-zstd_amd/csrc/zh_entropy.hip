@@ -78,6 +78,26 @@ __device__ __forceinline__ u32 highbit32(u32 v) { return 31u - (u32)__builtin_cl
 __device__ __forceinline__ u32 ll_code(u32 ll) { return ll > 63 ? highbit32(ll) + 19 : c_LL_code[ll]; }
 __device__ __forceinline__ u32 ml_code(u32 mlBase) { return mlBase > 127 ? highbit32(mlBase) + 36 : c_ML_code[mlBase]; }
 __device__ __forceinline__ u32 lane_id() { return threadIdx.x; }
+// Code tables held across the wave (lane x holds entry x), looked up with ds_bpermute
+// instead of a constant-memory load per lookup.  All lanes must execute the lookups.
+struct CodeTabs {
+  u32 llc, mlc0, mlc1, llb, mlb;
+  __device__ __forceinline__ void load() {
+    u32 const l = lane_id();
+    llc = c_LL_code[l]; mlc0 = c_ML_code[l]; mlc1 = c_ML_code[64 + l];
+    llb = l < 36 ? c_LL_bits[l] : 0u; mlb = l < 53 ? c_ML_bits[l] : 0u;
+  }
+  __device__ __forceinline__ u32 ll_code(u32 ll) const {
+    u32 const c = (u32)__shfl((int)llc, (int)(ll & 63u), 64);
+    return ll > 63 ? highbit32(ll) + 19 : c;
+  }
+  __device__ __forceinline__ u32 ml_code(u32 m) const {
+    u32 const a = (u32)__shfl((int)mlc0, (int)(m & 63u), 64), b = (u32)__shfl((int)mlc1, (int)(m & 63u), 64);
+    return m > 127 ? highbit32(m) + 36 : (m < 64 ? a : b);
+  }
+  __device__ __forceinline__ u32 ll_bits(u32 c) const { return (u32)__shfl((int)llb, (int)(c & 63u), 64); }
+  __device__ __forceinline__ u32 ml_bits(u32 c) const { return (u32)__shfl((int)mlb, (int)(c & 63u), 64); }
+};
 __device__ __forceinline__ void wave_sync() { __syncthreads(); }  // one wave per workgroup
 
 __device__ __forceinline__ u32 wave_excl_scan(u32 v, u32 &total) {
@@ -1042,10 +1062,12 @@ extern "C" __global__ __launch_bounds__(K2_THREADS) void zh_entropy_kernel(const
     {
       u32 carryCum = 0, carryOff = 0, openIdx = 0, openLL = 0, openMl = 0, openOff = 0;
       bool open = false;
+      u64 nrec = lane < nseq_raw ? seq[lane] : 0;  // next chunk's records, loaded a chunk ahead
       for (u32 base = 0; base < nseq_raw; base += 64) {
         u32 const i = base + lane;
         bool const valid = i < nseq_raw;
-        u64 const rec = valid ? seq[i] : 0;
+        u64 const rec = nrec;
+        nrec = i + 64 < nseq_raw ? seq[i + 64] : 0;  // (this chunk writes only indices <= i)
         u32 const cum = (u32)(rec & 0x1FFFFu), ml = (u32)((rec >> 17) & 255u), off = (u32)((rec >> 25) & 0xFFFFu);
         u32 pc = __shfl_up(cum, 1, 64), po = __shfl_up(off, 1, 64);
         if (lane == 0) { pc = carryCum; po = carryOff; }
@@ -1119,10 +1141,14 @@ extern "C" __global__ __launch_bounds__(K2_THREADS) void zh_entropy_kernel(const
       u32 cr0 = 1, cr1 = 4, cr2 = 8;  // reps before the batch's first sequence
       if (!(d.flags & ZH_F_FIRST)) { cr0 = cr1 = cr2 = 0; }
       u64 const below = (1ull << lane) - 1ull;
+      CodeTabs ct;
+      ct.load();
+      u64 nrec = lane < nbSeq ? seq[lane] : 0;
       for (u32 base = 0; base < nbSeq; base += 64) {
         u32 const i = base + lane;
         bool const valid = i < nbSeq;
-        u64 const rec = valid ? seq[i] : 0;
+        u64 const rec = nrec;
+        nrec = i + 64 < nbSeq ? seq[i + 64] : 0;
         u32 const ll = (u32)(rec & 0x1FFFFu), ml = (u32)((rec >> 17) & 0x1FFFFu), off = (u32)(rec >> 34);
         u32 r0 = __shfl_up(off, 1, 64);
         if (lane == 0) r0 = cr0;
@@ -1147,10 +1173,11 @@ extern "C" __global__ __launch_bounds__(K2_THREADS) void zh_entropy_kernel(const
         cr0 = __shfl(off, lastLane, 64);
         cr1 = __shfl(n1, lastLane, 64);
         cr2 = __shfl(n2, lastLane, 64);
+        u32 const mlb = ml - 3;
+        u32 const llc = ct.ll_code(ll), mlc = ct.ml_code(mlb);
         if (valid) {
-          u32 const mlb = ml - 3;
-          atomicAdd(&hLL[ll_code(ll)], 1u);
-          atomicAdd(&hML[ml_code(mlb)], 1u);
+          atomicAdd(&hLL[llc], 1u);
+          atomicAdd(&hML[mlc], 1u);
           atomicAdd(&hOF[highbit32(ob)], 1u);
           seq[i] = (u64)ll | ((u64)mlb << 17) | ((u64)ob << 34);
         }
@@ -1239,12 +1266,16 @@ extern "C" __global__ __launch_bounds__(K2_THREADS) void zh_entropy_kernel(const
       u32 const csh = lane == 0 ? 0u : lane == 1 ? 8u : 16u;
       u32 sreg = 0;
       BitSink bs{op, 0};
+      nrec = lane < nbSeq ? seq[nbSeq - 1 - lane] : 0;
       for (u32 e0 = 0; e0 < nbSeq; e0 += 64) {
         u32 const e = e0 + lane;
         bool const valid = e < nbSeq;
-        u64 const rec = valid ? seq[nbSeq - 1 - e] : 0;
+        u64 const rec = nrec;
+        nrec = e + 64 < nbSeq ? seq[nbSeq - 1 - (e + 64)] : 0;
         u32 const ll = (u32)(rec & 0x1FFFFu), mlb = (u32)((rec >> 17) & 0x1FFFFu), ob = (u32)(rec >> 34);
-        u32 const llc = valid ? ll_code(ll) : 0, mlc = valid ? ml_code(mlb) : 0, ofc = valid ? highbit32(ob) : 0;
+        u32 const llc0 = ct.ll_code(ll), mlc0 = ct.ml_code(mlb);
+        u32 const llc = valid ? llc0 : 0, mlc = valid ? mlc0 : 0, ofc = valid ? highbit32(ob) : 0;
+        u32 const llbits = ct.ll_bits(llc), mlbits = ct.ml_bits(mlc);
         ccd[lane] = llc | (ofc << 8) | (mlc << 16);
         wave_sync();
         if (lane < 3) {
@@ -1282,7 +1313,7 @@ extern "C" __global__ __launch_bounds__(K2_THREADS) void zh_entropy_kernel(const
           nLL = (s_L + symLL[llc].dNb) >> 16; vLL = s_L;
         }
         u32 v6[6] = {vOF, vML, vLL, ll, mlb, ob};
-        u32 n6[6] = {nOF, nML, nLL, valid ? (u32)c_LL_bits[llc] : 0u, valid ? (u32)c_ML_bits[mlc] : 0u, ofc};
+        u32 n6[6] = {nOF, nML, nLL, valid ? llbits : 0u, valid ? mlbits : 0u, ofc};
         sink_append<6>(bs, o, sw, v6, n6);
       }
       u32 const sLL = __builtin_amdgcn_readlane(sreg, 0), sOF = __builtin_amdgcn_readlane(sreg, 1), sML = __builtin_amdgcn_readlane(sreg, 2);

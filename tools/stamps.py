@@ -37,7 +37,7 @@ off = a256(off + 0)
 blocks = base + off
 WS = 13120 * 8 + 65536 + 256
 h = temp.cpu().numpy()
-raw = np.array([h[blocks + b * WS + 13120 * 8 + 65536 + 16: blocks + b * WS + 13120 * 8 + 65536 + 16 + 23 * 4].view(np.uint32) for b in range(n)])
+raw = np.array([h[blocks + b * WS + 13120 * 8 + 65536 + 16: blocks + b * WS + 13120 * 8 + 65536 + 16 + 48 * 4].view(np.uint32) for b in range(n)])
 st = raw[:, :6]
 k2 = raw[:, 6:15].astype(np.float64)
 names = ["stage", "A(insert)", "B(lengths+exit)", "J(jacobi)", "E(emit)", "rounds"]
@@ -54,7 +54,7 @@ print(kind, "K2 mean cycles/block", int(t2))
 for k, nm in enumerate(k2n):
     print(f"  {nm:20s} mean {k2[:, k].mean():12.0f}  share {k2[:, k].mean() / t2 * 100:5.1f}%")
 print(f"  of huf_build: parallel tree {np.array([h[blocks + b * WS + 13120 * 8 + 65536 + 16 + 42 * 4: blocks + b * WS + 13120 * 8 + 65536 + 16 + 43 * 4].view(np.uint32)[0] for b in range(n)]).mean():.0f}")
-print(f"  chain rounds mean {raw[:, 18].mean():.2f} max {raw[:, 18].max()}  raw seqs mean {raw[:, 19].mean():.0f}")
+print(f"  of fse_chains: serial chain steps only {raw[:, 18].mean():.0f}  raw seqs mean {raw[:, 19].mean():.0f}")
 # wall clock per block (s_memrealtime, 100 MHz) and placement
 rt = np.array([h[blocks + b * WS + 13120 * 8 + 65536 + 16 + 23 * 4: blocks + b * WS + 13120 * 8 + 65536 + 16 + 28 * 4].view(np.uint32) for b in range(n)]).astype(np.int64)
 dur = (rt[:, 1] - rt[:, 0]) & 0xFFFFFFFF
