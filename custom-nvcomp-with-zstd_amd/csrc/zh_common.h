@@ -30,13 +30,29 @@ enum : u32 {
 
 // Per-block workspace carved from the caller's temp buffer.
 //   seq   : ZH_SEQ_CAP u64 records (K1: cumLit | ml<<17 | off<<25; K2 rewrites in place)
-//   lits  : ZH_BLOCK_MAX literal bytes
+//   lits  : ZH_BLOCK_MAX literal bytes; after the literals section is written, the FSE
+//           states before each encode step (u16, LL | OF | ML arrays of nbSeq each)
 //   meta  : u32[4] = {nseq, nlit, rle, 0}
 #define ZH_SEQ_CAP 13120u
 #define ZH_SEQ_BYTES (ZH_SEQ_CAP * 8u)
-#define ZH_LIT_BYTES ((u32)ZH_BLOCK_MAX)
+#define ZH_LIT_BYTES (6u * ZH_SEQ_CAP > (u32)ZH_BLOCK_MAX ? 6u * ZH_SEQ_CAP : (u32)ZH_BLOCK_MAX)
 #define ZH_META_BYTES 256u  // u32[4] counters + u32[60] diagnostic stamps (-DZH_STAMPS builds)
-#define ZH_WS_BLOCK_BYTES (ZH_SEQ_BYTES + ZH_LIT_BYTES + ZH_META_BYTES)
+//   fse   : hand-off from the entropy kernel to the FSE chain and packing kernels:
+//           the block's three FSE tables (state tables + symbol transforms, ZH_FSE_TAB_BYTES)
+//           then u32 fields at ZH_FSE_FIELDS (ZH_FF_* indices)
+#define ZH_FSE_BYTES 4096u
+#define ZH_FSE_TAB_BYTES 3528u  // stLL u16[512] | stOF u16[256] | stML u16[512] | symLL[36] | symOF[32] | symML[53] (8 B each)
+#define ZH_FSE_FIELDS 3840u
+#define ZH_WS_BLOCK_BYTES (ZH_SEQ_BYTES + ZH_LIT_BYTES + ZH_META_BYTES + ZH_FSE_BYTES)
+enum : u32 {
+  ZH_FT_STLL = 0, ZH_FT_STOF = 1024, ZH_FT_STML = 1536, ZH_FT_SYLL = 2560, ZH_FT_SYOF = 2848, ZH_FT_SYML = 3104,  // byte offsets
+  ZH_FF_NEED = 0,   // 1: the sequence bitstream is left to the chain + packing kernels
+  ZH_FF_NBSEQ = 1,  // sequences (after merging)
+  ZH_FF_OP = 2,     // output offset where the sequence bitstream starts
+  ZH_FF_BLK = 3,    // output offset of the block header
+  ZH_FF_LOGS = 4,   // logLL | logOF << 8 | logML << 16
+  ZH_FF_SLL = 5, ZH_FF_SOF = 6, ZH_FF_SML = 7,  // final FSE states (chain kernel)
+};
 
 struct ZhWorkspace {
   u8 *base;          // nblocks * ZH_WS_BLOCK_BYTES
@@ -44,6 +60,8 @@ struct ZhWorkspace {
   __device__ u8 *lits(u32 b) const { return base + (size_t)b * ZH_WS_BLOCK_BYTES + ZH_SEQ_BYTES; }
   __device__ u32 *meta(u32 b) const { return (u32 *)(base + (size_t)b * ZH_WS_BLOCK_BYTES + ZH_SEQ_BYTES + ZH_LIT_BYTES); }
   __device__ u32 *dbg(u32 b) const { return meta(b) + 4; }
+  __device__ u8 *fse(u32 b) const { return base + (size_t)b * ZH_WS_BLOCK_BYTES + ZH_SEQ_BYTES + ZH_LIT_BYTES + ZH_META_BYTES; }
+  __device__ u32 *fsef(u32 b) const { return (u32 *)(fse(b) + ZH_FSE_FIELDS); }
 };
 
 // Status codes written per item (values of cuda_zstd::Status).

@@ -849,6 +849,36 @@ __device__ __forceinline__ void copy_bytes(const Out &o, u32 pos, const u8 *src,
 #endif
 
 // ============================================================================
+// Raw fallback (ZSTD_compressBlock_internal: a compressed body of >= n - minGain bytes is
+// replaced by the raw block) and the block header; returns the block's end offset.
+__device__ u32 finish_block(const ZhBlockDesc &d, const Out &o, u32 blk, u32 op, bool early_raw) {
+  u32 const lane = lane_id(), n = d.n, last = (d.flags & ZH_F_LAST) ? 1u : 0u, body0 = blk + 3;
+  u32 const body = op - body0;
+  u32 const minGain = (n >> 6) + 2;
+  u32 const maxC = n > minGain ? n - minGain : 0;
+  if (!early_raw && body < maxC) {
+    u32 const hdr = last + (2u << 1) + (body << 3);
+    if (lane == 0) { o.put(blk, (u8)hdr); o.put(blk + 1, (u8)(hdr >> 8)); o.put(blk + 2, (u8)(hdr >> 16)); }
+    return op;
+  }
+  u32 const hdr = last + (n << 3);
+  wave_sync();
+  if (lane == 0) { o.put(blk, (u8)hdr); o.put(blk + 1, (u8)(hdr >> 8)); o.put(blk + 2, (u8)(hdr >> 16)); }
+  copy_bytes(o, body0, d.src, n);
+  return body0 + n;
+}
+
+__device__ __forceinline__ void write_status(const ZhBlockDesc &d, u32 b, u32 total, u64 *item_size, u32 *item_status, u32 *blk_size) {
+  if (lane_id() == 0) {
+    if (d.flags & ZH_F_DIRECT) {
+      item_size[d.item] = total;
+      item_status[d.item] = total <= d.dst_cap ? ZH_ST_OK : ZH_ST_TOO_SMALL;
+    } else {
+      blk_size[b] = total <= d.dst_cap ? total : 0xFFFFFFFFu;
+    }
+  }
+}
+
 extern "C" __global__ __launch_bounds__(K2_THREADS) void zh_entropy_kernel(const ZhBlockDesc *__restrict__ blocks, ZhWorkspace ws, u32 window_log,
                                                                              u32 cfg_block_size, u64 *__restrict__ item_size,
                                                                              u32 *__restrict__ item_status, u32 *__restrict__ blk_size) {
@@ -910,7 +940,8 @@ extern "C" __global__ __launch_bounds__(K2_THREADS) void zh_entropy_kernel(const
   u32 const body0 = blk + 3;
   u32 const last = (d.flags & ZH_F_LAST) ? 1u : 0u;
   u32 total;
-  bool raw = false, early_raw = false;
+  bool early_raw = false, handoff = false;
+  if (lane == 0) ws.fsef(b)[ZH_FF_NEED] = 0;
 
   if (rle) {
     u32 const hdr = last + (1u << 1) + (n << 3);
@@ -1179,7 +1210,8 @@ extern "C" __global__ __launch_bounds__(K2_THREADS) void zh_entropy_kernel(const
           atomicAdd(&hLL[llc], 1u);
           atomicAdd(&hML[mlc], 1u);
           atomicAdd(&hOF[highbit32(ob)], 1u);
-          seq[i] = (u64)ll | ((u64)mlb << 17) | ((u64)ob << 34);
+          // + the LL / ML codes in the spare top bits (ob < 2^17: offsets stay inside the block)
+          seq[i] = (u64)ll | ((u64)mlb << 17) | ((u64)ob << 34) | ((u64)llc << 51) | ((u64)mlc << 57);
         }
       }
       wave_sync();
@@ -1191,8 +1223,8 @@ extern "C" __global__ __launch_bounds__(K2_THREADS) void zh_entropy_kernel(const
       {
         u32 *first_code = scr->wcount, *last_code = scr->wcount + 4, *types = scr->wcount + 8, *logs = scr->wcount + 12;
         if (lane == 0) {
-          first_code[0] = ll_code((u32)(rec0 & 0x1FFFFu)); first_code[1] = highbit32((u32)(rec0 >> 34)); first_code[2] = ml_code((u32)((rec0 >> 17) & 0x1FFFFu));
-          last_code[0] = ll_code((u32)(recL & 0x1FFFFu)); last_code[1] = highbit32((u32)(recL >> 34)); last_code[2] = ml_code((u32)((recL >> 17) & 0x1FFFFu));
+          first_code[0] = ll_code((u32)(rec0 & 0x1FFFFu)); first_code[1] = highbit32((u32)(rec0 >> 34) & 0x1FFFFu); first_code[2] = ml_code((u32)((rec0 >> 17) & 0x1FFFFu));
+          last_code[0] = ll_code((u32)(recL & 0x1FFFFu)); last_code[1] = highbit32((u32)(recL >> 34) & 0x1FFFFu); last_code[2] = ml_code((u32)((recL >> 17) & 0x1FFFFu));
           misc[0] = 0;
         }
         for (int t = 0; t < 3; t++) {
@@ -1255,117 +1287,238 @@ extern "C" __global__ __launch_bounds__(K2_THREADS) void zh_entropy_kernel(const
       u32 const logLL = misc[2], logOF = misc[3], logML = misc[4];
       ZH_STAMP(6);  // FSE tables (serial)
 
-      // pass C: FSE state chains + bit packing, 64 encode steps (sequence nbSeq-1-e)
-      // per chunk.  All lanes stage the chunk's codes in LDS; lanes 0, 1, 2 advance the
-      // LL / OF / ML state through it (the chain is serial by format: one LDS round trip
-      // per step, the three tables side by side); then all lanes pack the chunk's bits.
-      u32 *ccd = (u32 *)(smem + OFF_TSYM);          // 64 x (llc | ofc << 8 | mlc << 16)
-      u16 *cst = (u16 *)(smem + OFF_TSYM + 256);    // 64 x 3 states before each step
-      const u16 *stT = lane == 0 ? stLL : lane == 1 ? stOF : stML;
-      const FseSym *syT = lane == 0 ? symLL : lane == 1 ? symOF : symML;
-      u32 const csh = lane == 0 ? 0u : lane == 1 ? 8u : 16u;
-      u32 sreg = 0;
-      BitSink bs{op, 0};
-      nrec = lane < nbSeq ? seq[nbSeq - 1 - lane] : 0;
-      for (u32 e0 = 0; e0 < nbSeq; e0 += 64) {
-        u32 const e = e0 + lane;
-        bool const valid = e < nbSeq;
-        u64 const rec = nrec;
-        nrec = e + 64 < nbSeq ? seq[nbSeq - 1 - (e + 64)] : 0;
-        u32 const ll = (u32)(rec & 0x1FFFFu), mlb = (u32)((rec >> 17) & 0x1FFFFu), ob = (u32)(rec >> 34);
-        u32 const llc0 = ct.ll_code(ll), mlc0 = ct.ml_code(mlb);
-        u32 const llc = valid ? llc0 : 0, mlc = valid ? mlc0 : 0, ofc = valid ? highbit32(ob) : 0;
-        u32 const llbits = ct.ll_bits(llc), mlbits = ct.ml_bits(mlc);
-        ccd[lane] = llc | (ofc << 8) | (mlc << 16);
-        wave_sync();
-        if (lane < 3) {
-          u32 const cnt = min(64u, nbSeq - e0);
-          u32 k0 = 0;
-          if (e0 == 0) {  // FSE_initCState2 with the last sequence's symbol
-            FseSym const tr = syT[(ccd[0] >> csh) & 255u];
-            u32 const nb = (tr.dNb + (1u << 15)) >> 16;
-            sreg = stT[(((nb << 16) - tr.dNb) >> nb) + tr.dFS];
-            k0 = 1;
-          }
-          for (u32 k8 = k0; k8 < cnt; k8 += 8) {
-            FseSym tr[8];
-#pragma unroll
-            for (u32 k = 0; k < 8; k++) tr[k] = syT[(ccd[min(k8 + k, 63u)] >> csh) & 255u];
-            u32 sv[8];
-#pragma unroll
-            for (u32 k = 0; k < 8; k++) {
-              sv[k] = sreg;
-              if (k8 + k < cnt) {
-                u32 const nb = (sreg + tr[k].dNb) >> 16;
-                sreg = stT[(sreg >> nb) + tr[k].dFS];
-              }
-            }
-#pragma unroll
-            for (u32 k = 0; k < 8; k++) if (k8 + k < cnt) cst[3 * (k8 + k) + lane] = (u16)sv[k];
-          }
-        }
-        wave_sync();
-        u32 vOF = 0, nOF = 0, vML = 0, nML = 0, vLL = 0, nLL = 0;
-        if (valid && e > 0) {
-          u32 const s_L = cst[3 * lane], s_O = cst[3 * lane + 1], s_M = cst[3 * lane + 2];
-          nOF = (s_O + symOF[ofc].dNb) >> 16; vOF = s_O;
-          nML = (s_M + symML[mlc].dNb) >> 16; vML = s_M;
-          nLL = (s_L + symLL[llc].dNb) >> 16; vLL = s_L;
-        }
-        u32 v6[6] = {vOF, vML, vLL, ll, mlb, ob};
-        u32 n6[6] = {nOF, nML, nLL, valid ? llbits : 0u, valid ? mlbits : 0u, ofc};
-        sink_append<6>(bs, o, sw, v6, n6);
-      }
-      u32 const sLL = __builtin_amdgcn_readlane(sreg, 0), sOF = __builtin_amdgcn_readlane(sreg, 1), sML = __builtin_amdgcn_readlane(sreg, 2);
-      ZH_STAMP(9);  // FSE chains + packing
+      // hand-off: the FSE state chains run in zh_fse_chain_kernel (lanes = blocks x
+      // tables, so many serial chains share a wave) and the bitstream is packed by
+      // zh_seq_pack_kernel, which also finishes the block
+      u8 *fz = ws.fse(b);
       {
-        u32 v3[3] = {sML, sOF, sLL};
-        u32 n3[3] = {lane == 0 ? logML : 0u, lane == 0 ? logOF : 0u, lane == 0 ? logLL : 0u};
-        sink_append<3>(bs, o, sw, v3, n3);
+        const u32 *sL = (const u32 *)stLL, *sO = (const u32 *)stOF, *sM = (const u32 *)stML;
+        for (u32 i = lane; i < 256; i += 64) ((u32 *)(fz + ZH_FT_STLL))[i] = sL[i];
+        for (u32 i = lane; i < 128; i += 64) ((u32 *)(fz + ZH_FT_STOF))[i] = sO[i];
+        for (u32 i = lane; i < 256; i += 64) ((u32 *)(fz + ZH_FT_STML))[i] = sM[i];
+        if (lane < 36) ((FseSym *)(fz + ZH_FT_SYLL))[lane] = symLL[lane];
+        if (lane < 32) ((FseSym *)(fz + ZH_FT_SYOF))[lane] = symOF[lane];
+        if (lane < 53) ((FseSym *)(fz + ZH_FT_SYML))[lane] = symML[lane];
+        u32 *ff = ws.fsef(b);
+        if (lane == 0) {
+          ff[ZH_FF_NBSEQ] = nbSeq; ff[ZH_FF_OP] = op; ff[ZH_FF_BLK] = blk;
+          ff[ZH_FF_LOGS] = logLL | (logOF << 8) | (logML << 16);
+          ff[ZH_FF_NEED] = 1;
+        }
       }
-      sink_close(bs, o, sw);
-      op = bs.pos;
-      ZH_STAMP(7);  // FSE chain + packing
+      handoff = true;
     }
 
     }  // !early_raw
-    u32 const body = op - body0;
-    u32 const minGain = (n >> 6) + 2;
-    u32 const maxC = n > minGain ? n - minGain : 0;
-    raw = early_raw || body >= maxC;
-    if (!raw) {
-      u32 const hdr = last + (2u << 1) + (body << 3);
-      if (lane == 0) { o.put(blk, (u8)hdr); o.put(blk + 1, (u8)(hdr >> 8)); o.put(blk + 2, (u8)(hdr >> 16)); }
-      total = op;
-    } else {
-      u32 const hdr = last + (n << 3);
-      wave_sync();
-      if (lane == 0) { o.put(blk, (u8)hdr); o.put(blk + 1, (u8)(hdr >> 8)); o.put(blk + 2, (u8)(hdr >> 16)); }
-      copy_bytes(o, body0, d.src, n);
-      total = body0 + n;
-    }
+    if (!handoff) total = finish_block(d, o, blk, op, early_raw);
   }
   ZH_STAMP(8);  // tail (raw copy etc.)
 #ifdef ZH_STAMPS
   if (lane == 0) { u32 *dbg = ws.dbg(b); for (int k = 0; k < 9; k++) dbg[6 + k] = st[k]; dbg[17] = st[9]; dbg[18] = st[10]; dbg[19] = nseq_raw; dbg[42] = st[11]; }
 #endif
-  if (lane == 0) {
-    if (d.flags & ZH_F_DIRECT) {
-      item_size[d.item] = total;
-      item_status[d.item] = total <= d.dst_cap ? ZH_ST_OK : ZH_ST_TOO_SMALL;
-    } else {
-      blk_size[b] = total <= d.dst_cap ? total : 0xFFFFFFFFu;
+  if (!handoff) write_status(d, b, total, item_size, item_status, blk_size);
+}
+
+// ======================= FSE state chains (K3) =======================
+// Lanes = (block, table): lane 3j + t runs table t (LL, OF, ML) of the workgroup's
+// block j; 11 blocks per wave, so 33 serial chains advance together instead of 3.
+// Encoding step e (e >= 1) encodes sequence nbSeq-1-e from the state the previous step
+// left (step 0 is FSE_initCState2 with the last sequence's code).  The state before
+// each step goes to the block's literal area (free by now) as u16 (table t at
+// [t * NS, t * NS + nbSeq), NS = nbSeq rounded up to 16); the final states go to the fse fields.
+constexpr u32 K3_BLOCKS = 11;  // 39 KB of LDS: 4 workgroups (one per SIMD) per CU
+constexpr u32 K3_CODES = 192;  // LDS: c_LL_code (64) + c_ML_code (128)
+constexpr u32 K3_LDS = K3_CODES + K3_BLOCKS * ZH_FSE_TAB_BYTES;
+constexpr u32 K3_BATCH = 16;   // records loaded ahead per lane
+constexpr u32 K3_TABW = ZH_FSE_TAB_BYTES / 4;
+
+extern "C" __global__ __launch_bounds__(64) void zh_fse_chain_kernel(const ZhBlockDesc *__restrict__ blocks, u32 nblocks, ZhWorkspace ws) {
+  extern __shared__ __attribute__((aligned(16))) u8 smem[];
+  u32 const lane = lane_id();
+  u32 const b0 = blockIdx.x * K3_BLOCKS;
+  u8 *codes = smem;
+  codes[lane] = c_LL_code[lane];
+  codes[64 + lane] = c_ML_code[lane];
+  codes[128 + lane] = c_ML_code[64 + lane];
+  // which of the workgroup's blocks have chains (lane j looks at block b0 + j)
+  bool const mine = lane < K3_BLOCKS && b0 + lane < nblocks && blocks[b0 + lane].n != 0 && ws.fsef(b0 + lane)[ZH_FF_NEED] != 0;
+  u64 const needm = __ballot(mine);
+  // stage the needed tables: 8 independent loads per lane in flight
+  u32 const nw = K3_BLOCKS * K3_TABW;
+  for (u32 w0 = 0; w0 < nw; w0 += 64 * 8) {
+    u32 v[8];
+#pragma unroll
+    for (u32 q = 0; q < 8; q++) {
+      u32 const w = w0 + 64 * q + lane, jj = w / K3_TABW;
+      v[q] = (w < nw && ((needm >> jj) & 1u)) ? ((const u32 *)ws.fse(b0 + jj))[w - jj * K3_TABW] : 0u;
+    }
+#pragma unroll
+    for (u32 q = 0; q < 8; q++) {
+      u32 const w = w0 + 64 * q + lane;
+      if (w < nw) ((u32 *)(smem + K3_CODES))[w] = v[q];
     }
   }
+  __syncthreads();
+  u32 const j = lane / 3, t = lane - 3 * j;
+  if (j >= K3_BLOCKS || !((needm >> j) & 1u)) return;
+  u32 const bb = b0 + j;
+  u32 *ff = ws.fsef(bb);
+  u32 const nbSeq = ff[ZH_FF_NBSEQ];
+  const u8 *tb = smem + K3_CODES + j * ZH_FSE_TAB_BYTES;
+  const u16 *stT = (const u16 *)(tb + (t == 0 ? ZH_FT_STLL : t == 1 ? ZH_FT_STOF : ZH_FT_STML));
+  const FseSym *syT = (const FseSym *)(tb + (t == 0 ? ZH_FT_SYLL : t == 1 ? ZH_FT_SYOF : ZH_FT_SYML));
+  const u64 *seq = ws.seq(bb);
+  u16 *gst = (u16 *)ws.lits(bb) + t * ((nbSeq + 15) & ~15u);  // 32-B aligned per table
+  // this lane's code of a record: LL / ML codes ride in the record's top bits (pass B)
+  u32 const csh = t == 0 ? 51u : 57u;
+  auto code_of = [&](u64 rec) -> u32 {
+    u32 const ofc = 31u - __builtin_clz(((u32)(rec >> 34) & 0x1FFFFu) | 1u);
+    return t == 1 ? ofc : (u32)(rec >> csh) & 63u;
+  };
+  u32 s;
+  {
+    FseSym const tr = syT[code_of(seq[nbSeq - 1])];  // FSE_initCState2
+    u32 const nb = (tr.dNb + (1u << 15)) >> 16;
+    s = stT[(((nb << 16) - tr.dNb) >> nb) + tr.dFS];
+  }
+  // batches of 16 steps aligned to the state array (entry 0 and entries >= nbSeq are
+  // padding), so each lane writes its 16 states with two 16-byte stores
+  u64 nx[2][K3_BATCH];  // two batches of records in flight ahead of the chain
+#pragma unroll
+  for (u32 q = 0; q < 2 * K3_BATCH; q++) nx[q / K3_BATCH][q % K3_BATCH] = seq[nbSeq - 1 - min(q, nbSeq - 1)];  // clamped: always valid
+#ifdef ZH_STAMPS
+  u64 const k3t0 = __builtin_amdgcn_s_memtime();
+  u64 k3chain = 0, k3codes = 0;
+#endif
+  for (u32 k0 = 0; k0 < nbSeq; k0 += K3_BATCH) {
+#ifdef ZH_STAMPS
+    u64 const kt0 = __builtin_amdgcn_s_memtime();
+#endif
+    u32 cd[K3_BATCH];
+#pragma unroll
+    for (u32 q = 0; q < K3_BATCH; q++) cd[q] = code_of(nx[0][q]);
+#pragma unroll
+    for (u32 q = 0; q < K3_BATCH; q++) {
+      nx[0][q] = nx[1][q];
+      nx[1][q] = seq[nbSeq - 1 - min(k0 + 2 * K3_BATCH + q, nbSeq - 1)];
+    }
+    // symbol transforms first (independent of the state), then the dependent chain:
+    // one LDS round trip per step, predicated without branches
+    u32 dnb[K3_BATCH];
+    s32 dfs[K3_BATCH];
+#pragma unroll
+    for (u32 q = 0; q < K3_BATCH; q++) {
+      FseSym const tr = syT[cd[q]];
+      bool const live = k0 + q >= 1 && k0 + q < nbSeq;
+      dnb[q] = live ? tr.dNb : 0u;           // a dead step maps s to stT[s + dfs] ...
+      dfs[q] = live ? tr.dFS : 0;
+    }
+#ifdef ZH_STAMPS
+    __asm__ volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    u64 const kt1 = __builtin_amdgcn_s_memtime();
+    k3codes += kt1 - kt0;
+#endif
+    u32 sv[K3_BATCH];
+#pragma unroll
+    for (u32 q = 0; q < K3_BATCH; q++) {
+      sv[q] = s;
+      u32 const nb = (s + dnb[q]) >> 16;
+      u32 const nx2 = stT[min((s >> nb) + (u32)dfs[q], 1023u)];
+      bool const live = k0 + q >= 1 && k0 + q < nbSeq;
+      s = live ? nx2 : s;                    // ... and is discarded
+    }
+#ifdef ZH_STAMPS
+    __asm__ volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    k3chain += __builtin_amdgcn_s_memtime() - kt1;
+#endif
+    uint4 *dst = (uint4 *)(gst + k0);
+    dst[0] = make_uint4(sv[0] | (sv[1] << 16), sv[2] | (sv[3] << 16), sv[4] | (sv[5] << 16), sv[6] | (sv[7] << 16));
+    dst[1] = make_uint4(sv[8] | (sv[9] << 16), sv[10] | (sv[11] << 16), sv[12] | (sv[13] << 16), sv[14] | (sv[15] << 16));
+  }
+  ff[ZH_FF_SLL + t] = s;
+#ifdef ZH_STAMPS
+  if (t == 0) { u32 *dbg = ws.dbg(bb); dbg[46] = (u32)(__builtin_amdgcn_s_memtime() - k3t0); dbg[47] = (u32)k3codes; dbg[48] = (u32)k3chain; dbg[49] = nbSeq; }
+#endif
+}
+
+// ======================= sequence bitstream packing (K2b) =======================
+// One wave per block left by the entropy kernel: FSE state bits and extra bits of 64
+// encode steps per bit-sink append, final state flush, then the block is finished
+// (raw fallback, header, status) exactly as the entropy kernel does for other blocks.
+constexpr u32 KP_SW = 0, KP_DNB = 4 * SW_WORDS, KP_LDS = KP_DNB + 4 * 128;
+
+extern "C" __global__ __launch_bounds__(64) void zh_seq_pack_kernel(const ZhBlockDesc *__restrict__ blocks, ZhWorkspace ws, u64 *__restrict__ item_size,
+                                                                     u32 *__restrict__ item_status, u32 *__restrict__ blk_size) {
+  extern __shared__ __attribute__((aligned(16))) u8 smem[];
+  u32 const b = blockIdx.x, lane = lane_id();
+  ZhBlockDesc const d = blocks[b];
+  if (d.n == 0) return;
+  const u32 *ff = ws.fsef(b);
+  if (ff[ZH_FF_NEED] == 0) return;
+  u32 *sw = (u32 *)(smem + KP_SW);
+  u32 *dNb = (u32 *)(smem + KP_DNB);  // LL [0, 36), OF [40, 72), ML [72, 125)
+  const u8 *fz = ws.fse(b);
+  if (lane < 36) dNb[lane] = ((const FseSym *)(fz + ZH_FT_SYLL))[lane].dNb;
+  if (lane < 32) dNb[40 + lane] = ((const FseSym *)(fz + ZH_FT_SYOF))[lane].dNb;
+  if (lane < 53) dNb[72 + lane] = ((const FseSym *)(fz + ZH_FT_SYML))[lane].dNb;
+  if (lane == 0) sw[0] = 0;
+  u32 const nbSeq = ff[ZH_FF_NBSEQ], logs = ff[ZH_FF_LOGS], blk = ff[ZH_FF_BLK];
+  u32 const logLL = logs & 255u, logOF = (logs >> 8) & 255u, logML = logs >> 16;
+  u32 const sLL = ff[ZH_FF_SLL], sOF = ff[ZH_FF_SOF], sML = ff[ZH_FF_SML];
+  Out const o{d.dst, d.dst_cap};
+  const u64 *seq = ws.seq(b);
+  u32 const NS = (nbSeq + 15) & ~15u;
+  const u16 *gLL = (const u16 *)ws.lits(b), *gOF = gLL + NS, *gML = gOF + NS;
+  CodeTabs ct;
+  ct.load();
+  wave_sync();
+  BitSink bs{ff[ZH_FF_OP], 0};
+  u64 nrec = lane < nbSeq ? seq[nbSeq - 1 - lane] : 0;
+  u32 nL = 0 < lane && lane < nbSeq ? gLL[lane] : 0u, nM = 0 < lane && lane < nbSeq ? gML[lane] : 0u, nO = 0 < lane && lane < nbSeq ? gOF[lane] : 0u;
+  for (u32 e0 = 0; e0 < nbSeq; e0 += 64) {
+    u32 const e = e0 + lane;
+    bool const valid = e < nbSeq;
+    u64 const rec = nrec;
+    u32 const s_L = nL, s_M = nM, s_O = nO;
+    u32 const en = e + 64;
+    nrec = en < nbSeq ? seq[nbSeq - 1 - en] : 0;  // next chunk in flight
+    nL = en < nbSeq ? gLL[en] : 0u; nM = en < nbSeq ? gML[en] : 0u; nO = en < nbSeq ? gOF[en] : 0u;
+    u32 const ll = (u32)(rec & 0x1FFFFu), mlb = (u32)((rec >> 17) & 0x1FFFFu), ob = (u32)(rec >> 34) & 0x1FFFFu;
+    u32 const llc = valid ? (u32)(rec >> 51) & 63u : 0, mlc = valid ? (u32)(rec >> 57) & 63u : 0, ofc = valid ? highbit32(ob) : 0;
+    u32 const llbits = ct.ll_bits(llc), mlbits = ct.ml_bits(mlc);
+    u32 vOF = 0, nOF = 0, vML = 0, nML = 0, vLL = 0, nLL = 0;
+    if (valid && e > 0) {
+      nOF = (s_O + dNb[40 + ofc]) >> 16; vOF = s_O;
+      nML = (s_M + dNb[72 + mlc]) >> 16; vML = s_M;
+      nLL = (s_L + dNb[llc]) >> 16; vLL = s_L;
+    }
+    u32 v6[6] = {vOF, vML, vLL, ll, mlb, ob};
+    u32 n6[6] = {nOF, nML, nLL, valid ? llbits : 0u, valid ? mlbits : 0u, ofc};
+    sink_append<6>(bs, o, sw, v6, n6);
+  }
+  {
+    u32 v3[3] = {sML, sOF, sLL};
+    u32 n3[3] = {lane == 0 ? logML : 0u, lane == 0 ? logOF : 0u, lane == 0 ? logLL : 0u};
+    sink_append<3>(bs, o, sw, v3, n3);
+  }
+  sink_close(bs, o, sw);
+  u32 const total = finish_block(d, o, blk, bs.pos, false);
+  write_status(d, b, total, item_size, item_status, blk_size);
 }
 
 extern "C" u32 zh_entropy_lds_bytes() { return K2_LDS; }
 
 namespace zh {
-hipError_t entropy_init() { return hipFuncSetAttribute((const void *)zh_entropy_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)K2_LDS); }
+hipError_t entropy_init() {
+  hipError_t e = hipFuncSetAttribute((const void *)zh_entropy_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)K2_LDS);
+  if (e == hipSuccess) e = hipFuncSetAttribute((const void *)zh_fse_chain_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)K3_LDS);
+  return e;
+}
 void entropy_launch(const ZhBlockDesc *d_descs, u32 nblocks, ZhWorkspace ws, u32 window_log, u32 cfg_block_size, u64 *d_item_size,
                     u32 *d_item_status, u32 *d_blk_size, hipStream_t stream) {
   hipLaunchKernelGGL(zh_entropy_kernel, dim3(nblocks), dim3(K2_THREADS), K2_LDS, stream, d_descs, ws, window_log, cfg_block_size, d_item_size,
                      d_item_status, d_blk_size);
+  hipLaunchKernelGGL(zh_fse_chain_kernel, dim3((nblocks + K3_BLOCKS - 1) / K3_BLOCKS), dim3(64), K3_LDS, stream, d_descs, nblocks, ws);
+  hipLaunchKernelGGL(zh_seq_pack_kernel, dim3(nblocks), dim3(64), KP_LDS, stream, d_descs, ws, d_item_size, d_item_status, d_blk_size);
 }
 }  // namespace zh
