@@ -30,12 +30,14 @@ enum : u32 {
 
 // Per-block workspace carved from the caller's temp buffer.
 //   seq   : ZH_SEQ_CAP u64 records (K1: cumLit | ml<<17 | off<<25; K2 rewrites in place)
-//   lits  : ZH_BLOCK_MAX literal bytes; after the literals section is written, the FSE
-//           states before each encode step (u16, LL | OF | ML arrays of nbSeq each)
+//   lits  : ZH_BLOCK_MAX literal bytes; once the literals section is written, the
+//           sequences' FSE codes and states in encoding order, per table (LL, OF, ML),
+//           NS = nbSeq rounded up to 32 entries each: states u16 [0, 6 NS), codes u8 [6 NS, 9 NS)
 //   meta  : u32[4] = {nseq, nlit, rle, 0}
 #define ZH_SEQ_CAP 13120u
 #define ZH_SEQ_BYTES (ZH_SEQ_CAP * 8u)
-#define ZH_LIT_BYTES (6u * ZH_SEQ_CAP > (u32)ZH_BLOCK_MAX ? 6u * ZH_SEQ_CAP : (u32)ZH_BLOCK_MAX)
+#define ZH_LIT_BYTES (9u * ZH_SEQ_CAP > (u32)ZH_BLOCK_MAX ? 9u * ZH_SEQ_CAP : (u32)ZH_BLOCK_MAX)
+static_assert(ZH_SEQ_CAP % 32 == 0, "state / code arrays are padded to 32 entries");
 #define ZH_META_BYTES 256u  // u32[4] counters + u32[60] diagnostic stamps (-DZH_STAMPS builds)
 //   fse   : hand-off from the entropy kernel to the FSE chain and packing kernels:
 //           the block's three FSE tables (state tables + symbol transforms, ZH_FSE_TAB_BYTES)

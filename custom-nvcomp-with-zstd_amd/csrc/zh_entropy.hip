@@ -512,61 +512,6 @@ __device__ u32 huf_set_max_height(HufNode *huffNode, u32 lastNonNull, u32 maxNbB
   return maxNbBits;
 }
 
-// returns maxNbBits (0 on error); fills hval/hnb for symbols 0..maxSV
-__device__ u32 huf_build_ctable(HufNode *huffNode0, u16 *hval, u8 *hnb, const u32 *count, u32 maxSV, u32 maxNbBits, SerialScratch *scr) {
-  HufNode *const huffNode = huffNode0 + 1;
-  int const STARTNODE = 256;
-  for (int i = 0; i < 2 * 256 + 2; i++) { huffNode0[i].count = 0; huffNode0[i].parent = 0; huffNode0[i].byte = 0; huffNode0[i].nbBits = 0; }
-  // HUF_sort
-  {
-    u32 *base = scr->base, *curr = scr->curr;
-    for (int r = 0; r < 32; r++) base[r] = 0;
-    for (u32 n = 0; n <= maxSV; n++) base[highbit32(count[n] + 1)]++;
-    for (u32 n = 30; n > 0; n--) base[n - 1] += base[n];
-    for (int r = 0; r < 32; r++) curr[r] = base[r];
-    for (u32 n = 0; n <= maxSV; n++) {
-      u32 const c = count[n];
-      u32 const r = highbit32(c + 1) + 1;
-      u32 pos = curr[r]++;
-      while ((pos > base[r]) && (c > huffNode[pos - 1].count)) { huffNode[pos] = huffNode[pos - 1]; pos--; }
-      huffNode[pos].count = c;
-      huffNode[pos].byte = (u8)n;
-    }
-  }
-  int nonNullRank = (int)maxSV;
-  while (huffNode[nonNullRank].count == 0) nonNullRank--;
-  int lowS = nonNullRank, nodeNb = STARTNODE;
-  int const nodeRoot = nodeNb + lowS - 1;
-  int lowN = nodeNb;
-  huffNode[nodeNb].count = huffNode[lowS].count + huffNode[lowS - 1].count;
-  huffNode[lowS].parent = huffNode[lowS - 1].parent = (u16)nodeNb;
-  nodeNb++;
-  lowS -= 2;
-  for (int n = nodeNb; n <= nodeRoot; n++) huffNode[n].count = 1u << 30;
-  huffNode0[0].count = 1u << 31;
-  while (nodeNb <= nodeRoot) {
-    int const n1 = (huffNode[lowS].count < huffNode[lowN].count) ? lowS-- : lowN++;
-    int const n2 = (huffNode[lowS].count < huffNode[lowN].count) ? lowS-- : lowN++;
-    huffNode[nodeNb].count = huffNode[n1].count + huffNode[n2].count;
-    huffNode[n1].parent = huffNode[n2].parent = (u16)nodeNb;
-    nodeNb++;
-  }
-  huffNode[nodeRoot].nbBits = 0;
-  for (int n = nodeRoot - 1; n >= STARTNODE; n--) huffNode[n].nbBits = huffNode[huffNode[n].parent].nbBits + 1;
-  for (int n = 0; n <= nonNullRank; n++) huffNode[n].nbBits = huffNode[huffNode[n].parent].nbBits + 1;
-  maxNbBits = huf_set_max_height(huffNode, (u32)nonNullRank, maxNbBits, scr);
-  if (maxNbBits > 12) return 0;
-  u16 *nbPerRank = scr->nbPerRank, *valPerRank = scr->valPerRank;
-  for (int i = 0; i < 13; i++) { nbPerRank[i] = 0; valPerRank[i] = 0; }
-  for (int n = 0; n <= nonNullRank; n++) nbPerRank[huffNode[n].nbBits]++;
-  {
-    u16 mn = 0;
-    for (int n = (int)maxNbBits; n > 0; n--) { valPerRank[n] = mn; mn += nbPerRank[n]; mn >>= 1; }
-  }
-  for (u32 n = 0; n <= maxSV; n++) hnb[huffNode[n].byte] = huffNode[n].nbBits;
-  for (u32 n = 0; n <= maxSV; n++) hval[n] = valPerRank[hnb[n]]++;
-  return maxNbBits;
-}
 
 // --- wave-parallel HUF_buildCTable (same result as huf_build_ctable above) ---
 // element e of a 256-key array lives in lane e/4, slot e%4
@@ -1174,6 +1119,8 @@ extern "C" __global__ __launch_bounds__(K2_THREADS) void zh_entropy_kernel(const
       u64 const below = (1ull << lane) - 1ull;
       CodeTabs ct;
       ct.load();
+      u32 const NS = (nbSeq + 31) & ~31u;
+      u8 *const cb = ws.lits(b) + 6 * NS;  // codes in encoding order (step nbSeq-1-i), per table
       u64 nrec = lane < nbSeq ? seq[lane] : 0;
       for (u32 base = 0; base < nbSeq; base += 64) {
         u32 const i = base + lane;
@@ -1212,6 +1159,8 @@ extern "C" __global__ __launch_bounds__(K2_THREADS) void zh_entropy_kernel(const
           atomicAdd(&hOF[highbit32(ob)], 1u);
           // + the LL / ML codes in the spare top bits (ob < 2^17: offsets stay inside the block)
           seq[i] = (u64)ll | ((u64)mlb << 17) | ((u64)ob << 34) | ((u64)llc << 51) | ((u64)mlc << 57);
+          u32 const k = nbSeq - 1 - i;
+          cb[k] = (u8)llc; cb[NS + k] = (u8)highbit32(ob); cb[2 * NS + k] = (u8)mlc;
         }
       }
       wave_sync();
@@ -1325,7 +1274,8 @@ extern "C" __global__ __launch_bounds__(K2_THREADS) void zh_entropy_kernel(const
 // Encoding step e (e >= 1) encodes sequence nbSeq-1-e from the state the previous step
 // left (step 0 is FSE_initCState2 with the last sequence's code).  The state before
 // each step goes to the block's literal area (free by now) as u16 (table t at
-// [t * NS, t * NS + nbSeq), NS = nbSeq rounded up to 16); the final states go to the fse fields.
+// [t * NS, t * NS + nbSeq), NS = nbSeq rounded up to 32); the codes come from pass B of
+// the entropy kernel (u8 arrays after the states); the final states go to the fse fields.
 constexpr u32 K3_BLOCKS = 11;  // 39 KB of LDS: 4 workgroups (one per SIMD) per CU
 constexpr u32 K3_CODES = 192;  // LDS: c_LL_code (64) + c_ML_code (128)
 constexpr u32 K3_LDS = K3_CODES + K3_BLOCKS * ZH_FSE_TAB_BYTES;
@@ -1367,52 +1317,40 @@ extern "C" __global__ __launch_bounds__(64) void zh_fse_chain_kernel(const ZhBlo
   const u8 *tb = smem + K3_CODES + j * ZH_FSE_TAB_BYTES;
   const u16 *stT = (const u16 *)(tb + (t == 0 ? ZH_FT_STLL : t == 1 ? ZH_FT_STOF : ZH_FT_STML));
   const FseSym *syT = (const FseSym *)(tb + (t == 0 ? ZH_FT_SYLL : t == 1 ? ZH_FT_SYOF : ZH_FT_SYML));
-  const u64 *seq = ws.seq(bb);
-  u16 *gst = (u16 *)ws.lits(bb) + t * ((nbSeq + 15) & ~15u);  // 32-B aligned per table
-  // this lane's code of a record: LL / ML codes ride in the record's top bits (pass B)
-  u32 const csh = t == 0 ? 51u : 57u;
-  auto code_of = [&](u64 rec) -> u32 {
-    u32 const ofc = 31u - __builtin_clz(((u32)(rec >> 34) & 0x1FFFFu) | 1u);
-    return t == 1 ? ofc : (u32)(rec >> csh) & 63u;
-  };
+  u32 const NS = (nbSeq + 31) & ~31u;
+  u16 *gst = (u16 *)ws.lits(bb) + t * NS;              // states (64-B aligned per table)
+  const u8 *cb = ws.lits(bb) + 6 * NS + t * NS;        // codes in encoding order
   u32 s;
   {
-    FseSym const tr = syT[code_of(seq[nbSeq - 1])];  // FSE_initCState2
+    FseSym const tr = syT[cb[0]];  // FSE_initCState2 with the last sequence's code
     u32 const nb = (tr.dNb + (1u << 15)) >> 16;
     s = stT[(((nb << 16) - tr.dNb) >> nb) + tr.dFS];
   }
-  // batches of 16 steps aligned to the state array (entry 0 and entries >= nbSeq are
-  // padding), so each lane writes its 16 states with two 16-byte stores
-  u64 nx[2][K3_BATCH];  // two batches of records in flight ahead of the chain
-#pragma unroll
-  for (u32 q = 0; q < 2 * K3_BATCH; q++) nx[q / K3_BATCH][q % K3_BATCH] = seq[nbSeq - 1 - min(q, nbSeq - 1)];  // clamped: always valid
+  // Batches of 16 steps: one 16-byte load of codes per lane (loaded two batches ahead,
+  // ping-pong buffers: no copies of loads in flight), symbol transforms, the dependent
+  // chain (one LDS round trip per step), two 16-byte stores of the states.  Steps
+  // outside [1, nbSeq) are dead (predicated; padding entries of both arrays).
 #ifdef ZH_STAMPS
   u64 const k3t0 = __builtin_amdgcn_s_memtime();
-  u64 k3chain = 0, k3codes = 0;
+  u64 k3chain = 0, k3codes = 0, k3wait = 0;
 #endif
-  for (u32 k0 = 0; k0 < nbSeq; k0 += K3_BATCH) {
+  uint4 ca = ((const uint4 *)cb)[0], cc = ((const uint4 *)cb)[1];
+  auto batch = [&](u32 k0, uint4 &c4) {
 #ifdef ZH_STAMPS
     u64 const kt0 = __builtin_amdgcn_s_memtime();
 #endif
-    u32 cd[K3_BATCH];
-#pragma unroll
-    for (u32 q = 0; q < K3_BATCH; q++) cd[q] = code_of(nx[0][q]);
-#pragma unroll
-    for (u32 q = 0; q < K3_BATCH; q++) {
-      nx[0][q] = nx[1][q];
-      nx[1][q] = seq[nbSeq - 1 - min(k0 + 2 * K3_BATCH + q, nbSeq - 1)];
-    }
-    // symbol transforms first (independent of the state), then the dependent chain:
-    // one LDS round trip per step, predicated without branches
+    u32 const w[4] = {c4.x, c4.y, c4.z, c4.w};
     u32 dnb[K3_BATCH];
     s32 dfs[K3_BATCH];
 #pragma unroll
     for (u32 q = 0; q < K3_BATCH; q++) {
-      FseSym const tr = syT[cd[q]];
+      FseSym const tr = syT[(w[q >> 2] >> (8 * (q & 3))) & 63u];
       bool const live = k0 + q >= 1 && k0 + q < nbSeq;
-      dnb[q] = live ? tr.dNb : 0u;           // a dead step maps s to stT[s + dfs] ...
+      dnb[q] = live ? tr.dNb : 0u;  // a dead step maps s to stT[s] ...
       dfs[q] = live ? tr.dFS : 0;
     }
+    u32 const kn = k0 + 2 * K3_BATCH;
+    if (kn < NS) c4 = *(const uint4 *)(cb + kn);
 #ifdef ZH_STAMPS
     __asm__ volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     u64 const kt1 = __builtin_amdgcn_s_memtime();
@@ -1425,7 +1363,7 @@ extern "C" __global__ __launch_bounds__(64) void zh_fse_chain_kernel(const ZhBlo
       u32 const nb = (s + dnb[q]) >> 16;
       u32 const nx2 = stT[min((s >> nb) + (u32)dfs[q], 1023u)];
       bool const live = k0 + q >= 1 && k0 + q < nbSeq;
-      s = live ? nx2 : s;                    // ... and is discarded
+      s = live ? nx2 : s;  // ... and is discarded
     }
 #ifdef ZH_STAMPS
     __asm__ volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -1434,6 +1372,10 @@ extern "C" __global__ __launch_bounds__(64) void zh_fse_chain_kernel(const ZhBlo
     uint4 *dst = (uint4 *)(gst + k0);
     dst[0] = make_uint4(sv[0] | (sv[1] << 16), sv[2] | (sv[3] << 16), sv[4] | (sv[5] << 16), sv[6] | (sv[7] << 16));
     dst[1] = make_uint4(sv[8] | (sv[9] << 16), sv[10] | (sv[11] << 16), sv[12] | (sv[13] << 16), sv[14] | (sv[15] << 16));
+  };
+  for (u32 k0 = 0; k0 < nbSeq; k0 += 2 * K3_BATCH) {  // NS is a multiple of 32
+    batch(k0, ca);
+    batch(k0 + K3_BATCH, cc);
   }
   ff[ZH_FF_SLL + t] = s;
 #ifdef ZH_STAMPS
@@ -1467,7 +1409,7 @@ extern "C" __global__ __launch_bounds__(64) void zh_seq_pack_kernel(const ZhBloc
   u32 const sLL = ff[ZH_FF_SLL], sOF = ff[ZH_FF_SOF], sML = ff[ZH_FF_SML];
   Out const o{d.dst, d.dst_cap};
   const u64 *seq = ws.seq(b);
-  u32 const NS = (nbSeq + 15) & ~15u;
+  u32 const NS = (nbSeq + 31) & ~31u;
   const u16 *gLL = (const u16 *)ws.lits(b), *gOF = gLL + NS, *gML = gOF + NS;
   CodeTabs ct;
   ct.load();

@@ -35,11 +35,11 @@ off = a256(off + n * 8)
 off = a256(off + n * 4)
 off = a256(off + 0)
 blocks = base + off
-WS = 13120 * 8 + 78720 + 256 + 4096
+WS = 13120 * 8 + 118080 + 256 + 4096
 h = temp.cpu().numpy()
-m0 = h[blocks + 13120 * 8 + 78720: blocks + 13120 * 8 + 78720 + 16].view(np.uint32)
+m0 = h[blocks + 13120 * 8 + 118080: blocks + 13120 * 8 + 118080 + 16].view(np.uint32)
 print('block 0 meta (nseq, nlit, rle):', m0[:3].tolist(), 'temp', temp.numel(), 'blocks off', blocks, 'n*WS', n * WS)
-raw = np.array([h[blocks + b * WS + 13120 * 8 + 78720 + 16: blocks + b * WS + 13120 * 8 + 78720 + 16 + 52 * 4].view(np.uint32) for b in range(n)])
+raw = np.array([h[blocks + b * WS + 13120 * 8 + 118080 + 16: blocks + b * WS + 13120 * 8 + 118080 + 16 + 52 * 4].view(np.uint32) for b in range(n)])
 st = raw[:, :6]
 k2 = raw[:, 6:15].astype(np.float64)
 names = ["stage", "A(insert)", "B(lengths+exit)", "J(jacobi)", "E(emit)", "rounds"]
@@ -55,11 +55,11 @@ t2 = k2.sum(1).mean()
 print(kind, "K2 mean cycles/block", int(t2))
 for k, nm in enumerate(k2n):
     print(f"  {nm:20s} mean {k2[:, k].mean():12.0f}  share {k2[:, k].mean() / t2 * 100:5.1f}%")
-print(f"  of huf_build: parallel tree {np.array([h[blocks + b * WS + 13120 * 8 + 78720 + 16 + 42 * 4: blocks + b * WS + 13120 * 8 + 78720 + 16 + 43 * 4].view(np.uint32)[0] for b in range(n)]).mean():.0f}")
-print(f"  K3 per block: total {raw[:, 46].mean():.0f}  codes+loads {raw[:, 47].mean():.0f}  chain {raw[:, 48].mean():.0f}  nbSeq {raw[:, 49].mean():.0f}")
+print(f"  of huf_build: parallel tree {np.array([h[blocks + b * WS + 13120 * 8 + 118080 + 16 + 42 * 4: blocks + b * WS + 13120 * 8 + 118080 + 16 + 43 * 4].view(np.uint32)[0] for b in range(n)]).mean():.0f}")
+print(f"  K3 per block: total {raw[:, 46].mean():.0f}  codes+loads {raw[:, 47].mean():.0f}  chain {raw[:, 48].mean():.0f}  (record wait {raw[:, 50].mean():.0f})  nbSeq {raw[:, 49].mean():.0f}")
 print(f"  of fse_chains: serial chain steps only {raw[:, 18].mean():.0f}  raw seqs mean {raw[:, 19].mean():.0f}")
 # wall clock per block (s_memrealtime, 100 MHz) and placement
-rt = np.array([h[blocks + b * WS + 13120 * 8 + 78720 + 16 + 23 * 4: blocks + b * WS + 13120 * 8 + 78720 + 16 + 28 * 4].view(np.uint32) for b in range(n)]).astype(np.int64)
+rt = np.array([h[blocks + b * WS + 13120 * 8 + 118080 + 16 + 23 * 4: blocks + b * WS + 13120 * 8 + 118080 + 16 + 28 * 4].view(np.uint32) for b in range(n)]).astype(np.int64)
 dur = (rt[:, 1] - rt[:, 0]) & 0xFFFFFFFF
 print(f"  block wall (realtime 100MHz ticks) mean {dur.mean():.0f} = {dur.mean() * 10:.0f} ns; memtime mean {rt[:, 4].mean():.0f} -> clock {rt[:, 4].mean() / (dur.mean() * 10):.2f} GHz")
 cu = (rt[:, 3] & 0xFFFFFFFF).astype(np.int64) * 1000 + ((rt[:, 2] >> 8) & 0xF) + 16 * ((rt[:, 2] >> 12) & 0x1) + 32 * ((rt[:, 2] >> 13) & 0x7)
@@ -69,6 +69,6 @@ busy = {}
 for c, d in zip(cu.tolist(), dur.tolist()):
     busy[c] = busy.get(c, 0) + d
 print(f"  per-CU busy fraction of span: mean {np.mean(list(busy.values())) / (t1 - t0):.3f}")
-mx = np.array([h[blocks + b * WS + 13120 * 8 + 78720 + 16 + 40 * 4: blocks + b * WS + 13120 * 8 + 78720 + 16 + 42 * 4].view(np.uint32) for b in range(n)])
+mx = np.array([h[blocks + b * WS + 13120 * 8 + 118080 + 16 + 40 * 4: blocks + b * WS + 13120 * 8 + 118080 + 16 + 42 * 4].view(np.uint32) for b in range(n)])
 if kind:
     print(f"  B-work max over worker waves {mx[:, 0].mean():.0f}   inserter busy max {mx[:, 1].mean():.0f}  (per block)")
