@@ -451,7 +451,7 @@ __device__ __forceinline__ u32 fse_step(const u16 *st, const FseSym *sym, u32 &s
   return v;
 }
 
-// ---------------- Huffman (libzstd v1.4.9 HUF_buildCTable; lane-0 serial) ----------------
+// ---------------- Huffman (libzstd v1.4.9 HUF_buildCTable) ----------------
 struct HufNode { u32 count; u16 parent; u8 byte; u8 nbBits; };
 
 __device__ u32 huf_set_max_height(HufNode *huffNode, u32 lastNonNull, u32 maxNbBits, SerialScratch *scr) {
@@ -513,7 +513,7 @@ __device__ u32 huf_set_max_height(HufNode *huffNode, u32 lastNonNull, u32 maxNbB
 }
 
 
-// --- wave-parallel HUF_buildCTable (same result as huf_build_ctable above) ---
+// --- wave-parallel HUF_buildCTable (same tree and code lengths as libzstd's serial build) ---
 // element e of a 256-key array lives in lane e/4, slot e%4
 __device__ __forceinline__ void bitonic_sort_desc_256(u32 (&key)[4]) {
   u32 const lane = lane_id();
