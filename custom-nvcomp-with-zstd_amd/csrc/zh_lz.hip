@@ -83,7 +83,10 @@ __device__ __forceinline__ u32 prefix8(const u32 *in32, u32 b, u32 olo, u32 ohi)
   u32 blo, bhi;
   ld64u(in32, b, blo, bhi);
   u32 const x = olo ^ blo, y = ohi ^ bhi;
-  return x ? (__builtin_ctz(x) >> 3) : (y ? 4 + (__builtin_ctz(y) >> 3) : 8u);
+  // branch-free (v_cndmask): divergent branches cost exec-mask work on the CU's
+  // shared scalar unit
+  u32 const cx = __builtin_ctzg(x, 32), cy = __builtin_ctzg(y, 32);
+  return (x ? cx : 32u + cy) >> 3;
 }
 
 // Extension of a chain head (p, q) whose first 8 bytes match: E = min(common prefix,
@@ -383,14 +386,22 @@ extern "C" __global__ __launch_bounds__(K1_THREADS) void zh_lz_kernel(const ZhBl
       for (u32 j = 0; j < SB; j++) {
         u32 const p = s + j;
         bool const v = p < se && p < lim;
-        cv[j] = v ? ci[cidx(cbase + j)] : 0u;
+        u32 const cw = ci[cidx(cbase + j)];
+        cv[j] = v ? cw : 0u;
         u32 olo, ohi;
         ld64u(in32, min(p, lim), olo, ohi);
         u32 const cL = cv[j] & 0xFFFFu, cS = cv[j] >> 16;
-        // (skipped by the whole wave when no lane has a candidate here: rare matches)
+        // wave-uniform skips (no lane has a candidate: rare matches), branch-free inside
         u32 xL = 0, xS = 0;
-        if (cL) xL = prefix8(in32, cL - 1, olo, ohi);
-        if (cS && cS != cL) xS = prefix8(in32, cS - 1, olo, ohi);
+        if (__ballot(cL != 0)) {
+          u32 const t = prefix8(in32, cL ? cL - 1 : 0u, olo, ohi);
+          xL = cL ? t : 0u;
+        }
+        bool const hasS = cS && cS != cL;
+        if (__ballot(hasS)) {
+          u32 const t = prefix8(in32, hasS ? cS - 1 : 0u, olo, ohi);
+          xS = hasS ? t : 0u;
+        }
         plp |= xL << (4 * j);
         psp |= xS << (4 * j);
       }
@@ -398,24 +409,30 @@ extern "C" __global__ __launch_bounds__(K1_THREADS) void zh_lz_kernel(const ZhBl
 #define PS(j) ((psp >> (4 * (j))) & 15u)
       // (2) chains: a candidate with 8 matching bytes that continues a previous-position
       //     candidate with the same offset (also 8 matching) is a follower; else a head
+      //     Bit-parallel over the thread's SB positions (bit j = position j), no branches:
+      //     e = 8 matching bytes (nibble bit 3 of the packed prefix; 0 without a
+      //     candidate), continuation = candidate == previous position's candidate + 1.
+      auto nib8 = [](u32 pk) {  // bit j = nibble j == 8
+        u32 const x = (pk >> 3) & 0x11111u;
+        return (x & 1u) | ((x >> 3) & 2u) | ((x >> 6) & 4u) | ((x >> 9) & 8u) | ((x >> 12) & 16u);
+      };
+      u32 const eL = nib8(plp), eS = nib8(psp);
       u32 dL = 0, dS = 0, fromSL = 0, fromSS = 0, heads = 0;  // heads: bit j = L, bit 8 + j = S
+      if (__ballot((eL | eS) != 0)) {  // (wave-uniform skip: no 8-byte match in the wave)
+        u32 mLL = 0, mLS = 0, mSL = 0, mSS = 0;  // bit j: cX_j == cY_{j-1} + 1
 #pragma unroll
-      for (u32 j = 0; j < SB; j++) {
-        u32 const cL = cv[j] & 0xFFFFu, cS = cv[j] >> 16;
-        bool const eL = cL && PL(j) == 8, eS = cS && cS != cL && PS(j) == 8;
-        u32 const pcL = j ? (cv[j - 1] & 0xFFFFu) : 0u, pcS = j ? (cv[j - 1] >> 16) : 0u;
-        bool const peL = j && pcL && PL(j - 1) == 8;
-        bool const peS = j && pcS && pcS != pcL && PS(j - 1) == 8;
-        if (eL) {
-          if (peL && cL == pcL + 1) dL |= 1u << j;
-          else if (peS && cL == pcS + 1) { dL |= 1u << j; fromSL |= 1u << j; }
-          else heads |= 1u << j;
+        for (u32 j = 1; j < SB; j++) {
+          u32 const cL = cv[j] & 0xFFFFu, cS = cv[j] >> 16, pL1 = (cv[j - 1] & 0xFFFFu) + 1, pS1 = (cv[j - 1] >> 16) + 1;
+          mLL |= cL == pL1 ? 1u << j : 0u;
+          mLS |= cL == pS1 ? 1u << j : 0u;
+          mSL |= cS == pL1 ? 1u << j : 0u;
+          mSS |= cS == pS1 ? 1u << j : 0u;
         }
-        if (eS) {
-          if (peL && cS == pcL + 1) dS |= 1u << j;
-          else if (peS && cS == pcS + 1) { dS |= 1u << j; fromSS |= 1u << j; }
-          else heads |= 1u << (8 + j);
-        }
+        u32 const peL = eL << 1, peS = eS << 1;
+        u32 const fLL = eL & peL & mLL, fLS = eL & ~fLL & peS & mLS;
+        u32 const fSL = eS & peL & mSL, fSS = eS & ~fSL & peS & mSS;
+        dL = fLL | fLS; dS = fSL | fSS; fromSL = fLS; fromSS = fSS;
+        heads = (eL & ~dL) | ((eS & ~dS) << 8);
       }
       // (3) extend the heads, compacted across the wave: heads are ranked in (lane, bit)
       //     order and handed out 64 at a time, one per lane (wave-private LDS slots;
