@@ -49,7 +49,7 @@ constexpr u32 OFF_CI = OFF_TS + 4 * HS_SIZE;
 constexpr u32 CI_WORDS = ZH_WINDOW + 8;  // + the lookahead slot of position `we`
 __device__ __forceinline__ u32 cidx(u32 i) { return i; }
 constexpr u32 OFF_EXB = OFF_CI + 4 * CI_WORDS;      // u8 per position: its parse segment exit (relative)
-constexpr u32 OFF_SEG = OFF_EXB + ZH_WINDOW;        // parse segment entries + the window exit
+constexpr u32 OFF_SEG = OFF_EXB + ZH_WINDOW + 16;   // parse segment entries + the window exit (exb: + a junk byte)
 constexpr u32 NWW = INS_TID / 64;                   // worker waves
 constexpr u32 PR = (ZH_WINDOW + INS_TID - 1) / INS_TID;  // lane-per-position rounds over a window
 constexpr u32 WP_OFF = 80, WP_TOT = 160;
@@ -211,11 +211,16 @@ __device__ __forceinline__ void dump_window(u8 *ci8, u32 lane_, const u32 (&creg
 // k < 6, and X[6] = the segment exit, relative to the segment start (values >= the
 // segment length mean "left the segment").  Returns the match info of i if the parse
 // takes a match there, else 0.
+// v from lane `src` (< 64) of the wave: ds_bpermute on a byte address, no lane-base math
+__device__ __forceinline__ u32 bperm(u32 v, u32 src) { return (u32)__builtin_amdgcn_ds_bpermute((int)(src << 2), (int)v); }
+
 __device__ __forceinline__ u32 parse_steps(const u32 *ci, u32 i, u32 wn, u32 la, u32 lane, u32 (&X)[7]) {
   u32 const sb = i & ~63u;
   u32 const slen = wn > sb ? min(64u, wn - sb) : 0u;
-  u32 const inf = i < wn ? ci[i] : 0u;
-  u32 const inf1 = i + 1 < wn ? ci[i + 1] : la;
+  // unconditional (clamped) loads, then selects: no exec-mask branches
+  u32 const r0 = ci[min(i, (u32)ZH_WINDOW)], r1 = ci[min(i + 1, (u32)ZH_WINDOW)];
+  u32 const inf = i < wn ? r0 : 0u;
+  u32 const inf1 = i + 1 < wn ? r1 : la;
   u32 const l = inf & 255u;
   bool const tk = l != 0 && (inf1 & 255u) <= l;
   u32 x = lane + (tk ? l : 1u);
@@ -223,7 +228,7 @@ __device__ __forceinline__ u32 parse_steps(const u32 *ci, u32 i, u32 wn, u32 la,
 #pragma unroll
     for (u32 k = 0; k < 6; k++) {
       X[k] = x;
-      u32 const y = __shfl(x, min(x, 63u), 64);
+      u32 const y = bperm(x, min(x, 63u));
       x = x < slen ? y : x;
     }
   } else {  // all literals in this segment: 2^k steps are 2^k positions
@@ -493,7 +498,7 @@ extern "C" __global__ __launch_bounds__(K1_THREADS) void zh_lz_kernel(const ZhBl
         u32 v = 0;
         if (lL && lL >= lS) v = ((p - (cL - 1)) << 8) | lL;
         else if (lS) v = ((p - (cS - 1)) << 8) | lS;
-        if (p < se) ci[cidx(cbase + j)] = v;
+        ci[p < se ? cidx(cbase + j) : ZH_WINDOW + 1 + j] = v;  // (past the run: junk slots)
       }
       if (tid == NB && we >= n) ci[cidx(ZH_WINDOW)] = 0;  // no position after the block
 #undef PL
@@ -526,7 +531,7 @@ extern "C" __global__ __launch_bounds__(K1_THREADS) void zh_lz_kernel(const ZhBl
       infr[rr] = parse_steps(ci, i, wn, la, lane, X);
 #pragma unroll
       for (u32 k = 0; k < 6; k++) xk[rr][k] = X[k];
-      if (i < wn) exb[i] = (u8)X[6];
+      exb[i < wn ? i : (u32)ZH_WINDOW] = (u8)X[6];  // (past the window: junk byte)
     }
     if (lane == 0) atomicAdd(&misc[MISC_ARR], 1u);
     __syncthreads();  // X: exits of all positions
@@ -570,7 +575,7 @@ extern "C" __global__ __launch_bounds__(K1_THREADS) void zh_lz_kernel(const ZhBl
       if (__ballot(infr[rr] != 0)) {
 #pragma unroll
         for (int k = 5; k >= 0; k--) {
-          u32 const y = __shfl(xk[rr][k], min(cur, 63u), 64);
+          u32 const y = bperm(xk[rr][k], min(cur, 63u));
           if (cur <= lane && y <= lane) cur = y;
         }
       } else {  // all literals: every position from the entry on is visited
