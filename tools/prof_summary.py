@@ -17,7 +17,7 @@ from collections import defaultdict
 tag = sys.argv[1] if len(sys.argv) > 1 else "r01"
 root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 src = os.path.join(root, "gpurun_out", f"prof_{tag}")
-ours = ("zh_lz_kernel", "zh_entropy_kernel", "zh_plan_kernel", "zh_gather_kernel")
+ours = ("zh_lz_kernel", "zh_entropy_kernel", "zh_fse_chain_kernel", "zh_seq_pack_kernel", "zh_plan_kernel", "zh_gather_kernel")
 
 stats = {}
 for r in csv.DictReader(open(os.path.join(src, "trace", "run_kernel_stats.csv"))):
