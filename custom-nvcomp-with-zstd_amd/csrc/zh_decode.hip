@@ -1,0 +1,963 @@
+// zh_decode.hip — gfx950 Zstandard decoder: RFC 8878 frames of any
+// origin (this library's or libzstd's), one workgroup of one wave64 per input buffer.
+//
+// Replaces the reference's GPU decompression path (src/cuda_zstd_manager.cu:3194-3706,
+// 4292-5530: block walk, literal/sequence decode, execution; Huffman decoder
+// src/cuda_zstd_huffman.cu:1572-1833, 2204-2438; FSE decoder src/cuda_zstd_fse.cu:3839-4300;
+// sequence execution src/cuda_zstd_sequence.cu:203-575).  The reference decodes one
+// block per host round trip with ~10 launches; here a whole batch of frames is one
+// launch and nothing returns to the host until the sizes/statuses are ready.
+//
+// Per input buffer (frames + skippable frames, concatenated), per block:
+//   literals   raw / RLE are used in place; Huffman (direct or FSE-compressed weights,
+//              1 or 4 streams, treeless reuse) decoded by lanes 0..3 into the item's
+//              workspace slot
+//   sequences  NCount / RLE / predefined / repeat tables (LDS), the interleaved FSE
+//              bitstream decoded serially (the format has one state chain per table),
+//              repcodes resolved on the fly, records (ll | ml-3 | offset) to the slot
+//   execution  the block's output is produced through a 4 KiB LDS window: the wave
+//              copies one sequence at a time with lanes = bytes (a match byte reads
+//              position start - off + (i mod off), so overlapping copies need no
+//              byte-serial loop); sources before the window come from the already
+//              flushed output in HBM, sources inside it from LDS (a wave's LDS ops
+//              execute in order); each full window is flushed with coalesced stores
+//   checksum   XXH64 of the frame's output (4 lanes = the 4 accumulators), low 32 bits
+//              compared with the frame's checksum field
+// Error behaviour follows libzstd 1.4.9 (ZSTD_decompress): corrupt input -> ERROR_CORRUPT_DATA,
+// too little output capacity -> ERROR_BUFFER_TOO_SMALL, bad magic -> ERROR_INVALID_MAGIC,
+// checksum mismatch -> ERROR_CHECKSUM_FAILED, dictionary frames -> ERROR_DICTIONARY_MISMATCH.
+#include "zh_common.h"
+#include "zh_launch.h"
+
+typedef int64_t s64;
+
+namespace {
+
+constexpr u32 DEC_THREADS = 64;
+constexpr u32 DEC_STAGE = 4096;   // output window (LDS)
+constexpr u32 DEC_LSTAGE = 4096;  // literal window (LDS)
+constexpr u32 HUF_LOG_MAX = 11;   // RFC 8878 §4.2.1: Max_Number_of_Bits <= 11
+constexpr u32 BLOCKSIZE_MAX = 128u * 1024u;
+constexpr u32 OFF_LIMIT = 1u << 30;  // offsets are stored in 30 bits (windows up to 1 GiB)
+
+enum : u32 { ST_OK = 0, ST_INVALID = 2, ST_MAGIC = 5, ST_CORRUPT = 6, ST_SMALL = 7, ST_DICT = 9, ST_CHECKSUM = 10 };
+
+// sequence code tables (RFC 8878 §3.1.1.3.2.1.1): baseline | extra bits << 24
+__constant__ u32 c_LL_info[36] = {
+    0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15,
+    16 | 1u << 24, 18 | 1u << 24, 20 | 1u << 24, 22 | 1u << 24, 24 | 2u << 24, 28 | 2u << 24, 32 | 3u << 24, 40 | 3u << 24,
+    48 | 4u << 24, 64 | 6u << 24, 128 | 7u << 24, 256 | 8u << 24, 512 | 9u << 24, 1024 | 10u << 24, 2048 | 11u << 24,
+    4096 | 12u << 24, 8192 | 13u << 24, 16384 | 14u << 24, 32768 | 15u << 24, 65536 | 16u << 24};
+__constant__ u32 c_ML_info[53] = {
+    3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16, 17, 18, 19, 20, 21, 22, 23, 24, 25, 26, 27, 28, 29, 30, 31, 32, 33, 34,
+    35 | 1u << 24, 37 | 1u << 24, 39 | 1u << 24, 41 | 1u << 24, 43 | 2u << 24, 47 | 2u << 24, 51 | 3u << 24, 59 | 3u << 24,
+    67 | 4u << 24, 83 | 4u << 24, 99 | 5u << 24, 131 | 7u << 24, 259 | 8u << 24, 515 | 9u << 24, 1027 | 10u << 24,
+    2051 | 11u << 24, 4099 | 12u << 24, 8195 | 13u << 24, 16387 | 14u << 24, 32771 | 15u << 24, 65539 | 16u << 24};
+// predefined distributions (RFC 8878 §3.1.1.3.2.2.1-3)
+__constant__ s16 c_LL_norm[36] = {4, 3, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 1, 1, 1, 2, 2, 2, 2, 2, 2, 2, 2, 2, 3, 2, 1, 1, 1, 1, 1, -1, -1, -1, -1};
+__constant__ s16 c_ML_norm[53] = {1, 4, 3, 2, 2, 2, 2, 2, 2, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1,
+                                  1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, -1, -1, -1, -1, -1, -1, -1};
+__constant__ s16 c_OF_norm[29] = {1, 1, 1, 1, 1, 1, 2, 2, 2, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, -1, -1, -1, -1, -1};
+
+// table slots: LL, OF, ML (the order of the Symbol_Compression_Modes fields)
+constexpr u32 TAB_LL = 0, TAB_OF = 1, TAB_ML = 2;
+__device__ __forceinline__ u32 tab_off(u32 t) { return t == 0 ? 0u : t == 1 ? 512u : 768u; }
+__device__ __forceinline__ u32 tab_maxsv(u32 t) { return t == 0 ? 35u : t == 1 ? 31u : 52u; }
+__device__ __forceinline__ u32 tab_maxlog(u32 t) { return t == 1 ? 8u : 9u; }
+constexpr u32 TAB_NONE = 0xFFFFu, TAB_PREDEF = 0xFFFEu;  // tkind; else RLE symbol | 0x100, or 0 = FSE
+
+struct DecLds {
+  u32 fse[1280];  // LL [0,512) OF [512,768) ML [768,1280): sym | nbBits << 8 | newState << 16
+  union {
+    struct {
+      u16 dt[1 << HUF_LOG_MAX];  // Huffman decode table: sym | nbBits << 8
+      u32 wt[64];                // FSE table of the Huffman weights (log <= 6)
+      u8 symlist[256];           // symbols grouped by weight
+    } h;
+    struct {
+      u8 out[DEC_STAGE + 16];
+      u8 lit[DEC_LSTAGE + 16];
+    } x;
+  } u;
+  u32 info[2][64];  // LL / ML code info (baseline | bits << 24), copied from constants
+  s16 norm[256];    // NCount scratch
+  u16 next[256];    // FSE build scratch (symbolNext)
+  u8 hufw[256];     // Huffman weights of the last table (treeless literals rebuild from them)
+  u32 tlog[3];      // table logs
+  u32 tkind[3];     // TAB_NONE / TAB_PREDEF / RLE symbol | 0x100 / 0 = FSE
+  u32 hlog, hnsym, hvalid;
+  u32 err;   // serial-section status (lane 0 writes)
+  u32 used;  // serial-section byte count (lane 0 writes)
+};
+
+__device__ __forceinline__ u32 hb32(u32 v) { return 31u - (u32)__builtin_clz(v); }
+__device__ __forceinline__ u32 lane_id() { return threadIdx.x; }
+
+// ---- global reads of compressed bytes --------------------------------------------------
+// 8 bytes at p, all of them inside the input: only aligned dwords that hold at least one
+// of those bytes are loaded, so a read never touches a page the buffer does not reach.
+__device__ __forceinline__ u64 ldg64(const u8 *p) {
+  uintptr_t const a = (uintptr_t)p;
+  const u32 *w = (const u32 *)(a & ~(uintptr_t)3);
+  u32 const sh = (u32)(a & 3);
+  u32 const w0 = w[0], w1 = w[1];
+  u32 w2 = 0;
+  if (sh) w2 = w[2];
+  u32 const lo = __builtin_amdgcn_alignbyte(w1, w0, sh);
+  u32 const hi = __builtin_amdgcn_alignbyte(w2, w1, sh);
+  return ((u64)hi << 32) | lo;
+}
+__device__ __forceinline__ u32 rd16(const u8 *p) { return p[0] | (u32)p[1] << 8; }
+__device__ __forceinline__ u32 rd24(const u8 *p) { return p[0] | (u32)p[1] << 8 | (u32)p[2] << 16; }
+__device__ __forceinline__ u32 rd32(const u8 *p) { return p[0] | (u32)p[1] << 8 | (u32)p[2] << 16 | (u32)p[3] << 24; }
+
+// Backward bit reader (RFC 8878 §4.1: streams are read from the end; the last byte's
+// highest set bit marks the start).  pos = bits not yet consumed; reads past the start
+// return zeros and drive pos negative (libzstd's "overflow").
+struct BitRev {
+  const u8 *p;
+  s32 n, pos, cb;
+  u64 c;  // bytes [cb, cb + 8) of the stream (zero-extended for streams under 8 bytes)
+  __device__ __forceinline__ void fill(s32 b) {
+    cb = b;
+    if (n >= 8) {
+      c = ldg64(p + b);
+    } else {
+      u64 v = 0;
+      for (s32 i = 0; i < n; i++) v |= (u64)p[i] << (8 * i);
+      c = v;
+    }
+  }
+  __device__ __forceinline__ bool init(const u8 *s, u32 sz) {
+    p = s;
+    n = (s32)sz;
+    pos = 0;
+    cb = 0;
+    c = 0;
+    if (sz == 0) return false;
+    u32 const last = s[sz - 1];
+    if (!last) return false;
+    pos = 8 * ((s32)sz - 1) + (s32)hb32(last);
+    fill(n >= 8 ? n - 8 : 0);
+    return true;
+  }
+  // the k (<= 56) bits below pos, bit pos-1 as the MSB
+  __device__ __forceinline__ u64 peek(u32 k) {
+    s32 const lo = pos - (s32)k;
+    if (lo < 8 * cb) {
+      s32 nb = ((pos + 7) >> 3) - 8;
+      nb = nb < 0 ? 0 : nb;
+      if (n < 8) nb = 0;
+      else if (nb > n - 8) nb = n - 8;
+      if (nb != cb) fill(nb);
+    }
+    u64 const m = k ? (~0ull >> (64 - k)) : 0ull;
+    if (lo >= 8 * cb) return (c >> (lo - 8 * cb)) & m;
+    s32 const sh = 8 * cb - lo;  // cb == 0 here: missing low bits are zeros
+    return sh < 64 ? (c << sh) & m : 0ull;
+  }
+  __device__ __forceinline__ u32 read(u32 k) {
+    u32 const v = (u32)peek(k);
+    pos -= (s32)k;
+    return v;
+  }
+};
+
+// Forward 32-bit window at a bit position (NCount headers), zeros past the end.
+__device__ __forceinline__ u32 fwd32(const u8 *p, u32 avail, u32 bitpos) {
+  u32 const b = bitpos >> 3;
+  u64 v = 0;
+#pragma unroll
+  for (u32 i = 0; i < 5; i++)
+    if (b + i < avail) v |= (u64)p[b + i] << (8 * i);
+  return (u32)(v >> (bitpos & 7));
+}
+
+// FSE_readNCount (libzstd lib/common/entropy_common.c, RFC 8878 §4.1.1).  Fills
+// norm[0..maxSV] (zeros past the last coded symbol).  Returns bytes used, 0 on error.
+__device__ u32 read_ncount(const u8 *p, u32 avail, s16 *norm, u32 maxSV, u32 maxLog, u32 &tableLog) {
+  if (avail == 0) return 0;
+  u32 nbBits = (fwd32(p, avail, 0) & 15u) + 5u;
+  if (nbBits > maxLog) return 0;
+  tableLog = nbBits;
+  u32 bitpos = 4;
+  s32 remaining = (1 << nbBits) + 1;
+  s32 threshold = 1 << nbBits;
+  nbBits++;
+  u32 sym = 0;
+  bool prev0 = false;
+  while (remaining > 1 && sym <= maxSV) {
+    if (prev0) {
+      u32 n0 = sym, r;
+      do {
+        r = fwd32(p, avail, bitpos) & 3u;
+        bitpos += 2;
+        n0 += r;
+      } while (r == 3 && bitpos < 8 * avail + 32);
+      if (n0 > maxSV) return 0;
+      while (sym < n0) norm[sym++] = 0;
+    }
+    u32 const bs = fwd32(p, avail, bitpos);
+    s32 const mx = (2 * threshold - 1) - remaining;
+    s32 count;
+    if ((s32)(bs & (u32)(threshold - 1)) < mx) {
+      count = (s32)(bs & (u32)(threshold - 1));
+      bitpos += nbBits - 1;
+    } else {
+      count = (s32)(bs & (u32)(2 * threshold - 1));
+      if (count >= threshold) count -= mx;
+      bitpos += nbBits;
+    }
+    count--;
+    remaining -= count < 0 ? -count : count;
+    norm[sym++] = (s16)count;
+    prev0 = count == 0;
+    while (remaining < threshold) {
+      nbBits--;
+      threshold >>= 1;
+    }
+  }
+  if (remaining != 1) return 0;
+  for (u32 s = sym; s <= maxSV; s++) norm[s] = 0;
+  u32 const used = (bitpos + 7) >> 3;
+  return used <= avail ? used : 0u;
+}
+
+// FSE_buildDTable (libzstd lib/common/fse_decompress.c): T[u] = sym | nbBits << 8 | newState << 16.
+__device__ bool build_dtable(u32 *T, const s16 *norm, u32 maxSV, u32 tlog, u16 *next) {
+  u32 const size = 1u << tlog, mask = size - 1;
+  u32 high = size - 1;
+  for (u32 s = 0; s <= maxSV; s++) {
+    if (norm[s] == -1) {
+      T[high--] = s;
+      next[s] = 1;
+    } else {
+      next[s] = (u16)(norm[s] > 0 ? norm[s] : 0);
+    }
+  }
+  u32 const step = (size >> 1) + (size >> 3) + 3;
+  u32 pos = 0;
+  for (u32 s = 0; s <= maxSV; s++) {
+    s32 const k = norm[s];
+    for (s32 i = 0; i < k; i++) {
+      T[pos] = s;
+      pos = (pos + step) & mask;
+      while (pos > high) pos = (pos + step) & mask;
+    }
+  }
+  if (pos != 0) return false;
+  for (u32 u = 0; u < size; u++) {
+    u32 const s = T[u] & 0xFFu;
+    u32 const ns = next[s]++;
+    u32 const nb = tlog - hb32(ns);
+    T[u] = s | nb << 8 | ((ns << nb) - size) << 16;
+  }
+  return true;
+}
+
+// m mod d for m < 2^18 (float quotient, one correction each way)
+__device__ __forceinline__ u32 umod(u32 m, u32 d) {
+  u32 const q = (u32)((float)m * __builtin_amdgcn_rcpf((float)d));
+  s32 r = (s32)(m - q * d);
+  if (r < 0) r += (s32)d;
+  if ((u32)r >= d) r -= (s32)d;
+  return (u32)r;
+}
+
+// ---- Huffman ------------------------------------------------------------------------------
+// HUF_readStats (libzstd lib/common/entropy_common.c) on lane 0: weights -> L.hufw, L.hlog,
+// L.hnsym.  Returns the header bytes consumed, 0 on error.
+__device__ u32 huf_read_weights(DecLds &L, const u8 *p, u32 avail) {
+  if (avail < 1) return 0;
+  u32 const hb = p[0];
+  u32 nw = 0, used;
+  for (u32 i = 0; i < 256; i++) L.hufw[i] = 0;
+  if (hb >= 128) {
+    nw = hb - 127;
+    used = 1 + (nw + 1) / 2;
+    if (used > avail) return 0;
+    for (u32 i = 0; i < nw; i++) {
+      u32 const b = p[1 + i / 2];
+      L.hufw[i] = (u8)((i & 1) ? (b & 15u) : (b >> 4));
+    }
+  } else {
+    used = 1 + hb;
+    if (used > avail) return 0;
+    u32 wlog;
+    u32 const nc = read_ncount(p + 1, hb, L.norm, 255, 6, wlog);
+    if (!nc) return 0;
+    if (!build_dtable(L.u.h.wt, L.norm, 255, wlog, L.next)) return 0;
+    BitRev r;
+    if (!r.init(p + 1 + nc, hb - nc)) return 0;
+    u32 s1 = r.read(wlog), s2 = r.read(wlog);
+    // two interleaved states; the stream ends when a state update overflows
+    for (;;) {
+      if (nw > 253) return 0;
+      u32 e = L.u.h.wt[s1];
+      L.hufw[nw++] = (u8)(e & 0xFF);
+      s1 = (e >> 16) + r.read((e >> 8) & 0xFF);
+      if (r.pos < 0) { L.hufw[nw++] = (u8)(L.u.h.wt[s2] & 0xFF); break; }
+      e = L.u.h.wt[s2];
+      L.hufw[nw++] = (u8)(e & 0xFF);
+      s2 = (e >> 16) + r.read((e >> 8) & 0xFF);
+      if (r.pos < 0) { L.hufw[nw++] = (u8)(L.u.h.wt[s1] & 0xFF); break; }
+    }
+  }
+  u32 rs[16] = {};
+  u32 sum = 0;
+  for (u32 i = 0; i < nw; i++) {
+    u32 const w = L.hufw[i];
+    if (w >= 12) return 0;
+    rs[w]++;
+    sum += (1u << w) >> 1;
+  }
+  if (sum == 0) return 0;
+  u32 const tlog = hb32(sum) + 1;
+  if (tlog > HUF_LOG_MAX) return 0;
+  u32 const rest = (1u << tlog) - sum;
+  if (rest & (rest - 1)) return 0;
+  u32 const lastw = hb32(rest) + 1;
+  L.hufw[nw] = (u8)lastw;
+  rs[lastw]++;
+  if (rs[1] < 2 || (rs[1] & 1)) return 0;
+  L.hlog = tlog;
+  L.hnsym = nw + 1;
+  return used;
+}
+
+// HUF_readDTableX1 fill, lane-parallel: weight classes in ascending weight order, symbols
+// ascending inside a class, 2^(w-1) entries per symbol.
+__device__ void huf_build_dtable(DecLds &L) {
+  u32 const lane = lane_id();
+  u32 const tlog = L.hlog;
+  u32 w4[4];
+#pragma unroll
+  for (u32 k = 0; k < 4; k++) w4[k] = L.hufw[64 * k + lane];
+  u32 cnt[12], rk[12], cs[12], run[12];
+  u32 rank = 0, cls = 0;
+#pragma unroll
+  for (u32 w = 1; w <= 11; w++) {
+    u32 c = 0;
+#pragma unroll
+    for (u32 k = 0; k < 4; k++) c += (u32)__popcll(__ballot(w4[k] == w));
+    cnt[w] = c;
+    rk[w] = rank;
+    cs[w] = cls;
+    run[w] = 0;
+    rank += c << (w - 1);
+    cls += c;
+  }
+#pragma unroll
+  for (u32 k = 0; k < 4; k++) {
+#pragma unroll
+    for (u32 w = 1; w <= 11; w++) {
+      u64 const m = __ballot(w4[k] == w);
+      if (w4[k] == w) {
+        u32 const r = __builtin_amdgcn_mbcnt_hi((u32)(m >> 32), __builtin_amdgcn_mbcnt_lo((u32)m, 0u));
+        L.u.h.symlist[cs[w] + run[w] + r] = (u8)(64 * k + lane);
+      }
+      run[w] += (u32)__popcll(m);
+    }
+  }
+  __syncthreads();
+  for (u32 e = lane; e < (1u << tlog); e += 64) {
+    u32 w = 1;
+#pragma unroll
+    for (u32 v = 2; v <= 11; v++) w = (cnt[v] && e >= rk[v]) ? v : w;
+    u32 const idx = (e - rk[w]) >> (w - 1);
+    u32 const s = L.u.h.symlist[cs[w] + idx];
+    L.u.h.dt[e] = (u16)(s | (tlog + 1 - w) << 8);
+  }
+  __syncthreads();
+}
+
+// ---- block pieces ---------------------------------------------------------------------------
+struct LitSrc {
+  const u8 *g;  // literal bytes in HBM (input for raw literals, the slot for Huffman), or null
+  u32 rle;      // RLE byte when g == null
+  u32 n;        // regenerated size
+};
+
+struct Slot {
+  u8 *lit;
+  u64 *seq;
+  u32 lit_cap, seq_cap;
+};
+
+// Wave copy of n bytes global -> global (raw blocks): dword stores, source realigned
+// with alignbyte, 8 independent loads per lane in flight.
+__device__ void wave_copy(u8 *dst, const u8 *src, u32 n) {
+  u32 const lane = lane_id();
+  u32 const h = min((u32)((4u - ((uintptr_t)dst & 3u)) & 3u), n);
+  u32 const nw = (n - h) >> 2;
+  const u8 *const s0 = src + h;
+  u32 const sa = (u32)((uintptr_t)s0 & 3u);
+  const u32 *const s32 = (const u32 *)(s0 - sa);
+  u32 *const d32 = (u32 *)(dst + h);
+  constexpr u32 U = 8;
+  for (u32 w0 = 0; w0 < nw; w0 += 64 * U) {
+    u32 v[U];
+#pragma unroll
+    for (u32 u = 0; u < U; u++) {
+      u32 const w = w0 + 64 * u + lane;
+      if (w < nw) {
+        u32 const A = s32[w];
+        u32 const B = sa ? s32[w + 1] : A;  // word w+1 holds a source byte when sa != 0
+        v[u] = __builtin_amdgcn_alignbyte(B, A, sa);
+      }
+    }
+#pragma unroll
+    for (u32 u = 0; u < U; u++) {
+      u32 const w = w0 + 64 * u + lane;
+      if (w < nw) d32[w] = v[u];
+    }
+  }
+  if (lane < h) dst[lane] = src[lane];
+  for (u32 i = h + 4 * nw + lane; i < n; i += 64) dst[i] = src[i];
+}
+
+__device__ void wave_fill(u8 *dst, u32 v, u32 n) {
+  u32 const lane = lane_id();
+  u32 const h = min((u32)((4u - ((uintptr_t)dst & 3u)) & 3u), n);
+  u32 const nw = (n - h) >> 2;
+  u32 *const d32 = (u32 *)(dst + h);
+  u32 const v4 = v * 0x01010101u;
+  for (u32 w = lane; w < nw; w += 64) d32[w] = v4;
+  if (lane < h) dst[lane] = (u8)v;
+  for (u32 i = h + 4 * nw + lane; i < n; i += 64) dst[i] = (u8)v;
+}
+
+// Literals section (RFC 8878 §3.1.1.3.1).  Returns section bytes, 0 on error (status in st).
+__device__ u32 decode_literals(DecLds &L, const u8 *bp, u32 bsz, const Slot &sl, LitSrc &lits, u32 &st) {
+  u32 const lane = lane_id();
+  if (bsz < 1) { st = ST_CORRUPT; return 0; }
+  u32 const h0 = bp[0];
+  u32 const lt = h0 & 3u, sf = (h0 >> 2) & 3u;
+  if (lt <= 1) {  // raw / RLE
+    u32 hs, n;
+    if (sf == 1) {
+      if (bsz < 2) { st = ST_CORRUPT; return 0; }
+      hs = 2;
+      n = rd16(bp) >> 4;
+    } else if (sf == 3) {
+      if (bsz < 3) { st = ST_CORRUPT; return 0; }
+      hs = 3;
+      n = rd24(bp) >> 4;
+    } else {
+      hs = 1;
+      n = h0 >> 3;
+    }
+    if (n > BLOCKSIZE_MAX) { st = ST_CORRUPT; return 0; }
+    lits.n = n;
+    if (lt == 0) {
+      if (hs + n > bsz) { st = ST_CORRUPT; return 0; }
+      lits.g = bp + hs;
+      lits.rle = 0;
+      return hs + n;
+    }
+    if (hs + 1 > bsz) { st = ST_CORRUPT; return 0; }
+    lits.g = nullptr;
+    lits.rle = bp[hs];
+    return hs + 1;
+  }
+  // Huffman-coded (2) or treeless (3)
+  u32 const hs = sf <= 1 ? 3u : sf == 2 ? 4u : 5u;
+  if (bsz < hs) { st = ST_CORRUPT; return 0; }
+  u64 const hv = sf <= 1 ? (u64)rd24(bp) : sf == 2 ? (u64)rd32(bp) : ((u64)rd32(bp) | (u64)bp[4] << 32);
+  u32 n, cs;
+  if (sf <= 1) {
+    n = (u32)(hv >> 4) & 0x3FFu;
+    cs = (u32)(hv >> 14) & 0x3FFu;
+  } else if (sf == 2) {
+    n = (u32)(hv >> 4) & 0x3FFFu;
+    cs = (u32)(hv >> 18) & 0x3FFFu;
+  } else {
+    n = (u32)(hv >> 4) & 0x3FFFFu;
+    cs = (u32)(hv >> 22) & 0x3FFFFu;
+  }
+  u32 const ns = sf == 0 ? 1u : 4u;
+  if (n > BLOCKSIZE_MAX || hs + cs > bsz) { st = ST_CORRUPT; return 0; }
+  if (n > sl.lit_cap) { st = ST_SMALL; return 0; }
+  const u8 *p = bp + hs;
+  u32 rem = cs;
+  if (lt == 2) {
+    if (lane == 0) {
+      u32 const used = huf_read_weights(L, p, rem);
+      L.err = used ? 0u : 1u;
+      L.hvalid = used ? 1u : 0u;
+      L.used = used;
+    }
+    __syncthreads();
+    if (L.err) { st = ST_CORRUPT; return 0; }
+    u32 const used = L.used;
+    p += used;
+    rem -= used;
+  } else if (!L.hvalid) {
+    st = ST_CORRUPT;
+    return 0;
+  }
+  huf_build_dtable(L);
+  u32 const tlog = L.hlog;
+  // streams
+  const u8 *sp[4];
+  u32 ssz[4], cnt[4], off[4];
+  if (ns == 1) {
+    sp[0] = p;
+    ssz[0] = rem;
+    cnt[0] = n;
+    off[0] = 0;
+    for (u32 k = 1; k < 4; k++) { sp[k] = p; ssz[k] = 0; cnt[k] = 0; off[k] = 0; }
+  } else {
+    if (rem < 10) { st = ST_CORRUPT; return 0; }
+    u32 const s1 = rd16(p), s2 = rd16(p + 2), s3 = rd16(p + 4);
+    u32 const t = 6 + s1 + s2 + s3;
+    if (t >= rem) { st = ST_CORRUPT; return 0; }
+    u32 const seg = (n + 3) / 4;
+    if (3 * seg > n) { st = ST_CORRUPT; return 0; }
+    sp[0] = p + 6;
+    ssz[0] = s1;
+    sp[1] = sp[0] + s1;
+    ssz[1] = s2;
+    sp[2] = sp[1] + s2;
+    ssz[2] = s3;
+    sp[3] = sp[2] + s3;
+    ssz[3] = rem - t;
+    for (u32 k = 0; k < 4; k++) {
+      cnt[k] = k < 3 ? seg : n - 3 * seg;
+      off[k] = k * seg;
+    }
+  }
+  bool bad = false;
+  if (lane < ns) {
+    const u8 *mp = sp[0];
+    u32 msz = ssz[0], mc = cnt[0], mo = off[0];
+    for (u32 k = 1; k < 4; k++)
+      if (lane == k) { mp = sp[k]; msz = ssz[k]; mc = cnt[k]; mo = off[k]; }
+    BitRev r;
+    if (!r.init(mp, msz)) {
+      bad = true;
+    } else {
+      u8 *o = sl.lit + mo;
+      for (u32 i = 0; i < mc; i++) {
+        u32 const e = L.u.h.dt[(u32)r.peek(tlog)];
+        o[i] = (u8)e;
+        r.pos -= (s32)(e >> 8);
+      }
+      bad = r.pos != 0;
+    }
+  }
+  if (__ballot(bad)) { st = ST_CORRUPT; return 0; }
+  lits.g = sl.lit;
+  lits.rle = 0;
+  lits.n = n;
+  return hs + cs;
+}
+
+// One sequence table (mode 0 predefined, 1 RLE, 2 FSE, 3 repeat) on lane 0.
+// Returns bytes consumed (>= 0) or -1 on error.
+__device__ s32 seq_table(DecLds &L, u32 t, u32 mode, const u8 *p, u32 avail) {
+  u32 *T = L.fse + tab_off(t);
+  u32 const maxSV = tab_maxsv(t);
+  if (mode == 0) {
+    if (L.tkind[t] == TAB_PREDEF) return 0;
+    u32 const nsym = t == TAB_LL ? 36u : t == TAB_ML ? 53u : 29u;
+    const s16 *src = t == TAB_LL ? c_LL_norm : t == TAB_ML ? c_ML_norm : c_OF_norm;
+    for (u32 s = 0; s <= maxSV; s++) L.norm[s] = s < nsym ? src[s] : (s16)0;
+    u32 const lg = t == TAB_OF ? 5u : 6u;
+    if (!build_dtable(T, L.norm, maxSV, lg, L.next)) return -1;
+    L.tlog[t] = lg;
+    L.tkind[t] = TAB_PREDEF;
+    return 0;
+  }
+  if (mode == 1) {
+    if (avail < 1) return -1;
+    u32 const s = p[0];
+    if (s > maxSV) return -1;
+    T[0] = s;  // nbBits 0, newState 0
+    L.tlog[t] = 0;
+    L.tkind[t] = 0x100u | s;
+    return 1;
+  }
+  if (mode == 2) {
+    u32 lg;
+    u32 const used = read_ncount(p, avail, L.norm, maxSV, tab_maxlog(t), lg);
+    if (!used) return -1;
+    if (!build_dtable(T, L.norm, maxSV, lg, L.next)) return -1;
+    L.tlog[t] = lg;
+    L.tkind[t] = 0;
+    return (s32)used;
+  }
+  return L.tkind[t] == TAB_NONE ? -1 : 0;  // repeat
+}
+
+// XXH64 (seed 0) of n bytes at p, lanes 0..3 = the four accumulators; result on every lane.
+__device__ u64 xxh64(const u8 *p, u64 n) {
+  constexpr u64 P1 = 0x9E3779B185EBCA87ull, P2 = 0xC2B2AE3D27D4EB4Full, P3 = 0x165667B19E3779F9ull, P4 = 0x85EBCA77C2B2AE63ull,
+                P5 = 0x27D4EB2F165667C5ull;
+  auto rotl = [](u64 x, u32 r) { return (x << r) | (x >> (64 - r)); };
+  auto round = [&](u64 acc, u64 in) { return rotl(acc + in * P2, 31) * P1; };
+  u32 const lane = lane_id();
+  u64 h;
+  u64 const nst = n / 32;
+  if (n >= 32) {
+    u64 v = lane == 0 ? P1 + P2 : lane == 1 ? P2 : lane == 2 ? 0ull : (u64)0 - P1;
+    if (lane < 4) {
+      u64 k = 0;
+      for (; k + 4 <= nst; k += 4) {
+        u64 a[4];
+#pragma unroll
+        for (u32 j = 0; j < 4; j++) a[j] = ldg64(p + 32 * (k + j) + 8 * lane);
+#pragma unroll
+        for (u32 j = 0; j < 4; j++) v = round(v, a[j]);
+      }
+      for (; k < nst; k++) v = round(v, ldg64(p + 32 * k + 8 * lane));
+    }
+    u64 const v1 = __shfl(v, 0, 64), v2 = __shfl(v, 1, 64), v3 = __shfl(v, 2, 64), v4 = __shfl(v, 3, 64);
+    h = rotl(v1, 1) + rotl(v2, 7) + rotl(v3, 12) + rotl(v4, 18);
+    h = (h ^ round(0, v1)) * P1 + P4;
+    h = (h ^ round(0, v2)) * P1 + P4;
+    h = (h ^ round(0, v3)) * P1 + P4;
+    h = (h ^ round(0, v4)) * P1 + P4;
+  } else {
+    h = P5;
+  }
+  h += n;
+  const u8 *q = p + 32 * nst;
+  u64 r = n - 32 * nst;
+  while (r >= 8) {
+    h ^= round(0, ldg64(q));
+    h = rotl(h, 27) * P1 + P4;
+    q += 8;
+    r -= 8;
+  }
+  if (r >= 4) {
+    h ^= (u64)rd32(q) * P1;
+    h = rotl(h, 23) * P2 + P3;
+    q += 4;
+    r -= 4;
+  }
+  while (r) {
+    h ^= (u64)(*q) * P5;
+    h = rotl(h, 11) * P1;
+    q++;
+    r--;
+  }
+  h ^= h >> 33;
+  h *= P2;
+  h ^= h >> 29;
+  h *= P3;
+  h ^= h >> 32;
+  return h;
+}
+
+__device__ __forceinline__ u32 to_nvcomp(u32 s) {
+  switch (s) {
+    case ST_OK: return 0;
+    case ST_INVALID: return 2;
+    case ST_CORRUPT: return 6;
+    case ST_SMALL: return 7;
+    case ST_CHECKSUM: return 10;
+    default: return 1;
+  }
+}
+
+}  // namespace
+
+// One workgroup (one wave) per input buffer.
+extern "C" __global__ __launch_bounds__(DEC_THREADS) void zh_decode_kernel(ZhDecArgs a) {
+  __shared__ DecLds L;
+  u32 const item = blockIdx.x, lane = lane_id();
+  const u8 *const src = (const u8 *)(a.in_ptrs ? a.in_ptrs[item] : a.one_in);
+  u64 const srcn = a.in_ptrs ? (u64)a.in_sizes[item] : a.one_in_size;
+  u8 *const dst = (u8 *)(a.in_ptrs ? a.out_ptrs[item] : a.one_out);
+  u64 const cap = a.out_caps ? (u64)a.out_caps[item] : a.out_cap_all;
+  Slot sl;
+  sl.lit = a.ws + (size_t)item * a.slot_bytes;
+  sl.lit_cap = a.block_cap;
+  sl.seq = (u64 *)(sl.lit + a.lit_bytes);
+  sl.seq_cap = a.seq_cap;
+  if (lane < 36) L.info[0][lane] = c_LL_info[lane];
+  if (lane < 53) L.info[1][lane] = c_ML_info[lane];
+  __syncthreads();
+
+  u32 st = ST_OK;
+  u64 produced = 0, ip = 0;
+  if (!src || (!dst && cap)) st = ST_INVALID;
+  while (st == ST_OK && ip < srcn) {
+    // ---- frame header (RFC 8878 §3.1.1.1)
+    if (srcn - ip < 4) { st = ST_CORRUPT; break; }
+    u32 const magic = rd32(src + ip);
+    if ((magic & 0xFFFFFFF0u) == 0x184D2A50u) {  // skippable frame
+      if (srcn - ip < 8) { st = ST_CORRUPT; break; }
+      u64 const sk = 8ull + rd32(src + ip + 4);
+      if (sk > srcn - ip) { st = ST_CORRUPT; break; }
+      ip += sk;
+      continue;
+    }
+    if (magic != ZH_MAGIC) { st = ip == 0 ? ST_MAGIC : ST_CORRUPT; break; }
+    ip += 4;
+    if (srcn - ip < 1) { st = ST_CORRUPT; break; }
+    u32 const fhd = src[ip];
+    u32 const fcsf = fhd >> 6, single = (fhd >> 5) & 1u, chk = (fhd >> 2) & 1u, didf = fhd & 3u;
+    if (fhd & 8u) { st = ST_CORRUPT; break; }
+    u32 const didn = didf == 0 ? 0u : didf == 1 ? 1u : didf == 2 ? 2u : 4u;
+    u32 const fcsn = fcsf == 0 ? (single ? 1u : 0u) : fcsf == 1 ? 2u : fcsf == 2 ? 4u : 8u;
+    u64 const hsz = 1ull + (single ? 0u : 1u) + didn + fcsn;
+    if (srcn - ip < hsz) { st = ST_CORRUPT; break; }
+    const u8 *h = src + ip + 1;
+    if (!single) {
+      u32 const wd = *h++;
+      if (10 + (wd >> 3) > 30) { st = ST_CORRUPT; break; }
+    }
+    u32 did = 0;
+    for (u32 i = 0; i < didn; i++) did |= (u32)h[i] << (8 * i);
+    h += didn;
+    u64 fcs = ~0ull;
+    if (fcsn == 1) fcs = h[0];
+    else if (fcsn == 2) fcs = rd16(h) + 256ull;
+    else if (fcsn == 4) fcs = rd32(h);
+    else if (fcsn == 8) fcs = (u64)rd32(h) | (u64)rd32(h + 4) << 32;
+    if (did != 0) { st = ST_DICT; break; }
+    ip += hsz;
+    if (fcs != ~0ull && fcs > cap - produced) { st = ST_SMALL; break; }
+    u64 const fstart = produced;
+    // frame state: repcodes, table kinds
+    u32 rep0 = 1, rep1 = 4, rep2 = 8;
+    if (lane == 0) {
+      L.tkind[0] = L.tkind[1] = L.tkind[2] = TAB_NONE;
+      L.hvalid = 0;
+    }
+    __syncthreads();
+    // ---- blocks (RFC 8878 §3.1.1.2)
+    for (;;) {
+      if (srcn - ip < 3) { st = ST_CORRUPT; break; }
+      u32 const bh = rd24(src + ip);
+      u32 const last = bh & 1u, bt = (bh >> 1) & 3u, bsz = bh >> 3;
+      ip += 3;
+      u8 *const ob = dst + produced;  // this block's first output byte
+      if (bt == 0) {
+        if (srcn - ip < bsz) { st = ST_CORRUPT; break; }
+        if (bsz > cap - produced) { st = ST_SMALL; break; }
+        wave_copy(ob, src + ip, bsz);
+        ip += bsz;
+        produced += bsz;
+      } else if (bt == 1) {
+        if (srcn - ip < 1) { st = ST_CORRUPT; break; }
+        if (bsz > cap - produced) { st = ST_SMALL; break; }
+        wave_fill(ob, src[ip], bsz);
+        ip += 1;
+        produced += bsz;
+      } else if (bt == 2) {
+        if (bsz >= BLOCKSIZE_MAX || srcn - ip < bsz) { st = ST_CORRUPT; break; }
+        const u8 *const bp = src + ip;
+        LitSrc lits;
+        u32 const ls = decode_literals(L, bp, bsz, sl, lits, st);
+        if (!ls) break;
+        // ---- sequences section header (RFC 8878 §3.1.1.3.2.1)
+        const u8 *sp = bp + ls;
+        u32 rem = bsz - ls;
+        if (rem < 1) { st = ST_CORRUPT; break; }
+        u32 nseq = sp[0];
+        if (nseq == 0) {
+          if (rem != 1) { st = ST_CORRUPT; break; }
+          sp += 1;
+          rem -= 1;
+        } else if (nseq < 128) {
+          sp += 1;
+          rem -= 1;
+        } else if (nseq < 255) {
+          if (rem < 2) { st = ST_CORRUPT; break; }
+          nseq = ((nseq - 128) << 8) + sp[1];
+          sp += 2;
+          rem -= 2;
+        } else {
+          if (rem < 3) { st = ST_CORRUPT; break; }
+          nseq = rd16(sp + 1) + 0x7F00u;
+          sp += 3;
+          rem -= 3;
+        }
+        u64 sumML = 0, sumLL = 0;
+        if (nseq) {
+          if (nseq > sl.seq_cap) { st = nseq > BLOCKSIZE_MAX / 3 + 1 ? ST_CORRUPT : ST_SMALL; break; }
+          if (rem < 1) { st = ST_CORRUPT; break; }
+          u32 const modes = sp[0];
+          sp += 1;
+          rem -= 1;
+          if (modes & 3u) { st = ST_CORRUPT; break; }
+          if (lane == 0) {
+            u32 e = 0, used = 0;
+            u32 const md[3] = {modes >> 6, (modes >> 4) & 3u, (modes >> 2) & 3u};
+            for (u32 t = 0; t < 3 && !e; t++) {
+              s32 const u = seq_table(L, t, md[t], sp + used, rem - used);
+              if (u < 0) e = 1;
+              else used += (u32)u;
+            }
+            L.err = e;
+            L.used = used;
+          }
+          __syncthreads();
+          if (L.err) { st = ST_CORRUPT; break; }
+          sp += L.used;
+          rem -= L.used;
+          // ---- sequence bitstream (RFC 8878 §3.1.1.3.2.2): every lane decodes redundantly
+          // (uniform control flow, no exec-mask work); lane j keeps record j of each 64
+          BitRev r;
+          if (!r.init(sp, rem)) { st = ST_CORRUPT; break; }
+          u32 const lgLL = L.tlog[TAB_LL], lgOF = L.tlog[TAB_OF], lgML = L.tlog[TAB_ML];
+          const u32 *TLL = L.fse + tab_off(TAB_LL), *TOF = L.fse + tab_off(TAB_OF), *TML = L.fse + tab_off(TAB_ML);
+          u32 sLL = r.read(lgLL), sOF = r.read(lgOF), sML = r.read(lgML);
+          bool big = false;
+          u64 rec = 0;
+          for (u32 i = 0; i < nseq; i++) {
+            u32 const eLL = TLL[sLL], eOF = TOF[sOF], eML = TML[sML];
+            u32 const ofc = eOF & 0xFFu;
+            u32 const ofv = (1u << ofc) + r.read(ofc);
+            u32 const mi = L.info[1][eML & 0xFFu];
+            u32 const ml = (mi & 0xFFFFFFu) + r.read(mi >> 24);
+            u32 const li = L.info[0][eLL & 0xFFu];
+            u32 const ll = (li & 0xFFFFFFu) + r.read(li >> 24);
+            u32 off;
+            if (ofv > 3) {
+              off = ofv - 3;
+              rep2 = rep1;
+              rep1 = rep0;
+              rep0 = off;
+            } else {
+              u32 const idx = ofv - 1 + (ll == 0 ? 1u : 0u);
+              if (idx == 0) {
+                off = rep0;
+              } else {
+                off = idx == 3 ? rep0 - 1 : idx == 1 ? rep1 : rep2;
+                off += off == 0 ? 1u : 0u;  // libzstd: a zero offset is forced to 1
+                if (idx != 1) rep2 = rep1;
+                rep1 = rep0;
+                rep0 = off;
+              }
+            }
+            big |= off >= OFF_LIMIT;
+            sumLL += ll;
+            sumML += ml;
+            u64 const v = (u64)ll | (u64)(ml - 3) << 17 | (u64)off << 34;
+            rec = lane == (i & 63u) ? v : rec;
+            if ((i & 63u) == 63u || i + 1 == nseq) {
+              if (lane <= (i & 63u)) sl.seq[(i & ~63u) + lane] = rec;
+            }
+            if (i + 1 < nseq) {
+              sLL = (eLL >> 16) + r.read((eLL >> 8) & 0xFFu);
+              sML = (eML >> 16) + r.read((eML >> 8) & 0xFFu);
+              sOF = (eOF >> 16) + r.read((eOF >> 8) & 0xFFu);
+            }
+          }
+          if (r.pos > 0 || big) { st = ST_CORRUPT; break; }
+        } else if (rem != 0) {
+          st = ST_CORRUPT;
+          break;
+        }
+        if (sumLL > lits.n) { st = ST_CORRUPT; break; }
+        u64 const total = lits.n + sumML;
+        if (total > cap - produced) { st = ST_SMALL; break; }
+        __threadfence_block();  // the records (and Huffman literals) are read back below
+        __syncthreads();
+        // ---- execution through the LDS window
+        u32 const tl = lits.n - (u32)sumLL;
+        u64 const fpos = produced - fstart;  // frame bytes before this block
+        u32 q = 0, qd = 0, opos = 0, lpos = 0;
+        u64 batch = 0;
+        u32 qb = 0xFFFFFFFFu;
+        bool bad = false;
+        while (q <= nseq && !bad) {
+          u32 const gs = opos;
+          u32 const lw = min((u32)DEC_LSTAGE, lits.n - lpos);
+          if (lits.g) {
+            for (u32 i = lane; i < lw; i += 64) L.u.x.lit[i] = lits.g[lpos + i];
+          } else {
+            for (u32 i = lane; i < lw; i += 64) L.u.x.lit[i] = (u8)lits.rle;
+          }
+          u32 wpos = 0, lused = 0;
+          while (q <= nseq) {
+            u32 ll, ml, off;
+            if (q < nseq) {
+              if ((q & ~63u) != qb) {
+                qb = q & ~63u;
+                batch = qb + lane < nseq ? sl.seq[qb + lane] : 0ull;
+              }
+              u32 const j = q & 63u;
+              u32 const lo = __builtin_amdgcn_readlane((u32)batch, j);
+              u32 const hi = __builtin_amdgcn_readlane((u32)(batch >> 32), j);
+              ll = lo & 0x1FFFFu;
+              ml = ((lo >> 17) | (hi & 3u) << 15) + 3u;
+              off = hi >> 2;
+            } else {
+              ll = tl;
+              ml = 0;
+              off = 0;
+            }
+            if (qd < ll) {
+              u32 const k = min(ll - qd, min(DEC_STAGE - wpos, lw - lused));
+              for (u32 i = lane; i < k; i += 64) L.u.x.out[wpos + i] = L.u.x.lit[lused + i];
+              wpos += k;
+              lused += k;
+              qd += k;
+              if (qd < ll) break;
+            }
+            u32 const m0 = qd - ll;
+            if (m0 < ml) {
+              u32 const k = min(ml - m0, DEC_STAGE - wpos);
+              s64 const mstart = (s64)gs + wpos - m0;  // block-relative
+              if ((s64)fpos + mstart < (s64)off) { bad = true; break; }
+              s64 const base = mstart - off;
+              for (u32 i = lane; i < k; i += 64) {
+                u32 const m = m0 + i;
+                s64 const s = base + (m < off ? m : umod(m, off));
+                u8 const v = s >= (s64)gs ? L.u.x.out[(u32)(s - gs)] : ob[s];
+                L.u.x.out[wpos + i] = v;
+              }
+              wpos += k;
+              qd += k;
+              if (qd < ll + ml) break;
+            }
+            q++;
+            qd = 0;
+            if (wpos == DEC_STAGE) break;
+          }
+          // flush the window
+          u8 *const d = ob + gs;
+          for (u32 i = lane; i < wpos; i += 64) d[i] = L.u.x.out[i];
+          __threadfence_block();
+          opos = gs + wpos;
+          lpos += lused;
+          if (q > nseq) break;
+        }
+        if (bad) { st = ST_CORRUPT; break; }
+        produced += total;
+        ip += bsz;
+      } else {
+        st = ST_CORRUPT;
+        break;
+      }
+      __threadfence_block();
+      if (last) break;
+    }
+    if (st != ST_OK) break;
+    if (fcs != ~0ull && produced - fstart != fcs) { st = ST_CORRUPT; break; }
+    if (chk) {
+      if (srcn - ip < 4) { st = ST_CORRUPT; break; }
+      u64 const hx = xxh64(dst + fstart, produced - fstart);
+      if ((u32)hx != rd32(src + ip)) { st = ST_CHECKSUM; break; }
+      ip += 4;
+    }
+  }
+  if (lane == 0) {
+    a.out_sizes[item] = st == ST_OK ? produced : 0ull;
+    if (a.statuses) a.statuses[item] = a.nvcomp_codes ? to_nvcomp(st) : st;
+  }
+}
+
+namespace zh {
+u32 dec_lds_bytes() { return (u32)sizeof(DecLds); }
+hipError_t launch_decompress(const ZhDecArgs &a, u32 nitems, hipStream_t stream) {
+  if (!nitems) return hipSuccess;
+  hipLaunchKernelGGL(zh_decode_kernel, dim3(nitems), dim3(DEC_THREADS), 0, stream, a);
+  return hipGetLastError();
+}
+}  // namespace zh

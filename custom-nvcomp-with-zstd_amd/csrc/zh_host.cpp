@@ -243,6 +243,56 @@ struct WsLayout {
 
 inline size_t blocks_of(size_t n) { return (n + ZH_BLOCK_MAX - 1) / ZH_BLOCK_MAX; }
 
+// Decoder workspace (zh_decode.hip): per-item arrays (host-array entry points upload
+// them), then one slot per item holding the literals and sequence records of the block
+// being decoded.  A slot is sized for blocks of block_cap regenerated bytes: 128 KiB
+// (the format's maximum) unless every output capacity is smaller.
+struct DecLayout {
+  size_t in_ptrs, in_sizes, out_ptrs, caps, out_sizes, statuses, slots, total;
+  u32 block_cap, lit_bytes, seq_cap;
+  u64 slot_bytes;
+  static constexpr size_t kBlockMax = 128 * 1024;
+  static DecLayout make(size_t n, size_t max_block) {
+    DecLayout L{};
+    L.block_cap = (u32)std::min(std::max<size_t>(max_block, 64), kBlockMax);
+    L.lit_bytes = (u32)align256(L.block_cap + 64);
+    L.seq_cap = L.block_cap / 3 + 2;
+    L.slot_bytes = L.lit_bytes + align256((size_t)L.seq_cap * 8);
+    size_t o = 0;
+    L.in_ptrs = o; o = align256(o + n * 8);
+    L.in_sizes = o; o = align256(o + n * 8);
+    L.out_ptrs = o; o = align256(o + n * 8);
+    L.caps = o; o = align256(o + n * 8);
+    L.out_sizes = o; o = align256(o + n * 8);
+    L.statuses = o; o = align256(o + n * 4);
+    L.slots = o; o = align256(o + n * L.slot_bytes);
+    L.total = o + 256;  // slack for base alignment
+    return L;
+  }
+  ZhDecArgs args(u8 *base) const {
+    ZhDecArgs a{};
+    a.ws = base + slots;
+    a.slot_bytes = slot_bytes;
+    a.lit_bytes = lit_bytes;
+    a.block_cap = block_cap;
+    a.seq_cap = seq_cap;
+    return a;
+  }
+};
+
+Status from_dec_status(u32 s) {
+  switch (s) {
+    case 0: return Status::SUCCESS;
+    case 2: return Status::ERROR_INVALID_PARAMETER;
+    case 5: return Status::ERROR_INVALID_MAGIC;
+    case 6: return Status::ERROR_CORRUPT_DATA;
+    case 7: return Status::ERROR_BUFFER_TOO_SMALL;
+    case 9: return Status::ERROR_DICTIONARY_MISMATCH;
+    case 10: return Status::ERROR_CHECKSUM_FAILED;
+    default: return Status::ERROR_DECOMPRESSION;
+  }
+}
+
 std::once_flag g_init_flag;
 hipError_t g_init_err = hipSuccess;
 Status ensure_kernels() {
@@ -352,6 +402,84 @@ class ZstdBatchManager::Impl {
     stats.num_blocks += nblocks;
     return all_ok ? Status::SUCCESS : Status::ERROR_GENERIC;
   }
+
+  // Decode a list of buffers given as host arrays of device pointers (one launch of
+  // zh_decode_kernel, one host synchronisation).  out_sizes: in = capacity, out = bytes.
+  Status run_decompress(const void *const *in_ptrs, const size_t *in_sizes, size_t count, void *const *out_ptrs, size_t *out_sizes,
+                        Status *statuses, void *temp, size_t temp_size, hipStream_t stream) {
+    Status s = ensure_kernels();
+    if (s != Status::SUCCESS) return s;
+    size_t maxcap = 0;
+    for (size_t i = 0; i < count; i++) maxcap = std::max(maxcap, out_sizes[i]);
+    DecLayout L = DecLayout::make(count, maxcap);
+    if (!temp || temp_size < L.total) return Status::ERROR_BUFFER_TOO_SMALL;
+    u8 *base = (u8 *)(((uintptr_t)temp + 255) & ~(uintptr_t)255);
+    size_t const up = L.out_sizes, down = L.slots - L.out_sizes;
+    u8 *h = (u8 *)host_scratch(up + down);
+    if (!h) return Status::ERROR_OUT_OF_MEMORY;
+    for (size_t i = 0; i < count; i++) {
+      ((const void **)(h + L.in_ptrs))[i] = in_ptrs[i];
+      ((size_t *)(h + L.in_sizes))[i] = in_sizes[i];
+      ((void **)(h + L.out_ptrs))[i] = out_ptrs[i];
+      ((size_t *)(h + L.caps))[i] = out_sizes[i];
+    }
+    if (hipMemcpyAsync(base, h, up, hipMemcpyHostToDevice, stream) != hipSuccess) return Status::ERROR_CUDA_ERROR;
+    ZhDecArgs a = L.args(base);
+    a.in_ptrs = (const void *const *)(base + L.in_ptrs);
+    a.in_sizes = (const size_t *)(base + L.in_sizes);
+    a.out_ptrs = (void *const *)(base + L.out_ptrs);
+    a.out_caps = (const size_t *)(base + L.caps);
+    a.out_sizes = (size_t *)(base + L.out_sizes);
+    a.statuses = (u32 *)(base + L.statuses);
+    if (zh::launch_decompress(a, (u32)count, stream) != hipSuccess) return Status::ERROR_CUDA_ERROR;
+    if (hipMemcpyAsync(h + up, base + L.out_sizes, down, hipMemcpyDeviceToHost, stream) != hipSuccess) return Status::ERROR_CUDA_ERROR;
+    if (hipStreamSynchronize(stream) != hipSuccess) return Status::ERROR_CUDA_ERROR;
+    const size_t *hsz = (const size_t *)(h + up);
+    const u32 *hst = (const u32 *)(h + up + (L.statuses - L.out_sizes));
+    bool all_ok = true;
+    for (size_t i = 0; i < count; i++) {
+      Status st = from_dec_status(hst[i]);
+      statuses[i] = st;
+      if (st == Status::SUCCESS) {
+        out_sizes[i] = hsz[i];
+        stats.bytes_decompressed += hsz[i];
+      } else {
+        all_ok = false;
+      }
+    }
+    return all_ok ? Status::SUCCESS : Status::ERROR_GENERIC;
+  }
+
+  // One buffer, no pointer-array upload (ZhDecArgs single-item fields).  Synchronous
+  // unless d_actual is given (then the size lands there, stream-ordered, 0 on error).
+  Status run_decompress_one(const void *in, size_t n, void *out, size_t cap, size_t *h_actual, size_t *d_actual, void *temp, size_t temp_size,
+                            hipStream_t stream) {
+    Status s = ensure_kernels();
+    if (s != Status::SUCCESS) return s;
+    DecLayout L = DecLayout::make(1, cap);
+    if (!temp || temp_size < L.total) return Status::ERROR_BUFFER_TOO_SMALL;
+    u8 *base = (u8 *)(((uintptr_t)temp + 255) & ~(uintptr_t)255);
+    ZhDecArgs a = L.args(base);
+    a.one_in = in;
+    a.one_in_size = n;
+    a.one_out = out;
+    a.out_cap_all = cap;
+    a.out_sizes = d_actual ? d_actual : (size_t *)(base + L.out_sizes);
+    a.statuses = (u32 *)(base + L.statuses);
+    if (zh::launch_decompress(a, 1, stream) != hipSuccess) return Status::ERROR_CUDA_ERROR;
+    if (d_actual) return Status::SUCCESS;
+    u8 *h = (u8 *)host_scratch(16);
+    if (!h) return Status::ERROR_OUT_OF_MEMORY;
+    if (hipMemcpyAsync(h, base + L.out_sizes, 8, hipMemcpyDeviceToHost, stream) != hipSuccess) return Status::ERROR_CUDA_ERROR;
+    if (hipMemcpyAsync(h + 8, base + L.statuses, 4, hipMemcpyDeviceToHost, stream) != hipSuccess) return Status::ERROR_CUDA_ERROR;
+    if (hipStreamSynchronize(stream) != hipSuccess) return Status::ERROR_CUDA_ERROR;
+    Status st = from_dec_status(*(const u32 *)(h + 8));
+    if (st == Status::SUCCESS) {
+      *h_actual = *(const size_t *)h;
+      stats.bytes_decompressed += *h_actual;
+    }
+    return st;
+  }
 };
 
 ZstdBatchManager::ZstdBatchManager() : pimpl_(new Impl(CompressionConfig::from_level(3))) {}
@@ -370,7 +498,8 @@ size_t ZstdBatchManager::get_compress_temp_size(size_t n) const {
   size_t nb = std::max<size_t>(1, blocks_of(n));
   return WsLayout::make(nb, 1, nb > 1).total;
 }
-size_t ZstdBatchManager::get_decompress_temp_size(size_t) const { return 0; }
+// one slot for 128 KiB blocks (reference src/cuda_zstd_manager.cu:1373-1408 also sizes for one block)
+size_t ZstdBatchManager::get_decompress_temp_size(size_t) const { return DecLayout::make(1, DecLayout::kBlockMax).total; }
 size_t ZstdBatchManager::get_max_compressed_size(size_t n) const { return estimate_compressed_size(n, pimpl_->config.level); }
 
 Status ZstdBatchManager::compress(const void *in, size_t n, void *out, size_t *out_size, void *temp, size_t temp_size, const void *dict_buffer,
@@ -398,11 +527,18 @@ Status ZstdBatchManager::compress(const void *in, size_t n, void *out, size_t *o
   return st;
 }
 
-Status ZstdBatchManager::decompress(const void *in, size_t n, void *out, size_t *out_size, void *, size_t, hipStream_t stream) {
+// GPU decode (zh_decode.hip) of device-resident frames; validation order of the
+// reference (src/cuda_zstd_manager.cu:3203-3212).  *out_size: capacity in, bytes out.
+Status ZstdBatchManager::decompress(const void *in, size_t n, void *out, size_t *out_size, void *temp, size_t temp_size, hipStream_t stream) {
   std::lock_guard<std::mutex> lock(pimpl_->api_mutex);
-  if (!in || !out || !out_size) return Status::ERROR_INVALID_PARAMETER;
-  Status s = cpu_decompress(in, n, out, out_size, stream);
-  if (s == Status::SUCCESS) pimpl_->stats.bytes_decompressed += *out_size;
+  if (!in || !out || !out_size || !temp || n < 4) return Status::ERROR_INVALID_PARAMETER;
+  if (temp_size < get_decompress_temp_size(n)) return Status::ERROR_BUFFER_TOO_SMALL;
+  if (!is_device_ptr(in) || !is_device_ptr(out)) return Status::ERROR_INVALID_PARAMETER;  // device-resident API
+  auto t0 = std::chrono::steady_clock::now();
+  size_t got = 0;
+  Status s = pimpl_->run_decompress_one(in, n, out, *out_size, &got, nullptr, temp, temp_size, stream);
+  if (s == Status::SUCCESS) *out_size = got;
+  pimpl_->stats.decompression_time_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
   return s;
 }
 
@@ -430,7 +566,9 @@ size_t ZstdBatchManager::get_batch_compress_temp_size(const std::vector<size_t> 
   for (size_t s : sizes) { size_t k = blocks_of(s); nb += k; staged |= k > 1; }
   return WsLayout::make(nb, sizes.size(), staged).total;
 }
-size_t ZstdBatchManager::get_batch_decompress_temp_size(const std::vector<size_t> &) const { return 0; }
+size_t ZstdBatchManager::get_batch_decompress_temp_size(const std::vector<size_t> &sizes) const {
+  return DecLayout::make(std::max<size_t>(1, sizes.size()), DecLayout::kBlockMax).total;
+}
 
 Status ZstdBatchManager::compress_batch(const std::vector<BatchItem> &items, void *temp, size_t temp_size, hipStream_t stream) {
   std::lock_guard<std::mutex> lock(pimpl_->api_mutex);
@@ -470,34 +608,61 @@ Status ZstdBatchManager::compress_batch(const std::vector<BatchItem> &items, voi
   return any_bad ? Status::ERROR_GENERIC : Status::SUCCESS;
 }
 
-Status ZstdBatchManager::decompress_batch(const std::vector<BatchItem> &items, void *, size_t, hipStream_t stream) {
-  auto &mut = const_cast<std::vector<BatchItem> &>(items);
-  bool ok = true;
-  for (auto &it : mut) {
-    it.status = cpu_decompress(it.input_ptr, it.input_size, it.output_ptr, &it.output_size, stream);
-    ok &= it.status == Status::SUCCESS;
+// ZstdBatchManager::decompress_batch (reference src/cuda_zstd_manager.cu:5799-5885): every
+// item decoded by one launch; output_size in = capacity, out = bytes; per-item status.
+Status ZstdBatchManager::decompress_batch(const std::vector<BatchItem> &items, void *temp, size_t temp_size, hipStream_t stream) {
+  std::lock_guard<std::mutex> lock(pimpl_->api_mutex);
+  if (items.empty()) return Status::SUCCESS;
+  auto &mut = const_cast<std::vector<BatchItem> &>(items);  // the reference writes sizes/status through const
+  std::vector<const void *> ip;
+  std::vector<void *> op;
+  std::vector<size_t> isz, osz, idx;
+  bool any_bad = false;
+  for (size_t i = 0; i < items.size(); i++) {
+    if (!items[i].input_ptr || !items[i].output_ptr || items[i].input_size < 4) {
+      mut[i].status = Status::ERROR_INVALID_PARAMETER;
+      any_bad = true;
+      continue;
+    }
+    ip.push_back(items[i].input_ptr);
+    op.push_back(items[i].output_ptr);
+    isz.push_back(items[i].input_size);
+    osz.push_back(items[i].output_size);
+    idx.push_back(i);
   }
-  return ok ? Status::SUCCESS : Status::ERROR_GENERIC;
+  if (idx.empty()) return Status::ERROR_GENERIC;
+  auto t0 = std::chrono::steady_clock::now();
+  std::vector<Status> st(idx.size());
+  Status r = pimpl_->run_decompress(ip.data(), isz.data(), idx.size(), op.data(), osz.data(), st.data(), temp, temp_size, stream);
+  pimpl_->stats.decompression_time_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  if (r != Status::SUCCESS && r != Status::ERROR_GENERIC) return r;
+  for (size_t j = 0; j < idx.size(); j++) {
+    mut[idx[j]].status = st[j];
+    if (st[j] == Status::SUCCESS) mut[idx[j]].output_size = osz[j];
+    else any_bad = true;
+  }
+  return any_bad ? Status::ERROR_GENERIC : Status::SUCCESS;
 }
 
-Status ZstdBatchManager::decompress_to_preallocated(const void *in, size_t n, void *out, size_t cap, size_t *actual, void *, size_t,
+Status ZstdBatchManager::decompress_to_preallocated(const void *in, size_t n, void *out, size_t cap, size_t *actual, void *temp, size_t temp_size,
                                                     hipStream_t stream) {
-  if (!actual) return Status::ERROR_INVALID_PARAMETER;
+  if (!in || !out || !actual) return Status::ERROR_INVALID_PARAMETER;
+  if (cap == 0) return Status::ERROR_BUFFER_TOO_SMALL;  // reference tests/test_inference_api.cu:581-586
   *actual = cap;
-  return cpu_decompress(in, n, out, actual, stream);
+  return decompress(in, n, out, actual, temp, temp_size, stream);
 }
 Status ZstdBatchManager::decompress_batch_preallocated(std::vector<BatchItem> &items, void *t, size_t ts, hipStream_t stream) {
   return decompress_batch(items, t, ts, stream);
 }
-Status ZstdBatchManager::decompress_async_no_sync(const void *in, size_t n, void *out, size_t cap, size_t *d_actual, void *, size_t,
+// stream-ordered: nothing is synchronised; *d_actual (device) receives the size, 0 on error
+Status ZstdBatchManager::decompress_async_no_sync(const void *in, size_t n, void *out, size_t cap, size_t *d_actual, void *temp, size_t temp_size,
                                                   hipStream_t stream) {
-  size_t got = cap;
-  Status s = cpu_decompress(in, n, out, &got, stream);
-  if (s != Status::SUCCESS) return s;
-  u64 v = got;
-  return copy_any(d_actual, &v, sizeof(v), stream);
+  std::lock_guard<std::mutex> lock(pimpl_->api_mutex);
+  if (!in || !out || !d_actual || !temp || n < 4) return Status::ERROR_INVALID_PARAMETER;
+  if (temp_size < get_decompress_temp_size(n)) return Status::ERROR_BUFFER_TOO_SMALL;
+  return pimpl_->run_decompress_one(in, n, out, cap, nullptr, d_actual, temp, temp_size, stream);
 }
-size_t ZstdBatchManager::get_inference_workspace_size(size_t, size_t) const { return 0; }
+size_t ZstdBatchManager::get_inference_workspace_size(size_t, size_t max_out) const { return DecLayout::make(1, max_out).total; }
 Status ZstdBatchManager::allocate_inference_workspace(size_t a, size_t b, void **ptr, size_t *size) {
   if (!ptr || !size) return Status::ERROR_INVALID_PARAMETER;
   *size = std::max<size_t>(256, get_inference_workspace_size(a, b));
@@ -533,6 +698,32 @@ Status ZstdBatchManager::compress_batch_device(const void *const *d_in_ptrs, con
   return e == hipSuccess ? Status::SUCCESS : Status::ERROR_CUDA_ERROR;
 }
 
+size_t ZstdBatchManager::get_batch_device_decompress_temp_size(size_t count, size_t max_out) {
+  return DecLayout::make(std::max<size_t>(1, count), max_out).total;
+}
+
+Status ZstdBatchManager::decompress_batch_device(const void *const *d_in_ptrs, const size_t *d_in_sizes, const size_t *d_out_caps, size_t max_out,
+                                                 size_t count, void *const *d_out_ptrs, size_t *d_out_sizes, int *d_statuses, void *temp,
+                                                 size_t temp_size, hipStream_t stream) {
+  Status s = ensure_kernels();
+  if (s != Status::SUCCESS) return s;
+  if (!count) return Status::SUCCESS;
+  if (!d_in_ptrs || !d_in_sizes || !d_out_ptrs || !d_out_sizes || max_out == 0) return Status::ERROR_INVALID_PARAMETER;
+  DecLayout L = DecLayout::make(count, max_out);
+  if (!temp || temp_size < L.total) return Status::ERROR_BUFFER_TOO_SMALL;
+  u8 *base = (u8 *)(((uintptr_t)temp + 255) & ~(uintptr_t)255);
+  ZhDecArgs a = L.args(base);
+  a.in_ptrs = d_in_ptrs;
+  a.in_sizes = d_in_sizes;
+  a.out_ptrs = d_out_ptrs;
+  a.out_caps = d_out_caps;
+  a.out_cap_all = max_out;
+  a.out_sizes = d_out_sizes;
+  a.statuses = d_statuses ? (u32 *)d_statuses : (u32 *)(base + L.statuses);
+  a.nvcomp_codes = 1;
+  return zh::launch_decompress(a, (u32)count, stream) == hipSuccess ? Status::SUCCESS : Status::ERROR_CUDA_ERROR;
+}
+
 // ============================================================================
 // Streaming manager: each chunk an independent frame (reference :6306-6310)
 // ============================================================================
@@ -562,7 +753,18 @@ Status ZstdStreamingManager::init_compression(hipStream_t, size_t max_chunk) {
   return Status::SUCCESS;
 }
 Status ZstdStreamingManager::init_compression_with_history(hipStream_t s, size_t m) { return init_compression(s, m); }
-Status ZstdStreamingManager::init_decompression(hipStream_t) { pimpl_->decomp = true; return Status::SUCCESS; }
+Status ZstdStreamingManager::init_decompression(hipStream_t) {
+  size_t need = pimpl_->mgr.get_decompress_temp_size(0);
+  if (need > pimpl_->ws_size) {
+    if (pimpl_->ws) (void)hipFree(pimpl_->ws);
+    pimpl_->ws = nullptr;
+    pimpl_->ws_size = 0;
+    if (hipMalloc(&pimpl_->ws, need) != hipSuccess) return Status::ERROR_OUT_OF_MEMORY;
+    pimpl_->ws_size = need;
+  }
+  pimpl_->decomp = true;
+  return Status::SUCCESS;
+}
 Status ZstdStreamingManager::compress_chunk(const void *in, size_t n, void *out, size_t *out_size, bool, hipStream_t stream) {
   if (!pimpl_->comp) return Status::ERROR_NOT_INITIALIZED;
   size_t need = pimpl_->mgr.get_compress_temp_size(n);
@@ -578,7 +780,7 @@ Status ZstdStreamingManager::compress_chunk_with_history(const void *in, size_t 
 Status ZstdStreamingManager::decompress_chunk(const void *in, size_t n, void *out, size_t *out_size, bool *is_last, hipStream_t stream) {
   if (!pimpl_->decomp) return Status::ERROR_NOT_INITIALIZED;
   if (is_last) *is_last = true;
-  return pimpl_->mgr.decompress(in, n, out, out_size, nullptr, 0, stream);
+  return pimpl_->mgr.decompress(in, n, out, out_size, pimpl_->ws, pimpl_->ws_size, stream);
 }
 Status ZstdStreamingManager::reset() { pimpl_->comp = pimpl_->decomp = false; return Status::SUCCESS; }
 Status ZstdStreamingManager::reset_streaming() { return Status::SUCCESS; }
@@ -614,7 +816,15 @@ Status compress_simple(const void *in, size_t n, void *out, size_t *out_size, in
   (void)hipFree(ws);
   return s;
 }
-Status decompress_simple(const void *in, size_t n, void *out, size_t *out_size, hipStream_t stream) { return cpu_decompress(in, n, out, out_size, stream); }
+Status decompress_simple(const void *in, size_t n, void *out, size_t *out_size, hipStream_t stream) {
+  ZstdBatchManager m;
+  size_t need = m.get_decompress_temp_size(n);
+  void *ws = nullptr;
+  if (hipMalloc(&ws, need) != hipSuccess) return Status::ERROR_OUT_OF_MEMORY;
+  Status s = m.decompress(in, n, out, out_size, ws, need, stream);
+  (void)hipFree(ws);
+  return s;
+}
 
 Status get_decompressed_size(const void *data, size_t n, size_t *out) {
   if (!data || !out || n < 4) return Status::ERROR_INVALID_PARAMETER;
@@ -717,7 +927,9 @@ size_t NvcompV5BatchManager::get_compress_temp_size(const size_t *sizes, size_t 
   if (fetch_array(h, sizes, n, stream) != Status::SUCCESS) return 0;
   return pimpl_->mgr.get_batch_compress_temp_size(h);
 }
-size_t NvcompV5BatchManager::get_decompress_temp_size(const size_t *, size_t, hipStream_t) const { return 0; }
+size_t NvcompV5BatchManager::get_decompress_temp_size(const size_t *, size_t n, hipStream_t) const {
+  return pimpl_->mgr.get_batch_decompress_temp_size(std::vector<size_t>(n));
+}
 size_t NvcompV5BatchManager::get_max_compressed_chunk_size(size_t n) const { return pimpl_->mgr.get_max_compressed_size(n); }
 const CompressionStats &NvcompV5BatchManager::get_stats() const { return pimpl_->mgr.get_stats(); }
 
@@ -747,8 +959,12 @@ Status NvcompV5BatchManager::compress_async(const void *const *d_in, const size_
   return r != Status::SUCCESS ? r : w;
 }
 
+// NvcompV5BatchManager::decompress_async (reference src/cuda_zstd_nvcomp.cpp:540-610): arrays on
+// the host or the device; uncompressed_sizes in = capacity, out = bytes (0 for a failed item).
 Status NvcompV5BatchManager::decompress_async(const void *const *d_in, const size_t *in_sizes, size_t n, void *const *d_out, size_t *out_sizes,
-                                              void *, size_t, hipStream_t stream) {
+                                              void *temp, size_t temp_bytes, hipStream_t stream) {
+  if (!n) return Status::SUCCESS;
+  if (!d_in || !in_sizes || !d_out || !out_sizes) return Status::ERROR_INVALID_PARAMETER;
   std::vector<const void *> hin;
   std::vector<void *> hout;
   std::vector<size_t> hsz, hcap;
@@ -757,16 +973,17 @@ Status NvcompV5BatchManager::decompress_async(const void *const *d_in, const siz
   if (s == Status::SUCCESS) s = fetch_array(hsz, in_sizes, n, stream);
   if (s == Status::SUCCESS) s = fetch_array(hcap, (const size_t *)out_sizes, n, stream);
   if (s != Status::SUCCESS) return s;
-  bool ok = true;
+  std::vector<BatchItem> items(n);
   for (size_t i = 0; i < n; i++) {
-    size_t cap = hcap[i];
-    Status st = cpu_decompress(hin[i], hsz[i], hout[i], &cap, stream);
-    hcap[i] = st == Status::SUCCESS ? cap : 0;
-    ok &= st == Status::SUCCESS;
+    items[i].input_ptr = (void *)hin[i];
+    items[i].output_ptr = hout[i];
+    items[i].input_size = hsz[i];
+    items[i].output_size = hcap[i];
   }
-  if (is_device_ptr(out_sizes)) copy_any(out_sizes, hcap.data(), n * sizeof(size_t), stream);
-  else memcpy(out_sizes, hcap.data(), n * sizeof(size_t));
-  return ok ? Status::SUCCESS : Status::ERROR_GENERIC;
+  Status r = pimpl_->mgr.decompress_batch(items, temp, temp_bytes, stream);
+  for (size_t i = 0; i < n; i++) hcap[i] = items[i].status == Status::SUCCESS ? items[i].output_size : 0;
+  Status w = is_device_ptr(out_sizes) ? copy_any(out_sizes, hcap.data(), n * sizeof(size_t), stream) : (memcpy(out_sizes, hcap.data(), n * sizeof(size_t)), Status::SUCCESS);
+  return r != Status::SUCCESS ? r : w;
 }
 
 Status get_metadata_async(const void *d, size_t n, NvcompV5Metadata *m, hipStream_t) {
@@ -893,13 +1110,43 @@ Status HybridEngine::compress(const void *in, size_t n, void *out, size_t *out_s
   return s;
 }
 
+// same routing as compress (reference src/cuda_zstd_hybrid.cu:836-905): libzstd for host data /
+// FORCE_CPU, the gfx950 decoder for device data (host buffers staged through HBM when forced)
 Status HybridEngine::decompress(const void *in, size_t n, void *out, size_t *out_size, DataLocation il, DataLocation ol, HybridResult *res,
                                 hipStream_t stream) {
+  if (!in || !out || !out_size || n < 4) return Status::ERROR_INVALID_PARAMETER;
+  if (il == DataLocation::UNKNOWN) il = detect_location(in);
+  if (ol == DataLocation::UNKNOWN) ol = detect_location(out);
   auto t0 = std::chrono::steady_clock::now();
-  Status s = cpu_decompress(in, n, out, out_size, stream);
+  ExecutionBackend be = query_routing(n, il, ol, false);
+  Status s;
+  if (be == ExecutionBackend::CPU_LIBZSTD) {
+    s = cpu_decompress(in, n, out, out_size, stream);
+  } else {
+    const void *din = in;
+    void *dout = out, *tmp_in = nullptr, *tmp_out = nullptr, *ws = nullptr;
+    size_t const cap = *out_size;
+    s = Status::SUCCESS;
+    if (il != DataLocation::DEVICE) {
+      if (hipMalloc(&tmp_in, n) != hipSuccess) s = Status::ERROR_OUT_OF_MEMORY;
+      else s = copy_any(tmp_in, in, n, stream);
+      din = tmp_in;
+    }
+    if (s == Status::SUCCESS && ol != DataLocation::DEVICE) {
+      if (hipMalloc(&tmp_out, std::max<size_t>(cap, 1)) != hipSuccess) s = Status::ERROR_OUT_OF_MEMORY;
+      dout = tmp_out;
+    }
+    size_t need = pimpl_->mgr.get_decompress_temp_size(n);
+    if (s == Status::SUCCESS && hipMalloc(&ws, need) != hipSuccess) s = Status::ERROR_OUT_OF_MEMORY;
+    if (s == Status::SUCCESS) s = pimpl_->mgr.decompress(din, n, dout, out_size, ws, need, stream);
+    if (s == Status::SUCCESS && tmp_out) s = copy_any(out, tmp_out, *out_size, stream);
+    if (tmp_in) (void)hipFree(tmp_in);
+    if (tmp_out) (void)hipFree(tmp_out);
+    if (ws) (void)hipFree(ws);
+  }
   double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
   if (res) {
-    res->backend_used = ExecutionBackend::CPU_LIBZSTD;
+    res->backend_used = be;
     res->input_location = il;
     res->output_location = ol;
     res->total_time_ms = ms;
@@ -1021,6 +1268,27 @@ int cuda_zstd_compress_batch(cuda_zstd_manager_t *m, const void *const *in_ptrs,
   }
   return status_to_nvcomp_error(s);
 }
+size_t cuda_zstd_get_batch_decompress_workspace_size(cuda_zstd_manager_t *m, const size_t *sizes, size_t count) {
+  if (!m || !m->manager || (!sizes && count)) return 0;
+  return m->manager->get_batch_decompress_temp_size(std::vector<size_t>(sizes, sizes + count));
+}
+int cuda_zstd_decompress_batch(cuda_zstd_manager_t *m, const void *const *in_ptrs, const size_t *in_sizes, size_t count, void *const *out_ptrs,
+                               size_t *out_sizes, int *statuses, void *ws, size_t ws_size, hipStream_t stream) {
+  if (!m || !m->manager || (count && (!in_ptrs || !in_sizes || !out_ptrs || !out_sizes))) return status_to_nvcomp_error(Status::ERROR_INVALID_PARAMETER);
+  std::vector<BatchItem> items(count);
+  for (size_t i = 0; i < count; i++) {
+    items[i].input_ptr = (void *)in_ptrs[i];
+    items[i].output_ptr = out_ptrs[i];
+    items[i].input_size = in_sizes[i];
+    items[i].output_size = out_sizes[i];
+  }
+  Status s = m->manager->decompress_batch(items, ws, ws_size, stream);
+  for (size_t i = 0; i < count; i++) {
+    out_sizes[i] = items[i].status == Status::SUCCESS ? items[i].output_size : 0;
+    if (statuses) statuses[i] = status_to_nvcomp_error(items[i].status);
+  }
+  return status_to_nvcomp_error(s);
+}
 
 nvcompZstdManagerHandle nvcomp_zstd_create_manager_v5(int level) {
   try {
@@ -1078,6 +1346,24 @@ int nvcomp_zstd_batched_compress_async_v5(nvcomp_zstd_batch_manager_t *m, const 
                                           size_t n, void *const *d_out, size_t *d_out_sizes, int *d_statuses, void *t, size_t tb, hipStream_t s) {
   if (!m || !m->mgr) return status_to_nvcomp_error(Status::ERROR_INVALID_PARAMETER);
   return status_to_nvcomp_error(m->mgr->batch_manager().compress_batch_device(d_in, d_in_sizes, max_chunk, n, d_out, d_out_sizes, d_statuses, t, tb, s));
+}
+size_t nvcomp_zstd_batch_get_decompress_temp_size_v5(nvcomp_zstd_batch_manager_t *m, const size_t *sizes, size_t n) {
+  return (m && m->mgr) ? m->mgr->get_decompress_temp_size(sizes, n) : 0;
+}
+int nvcomp_zstd_batch_decompress_async_v5(nvcomp_zstd_batch_manager_t *m, const void *const *in, const size_t *in_sizes, size_t n, void *const *out,
+                                          size_t *out_sizes, void *t, size_t tb, hipStream_t s) {
+  if (!m || !m->mgr) return status_to_nvcomp_error(Status::ERROR_INVALID_PARAMETER);
+  return status_to_nvcomp_error(m->mgr->decompress_async(in, in_sizes, n, out, out_sizes, t, tb, s));
+}
+size_t nvcomp_zstd_batched_decompress_get_temp_size_v5(size_t n, size_t max_out) {
+  return ZstdBatchManager::get_batch_device_decompress_temp_size(n, max_out);
+}
+int nvcomp_zstd_batched_decompress_async_v5(nvcomp_zstd_batch_manager_t *m, const void *const *d_in, const size_t *d_in_sizes,
+                                            const size_t *d_out_caps, size_t max_out, size_t n, void *const *d_out, size_t *d_out_sizes,
+                                            int *d_statuses, void *t, size_t tb, hipStream_t s) {
+  if (!m || !m->mgr) return status_to_nvcomp_error(Status::ERROR_INVALID_PARAMETER);
+  return status_to_nvcomp_error(
+      m->mgr->batch_manager().decompress_batch_device(d_in, d_in_sizes, d_out_caps, max_out, n, d_out, d_out_sizes, d_statuses, t, tb, s));
 }
 
 cuda_zstd_hybrid_engine_t *cuda_zstd_hybrid_create(const cuda_zstd_hybrid_config_t *c) {

@@ -13,7 +13,28 @@ struct ZhItemDesc {
 // Staging slot for one block of a multi-block frame: worst case = raw block + frame header.
 #define ZH_STAGE_SLOT ((u32)ZH_BLOCK_MAX + 64u)
 
+// Decoder launch (zh_decode.hip): one workgroup per input buffer; every array is a
+// device array indexed by item.  Item i's workspace slot is ws + i * slot_bytes:
+// block_cap literal bytes (padded to lit_bytes), then seq_cap u64 sequence records.
+struct ZhDecArgs {
+  const void *const *in_ptrs;  // null: a single item given by one_in / one_in_size / one_out
+  const void *one_in;
+  u64 one_in_size;
+  void *one_out;
+  const size_t *in_sizes;
+  void *const *out_ptrs;
+  const size_t *out_caps;  // per-item output capacity, or null: out_cap_all for every item
+  u64 out_cap_all;
+  size_t *out_sizes;       // bytes produced (0 on error)
+  u32 *statuses;           // optional: Status values, or nvcomp codes when nvcomp_codes
+  u8 *ws;
+  u64 slot_bytes;
+  u32 lit_bytes, block_cap, seq_cap, nvcomp_codes;
+};
+
 namespace zh {
+u32 dec_lds_bytes();
+hipError_t launch_decompress(const ZhDecArgs &a, u32 nitems, hipStream_t stream);
 hipError_t init_kernels();
 u32 lz_lds_bytes();
 u32 entropy_lds_bytes();

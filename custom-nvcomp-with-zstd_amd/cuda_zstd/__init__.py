@@ -58,6 +58,12 @@ def lib() -> ctypes.CDLL:
             "nvcomp_zstd_batch_compress_async_v5": (i, [vp, vp, vp, sz, vp, vp, vp, sz, vp]),
             "nvcomp_zstd_batched_compress_get_temp_size_v5": (sz, [sz, sz]),
             "nvcomp_zstd_batched_compress_async_v5": (i, [vp, vp, vp, sz, sz, vp, vp, vp, vp, sz, vp]),
+            "cuda_zstd_get_batch_decompress_workspace_size": (sz, [vp, psz, sz]),
+            "cuda_zstd_decompress_batch": (i, [vp, pvp, psz, sz, pvp, psz, pi, vp, sz, vp]),
+            "nvcomp_zstd_batch_get_decompress_temp_size_v5": (sz, [vp, psz, sz]),
+            "nvcomp_zstd_batch_decompress_async_v5": (i, [vp, vp, vp, sz, vp, vp, vp, sz, vp]),
+            "nvcomp_zstd_batched_decompress_get_temp_size_v5": (sz, [sz, sz]),
+            "nvcomp_zstd_batched_decompress_async_v5": (i, [vp, vp, vp, vp, sz, sz, vp, vp, vp, vp, sz, vp]),
             "cuda_zstd_hip_version": (ctypes.c_char_p, []),
             "cuda_zstd_hip_profile_enable": (None, [i]),
             "cuda_zstd_hip_profile_collect": (i, [ctypes.POINTER(ctypes.c_double)]),
@@ -165,6 +171,82 @@ class Manager:
         return res
 
 
+    def decompress(self, frame, capacity: int, stream=None):
+        """GPU-decode one device buffer (frames, concatenated) into a new device tensor of
+        at most `capacity` bytes (cuda_zstd_decompress)."""
+        torch = _torch()
+        frame = frame.contiguous().view(torch.uint8)
+        out = torch.empty(max(capacity, 1), dtype=torch.uint8, device=frame.device)
+        ws = self._workspace(lib().cuda_zstd_get_decompress_workspace_size(self._h, frame.numel()))
+        size = ctypes.c_size_t(capacity)
+        rc = lib().cuda_zstd_decompress(self._h, frame.data_ptr(), frame.numel(), out.data_ptr(), ctypes.byref(size), ws.data_ptr(), ws.numel(),
+                                        _stream_ptr(stream))
+        if rc:
+            raise ZstdError(rc, "cuda_zstd_decompress")
+        return out[: size.value]
+
+    def decompress_batch(self, frames: Sequence, capacities: Sequence[int], stream=None, raise_on_error=True):
+        """ZstdBatchManager::decompress_batch over device tensors: one GPU launch for all.
+        Returns the decoded tensors (and, with raise_on_error=False, the nvcomp codes)."""
+        torch = _torch()
+        n = len(frames)
+        ins = [f.contiguous().view(torch.uint8) for f in frames]
+        offs = [0]
+        for c in capacities:
+            offs.append(offs[-1] + ((max(c, 1) + 255) // 256) * 256)
+        out = torch.empty(max(offs[-1], 256), dtype=torch.uint8, device="cuda")
+        in_ptrs = (ctypes.c_void_p * n)(*[t.data_ptr() for t in ins])
+        out_ptrs = (ctypes.c_void_p * n)(*[out.data_ptr() + o for o in offs[:-1]])
+        in_sz = (ctypes.c_size_t * n)(*[t.numel() for t in ins])
+        out_sz = (ctypes.c_size_t * n)(*capacities)
+        st = (ctypes.c_int * n)()
+        ws = self._workspace(lib().cuda_zstd_get_batch_decompress_workspace_size(self._h, in_sz, n))
+        rc = lib().cuda_zstd_decompress_batch(self._h, in_ptrs, in_sz, n, out_ptrs, out_sz, st, ws.data_ptr(), ws.numel(), _stream_ptr(stream))
+        if rc and all(s == OK for s in st):
+            raise ZstdError(rc, "cuda_zstd_decompress_batch")
+        res = [out[offs[k] : offs[k] + out_sz[k]] for k in range(n)]
+        if raise_on_error:
+            for k in range(n):
+                if st[k] != OK:
+                    raise ZstdError(st[k], f"cuda_zstd_decompress_batch item {k}")
+            return res
+        return res, list(st)
+
+
+class BatchedDecompressor:
+    """Stream-ordered batched GPU decompression over device arrays
+    (nvcomp_zstd_batched_decompress_async_v5).  Used by bench.py --decompress."""
+
+    def __init__(self):
+        self._h = lib().nvcomp_zstd_batch_create_v5(3, 64 * 1024, 0)
+        if not self._h:
+            raise ZstdError(INVALID, "nvcomp_zstd_batch_create_v5")
+
+    def close(self):
+        if self._h:
+            lib().nvcomp_zstd_batch_destroy_v5(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    @staticmethod
+    def temp_size(num_chunks: int, max_out: int) -> int:
+        return lib().nvcomp_zstd_batched_decompress_get_temp_size_v5(num_chunks, max_out)
+
+    def decompress_async(self, d_in_ptrs, d_in_sizes, d_out_caps, max_out, d_out_ptrs, d_out_sizes, d_status, temp, stream=None):
+        n = d_in_ptrs.numel()
+        rc = lib().nvcomp_zstd_batched_decompress_async_v5(
+            self._h, d_in_ptrs.data_ptr(), d_in_sizes.data_ptr(), d_out_caps.data_ptr() if d_out_caps is not None else None, max_out, n,
+            d_out_ptrs.data_ptr(), d_out_sizes.data_ptr(), d_status.data_ptr() if d_status is not None else None, temp.data_ptr(), temp.numel(),
+            _stream_ptr(stream))
+        if rc:
+            raise ZstdError(rc, "nvcomp_zstd_batched_decompress_async_v5")
+
+
 class BatchedCompressor:
     """Stream-ordered batched compression of equal-capacity chunk slots
     (nvcomp_zstd_batched_compress_async_v5).  Used by bench.py."""
@@ -208,6 +290,14 @@ def compress(data, level: int = 3, stream=None):
 
 def compress_batch(chunks, level: int = 3, stream=None):
     return Manager(level).compress_batch(chunks, stream)
+
+
+def decompress(frame, capacity: int, stream=None):
+    return Manager(3).decompress(frame, capacity, stream)
+
+
+def decompress_batch(frames, capacities, stream=None):
+    return Manager(3).decompress_batch(frames, capacities, stream)
 
 
 def profile_enable(on: bool = True) -> None:

@@ -53,6 +53,13 @@ int cuda_zstd_compress_batch(cuda_zstd_manager_t *manager, const void *const *in
                              void *const *output_ptrs, size_t *output_sizes, int *statuses, void *workspace,
                              size_t workspace_size, hipStream_t stream);
 size_t cuda_zstd_get_max_compressed_size(cuda_zstd_manager_t *manager, size_t src_size);
+/* batch decompression (C counterpart of ZstdBatchManager::decompress_batch,
+ * reference include/cuda_zstd_manager.h:153-158, src/cuda_zstd_manager.cu:5799-5885): the GPU
+ * decoder, one launch for all items; out_sizes[i] capacity in, bytes out (0 on error). */
+size_t cuda_zstd_get_batch_decompress_workspace_size(cuda_zstd_manager_t *manager, const size_t *compressed_sizes, size_t count);
+int cuda_zstd_decompress_batch(cuda_zstd_manager_t *manager, const void *const *input_ptrs, const size_t *input_sizes, size_t count,
+                               void *const *output_ptrs, size_t *output_sizes, int *statuses, void *workspace, size_t workspace_size,
+                               hipStream_t stream);
 
 /* ---------------- nvCOMP v5 API (reference include/cuda_zstd_nvcomp.h:277-331) ---------------- */
 typedef void *nvcompZstdManagerHandle;
@@ -91,6 +98,26 @@ int nvcomp_zstd_batched_compress_async_v5(nvcomp_zstd_batch_manager_t *mgr, cons
                                           size_t num_chunks, void *const *d_compressed_ptrs, size_t *d_compressed_sizes,
                                           int *d_statuses, void *d_temp_storage, size_t temp_storage_bytes,
                                           hipStream_t stream);
+
+/* NvcompV5BatchManager::decompress_async as a C handle call (reference include/cuda_zstd_nvcomp.h:97-99,
+ * 119-125): host or device arrays, uncompressed_sizes[i] capacity in, bytes out; blocking on return. */
+size_t nvcomp_zstd_batch_get_decompress_temp_size_v5(nvcomp_zstd_batch_manager_t *mgr, const size_t *compressed_sizes, size_t num_chunks);
+int nvcomp_zstd_batch_decompress_async_v5(nvcomp_zstd_batch_manager_t *mgr, const void *const *d_compressed_ptrs,
+                                          const size_t *compressed_sizes, size_t num_chunks, void *const *d_uncompressed_ptrs,
+                                          size_t *uncompressed_sizes, void *d_temp_storage, size_t temp_storage_bytes, hipStream_t stream);
+
+/* Stream-ordered batched decompression (nvCOMP nvcompBatchedZstdDecompressAsync shape).
+ * All arrays are DEVICE arrays; nothing is synchronised.  d_uncompressed_caps[i] = output
+ * capacity (null: max_uncompressed_chunk_bytes for every chunk); d_actual_sizes[i] receives
+ * the bytes produced (0 on error); d_statuses[i] (optional) the nvcomp-style code.
+ * Decodes any RFC 8878 frame (concatenated and skippable frames included) whose blocks
+ * regenerate at most min(128 KiB, max_uncompressed_chunk_bytes) bytes of literals. */
+size_t nvcomp_zstd_batched_decompress_get_temp_size_v5(size_t num_chunks, size_t max_uncompressed_chunk_bytes);
+int nvcomp_zstd_batched_decompress_async_v5(nvcomp_zstd_batch_manager_t *mgr, const void *const *d_compressed_ptrs,
+                                            const size_t *d_compressed_sizes, const size_t *d_uncompressed_caps,
+                                            size_t max_uncompressed_chunk_bytes, size_t num_chunks, void *const *d_uncompressed_ptrs,
+                                            size_t *d_actual_sizes, int *d_statuses, void *d_temp_storage, size_t temp_storage_bytes,
+                                            hipStream_t stream);
 
 /* ---------------- hybrid API (reference include/cuda_zstd_hybrid.h:296-359) ---------------- */
 typedef struct cuda_zstd_hybrid_engine_t cuda_zstd_hybrid_engine_t;

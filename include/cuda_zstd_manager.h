@@ -105,6 +105,16 @@ class ZstdBatchManager : public ZstdManager {
                                hipStream_t stream);
   static size_t get_batch_device_temp_size(size_t count, size_t max_chunk_bytes);
 
+  // Stream-ordered batched decompression over device arrays (no host sync; GPU decoder,
+  // any RFC 8878 frames); used by nvcomp_zstd_batched_decompress_async_v5.
+  // d_out_caps[i] = output capacity (every capacity <= max_uncompressed_chunk_bytes, or null:
+  // max_uncompressed_chunk_bytes for all); d_out_sizes[i] = bytes produced (0 on error);
+  // d_statuses[i] (optional) = nvcomp-style code.
+  Status decompress_batch_device(const void *const *d_in_ptrs, const size_t *d_in_sizes, const size_t *d_out_caps,
+                                 size_t max_uncompressed_chunk_bytes, size_t count, void *const *d_out_ptrs, size_t *d_out_sizes,
+                                 int *d_statuses, void *temp_workspace, size_t temp_size, hipStream_t stream);
+  static size_t get_batch_device_decompress_temp_size(size_t count, size_t max_uncompressed_chunk_bytes);
+
  private:
   class Impl;
   std::unique_ptr<Impl> pimpl_;

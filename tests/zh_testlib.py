@@ -97,6 +97,32 @@ def zstd_decompress(frame, size):
     return dst[:r].tobytes()
 
 
+def zstd_compress(data, level=3, checksum=False, content_size=True, window_log=0):
+    """libzstd frame of `data` (ZSTD_compress2 with the given frame parameters).
+    ZSTD_cParameter values of zstd.h 1.4.x: compressionLevel 100, windowLog 101,
+    contentSizeFlag 200, checksumFlag 201."""
+    z = zstd()
+    assert z is not None, "libzstd not available"
+    z.ZSTD_createCCtx.restype = vp
+    z.ZSTD_freeCCtx.argtypes = [vp]
+    z.ZSTD_CCtx_setParameter.argtypes = [vp, ctypes.c_int, ctypes.c_int]
+    z.ZSTD_CCtx_setParameter.restype = ctypes.c_size_t
+    z.ZSTD_compress2.argtypes = [vp, vp, ctypes.c_size_t, vp, ctypes.c_size_t]
+    z.ZSTD_compress2.restype = ctypes.c_size_t
+    z.ZSTD_compressBound.restype = ctypes.c_size_t
+    src = np.ascontiguousarray(np.frombuffer(bytes(data), np.uint8))
+    cctx = z.ZSTD_createCCtx()
+    params = [(100, level), (201, int(checksum)), (200, int(content_size))] + ([(101, window_log)] if window_log else [])
+    for p, v in params:
+        assert not z.ZSTD_isError(z.ZSTD_CCtx_setParameter(cctx, p, v))
+    cap = int(z.ZSTD_compressBound(ctypes.c_size_t(len(src)))) + 64
+    out = np.zeros(cap, np.uint8)
+    r = z.ZSTD_compress2(cctx, out.ctypes.data, cap, src.ctypes.data if len(src) else None, len(src))
+    z.ZSTD_freeCCtx(cctx)
+    assert not z.ZSTD_isError(r), z.ZSTD_getErrorName(r)
+    return out[:r].tobytes()
+
+
 def special_inputs():
     """Edge cases the reference tests exercise (tests/test_compressible_data.cu:22-101,
     tests/test_c_api_edge_cases.cu): tiny, ragged, zeros, 0xFF, periodic, random."""
