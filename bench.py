@@ -84,6 +84,69 @@ def cpu_baseline(data, threads, seconds=1.5):
                       f"of the same 64 KiB chunks, {threads} threads, {el:.2f} s wall; ratio {done_bytes / max(comp_bytes, 1):.3f}"}
 
 
+def libzstd_roundtrip(frames, sizes, slot, host):
+    """Every rank-0 frame through stock libzstd (ZSTD_decompress), 16 host threads;
+    True iff all decode to their chunk.  None without libzstd."""
+    import concurrent.futures as cf
+
+    import zh_testlib as T
+
+    z = T.zstd()
+    if z is None:
+        return None
+    n = len(sizes)
+
+    def work(lo, hi):
+        dst = np.zeros(CHUNK, np.uint8)
+        vp = ctypes.c_void_p
+        for i in range(lo, hi):
+            r = z.ZSTD_decompress(dst.ctypes.data_as(vp), ctypes.c_size_t(CHUNK), ctypes.c_void_p(frames.ctypes.data + i * slot), ctypes.c_size_t(int(sizes[i])))
+            if r != CHUNK or not np.array_equal(dst, host[i * CHUNK:(i + 1) * CHUNK]):
+                return False
+        return True
+
+    step = (n + 15) // 16
+    with cf.ThreadPoolExecutor(16) as ex:
+        return all(ex.map(lambda k: work(k, min(n, k + step)), range(0, n, step)))
+
+
+def decompress_leg(d_in, d_out, out_ptrs, out_sizes, n, dev, steps, world):
+    """GPU decompression of the frames just produced, device-resident:
+    zh_decode_kernel through nvcomp_zstd_batched_decompress_async_v5, timed with events on
+    the launch stream after one warm-up; output compared with the input on the device."""
+    import cuda_zstd
+
+    bd = cuda_zstd.BatchedDecompressor()
+    back = torch.empty(n * CHUNK, dtype=torch.uint8, device=dev)
+    ar = torch.arange(n, dtype=torch.int64, device=dev)
+    back_ptrs = back.data_ptr() + ar * CHUNK
+    dsizes = torch.zeros(n, dtype=torch.int64, device=dev)
+    status = torch.full((n,), -1, dtype=torch.int32, device=dev)
+    temp = torch.empty(bd.temp_size(n, CHUNK), dtype=torch.uint8, device=dev)
+    run = lambda: bd.decompress_async(out_ptrs, out_sizes, None, CHUNK, back_ptrs, dsizes, status, temp)
+    run()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(steps):
+        run()
+    e1.record()
+    torch.cuda.synchronize(dev)
+    ms = e0.elapsed_time(e1) / steps
+    ok = bool((status == 0).all().item()) and bool((dsizes == CHUNK).all().item()) and torch.equal(back, d_in)
+    t = torch.tensor([ms], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    ms = t.item()
+    comp = float(out_sizes.sum().item())
+    del back, temp
+    return {"value": round(world * n * CHUNK / (ms / 1e3) / 1e9, 3), "unit": "GB/s (decompressed bytes)", "kernel": "zh_decode_kernel",
+            "ms_per_step": round(ms, 3), "steps": steps, "roundtrip_equal": ok,
+            "hbm_GBps_algorithmic": round((n * CHUNK + comp) / (ms / 1e3) / 1e9, 2)}
+
+
 def pmc_traffic(kernel):
     """HBM bytes per launch of `kernel` from the newest committed rocprofv3 PMC summary
     (profiles/*_rocprof_summary.json, written by tools/prof_summary.py: 2 x FETCH_SIZE +
@@ -106,7 +169,8 @@ def main():
     ap.add_argument("--dataset", default="mix", choices=sorted(SEEDS))
     ap.add_argument("--chunks", type=int, default=CHUNKS_PER_GPU, help="chunks per GPU")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--verify", action="store_true", help="libzstd-decode every rank-0 frame after timing")
+    ap.add_argument("--no-verify", action="store_true", help="skip the libzstd decode of every rank-0 frame after timing")
+    ap.add_argument("--no-decompress", action="store_true", help="skip the GPU decompression leg")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -175,12 +239,12 @@ def main():
         comp_all, k1, k2 = float(comp), stats[2].item(), stats[3].item()
 
     verified = None
-    if args.verify and rank == 0:
-        import zh_testlib as T
+    if not args.no_verify and rank == 0:
+        verified = libzstd_roundtrip(d_out.cpu().numpy(), out_sizes.cpu().numpy(), slot, host)
 
-        sizes = out_sizes.cpu().numpy()
-        hb = d_out.cpu().numpy()
-        verified = all(T.zstd_decompress(hb[i * slot:i * slot + sizes[i]].tobytes(), CHUNK) == host[i * CHUNK:(i + 1) * CHUNK].tobytes() for i in range(n))
+    dec = None
+    if not args.no_decompress:
+        dec = decompress_leg(d_in, d_out, out_ptrs, out_sizes, n, dev, min(args.steps, 5), world)
 
     if rank == 0:
         total_in = float(world * n * CHUNK)
@@ -202,6 +266,8 @@ def main():
                          "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
                          "algorithmic_bytes_per_launch": int(per_launch_bytes), "traffic_source": traffic_src},
         }
+        if dec is not None:
+            line["decompress"] = dec
         if not args.no_cpu_baseline:
             threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
             line["cpu_baseline"] = cpu_baseline(host, threads)

@@ -34,8 +34,9 @@ typedef int64_t s64;
 namespace {
 
 constexpr u32 DEC_THREADS = 64;
-constexpr u32 DEC_STAGE = 4096;   // output window (LDS)
-constexpr u32 DEC_LSTAGE = 4096;  // literal window (LDS)
+constexpr u32 DEC_STAGE = 8192;   // output window (LDS)
+constexpr u32 HSTAGE = 1024;      // per-stream LDS stage of a Huffman stream
+constexpr u32 SSTAGE = 4096;      // LDS stage of the sequence bitstream
 constexpr u32 HUF_LOG_MAX = 11;   // RFC 8878 §4.2.1: Max_Number_of_Bits <= 11
 constexpr u32 BLOCKSIZE_MAX = 128u * 1024u;
 constexpr u32 OFF_LIMIT = 1u << 30;  // offsets are stored in 30 bits (windows up to 1 GiB)
@@ -66,19 +67,22 @@ __device__ __forceinline__ u32 tab_maxsv(u32 t) { return t == 0 ? 35u : t == 1 ?
 __device__ __forceinline__ u32 tab_maxlog(u32 t) { return t == 1 ? 8u : 9u; }
 constexpr u32 TAB_NONE = 0xFFFFu, TAB_PREDEF = 0xFFFEu;  // tkind; else RLE symbol | 0x100, or 0 = FSE
 
+// The union's three views are used one after the other inside a block: Huffman decode,
+// sequence bitstream, execution window.
 struct DecLds {
   u32 fse[1280];  // LL [0,512) OF [512,768) ML [768,1280): sym | nbBits << 8 | newState << 16
   union {
     struct {
       u16 dt[1 << HUF_LOG_MAX];  // Huffman decode table: sym | nbBits << 8
-      u32 wt[64];                // FSE table of the Huffman weights (log <= 6)
-      u8 symlist[256];           // symbols grouped by weight
+      u8 hs[4][HSTAGE + 16];     // staged bytes of the 4 streams
     } h;
-    struct {
-      u8 out[DEC_STAGE + 16];
-      u8 lit[DEC_LSTAGE + 16];
-    } x;
+    u8 sstage[SSTAGE + 16];      // staged bytes of the sequence bitstream
+    u8 out[DEC_STAGE + 16];      // execution window
   } u;
+  u32 wt[64];       // FSE table of the Huffman weights (log <= 6)
+  u8 symlist[256];  // Huffman build: symbols grouped by weight
+  s32 wvs[68];      // execution window: virtual start of each sequence (binary search keys)
+  u32 wll[64], wlit[64], woff[64];  // execution window: literal length, first literal, offset
   u32 info[2][64];  // LL / ML code info (baseline | bits << 24), copied from constants
   s16 norm[256];    // NCount scratch
   u16 next[256];    // FSE build scratch (symbolNext)
@@ -107,9 +111,14 @@ __device__ __forceinline__ u64 ldg64(const u8 *p) {
   u32 const hi = __builtin_amdgcn_alignbyte(w2, w1, sh);
   return ((u64)hi << 32) | lo;
 }
-__device__ __forceinline__ u32 rd16(const u8 *p) { return p[0] | (u32)p[1] << 8; }
-__device__ __forceinline__ u32 rd24(const u8 *p) { return p[0] | (u32)p[1] << 8 | (u32)p[2] << 16; }
-__device__ __forceinline__ u32 rd32(const u8 *p) { return p[0] | (u32)p[1] << 8 | (u32)p[2] << 16 | (u32)p[3] << 24; }
+// Header fields are read as wave-uniform values (readfirstlane): every lane walks the same
+// frame, so the whole control flow of the kernel runs on the scalar unit (s_cbranch on
+// SCC, no exec-mask bookkeeping).  Inside lane-0-only sections the first active lane is 0.
+__device__ __forceinline__ u32 uni(u32 v) { return __builtin_amdgcn_readfirstlane(v); }
+__device__ __forceinline__ u32 ub(const u8 *p) { return uni(p[0]); }
+__device__ __forceinline__ u32 rd16(const u8 *p) { return uni(p[0] | (u32)p[1] << 8); }
+__device__ __forceinline__ u32 rd24(const u8 *p) { return uni(p[0] | (u32)p[1] << 8 | (u32)p[2] << 16); }
+__device__ __forceinline__ u32 rd32(const u8 *p) { return uni(p[0] | (u32)p[1] << 8 | (u32)p[2] << 16 | (u32)p[3] << 24); }
 
 // Backward bit reader (RFC 8878 §4.1: streams are read from the end; the last byte's
 // highest set bit marks the start).  pos = bits not yet consumed; reads past the start
@@ -160,6 +169,104 @@ struct BitRev {
     u32 const v = (u32)peek(k);
     pos -= (s32)k;
     return v;
+  }
+};
+
+// ---- LDS-staged streams: the decoders read their bitstreams from LDS; a wave copies the
+// next stretch of a stream in one burst (all loads in flight), so a refill costs one HBM
+// round trip per stage instead of one per 8 bytes.
+// Copy stream bytes [lo, hi) of p to stage (wave-cooperative: every lane calls it).  Aligned
+// dword loads only; the dword after a word is read only when it still holds a range byte.
+__device__ void stage_copy(u8 *stage, const u8 *p, u32 lo, u32 hi) {
+  u32 const lane = lane_id();
+  const u8 *const s0 = p + lo;
+  u32 const sa = (u32)((uintptr_t)s0 & 3u);
+  const u32 *const s32 = (const u32 *)(s0 - sa);
+  u32 const nb = hi - lo, ndw = (nb + 3) >> 2, lim = sa + nb;
+  u32 *const d32 = (u32 *)stage;
+  constexpr u32 U = 4;
+  for (u32 w0 = 0; w0 < ndw; w0 += 64 * U) {
+    u32 v[U];
+#pragma unroll
+    for (u32 u = 0; u < U; u++) {
+      u32 const w = w0 + 64 * u + lane;
+      v[u] = 0;
+      if (w < ndw) {
+        u32 const A = s32[w];
+        u32 const B = (sa && 4 * (w + 1) < lim) ? s32[w + 1] : 0u;
+        v[u] = __builtin_amdgcn_alignbyte(B, A, sa);
+      }
+    }
+#pragma unroll
+    for (u32 u = 0; u < U; u++) {
+      u32 const w = w0 + 64 * u + lane;
+      if (w < ndw) d32[w] = v[u];
+    }
+  }
+}
+
+// 8 bytes at byte offset o of a 4-aligned LDS stage (padded by 12 bytes)
+__device__ __forceinline__ u64 lds64(const u8 *stage, u32 o) {
+  const u32 *w = (const u32 *)(stage + (o & ~3u));
+  u32 const sh = o & 3u;
+  u32 const w0 = w[0], w1 = w[1], w2 = w[2];
+  return ((u64)__builtin_amdgcn_alignbyte(w2, w1, sh) << 32) | __builtin_amdgcn_alignbyte(w1, w0, sh);
+}
+
+// Backward bit reader over an LDS stage holding stream bytes [slo, min(n, slo + cap)).
+// peek() reports a needed restage instead of reading below slo.
+struct BitRevS {
+  const u8 *p;
+  s32 n, pos, cb, slo;
+  u64 c;  // bytes [cb, cb + 8) (zero-extended for streams under 8 bytes)
+  template <bool UNI = false>
+  __device__ __forceinline__ bool start(const u8 *s, u32 sz) {
+    p = s;
+    n = (s32)sz;
+    pos = 0;
+    cb = n + 1;   // no container yet
+    slo = n + 1;  // nothing staged
+    c = 0;
+    if (sz == 0) return false;
+    u32 const last = UNI ? ub(s + sz - 1) : s[sz - 1];
+    if (!last) return false;
+    pos = 8 * ((s32)sz - 1) + (s32)hb32(last);
+    return true;
+  }
+  // container base the next read of k bits needs (valid when lo < 8 cb)
+  __device__ __forceinline__ s32 want(u32 k) const {
+    s32 nb = ((pos + 7) >> 3) - 8;
+    nb = nb < 0 ? 0 : nb;
+    return n < 8 ? 0 : (nb > n - 8 ? n - 8 : nb);
+  }
+  // stage window for a restage: [lo, hi)
+  __device__ __forceinline__ void stage_range(s32 cap, u32 &lo, u32 &hi) const {
+    s32 h = n < 8 ? n : want(0) + 8;
+    s32 l = h - cap;
+    lo = (u32)(l < 0 ? 0 : l);
+    hi = (u32)h;
+  }
+  // refill the container if the next k bits need it; false = restage first.  UNI: every
+  // lane holds the same reader (the sequence decoder): the container is made uniform too.
+  template <bool UNI = false>
+  __device__ __forceinline__ bool ensure(const u8 *stage, u32 k) {
+    s32 const lo = pos - (s32)k;
+    if (lo >= 8 * cb) return true;
+    s32 const nb = want(k);
+    if (nb == cb) return true;  // (reads below the stream start: zeros)
+    if (nb < slo) return false;
+    c = lds64(stage, (u32)(nb - slo));
+    if (UNI) c = ((u64)uni((u32)(c >> 32)) << 32) | uni((u32)c);
+    if (n < 8) c &= ~0ull >> (64 - 8 * n);
+    cb = nb;
+    return true;
+  }
+  __device__ __forceinline__ u64 bits(u32 k) const {
+    s32 const lo = pos - (s32)k;
+    u64 const m = k ? (~0ull >> (64 - k)) : 0ull;
+    if (lo >= 8 * cb) return (c >> (lo - 8 * cb)) & m;
+    s32 const sh = 8 * cb - lo;  // cb == 0: missing low bits are zeros
+    return sh < 64 ? (c << sh) & m : 0ull;
   }
 };
 
@@ -286,21 +393,21 @@ __device__ u32 huf_read_weights(DecLds &L, const u8 *p, u32 avail) {
     u32 wlog;
     u32 const nc = read_ncount(p + 1, hb, L.norm, 255, 6, wlog);
     if (!nc) return 0;
-    if (!build_dtable(L.u.h.wt, L.norm, 255, wlog, L.next)) return 0;
+    if (!build_dtable(L.wt, L.norm, 255, wlog, L.next)) return 0;
     BitRev r;
     if (!r.init(p + 1 + nc, hb - nc)) return 0;
     u32 s1 = r.read(wlog), s2 = r.read(wlog);
     // two interleaved states; the stream ends when a state update overflows
     for (;;) {
       if (nw > 253) return 0;
-      u32 e = L.u.h.wt[s1];
+      u32 e = L.wt[s1];
       L.hufw[nw++] = (u8)(e & 0xFF);
       s1 = (e >> 16) + r.read((e >> 8) & 0xFF);
-      if (r.pos < 0) { L.hufw[nw++] = (u8)(L.u.h.wt[s2] & 0xFF); break; }
-      e = L.u.h.wt[s2];
+      if (r.pos < 0) { L.hufw[nw++] = (u8)(L.wt[s2] & 0xFF); break; }
+      e = L.wt[s2];
       L.hufw[nw++] = (u8)(e & 0xFF);
       s2 = (e >> 16) + r.read((e >> 8) & 0xFF);
-      if (r.pos < 0) { L.hufw[nw++] = (u8)(L.u.h.wt[s1] & 0xFF); break; }
+      if (r.pos < 0) { L.hufw[nw++] = (u8)(L.wt[s1] & 0xFF); break; }
     }
   }
   u32 rs[16] = {};
@@ -329,7 +436,7 @@ __device__ u32 huf_read_weights(DecLds &L, const u8 *p, u32 avail) {
 // ascending inside a class, 2^(w-1) entries per symbol.
 __device__ void huf_build_dtable(DecLds &L) {
   u32 const lane = lane_id();
-  u32 const tlog = L.hlog;
+  u32 const tlog = uni(L.hlog);
   u32 w4[4];
 #pragma unroll
   for (u32 k = 0; k < 4; k++) w4[k] = L.hufw[64 * k + lane];
@@ -354,7 +461,7 @@ __device__ void huf_build_dtable(DecLds &L) {
       u64 const m = __ballot(w4[k] == w);
       if (w4[k] == w) {
         u32 const r = __builtin_amdgcn_mbcnt_hi((u32)(m >> 32), __builtin_amdgcn_mbcnt_lo((u32)m, 0u));
-        L.u.h.symlist[cs[w] + run[w] + r] = (u8)(64 * k + lane);
+        L.symlist[cs[w] + run[w] + r] = (u8)(64 * k + lane);
       }
       run[w] += (u32)__popcll(m);
     }
@@ -365,7 +472,7 @@ __device__ void huf_build_dtable(DecLds &L) {
 #pragma unroll
     for (u32 v = 2; v <= 11; v++) w = (cnt[v] && e >= rk[v]) ? v : w;
     u32 const idx = (e - rk[w]) >> (w - 1);
-    u32 const s = L.u.h.symlist[cs[w] + idx];
+    u32 const s = L.symlist[cs[w] + idx];
     L.u.h.dt[e] = (u16)(s | (tlog + 1 - w) << 8);
   }
   __syncthreads();
@@ -431,7 +538,7 @@ __device__ void wave_fill(u8 *dst, u32 v, u32 n) {
 __device__ u32 decode_literals(DecLds &L, const u8 *bp, u32 bsz, const Slot &sl, LitSrc &lits, u32 &st) {
   u32 const lane = lane_id();
   if (bsz < 1) { st = ST_CORRUPT; return 0; }
-  u32 const h0 = bp[0];
+  u32 const h0 = ub(bp);
   u32 const lt = h0 & 3u, sf = (h0 >> 2) & 3u;
   if (lt <= 1) {  // raw / RLE
     u32 hs, n;
@@ -457,13 +564,13 @@ __device__ u32 decode_literals(DecLds &L, const u8 *bp, u32 bsz, const Slot &sl,
     }
     if (hs + 1 > bsz) { st = ST_CORRUPT; return 0; }
     lits.g = nullptr;
-    lits.rle = bp[hs];
+    lits.rle = ub(bp + hs);
     return hs + 1;
   }
   // Huffman-coded (2) or treeless (3)
   u32 const hs = sf <= 1 ? 3u : sf == 2 ? 4u : 5u;
   if (bsz < hs) { st = ST_CORRUPT; return 0; }
-  u64 const hv = sf <= 1 ? (u64)rd24(bp) : sf == 2 ? (u64)rd32(bp) : ((u64)rd32(bp) | (u64)bp[4] << 32);
+  u64 const hv = sf <= 1 ? (u64)rd24(bp) : sf == 2 ? (u64)rd32(bp) : ((u64)rd32(bp) | (u64)ub(bp + 4) << 32);
   u32 n, cs;
   if (sf <= 1) {
     n = (u32)(hv >> 4) & 0x3FFu;
@@ -488,16 +595,16 @@ __device__ u32 decode_literals(DecLds &L, const u8 *bp, u32 bsz, const Slot &sl,
       L.used = used;
     }
     __syncthreads();
-    if (L.err) { st = ST_CORRUPT; return 0; }
-    u32 const used = L.used;
+    if (uni(L.err)) { st = ST_CORRUPT; return 0; }
+    u32 const used = uni(L.used);
     p += used;
     rem -= used;
-  } else if (!L.hvalid) {
+  } else if (!uni(L.hvalid)) {
     st = ST_CORRUPT;
     return 0;
   }
   huf_build_dtable(L);
-  u32 const tlog = L.hlog;
+  u32 const tlog = uni(L.hlog);
   // streams
   const u8 *sp[4];
   u32 ssz[4], cnt[4], off[4];
@@ -527,25 +634,40 @@ __device__ u32 decode_literals(DecLds &L, const u8 *bp, u32 bsz, const Slot &sl,
       off[k] = k * seg;
     }
   }
-  bool bad = false;
-  if (lane < ns) {
-    const u8 *mp = sp[0];
-    u32 msz = ssz[0], mc = cnt[0], mo = off[0];
-    for (u32 k = 1; k < 4; k++)
-      if (lane == k) { mp = sp[k]; msz = ssz[k]; mc = cnt[k]; mo = off[k]; }
-    BitRev r;
-    if (!r.init(mp, msz)) {
-      bad = true;
-    } else {
-      u8 *o = sl.lit + mo;
-      for (u32 i = 0; i < mc; i++) {
-        u32 const e = L.u.h.dt[(u32)r.peek(tlog)];
-        o[i] = (u8)e;
-        r.pos -= (s32)(e >> 8);
-      }
-      bad = r.pos != 0;
+  // lanes 0..ns-1 decode one stream each, reading it from an LDS stage; a lane whose
+  // stage runs out stops, and the wave restages every such stream in one burst per round
+  const u8 *mp = sp[0];
+  u32 msz = ssz[0], mc = cnt[0], mo = off[0];
+  for (u32 k = 1; k < 4; k++)
+    if (lane == k) { mp = sp[k]; msz = ssz[k]; mc = cnt[k]; mo = off[k]; }
+  bool const act = lane < ns;
+  BitRevS r;
+  bool bad = !r.start(mp, act ? msz : 0u) && act;
+  u32 const mcnt = act && !bad ? mc : 0u;
+  u8 *const o = sl.lit + mo;
+  u8 *const stg = L.u.h.hs[lane & 3u];
+  u32 i = 0;
+  for (;;) {
+    bool need = false;
+    while (i < mcnt) {
+      if (!r.ensure(stg, tlog)) { need = true; break; }
+      u32 const e = L.u.h.dt[(u32)r.bits(tlog)];
+      o[i++] = (u8)e;
+      r.pos -= (s32)(e >> 8);
     }
+    u64 const nm = __ballot(need);
+    if (!nm) break;
+    u32 lo, hi;
+    r.stage_range(HSTAGE, lo, hi);
+    for (u32 k = 0; k < 4; k++) {
+      if (!((nm >> k) & 1u)) continue;
+      u32 const lk = __builtin_amdgcn_readlane(lo, k), hk = __builtin_amdgcn_readlane(hi, k);
+      stage_copy(L.u.h.hs[k], sp[k], lk, hk);
+      if (lane == k) r.slo = (s32)lk;
+    }
+    __syncthreads();
   }
+  bad |= act && r.pos != 0;
   if (__ballot(bad)) { st = ST_CORRUPT; return 0; }
   lits.g = sl.lit;
   lits.rle = 0;
@@ -663,6 +785,19 @@ __device__ __forceinline__ u32 to_nvcomp(u32 s) {
 
 }  // namespace
 
+// Diagnostic build only (-DZH_STAMPS): per-phase s_memtime cycles of each item, written
+// to the first 64 bytes of its workspace slot when it finishes (tools/dec_stamps.py).
+#ifdef ZH_STAMPS
+#define DSTAMP(k)                              \
+  do {                                         \
+    u64 _t = __builtin_amdgcn_s_memtime();     \
+    stv[k] += _t - stp;                        \
+    stp = _t;                                  \
+  } while (0)
+#else
+#define DSTAMP(k) do { } while (0)
+#endif
+
 // One workgroup (one wave) per input buffer.
 extern "C" __global__ __launch_bounds__(DEC_THREADS) void zh_decode_kernel(ZhDecArgs a) {
   __shared__ DecLds L;
@@ -676,6 +811,7 @@ extern "C" __global__ __launch_bounds__(DEC_THREADS) void zh_decode_kernel(ZhDec
   sl.lit_cap = a.block_cap;
   sl.seq = (u64 *)(sl.lit + a.lit_bytes);
   sl.seq_cap = a.seq_cap;
+  if (lane < 4) L.wvs[64 + lane] = 0x7FFFFFFF;
   if (lane < 36) L.info[0][lane] = c_LL_info[lane];
   if (lane < 53) L.info[1][lane] = c_ML_info[lane];
   __syncthreads();
@@ -683,6 +819,9 @@ extern "C" __global__ __launch_bounds__(DEC_THREADS) void zh_decode_kernel(ZhDec
   u32 st = ST_OK;
   u64 produced = 0, ip = 0;
   if (!src || (!dst && cap)) st = ST_INVALID;
+#ifdef ZH_STAMPS
+  u64 stv[8] = {}, stp = __builtin_amdgcn_s_memtime();
+#endif
   while (st == ST_OK && ip < srcn) {
     // ---- frame header (RFC 8878 §3.1.1.1)
     if (srcn - ip < 4) { st = ST_CORRUPT; break; }
@@ -697,7 +836,7 @@ extern "C" __global__ __launch_bounds__(DEC_THREADS) void zh_decode_kernel(ZhDec
     if (magic != ZH_MAGIC) { st = ip == 0 ? ST_MAGIC : ST_CORRUPT; break; }
     ip += 4;
     if (srcn - ip < 1) { st = ST_CORRUPT; break; }
-    u32 const fhd = src[ip];
+    u32 const fhd = ub(src + ip);
     u32 const fcsf = fhd >> 6, single = (fhd >> 5) & 1u, chk = (fhd >> 2) & 1u, didf = fhd & 3u;
     if (fhd & 8u) { st = ST_CORRUPT; break; }
     u32 const didn = didf == 0 ? 0u : didf == 1 ? 1u : didf == 2 ? 2u : 4u;
@@ -706,14 +845,14 @@ extern "C" __global__ __launch_bounds__(DEC_THREADS) void zh_decode_kernel(ZhDec
     if (srcn - ip < hsz) { st = ST_CORRUPT; break; }
     const u8 *h = src + ip + 1;
     if (!single) {
-      u32 const wd = *h++;
+      u32 const wd = ub(h++);
       if (10 + (wd >> 3) > 30) { st = ST_CORRUPT; break; }
     }
     u32 did = 0;
-    for (u32 i = 0; i < didn; i++) did |= (u32)h[i] << (8 * i);
+    for (u32 i = 0; i < didn; i++) did |= ub(h + i) << (8 * i);
     h += didn;
     u64 fcs = ~0ull;
-    if (fcsn == 1) fcs = h[0];
+    if (fcsn == 1) fcs = ub(h);
     else if (fcsn == 2) fcs = rd16(h) + 256ull;
     else if (fcsn == 4) fcs = rd32(h);
     else if (fcsn == 8) fcs = (u64)rd32(h) | (u64)rd32(h + 4) << 32;
@@ -744,20 +883,22 @@ extern "C" __global__ __launch_bounds__(DEC_THREADS) void zh_decode_kernel(ZhDec
       } else if (bt == 1) {
         if (srcn - ip < 1) { st = ST_CORRUPT; break; }
         if (bsz > cap - produced) { st = ST_SMALL; break; }
-        wave_fill(ob, src[ip], bsz);
+        wave_fill(ob, ub(src + ip), bsz);
         ip += 1;
         produced += bsz;
       } else if (bt == 2) {
         if (bsz >= BLOCKSIZE_MAX || srcn - ip < bsz) { st = ST_CORRUPT; break; }
         const u8 *const bp = src + ip;
         LitSrc lits;
+        DSTAMP(0);
         u32 const ls = decode_literals(L, bp, bsz, sl, lits, st);
+        DSTAMP(1);
         if (!ls) break;
         // ---- sequences section header (RFC 8878 §3.1.1.3.2.1)
         const u8 *sp = bp + ls;
         u32 rem = bsz - ls;
         if (rem < 1) { st = ST_CORRUPT; break; }
-        u32 nseq = sp[0];
+        u32 nseq = ub(sp);
         if (nseq == 0) {
           if (rem != 1) { st = ST_CORRUPT; break; }
           sp += 1;
@@ -767,7 +908,7 @@ extern "C" __global__ __launch_bounds__(DEC_THREADS) void zh_decode_kernel(ZhDec
           rem -= 1;
         } else if (nseq < 255) {
           if (rem < 2) { st = ST_CORRUPT; break; }
-          nseq = ((nseq - 128) << 8) + sp[1];
+          nseq = ((nseq - 128) << 8) + ub(sp + 1);
           sp += 2;
           rem -= 2;
         } else {
@@ -780,7 +921,7 @@ extern "C" __global__ __launch_bounds__(DEC_THREADS) void zh_decode_kernel(ZhDec
         if (nseq) {
           if (nseq > sl.seq_cap) { st = nseq > BLOCKSIZE_MAX / 3 + 1 ? ST_CORRUPT : ST_SMALL; break; }
           if (rem < 1) { st = ST_CORRUPT; break; }
-          u32 const modes = sp[0];
+          u32 const modes = ub(sp);
           sp += 1;
           rem -= 1;
           if (modes & 3u) { st = ST_CORRUPT; break; }
@@ -796,26 +937,45 @@ extern "C" __global__ __launch_bounds__(DEC_THREADS) void zh_decode_kernel(ZhDec
             L.used = used;
           }
           __syncthreads();
-          if (L.err) { st = ST_CORRUPT; break; }
-          sp += L.used;
-          rem -= L.used;
+          if (uni(L.err)) { st = ST_CORRUPT; break; }
+          DSTAMP(2);
+          u32 const tused = uni(L.used);
+          sp += tused;
+          rem -= tused;
           // ---- sequence bitstream (RFC 8878 §3.1.1.3.2.2): every lane decodes redundantly
           // (uniform control flow, no exec-mask work); lane j keeps record j of each 64
-          BitRev r;
-          if (!r.init(sp, rem)) { st = ST_CORRUPT; break; }
-          u32 const lgLL = L.tlog[TAB_LL], lgOF = L.tlog[TAB_OF], lgML = L.tlog[TAB_ML];
+          BitRevS r;
+          if (!r.start<true>(sp, rem)) { st = ST_CORRUPT; break; }
+          u8 *const stg = L.u.sstage;
+          // read k bits; the bitstream comes from an LDS stage refilled SSTAGE bytes at a time
+          auto rd = [&](u32 k) -> u32 {
+            if (!r.ensure<true>(stg, k)) {
+              u32 lo, hi;
+              r.stage_range(SSTAGE, lo, hi);
+              stage_copy(stg, sp, lo, hi);
+              __syncthreads();
+              r.slo = (s32)uni(lo);
+              r.ensure<true>(stg, k);
+            }
+            u32 const v = (u32)r.bits(k);
+            r.pos -= (s32)k;
+            return v;
+          };
+          u32 const lgLL = uni(L.tlog[TAB_LL]), lgOF = uni(L.tlog[TAB_OF]), lgML = uni(L.tlog[TAB_ML]);
           const u32 *TLL = L.fse + tab_off(TAB_LL), *TOF = L.fse + tab_off(TAB_OF), *TML = L.fse + tab_off(TAB_ML);
-          u32 sLL = r.read(lgLL), sOF = r.read(lgOF), sML = r.read(lgML);
+          u32 sLL = rd(lgLL), sOF = rd(lgOF), sML = rd(lgML);
           bool big = false;
           u64 rec = 0;
           for (u32 i = 0; i < nseq; i++) {
-            u32 const eLL = TLL[sLL], eOF = TOF[sOF], eML = TML[sML];
+            // (table entries made wave-uniform: the chain runs in SGPRs)
+            u32 const eLL = __builtin_amdgcn_readfirstlane(TLL[sLL]), eOF = __builtin_amdgcn_readfirstlane(TOF[sOF]),
+                      eML = __builtin_amdgcn_readfirstlane(TML[sML]);
             u32 const ofc = eOF & 0xFFu;
-            u32 const ofv = (1u << ofc) + r.read(ofc);
-            u32 const mi = L.info[1][eML & 0xFFu];
-            u32 const ml = (mi & 0xFFFFFFu) + r.read(mi >> 24);
-            u32 const li = L.info[0][eLL & 0xFFu];
-            u32 const ll = (li & 0xFFFFFFu) + r.read(li >> 24);
+            u32 const ofv = (1u << ofc) + rd(ofc);
+            u32 const mi = __builtin_amdgcn_readfirstlane(L.info[1][eML & 0xFFu]);
+            u32 const ml = (mi & 0xFFFFFFu) + rd(mi >> 24);
+            u32 const li = __builtin_amdgcn_readfirstlane(L.info[0][eLL & 0xFFu]);
+            u32 const ll = (li & 0xFFFFFFu) + rd(li >> 24);
             u32 off;
             if (ofv > 3) {
               off = ofv - 3;
@@ -843,12 +1003,13 @@ extern "C" __global__ __launch_bounds__(DEC_THREADS) void zh_decode_kernel(ZhDec
               if (lane <= (i & 63u)) sl.seq[(i & ~63u) + lane] = rec;
             }
             if (i + 1 < nseq) {
-              sLL = (eLL >> 16) + r.read((eLL >> 8) & 0xFFu);
-              sML = (eML >> 16) + r.read((eML >> 8) & 0xFFu);
-              sOF = (eOF >> 16) + r.read((eOF >> 8) & 0xFFu);
+              sLL = (eLL >> 16) + rd((eLL >> 8) & 0xFFu);
+              sML = (eML >> 16) + rd((eML >> 8) & 0xFFu);
+              sOF = (eOF >> 16) + rd((eOF >> 8) & 0xFFu);
             }
           }
           if (r.pos > 0 || big) { st = ST_CORRUPT; break; }
+          DSTAMP(3);
         } else if (rem != 0) {
           st = ST_CORRUPT;
           break;
@@ -858,76 +1019,124 @@ extern "C" __global__ __launch_bounds__(DEC_THREADS) void zh_decode_kernel(ZhDec
         if (total > cap - produced) { st = ST_SMALL; break; }
         __threadfence_block();  // the records (and Huffman literals) are read back below
         __syncthreads();
-        // ---- execution through the LDS window
+        // ---- execution, DEC_STAGE output bytes per window.  Lanes = the next 64 sequences
+        // (prefix sums give their window positions).  Pass A, lanes = output bytes: literal
+        // bytes, and match bytes whose source lies before the window (already in HBM), are
+        // gathered with all loads of a round in flight.  Pass B, in sequence order, lanes =
+        // bytes of one match: the match bytes whose source lies inside the window, from LDS
+        // (a wave's LDS operations execute in order).  Then one coalesced flush.
         u32 const tl = lits.n - (u32)sumLL;
-        u64 const fpos = produced - fstart;  // frame bytes before this block
-        u32 q = 0, qd = 0, opos = 0, lpos = 0;
-        u64 batch = 0;
-        u32 qb = 0xFFFFFFFFu;
+        s64 const fpos = (s64)(produced - fstart);  // frame bytes before this block
+        u32 q = 0, qd = 0, opos = 0, lcur = 0;
         bool bad = false;
-        while (q <= nseq && !bad) {
+        while (q <= nseq) {
           u32 const gs = opos;
-          u32 const lw = min((u32)DEC_LSTAGE, lits.n - lpos);
-          if (lits.g) {
-            for (u32 i = lane; i < lw; i += 64) L.u.x.lit[i] = lits.g[lpos + i];
+          u32 const idx = q + lane;
+          bool const valid = idx <= nseq;
+          u32 ll = 0, ml = 0, off = 1;
+          if (idx < nseq) {
+            u64 const v = sl.seq[idx];
+            ll = (u32)v & 0x1FFFFu;
+            ml = ((u32)(v >> 17) & 0x1FFFFu) + 3u;
+            off = (u32)(v >> 34);
+          } else if (idx == nseq) {
+            ll = tl;
+          }
+          u32 const span = ll + ml;
+          u32 incl = span, linc = ll;
+#pragma unroll
+          for (u32 dd = 1; dd < 64; dd <<= 1) {
+            u32 const t = __shfl_up(incl, dd, 64), tl2 = __shfl_up(linc, dd, 64);
+            if (lane >= dd) { incl += t; linc += tl2; }
+          }
+          s32 const vs = (s32)(incl - span) - (s32)qd;  // window-relative start (q: qd bytes done)
+          s32 const ve = (s32)incl - (s32)qd;
+          u32 const lit0 = lcur + linc - ll;
+          u32 const tot = __builtin_amdgcn_readlane(incl, 63) - qd;
+          u32 const wlen = min((u32)DEC_STAGE, tot);
+          s32 const ms = vs + (s32)ll;  // window-relative match start
+          // an offset reaching before the frame start is corrupt (checked before any read)
+          bool const obad = valid && ml && vs < (s32)wlen && fpos + (s64)gs + ms - (s64)off < 0;
+          if (__ballot(obad)) { bad = true; break; }
+          L.wvs[lane] = valid && vs < (s32)wlen ? vs : 0x7FFFFFFF;
+          L.wll[lane] = ll;
+          L.wlit[lane] = lit0;
+          L.woff[lane] = off;
+          __syncthreads();
+          // pass A
+          constexpr u32 UA = 8;
+          for (u32 x0 = 0; x0 < wlen; x0 += 64 * UA) {
+            const u8 *ad[UA];
+            bool w[UA];
+#pragma unroll
+            for (u32 t = 0; t < UA; t++) {
+              u32 const x = x0 + 64 * t + lane;
+              u32 j = 0;
+#pragma unroll
+              for (u32 stp = 32; stp; stp >>= 1) j += L.wvs[j + stp] <= (s32)x ? stp : 0u;
+              u32 const d = (u32)((s32)x - L.wvs[j]);
+              u32 const llj = L.wll[j];
+              if (d < llj) {
+                ad[t] = lits.g ? lits.g + L.wlit[j] + d : nullptr;
+                w[t] = x < wlen;
+              } else {
+                u32 const m = d - llj, offj = L.woff[j];
+                s64 const sw = (s64)L.wvs[j] + llj - offj + (m < offj ? m : umod(m, offj));
+                ad[t] = ob + (s64)gs + sw;
+                w[t] = x < wlen && sw < 0;
+              }
+            }
+            u8 v[UA];
+#pragma unroll
+            for (u32 t = 0; t < UA; t++) v[t] = w[t] ? (ad[t] ? *ad[t] : (u8)lits.rle) : (u8)0;
+#pragma unroll
+            for (u32 t = 0; t < UA; t++)
+              if (w[t]) L.u.out[x0 + 64 * t + lane] = v[t];
+          }
+          // pass B: matches with a source inside the window, in order
+          s32 const mlo = ms < 0 ? -ms : 0;
+          s32 const mhi = min((s32)ml, (s32)wlen - ms);
+          bool const nearp = valid && mhi > mlo && ms - (s32)off + (s32)min(off, (u32)mhi) - 1 >= 0;
+          u64 nm = __ballot(nearp);
+          while (nm) {
+            u32 const j = (u32)__builtin_ctzll(nm);
+            nm &= nm - 1;
+            s32 const msj = __builtin_amdgcn_readlane(ms, j), loj = __builtin_amdgcn_readlane(mlo, j), hij = __builtin_amdgcn_readlane(mhi, j);
+            u32 const offj = __builtin_amdgcn_readlane(off, j);
+            for (s32 m = loj + (s32)lane; m < hij; m += 64) {
+              s32 const sw = msj - (s32)offj + (s32)((u32)m < offj ? (u32)m : umod((u32)m, offj));
+              if (sw >= 0) L.u.out[msj + m] = L.u.out[sw];
+            }
+          }
+          // flush the window: head bytes to a 4-B aligned destination, then dwords
+          {
+            u8 *const d = ob + gs;
+            u32 const h = min((u32)((4u - ((uintptr_t)d & 3u)) & 3u), wlen);
+            u32 const nw = (wlen - h) >> 2;
+            u32 *const d32 = (u32 *)(d + h);
+            for (u32 k = lane; k < nw; k += 64) {
+              u32 const o = h + 4 * k;
+              const u32 *wp = (const u32 *)(L.u.out + (o & ~3u));
+              d32[k] = __builtin_amdgcn_alignbyte(wp[1], wp[0], o & 3u);
+            }
+            if (lane < h) d[lane] = L.u.out[lane];
+            for (u32 k = h + 4 * nw + lane; k < wlen; k += 64) d[k] = L.u.out[k];
+          }
+          __threadfence_block();  // later windows read this one back from HBM
+          __syncthreads();
+          // advance: sequences that ended inside the window are done
+          u32 const k = (u32)__popcll(__ballot(valid && ve <= (s32)wlen));
+          if (k < 64) {
+            lcur = __builtin_amdgcn_readlane(lit0, k);
+            qd = (u32)((s32)wlen - __builtin_amdgcn_readlane(vs, k));
           } else {
-            for (u32 i = lane; i < lw; i += 64) L.u.x.lit[i] = (u8)lits.rle;
-          }
-          u32 wpos = 0, lused = 0;
-          while (q <= nseq) {
-            u32 ll, ml, off;
-            if (q < nseq) {
-              if ((q & ~63u) != qb) {
-                qb = q & ~63u;
-                batch = qb + lane < nseq ? sl.seq[qb + lane] : 0ull;
-              }
-              u32 const j = q & 63u;
-              u32 const lo = __builtin_amdgcn_readlane((u32)batch, j);
-              u32 const hi = __builtin_amdgcn_readlane((u32)(batch >> 32), j);
-              ll = lo & 0x1FFFFu;
-              ml = ((lo >> 17) | (hi & 3u) << 15) + 3u;
-              off = hi >> 2;
-            } else {
-              ll = tl;
-              ml = 0;
-              off = 0;
-            }
-            if (qd < ll) {
-              u32 const k = min(ll - qd, min(DEC_STAGE - wpos, lw - lused));
-              for (u32 i = lane; i < k; i += 64) L.u.x.out[wpos + i] = L.u.x.lit[lused + i];
-              wpos += k;
-              lused += k;
-              qd += k;
-              if (qd < ll) break;
-            }
-            u32 const m0 = qd - ll;
-            if (m0 < ml) {
-              u32 const k = min(ml - m0, DEC_STAGE - wpos);
-              s64 const mstart = (s64)gs + wpos - m0;  // block-relative
-              if ((s64)fpos + mstart < (s64)off) { bad = true; break; }
-              s64 const base = mstart - off;
-              for (u32 i = lane; i < k; i += 64) {
-                u32 const m = m0 + i;
-                s64 const s = base + (m < off ? m : umod(m, off));
-                u8 const v = s >= (s64)gs ? L.u.x.out[(u32)(s - gs)] : ob[s];
-                L.u.x.out[wpos + i] = v;
-              }
-              wpos += k;
-              qd += k;
-              if (qd < ll + ml) break;
-            }
-            q++;
+            lcur = __builtin_amdgcn_readlane(lit0, 63) + __builtin_amdgcn_readlane(ll, 63);
             qd = 0;
-            if (wpos == DEC_STAGE) break;
           }
-          // flush the window
-          u8 *const d = ob + gs;
-          for (u32 i = lane; i < wpos; i += 64) d[i] = L.u.x.out[i];
-          __threadfence_block();
-          opos = gs + wpos;
-          lpos += lused;
-          if (q > nseq) break;
+          q += k;
+          opos = gs + wlen;
         }
+        DSTAMP(4);
         if (bad) { st = ST_CORRUPT; break; }
         produced += total;
         ip += bsz;
@@ -947,6 +1156,10 @@ extern "C" __global__ __launch_bounds__(DEC_THREADS) void zh_decode_kernel(ZhDec
       ip += 4;
     }
   }
+#ifdef ZH_STAMPS
+  DSTAMP(5);
+  if (lane < 8) ((u64 *)sl.lit)[lane] = stv[lane];
+#endif
   if (lane == 0) {
     a.out_sizes[item] = st == ST_OK ? produced : 0ull;
     if (a.statuses) a.statuses[item] = a.nvcomp_codes ? to_nvcomp(st) : st;
