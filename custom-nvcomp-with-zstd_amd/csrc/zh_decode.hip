@@ -29,6 +29,9 @@
 #include "zh_common.h"
 #include "zh_launch.h"
 
+#include <cstdio>
+#include <cstdlib>
+
 typedef int64_t s64;
 
 namespace {
@@ -115,6 +118,7 @@ __device__ __forceinline__ u64 ldg64(const u8 *p) {
 // frame, so the whole control flow of the kernel runs on the scalar unit (s_cbranch on
 // SCC, no exec-mask bookkeeping).  Inside lane-0-only sections the first active lane is 0.
 __device__ __forceinline__ u32 uni(u32 v) { return __builtin_amdgcn_readfirstlane(v); }
+__device__ __forceinline__ u64 uni64(u64 v) { return ((u64)uni((u32)(v >> 32)) << 32) | uni((u32)v); }
 __device__ __forceinline__ u32 ub(const u8 *p) { return uni(p[0]); }
 __device__ __forceinline__ u32 rd16(const u8 *p) { return uni(p[0] | (u32)p[1] << 8); }
 __device__ __forceinline__ u32 rd24(const u8 *p) { return uni(p[0] | (u32)p[1] << 8 | (u32)p[2] << 16); }
@@ -785,6 +789,174 @@ __device__ __forceinline__ u32 to_nvcomp(u32 s) {
 
 }  // namespace
 
+// ---- execution of one block through the LDS window (see the header comment).
+  // ---- execution, DEC_STAGE output bytes per window.  Lanes = the next 64 sequences
+  // (prefix sums give their window positions).  Pass A, lanes = output bytes: literal
+  // bytes, and match bytes whose source lies before the window (already in HBM), are
+  // gathered with all loads of a round in flight.  Pass B, in sequence order, lanes =
+  // bytes of one match: the match bytes whose source lies inside the window, from LDS
+  // (a wave's LDS operations execute in order).  Then one coalesced flush.
+// Returns false when an offset reaches before the frame start.
+__device__ bool execute_block(DecLds &L, const Slot &sl, u8 *ob, s64 fpos, const LitSrc &lits, u32 nseq, u32 tl) {
+  u32 const lane = lane_id();
+  u32 q = 0, qd = 0, opos = 0, lcur = 0;
+  bool bad = false;
+  while (q <= nseq) {
+    u32 const gs = opos;
+    u32 const idx = q + lane;
+    bool const valid = idx <= nseq;
+    u32 ll = 0, ml = 0, off = 1;
+    if (idx < nseq) {
+      u64 const v = sl.seq[idx];
+      ll = (u32)v & 0x1FFFFu;
+      ml = ((u32)(v >> 17) & 0x1FFFFu) + 3u;
+      off = (u32)(v >> 34);
+    } else if (idx == nseq) {
+      ll = tl;
+    }
+    u32 const span = ll + ml;
+    u32 incl = span, linc = ll;
+#pragma unroll
+    for (u32 dd = 1; dd < 64; dd <<= 1) {
+      u32 const t = __shfl_up(incl, dd, 64), tl2 = __shfl_up(linc, dd, 64);
+      if (lane >= dd) { incl += t; linc += tl2; }
+    }
+    s32 const vs = (s32)(incl - span) - (s32)qd;  // window-relative start (q: qd bytes done)
+    s32 const ve = (s32)incl - (s32)qd;
+    u32 const lit0 = lcur + linc - ll;
+    u32 const tot = __builtin_amdgcn_readlane(incl, 63) - qd;
+    u32 const wlen = min((u32)DEC_STAGE, tot);
+    s32 const ms = vs + (s32)ll;  // window-relative match start
+    // an offset reaching before the frame start is corrupt (checked before any read)
+    bool const obad = valid && ml && vs < (s32)wlen && fpos + (s64)gs + ms - (s64)off < 0;
+    if (__ballot(obad)) { bad = true; break; }
+    L.wvs[lane] = valid && vs < (s32)wlen ? vs : 0x7FFFFFFF;
+    L.wll[lane] = ll;
+    L.wlit[lane] = lit0;
+    L.woff[lane] = off;
+    __syncthreads();
+    // pass A
+    constexpr u32 UA = 8;
+    for (u32 x0 = 0; x0 < wlen; x0 += 64 * UA) {
+      const u8 *ad[UA];
+      bool w[UA];
+#pragma unroll
+      for (u32 t = 0; t < UA; t++) {
+        u32 const x = x0 + 64 * t + lane;
+        u32 j = 0;
+#pragma unroll
+        for (u32 stp = 32; stp; stp >>= 1) j += L.wvs[j + stp] <= (s32)x ? stp : 0u;
+        u32 const d = (u32)((s32)x - L.wvs[j]);
+        u32 const llj = L.wll[j];
+        if (d < llj) {
+          ad[t] = lits.g ? lits.g + L.wlit[j] + d : nullptr;
+          w[t] = x < wlen;
+        } else {
+          u32 const m = d - llj, offj = L.woff[j];
+          s64 const sw = (s64)L.wvs[j] + llj - offj + (m < offj ? m : umod(m, offj));
+          ad[t] = ob + (s64)gs + sw;
+          w[t] = x < wlen && sw < 0;
+        }
+      }
+      u8 v[UA];
+#pragma unroll
+      for (u32 t = 0; t < UA; t++) v[t] = w[t] ? (ad[t] ? *ad[t] : (u8)lits.rle) : (u8)0;
+#pragma unroll
+      for (u32 t = 0; t < UA; t++)
+        if (w[t]) L.u.out[x0 + 64 * t + lane] = v[t];
+    }
+    // pass B: matches with a source inside the window, in order
+    s32 const mlo = ms < 0 ? -ms : 0;
+    s32 const mhi = min((s32)ml, (s32)wlen - ms);
+    bool const nearp = valid && mhi > mlo && ms - (s32)off + (s32)min(off, (u32)mhi) - 1 >= 0;
+    u64 nm = __ballot(nearp);
+    while (nm) {
+      u32 const j = (u32)__builtin_ctzll(nm);
+      nm &= nm - 1;
+      s32 const msj = __builtin_amdgcn_readlane(ms, j), loj = __builtin_amdgcn_readlane(mlo, j), hij = __builtin_amdgcn_readlane(mhi, j);
+      u32 const offj = __builtin_amdgcn_readlane(off, j);
+      for (s32 m = loj + (s32)lane; m < hij; m += 64) {
+        s32 const sw = msj - (s32)offj + (s32)((u32)m < offj ? (u32)m : umod((u32)m, offj));
+        if (sw >= 0) L.u.out[msj + m] = L.u.out[sw];
+      }
+    }
+    // flush the window: head bytes to a 4-B aligned destination, then dwords
+    {
+      u8 *const d = ob + gs;
+      u32 const h = min((u32)((4u - ((uintptr_t)d & 3u)) & 3u), wlen);
+      u32 const nw = (wlen - h) >> 2;
+      u32 *const d32 = (u32 *)(d + h);
+      for (u32 k = lane; k < nw; k += 64) {
+        u32 const o = h + 4 * k;
+        const u32 *wp = (const u32 *)(L.u.out + (o & ~3u));
+        d32[k] = __builtin_amdgcn_alignbyte(wp[1], wp[0], o & 3u);
+      }
+      if (lane < h) d[lane] = L.u.out[lane];
+      for (u32 k = h + 4 * nw + lane; k < wlen; k += 64) d[k] = L.u.out[k];
+    }
+    __threadfence_block();  // later windows read this one back from HBM
+    __syncthreads();
+    // advance: sequences that ended inside the window are done
+    u32 const k = (u32)__popcll(__ballot(valid && ve <= (s32)wlen));
+    if (k < 64) {
+      lcur = __builtin_amdgcn_readlane(lit0, k);
+      qd = (u32)((s32)wlen - __builtin_amdgcn_readlane(vs, k));
+    } else {
+      lcur = __builtin_amdgcn_readlane(lit0, 63) + __builtin_amdgcn_readlane(ll, 63);
+      qd = 0;
+    }
+    q += k;
+    opos = gs + wlen;
+  }
+  return !bad;
+}
+
+// ---- split pipeline.  A buffer holding one frame of one compressed block (every chunk
+// of a batch) is decoded by three kernels: phase 1 (this kernel) does the headers, the
+// literals and the sequence tables and leaves a hand-off record; zh_dec_seq_kernel runs
+// the sequence bitstreams of eight such buffers at once, one lane each (the serial FSE
+// chains of eight blocks interleave in one wave instead of one chain per wave); phase 3
+// executes the block and finishes the frame.  Anything else is decoded in phase 1.
+struct DecHandoff {
+  u32 tabs[1280];  // DecLds::fse of the block
+  u64 sp;          // sequence bitstream
+  u32 rem, nseq, lg, flag;  // bytes, sequences, logLL | logOF << 8 | logML << 16, 1 = deferred
+  u64 litg;        // literal bytes (null: RLE)
+  u32 litrle, litn;
+  u64 fcs, ipc;    // frame content size (~0: absent), checksum position (~0: none)
+  u64 sumLL, sumML;
+  u32 sbad, pad;
+};
+static_assert(sizeof(DecHandoff) <= ZH_DEC_HANDOFF_BYTES, "hand-off record");
+
+__device__ __forceinline__ DecHandoff *handoff(const ZhDecArgs &a, u32 item) {
+  return (DecHandoff *)(a.ws + (size_t)item * a.slot_bytes + a.ho_off);
+}
+
+// Offset_Value -> offset with the repeat-offset history (RFC 8878 §3.1.1.5; libzstd
+// ZSTD_decodeSequence: a zero offset is forced to 1)
+__device__ __forceinline__ u32 resolve_off(u32 ofv, u32 ll, u32 &rep0, u32 &rep1, u32 &rep2) {
+  u32 off;
+  if (ofv > 3) {
+    off = ofv - 3;
+    rep2 = rep1;
+    rep1 = rep0;
+    rep0 = off;
+  } else {
+    u32 const idx = ofv - 1 + (ll == 0 ? 1u : 0u);
+    if (idx == 0) {
+      off = rep0;
+    } else {
+      off = idx == 3 ? rep0 - 1 : idx == 1 ? rep1 : rep2;
+      off += off == 0 ? 1u : 0u;
+      if (idx != 1) rep2 = rep1;
+      rep1 = rep0;
+      rep0 = off;
+    }
+  }
+  return off;
+}
+
 // Diagnostic build only (-DZH_STAMPS): per-phase s_memtime cycles of each item, written
 // to the first 64 bytes of its workspace slot when it finishes (tools/dec_stamps.py).
 #ifdef ZH_STAMPS
@@ -815,6 +987,39 @@ extern "C" __global__ __launch_bounds__(DEC_THREADS) void zh_decode_kernel(ZhDec
   if (lane < 36) L.info[0][lane] = c_LL_info[lane];
   if (lane < 53) L.info[1][lane] = c_ML_info[lane];
   __syncthreads();
+
+  if (a.phase == 3) {  // finish a buffer deferred by phase 1 (its records are in the slot)
+    DecHandoff *const ho = handoff(a, item);
+    if (uni(ho->flag) != 1) return;
+    LitSrc lits;
+    lits.g = (const u8 *)uni64(ho->litg);
+    lits.rle = uni(ho->litrle);
+    lits.n = uni(ho->litn);
+    u32 const nseq = uni(ho->nseq);
+    u64 const sumLL = uni64(ho->sumLL), sumML = uni64(ho->sumML), fcs = uni64(ho->fcs), ipc = uni64(ho->ipc);
+    u32 st = ST_OK;
+    u64 produced = 0;
+    if (uni(ho->sbad) || sumLL > lits.n) {
+      st = ST_CORRUPT;
+    } else if (lits.n + sumML > cap) {
+      st = ST_SMALL;
+    } else if (!execute_block(L, sl, dst, 0, lits, nseq, lits.n - (u32)sumLL)) {
+      st = ST_CORRUPT;
+    } else {
+      produced = lits.n + sumML;
+      if (fcs != ~0ull && produced != fcs) st = ST_CORRUPT;
+    }
+    if (st == ST_OK && ipc != ~0ull) {
+      __threadfence_block();
+      if ((u32)xxh64(dst, produced) != rd32(src + ipc)) st = ST_CHECKSUM;
+    }
+    if (lane == 0) {
+      a.out_sizes[item] = st == ST_OK ? produced : 0ull;
+      if (a.statuses) a.statuses[item] = a.nvcomp_codes ? to_nvcomp(st) : st;
+    }
+    return;
+  }
+  if (a.phase == 1 && lane == 0) handoff(a, item)->flag = 0;
 
   u32 st = ST_OK;
   u64 produced = 0, ip = 0;
@@ -942,6 +1147,24 @@ extern "C" __global__ __launch_bounds__(DEC_THREADS) void zh_decode_kernel(ZhDec
           u32 const tused = uni(L.used);
           sp += tused;
           rem -= tused;
+          if (a.phase == 1 && produced == 0 && last && ip + bsz + (chk ? 4ull : 0ull) == srcn) {
+            // the buffer's only block: hand the sequence bitstream to zh_dec_seq_kernel
+            DecHandoff *const ho = handoff(a, item);
+            for (u32 w = lane; w < 1280; w += 64) ho->tabs[w] = L.fse[w];
+            if (lane == 0) {
+              ho->sp = (u64)sp;
+              ho->rem = rem;
+              ho->nseq = nseq;
+              ho->lg = L.tlog[TAB_LL] | L.tlog[TAB_OF] << 8 | L.tlog[TAB_ML] << 16;
+              ho->litg = (u64)lits.g;
+              ho->litrle = lits.rle;
+              ho->litn = lits.n;
+              ho->fcs = fcs;
+              ho->ipc = chk ? ip + bsz : ~0ull;
+              ho->flag = 1;
+            }
+            return;  // phase 3 writes the size and status
+          }
           // ---- sequence bitstream (RFC 8878 §3.1.1.3.2.2): every lane decodes redundantly
           // (uniform control flow, no exec-mask work); lane j keeps record j of each 64
           BitRevS r;
@@ -976,24 +1199,7 @@ extern "C" __global__ __launch_bounds__(DEC_THREADS) void zh_decode_kernel(ZhDec
             u32 const ml = (mi & 0xFFFFFFu) + rd(mi >> 24);
             u32 const li = __builtin_amdgcn_readfirstlane(L.info[0][eLL & 0xFFu]);
             u32 const ll = (li & 0xFFFFFFu) + rd(li >> 24);
-            u32 off;
-            if (ofv > 3) {
-              off = ofv - 3;
-              rep2 = rep1;
-              rep1 = rep0;
-              rep0 = off;
-            } else {
-              u32 const idx = ofv - 1 + (ll == 0 ? 1u : 0u);
-              if (idx == 0) {
-                off = rep0;
-              } else {
-                off = idx == 3 ? rep0 - 1 : idx == 1 ? rep1 : rep2;
-                off += off == 0 ? 1u : 0u;  // libzstd: a zero offset is forced to 1
-                if (idx != 1) rep2 = rep1;
-                rep1 = rep0;
-                rep0 = off;
-              }
-            }
+            u32 const off = resolve_off(ofv, ll, rep0, rep1, rep2);
             big |= off >= OFF_LIMIT;
             sumLL += ll;
             sumML += ml;
@@ -1019,123 +1225,9 @@ extern "C" __global__ __launch_bounds__(DEC_THREADS) void zh_decode_kernel(ZhDec
         if (total > cap - produced) { st = ST_SMALL; break; }
         __threadfence_block();  // the records (and Huffman literals) are read back below
         __syncthreads();
-        // ---- execution, DEC_STAGE output bytes per window.  Lanes = the next 64 sequences
-        // (prefix sums give their window positions).  Pass A, lanes = output bytes: literal
-        // bytes, and match bytes whose source lies before the window (already in HBM), are
-        // gathered with all loads of a round in flight.  Pass B, in sequence order, lanes =
-        // bytes of one match: the match bytes whose source lies inside the window, from LDS
-        // (a wave's LDS operations execute in order).  Then one coalesced flush.
         u32 const tl = lits.n - (u32)sumLL;
         s64 const fpos = (s64)(produced - fstart);  // frame bytes before this block
-        u32 q = 0, qd = 0, opos = 0, lcur = 0;
-        bool bad = false;
-        while (q <= nseq) {
-          u32 const gs = opos;
-          u32 const idx = q + lane;
-          bool const valid = idx <= nseq;
-          u32 ll = 0, ml = 0, off = 1;
-          if (idx < nseq) {
-            u64 const v = sl.seq[idx];
-            ll = (u32)v & 0x1FFFFu;
-            ml = ((u32)(v >> 17) & 0x1FFFFu) + 3u;
-            off = (u32)(v >> 34);
-          } else if (idx == nseq) {
-            ll = tl;
-          }
-          u32 const span = ll + ml;
-          u32 incl = span, linc = ll;
-#pragma unroll
-          for (u32 dd = 1; dd < 64; dd <<= 1) {
-            u32 const t = __shfl_up(incl, dd, 64), tl2 = __shfl_up(linc, dd, 64);
-            if (lane >= dd) { incl += t; linc += tl2; }
-          }
-          s32 const vs = (s32)(incl - span) - (s32)qd;  // window-relative start (q: qd bytes done)
-          s32 const ve = (s32)incl - (s32)qd;
-          u32 const lit0 = lcur + linc - ll;
-          u32 const tot = __builtin_amdgcn_readlane(incl, 63) - qd;
-          u32 const wlen = min((u32)DEC_STAGE, tot);
-          s32 const ms = vs + (s32)ll;  // window-relative match start
-          // an offset reaching before the frame start is corrupt (checked before any read)
-          bool const obad = valid && ml && vs < (s32)wlen && fpos + (s64)gs + ms - (s64)off < 0;
-          if (__ballot(obad)) { bad = true; break; }
-          L.wvs[lane] = valid && vs < (s32)wlen ? vs : 0x7FFFFFFF;
-          L.wll[lane] = ll;
-          L.wlit[lane] = lit0;
-          L.woff[lane] = off;
-          __syncthreads();
-          // pass A
-          constexpr u32 UA = 8;
-          for (u32 x0 = 0; x0 < wlen; x0 += 64 * UA) {
-            const u8 *ad[UA];
-            bool w[UA];
-#pragma unroll
-            for (u32 t = 0; t < UA; t++) {
-              u32 const x = x0 + 64 * t + lane;
-              u32 j = 0;
-#pragma unroll
-              for (u32 stp = 32; stp; stp >>= 1) j += L.wvs[j + stp] <= (s32)x ? stp : 0u;
-              u32 const d = (u32)((s32)x - L.wvs[j]);
-              u32 const llj = L.wll[j];
-              if (d < llj) {
-                ad[t] = lits.g ? lits.g + L.wlit[j] + d : nullptr;
-                w[t] = x < wlen;
-              } else {
-                u32 const m = d - llj, offj = L.woff[j];
-                s64 const sw = (s64)L.wvs[j] + llj - offj + (m < offj ? m : umod(m, offj));
-                ad[t] = ob + (s64)gs + sw;
-                w[t] = x < wlen && sw < 0;
-              }
-            }
-            u8 v[UA];
-#pragma unroll
-            for (u32 t = 0; t < UA; t++) v[t] = w[t] ? (ad[t] ? *ad[t] : (u8)lits.rle) : (u8)0;
-#pragma unroll
-            for (u32 t = 0; t < UA; t++)
-              if (w[t]) L.u.out[x0 + 64 * t + lane] = v[t];
-          }
-          // pass B: matches with a source inside the window, in order
-          s32 const mlo = ms < 0 ? -ms : 0;
-          s32 const mhi = min((s32)ml, (s32)wlen - ms);
-          bool const nearp = valid && mhi > mlo && ms - (s32)off + (s32)min(off, (u32)mhi) - 1 >= 0;
-          u64 nm = __ballot(nearp);
-          while (nm) {
-            u32 const j = (u32)__builtin_ctzll(nm);
-            nm &= nm - 1;
-            s32 const msj = __builtin_amdgcn_readlane(ms, j), loj = __builtin_amdgcn_readlane(mlo, j), hij = __builtin_amdgcn_readlane(mhi, j);
-            u32 const offj = __builtin_amdgcn_readlane(off, j);
-            for (s32 m = loj + (s32)lane; m < hij; m += 64) {
-              s32 const sw = msj - (s32)offj + (s32)((u32)m < offj ? (u32)m : umod((u32)m, offj));
-              if (sw >= 0) L.u.out[msj + m] = L.u.out[sw];
-            }
-          }
-          // flush the window: head bytes to a 4-B aligned destination, then dwords
-          {
-            u8 *const d = ob + gs;
-            u32 const h = min((u32)((4u - ((uintptr_t)d & 3u)) & 3u), wlen);
-            u32 const nw = (wlen - h) >> 2;
-            u32 *const d32 = (u32 *)(d + h);
-            for (u32 k = lane; k < nw; k += 64) {
-              u32 const o = h + 4 * k;
-              const u32 *wp = (const u32 *)(L.u.out + (o & ~3u));
-              d32[k] = __builtin_amdgcn_alignbyte(wp[1], wp[0], o & 3u);
-            }
-            if (lane < h) d[lane] = L.u.out[lane];
-            for (u32 k = h + 4 * nw + lane; k < wlen; k += 64) d[k] = L.u.out[k];
-          }
-          __threadfence_block();  // later windows read this one back from HBM
-          __syncthreads();
-          // advance: sequences that ended inside the window are done
-          u32 const k = (u32)__popcll(__ballot(valid && ve <= (s32)wlen));
-          if (k < 64) {
-            lcur = __builtin_amdgcn_readlane(lit0, k);
-            qd = (u32)((s32)wlen - __builtin_amdgcn_readlane(vs, k));
-          } else {
-            lcur = __builtin_amdgcn_readlane(lit0, 63) + __builtin_amdgcn_readlane(ll, 63);
-            qd = 0;
-          }
-          q += k;
-          opos = gs + wlen;
-        }
+        bool const bad = !execute_block(L, sl, ob, fpos, lits, nseq, tl);
         DSTAMP(4);
         if (bad) { st = ST_CORRUPT; break; }
         produced += total;
@@ -1166,11 +1258,143 @@ extern "C" __global__ __launch_bounds__(DEC_THREADS) void zh_decode_kernel(ZhDec
   }
 }
 
+// Sequence bitstreams of deferred buffers, lanes = buffers (64 per wave): the serial
+// FSE state chains of 64 blocks advance together, one instruction stream for all of
+// them.  Each lane reads its block's tables from the hand-off record (5 KB per block, L2 /
+// Infinity-Cache resident) and, per sequence, one 128-bit window of its bitstream below
+// its bit position (a worst-case sequence is 89 bits), so the six field reads of a
+// sequence are register shifts and the only memory latency per step is one round of
+// independent loads (window + three table entries).
+constexpr u32 D2_LANES = 64, SEQ_MAX_BITS = 31 + 16 + 16 + 9 + 9 + 8;
+
+// 16 bytes [wb, wb + 16) of stream p (n bytes, n >= 1), bytes outside [0, n) as zeros
+// (aligned dword loads of in-stream words only) -> (hi, lo)
+__device__ __forceinline__ void win_load(const u8 *p, s32 n, s32 wb, u64 &hi, u64 &lo) {
+  uintptr_t const a0 = (uintptr_t)p;
+  s32 const sh = (s32)(a0 & 3u);
+  const u32 *const w = (const u32 *)(a0 - (uintptr_t)sh);
+  // stream byte b lives in word (b + sh) >> 2; load the 5 words covering [wb, wb + 16)
+  s32 const q0 = (wb + sh) >> 2;
+  s32 const qlo = 0, qhi = (n - 1 + sh) >> 2;  // words holding stream bytes
+  u32 x[5];
+#pragma unroll
+  for (s32 k = 0; k < 5; k++) {
+    s32 const q = q0 + k;
+    x[k] = (q >= qlo && q <= qhi) ? w[q] : 0u;
+  }
+  u32 const o = (u32)((wb + sh) & 3);
+  u32 const b0 = __builtin_amdgcn_alignbyte(x[1], x[0], o), b1 = __builtin_amdgcn_alignbyte(x[2], x[1], o),
+            b2 = __builtin_amdgcn_alignbyte(x[3], x[2], o), b3 = __builtin_amdgcn_alignbyte(x[4], x[3], o);
+  lo = (u64)b1 << 32 | b0;
+  hi = (u64)b3 << 32 | b2;
+  // bytes of the first / last word outside the stream: zero them
+  s32 const below = -wb;  // window bytes before the stream start
+  if (below > 0) {
+    u32 const z = (u32)min(below, 16) * 8u;
+    if (z >= 64) { lo = 0; hi = z >= 128 ? 0 : hi & (~0ull << (z - 64)); }
+    else lo &= ~0ull << z;
+  }
+  s32 const above = wb + 16 - n;  // window bytes past the stream end
+  if (above > 0) {
+    u32 const z = (u32)min(above, 16) * 8u;
+    if (z >= 64) { hi = 0; lo = z >= 128 ? 0 : lo & (~0ull >> (z - 64)); }
+    else hi &= ~0ull >> z;
+  }
+}
+
+// k (<= 31) bits of the 128-bit window (hi:lo) below bit t (k <= t <= 128), branch-free
+__device__ __forceinline__ u32 win_bits(u64 hi, u64 lo, u32 t, u32 k) {
+  u32 const b = t - k;  // lowest bit
+  u64 const fromhi = hi >> ((b - 64) & 63u);
+  u64 const mixed = (lo >> (b & 63u)) | ((hi << 1) << (63u - (b & 63u)));
+  u64 const v = b >= 64 ? fromhi : mixed;
+  return (u32)v & (k ? (0xFFFFFFFFu >> (32 - k)) : 0u);
+}
+
+extern "C" __global__ __launch_bounds__(64) void zh_dec_seq_kernel(ZhDecArgs a, u32 nitems) {
+  __shared__ u32 info[2][64];
+  u32 const lane = lane_id();
+  if (lane < 36) info[0][lane] = c_LL_info[lane];
+  if (lane < 53) info[1][lane] = c_ML_info[lane];
+  __syncthreads();
+  u32 const it = blockIdx.x * D2_LANES + lane;
+  if (it >= nitems) return;
+  DecHandoff *const ho = handoff(a, it);
+  if (ho->flag != 1) return;
+  const u8 *const sp = (const u8 *)ho->sp;
+  u32 const nseq = ho->nseq, lg = ho->lg;
+  s32 const n = (s32)ho->rem;
+  const u32 *const TLL = ho->tabs, *const TOF = ho->tabs + 512, *const TML = ho->tabs + 768;
+  u64 *const seq = (u64 *)(a.ws + (size_t)it * a.slot_bytes + a.lit_bytes);
+  u32 const last = n > 0 ? sp[n - 1] : 0u;
+  bool bad = last == 0;
+  s32 pos = bad ? 0 : 8 * (n - 1) + (s32)hb32(last);
+  u32 rep0 = 1, rep1 = 4, rep2 = 8, sLL = 0, sOF = 0, sML = 0;
+  bool big = false;
+  u64 sumLL = 0, sumML = 0;
+  if (!bad) {
+    for (u32 i = 0; i <= nseq; i++) {  // step 0: initial states; step i: sequence i - 1
+      s32 const hb = (pos + 7) >> 3;
+      s32 const wb = hb - 16;
+      u64 whi, wlo;
+      win_load(sp, n, wb, whi, wlo);
+      u32 t = (u32)(pos - 8 * wb);  // bit position inside the window (121..128)
+      u32 const t0 = t;
+      auto rd = [&](u32 k) -> u32 {
+        t -= k;
+        return win_bits(whi, wlo, t + k, k);
+      };
+      if (i == 0) {
+        sLL = rd(lg & 0xFFu);
+        sOF = rd((lg >> 8) & 0xFFu);
+        sML = rd(lg >> 16);
+      } else {
+        u32 const eLL = TLL[sLL], eOF = TOF[sOF], eML = TML[sML];
+        u32 const ofc = eOF & 0xFFu;
+        u32 const ofv = (1u << ofc) + rd(ofc);
+        u32 const mi = info[1][eML & 0xFFu];
+        u32 const ml = (mi & 0xFFFFFFu) + rd(mi >> 24);
+        u32 const li = info[0][eLL & 0xFFu];
+        u32 const ll = (li & 0xFFFFFFu) + rd(li >> 24);
+        u32 const off = resolve_off(ofv, ll, rep0, rep1, rep2);
+        big |= off >= OFF_LIMIT;
+        sumLL += ll;
+        sumML += ml;
+        seq[i - 1] = (u64)ll | (u64)(ml - 3) << 17 | (u64)off << 34;
+        if (i < nseq) {
+          sLL = (eLL >> 16) + rd((eLL >> 8) & 0xFFu);
+          sML = (eML >> 16) + rd((eML >> 8) & 0xFFu);
+          sOF = (eOF >> 16) + rd((eOF >> 8) & 0xFFu);
+        }
+      }
+      pos -= (s32)(t0 - t);
+    }
+  }
+  ho->sumLL = sumLL;
+  ho->sumML = sumML;
+  ho->sbad = (bad || pos > 0 || big) ? 1u : 0u;
+}
+
 namespace zh {
 u32 dec_lds_bytes() { return (u32)sizeof(DecLds); }
-hipError_t launch_decompress(const ZhDecArgs &a, u32 nitems, hipStream_t stream) {
+hipError_t launch_decompress(const ZhDecArgs &a0, u32 nitems, hipStream_t stream) {
   if (!nitems) return hipSuccess;
+  // ZH_DEC_SYNC=1 (diagnostics only): synchronise and report after each of the three kernels
+  static const bool dbg = getenv("ZH_DEC_SYNC") != nullptr;
+  auto check = [&](const char *k) {
+    if (!dbg) return;
+    hipError_t e = hipStreamSynchronize(stream);
+    fprintf(stderr, "zh_decode: %s -> %s\n", k, hipGetErrorString(e));
+  };
+  ZhDecArgs a = a0;
+  a.phase = 1;
   hipLaunchKernelGGL(zh_decode_kernel, dim3(nitems), dim3(DEC_THREADS), 0, stream, a);
+  check("phase 1");
+  hipLaunchKernelGGL(zh_dec_seq_kernel, dim3((nitems + D2_LANES - 1) / D2_LANES), dim3(64), 0, stream, a, nitems);
+  check("sequences");
+  a.phase = 3;
+  hipLaunchKernelGGL(zh_decode_kernel, dim3(nitems), dim3(DEC_THREADS), 0, stream, a);
+  check("phase 3");
   return hipGetLastError();
 }
 }  // namespace zh

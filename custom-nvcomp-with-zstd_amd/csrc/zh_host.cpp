@@ -249,7 +249,7 @@ inline size_t blocks_of(size_t n) { return (n + ZH_BLOCK_MAX - 1) / ZH_BLOCK_MAX
 // (the format's maximum) unless every output capacity is smaller.
 struct DecLayout {
   size_t in_ptrs, in_sizes, out_ptrs, caps, out_sizes, statuses, slots, total;
-  u32 block_cap, lit_bytes, seq_cap;
+  u32 block_cap, lit_bytes, seq_cap, ho_off;
   u64 slot_bytes;
   static constexpr size_t kBlockMax = 128 * 1024;
   static DecLayout make(size_t n, size_t max_block) {
@@ -257,7 +257,8 @@ struct DecLayout {
     L.block_cap = (u32)std::min(std::max<size_t>(max_block, 64), kBlockMax);
     L.lit_bytes = (u32)align256(L.block_cap + 64);
     L.seq_cap = L.block_cap / 3 + 2;
-    L.slot_bytes = L.lit_bytes + align256((size_t)L.seq_cap * 8);
+    L.ho_off = (u32)(L.lit_bytes + align256((size_t)L.seq_cap * 8));
+    L.slot_bytes = L.ho_off + align256(ZH_DEC_HANDOFF_BYTES);
     size_t o = 0;
     L.in_ptrs = o; o = align256(o + n * 8);
     L.in_sizes = o; o = align256(o + n * 8);
@@ -276,6 +277,7 @@ struct DecLayout {
     a.lit_bytes = lit_bytes;
     a.block_cap = block_cap;
     a.seq_cap = seq_cap;
+    a.ho_off = ho_off;
     return a;
   }
 };

@@ -30,10 +30,14 @@ struct ZhDecArgs {
   u8 *ws;
   u64 slot_bytes;
   u32 lit_bytes, block_cap, seq_cap, nvcomp_codes;
+  u32 ho_off;  // offset of the item's hand-off record inside its slot (split pipeline)
+  u32 phase;   // 0: whole decode in one kernel; 1 / 3: first / last kernel of the split pipeline
 };
+#define ZH_DEC_HANDOFF_BYTES 5376u  // sizeof(DecHandoff), zh_decode.hip
 
 namespace zh {
 u32 dec_lds_bytes();
+// Split pipeline: phase-1 kernel, lanes=frames sequence kernel, phase-3 kernel.
 hipError_t launch_decompress(const ZhDecArgs &a, u32 nitems, hipStream_t stream);
 hipError_t init_kernels();
 u32 lz_lds_bytes();

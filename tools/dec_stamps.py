@@ -43,7 +43,7 @@ a256 = lambda v: (v + 255) // 256 * 256
 block_cap = min(max(cs, 64), 128 * 1024)
 lit_bytes = a256(block_cap + 64)
 seq_cap = block_cap // 3 + 2
-slot_bytes = lit_bytes + a256(seq_cap * 8)
+slot_bytes = lit_bytes + a256(seq_cap * 8) + a256(5376)  # + hand-off record (ZH_DEC_HANDOFF_BYTES)
 off = 0
 for k in (8, 8, 8, 8, 8, 4):
     off = a256(off + n * k)
