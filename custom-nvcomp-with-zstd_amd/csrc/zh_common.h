@@ -26,6 +26,7 @@ enum : u32 {
   ZH_F_FIRST = 1u,   // first block of its frame: writes the frame header, starts with reps {1,4,8}
   ZH_F_LAST = 2u,    // last block of its frame: Last_Block bit
   ZH_F_DIRECT = 4u,  // single-block frame written straight into the item's output
+  ZH_F_CHECKSUM = 8u,  // frame carries a content checksum (first block: FHD bit; zh_checksum_kernel appends it)
 };
 
 // Per-block workspace carved from the caller's temp buffer.

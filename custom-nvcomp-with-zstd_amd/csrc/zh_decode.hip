@@ -28,6 +28,7 @@
 // checksum mismatch -> ERROR_CHECKSUM_FAILED, dictionary frames -> ERROR_DICTIONARY_MISMATCH.
 #include "zh_common.h"
 #include "zh_launch.h"
+#include "zh_xxh64.h"
 
 #include <cstdio>
 #include <cstdlib>
@@ -716,66 +717,6 @@ __device__ s32 seq_table(DecLds &L, u32 t, u32 mode, const u8 *p, u32 avail) {
   return L.tkind[t] == TAB_NONE ? -1 : 0;  // repeat
 }
 
-// XXH64 (seed 0) of n bytes at p, lanes 0..3 = the four accumulators; result on every lane.
-__device__ u64 xxh64(const u8 *p, u64 n) {
-  constexpr u64 P1 = 0x9E3779B185EBCA87ull, P2 = 0xC2B2AE3D27D4EB4Full, P3 = 0x165667B19E3779F9ull, P4 = 0x85EBCA77C2B2AE63ull,
-                P5 = 0x27D4EB2F165667C5ull;
-  auto rotl = [](u64 x, u32 r) { return (x << r) | (x >> (64 - r)); };
-  auto round = [&](u64 acc, u64 in) { return rotl(acc + in * P2, 31) * P1; };
-  u32 const lane = lane_id();
-  u64 h;
-  u64 const nst = n / 32;
-  if (n >= 32) {
-    u64 v = lane == 0 ? P1 + P2 : lane == 1 ? P2 : lane == 2 ? 0ull : (u64)0 - P1;
-    if (lane < 4) {
-      u64 k = 0;
-      for (; k + 4 <= nst; k += 4) {
-        u64 a[4];
-#pragma unroll
-        for (u32 j = 0; j < 4; j++) a[j] = ldg64(p + 32 * (k + j) + 8 * lane);
-#pragma unroll
-        for (u32 j = 0; j < 4; j++) v = round(v, a[j]);
-      }
-      for (; k < nst; k++) v = round(v, ldg64(p + 32 * k + 8 * lane));
-    }
-    u64 const v1 = __shfl(v, 0, 64), v2 = __shfl(v, 1, 64), v3 = __shfl(v, 2, 64), v4 = __shfl(v, 3, 64);
-    h = rotl(v1, 1) + rotl(v2, 7) + rotl(v3, 12) + rotl(v4, 18);
-    h = (h ^ round(0, v1)) * P1 + P4;
-    h = (h ^ round(0, v2)) * P1 + P4;
-    h = (h ^ round(0, v3)) * P1 + P4;
-    h = (h ^ round(0, v4)) * P1 + P4;
-  } else {
-    h = P5;
-  }
-  h += n;
-  const u8 *q = p + 32 * nst;
-  u64 r = n - 32 * nst;
-  while (r >= 8) {
-    h ^= round(0, ldg64(q));
-    h = rotl(h, 27) * P1 + P4;
-    q += 8;
-    r -= 8;
-  }
-  if (r >= 4) {
-    h ^= (u64)rd32(q) * P1;
-    h = rotl(h, 23) * P2 + P3;
-    q += 4;
-    r -= 4;
-  }
-  while (r) {
-    h ^= (u64)(*q) * P5;
-    h = rotl(h, 11) * P1;
-    q++;
-    r--;
-  }
-  h ^= h >> 33;
-  h *= P2;
-  h ^= h >> 29;
-  h *= P3;
-  h ^= h >> 32;
-  return h;
-}
-
 __device__ __forceinline__ u32 to_nvcomp(u32 s) {
   switch (s) {
     case ST_OK: return 0;
@@ -1011,7 +952,7 @@ extern "C" __global__ __launch_bounds__(DEC_THREADS) void zh_decode_kernel(ZhDec
     }
     if (st == ST_OK && ipc != ~0ull) {
       __threadfence_block();
-      if ((u32)xxh64(dst, produced) != rd32(src + ipc)) st = ST_CHECKSUM;
+      if ((u32)zh_xxh64(dst, produced) != rd32(src + ipc)) st = ST_CHECKSUM;
     }
     if (lane == 0) {
       a.out_sizes[item] = st == ST_OK ? produced : 0ull;
@@ -1243,7 +1184,7 @@ extern "C" __global__ __launch_bounds__(DEC_THREADS) void zh_decode_kernel(ZhDec
     if (fcs != ~0ull && produced - fstart != fcs) { st = ST_CORRUPT; break; }
     if (chk) {
       if (srcn - ip < 4) { st = ST_CORRUPT; break; }
-      u64 const hx = xxh64(dst + fstart, produced - fstart);
+      u64 const hx = zh_xxh64(dst + fstart, produced - fstart);
       if ((u32)hx != rd32(src + ip)) { st = ST_CHECKSUM; break; }
       ip += 4;
     }

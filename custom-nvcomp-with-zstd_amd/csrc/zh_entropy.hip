@@ -855,7 +855,7 @@ extern "C" __global__ __launch_bounds__(K2_THREADS) void zh_entropy_kernel(const
   u32 st[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
 #endif
 
-  // ---- frame header (reference write_frame_header choices, no dict / checksum)
+  // ---- frame header (reference write_frame_header choices, no dict; checksum flag when asked)
   u32 pos = 0;
   if (d.flags & ZH_F_FIRST) {
     u64 const content = d.frame_size;
@@ -874,7 +874,7 @@ extern "C" __global__ __launch_bounds__(K2_THREADS) void zh_entropy_kernel(const
     if (lane == 0) {
       u32 p = 0;
       o.put(p++, 0x28); o.put(p++, 0xB5); o.put(p++, 0x2F); o.put(p++, 0xFD);
-      o.put(p++, (u8)((fcs_flag << 6) | (ss ? 0x20 : 0)));
+      o.put(p++, (u8)((fcs_flag << 6) | (ss ? 0x20 : 0) | ((d.flags & ZH_F_CHECKSUM) ? 0x04 : 0)));
       if (!ss) o.put(p++, (u8)((window_log - 10) << 3));
       u64 v = fcs_size == 2 ? content - 256 : content;
       for (u32 k = 0; k < fcs_size; k++) o.put(p++, (u8)(v >> (8 * k)));

@@ -370,7 +370,8 @@ class ZstdBatchManager::Impl {
         d.frame_size = n;
         d.n = (u32)std::min((size_t)ZH_BLOCK_MAX, n - k * ZH_BLOCK_MAX);
         d.item = (u32)i;
-        d.flags = (k == 0 ? ZH_F_FIRST : 0u) | (k + 1 == nb ? ZH_F_LAST : 0u) | (nb == 1 ? ZH_F_DIRECT : 0u);
+        d.flags = (k == 0 ? ZH_F_FIRST : 0u) | (k + 1 == nb ? ZH_F_LAST : 0u) | (nb == 1 ? ZH_F_DIRECT : 0u) |
+                  (config.checksum != ChecksumPolicy::NO_COMPUTE_NO_VERIFY ? ZH_F_CHECKSUM : 0u);
         if (nb == 1) {
           d.dst = (u8 *)out_ptrs[i];
           d.dst_cap = (u32)std::min(out_sizes[i], (size_t)0xFFFFFFFFu);
@@ -384,7 +385,8 @@ class ZstdBatchManager::Impl {
     ZhWorkspace ws{base + L.blocks};
     hipError_t e = zh::launch_compress((const ZhBlockDesc *)(base + L.descs), (u32)nblocks, ws, config.window_log, config.block_size,
                                        (u64 *)(base + L.item_size), (u32 *)(base + L.item_status), (u32 *)(base + L.blk_size),
-                                       (const ZhItemDesc *)(base + L.items), (u32)count, staged, stream);
+                                       (const ZhItemDesc *)(base + L.items), (u32)count, staged,
+                                       config.checksum != ChecksumPolicy::NO_COMPUTE_NO_VERIFY, stream);
     if (e != hipSuccess) return Status::ERROR_CUDA_ERROR;
     u64 *h_size = (u64 *)(h + up_bytes);
     u32 *h_status = (u32 *)(h_size + count);
@@ -691,12 +693,13 @@ Status ZstdBatchManager::compress_batch_device(const void *const *d_in_ptrs, con
   u64 const cap = estimate_compressed_size(max_chunk, pimpl_->config.level);
   u64 *item_size = (u64 *)d_out_sizes;
   u32 *item_status = d_statuses ? (u32 *)d_statuses : (u32 *)(base + L.item_status);
+  bool const ck = pimpl_->config.checksum != ChecksumPolicy::NO_COMPUTE_NO_VERIFY;
   hipError_t e = zh::launch_plan(d_in_ptrs, d_in_sizes, (u32)count, (u32)bpi, d_out_ptrs, cap, base + L.staging, (ZhBlockDesc *)(base + L.descs),
-                                 (ZhItemDesc *)(base + L.items), item_size, item_status, stream);
+                                 (ZhItemDesc *)(base + L.items), item_size, item_status, ck ? ZH_F_CHECKSUM : 0u, stream);
   if (e != hipSuccess) return Status::ERROR_CUDA_ERROR;
   ZhWorkspace ws{base + L.blocks};
   e = zh::launch_compress((const ZhBlockDesc *)(base + L.descs), (u32)nblocks, ws, pimpl_->config.window_log, pimpl_->config.block_size, item_size,
-                          item_status, (u32 *)(base + L.blk_size), (const ZhItemDesc *)(base + L.items), (u32)count, bpi > 1, stream);
+                          item_status, (u32 *)(base + L.blk_size), (const ZhItemDesc *)(base + L.items), (u32)count, bpi > 1, ck, stream);
   return e == hipSuccess ? Status::SUCCESS : Status::ERROR_CUDA_ERROR;
 }
 
@@ -900,6 +903,7 @@ NvcompV5Options to_nvcomp_v5_opts(const CompressionConfig &c) {
 CompressionConfig from_nvcomp_v5_opts(const NvcompV5Options &o) {
   CompressionConfig c = CompressionConfig::from_level(o.level);
   c.block_size = o.chunk_size;
+  c.checksum = o.enable_checksum ? ChecksumPolicy::COMPUTE_NO_VERIFY : ChecksumPolicy::NO_COMPUTE_NO_VERIFY;
   return c;
 }
 std::unique_ptr<ZstdManager> create_nvcomp_v5_manager(const NvcompV5Options &o) { return create_manager(from_nvcomp_v5_opts(o)); }
@@ -908,7 +912,12 @@ class NvcompV5BatchManager::Impl {
  public:
   NvcompV5Options opts;
   ZstdBatchManager mgr;
-  explicit Impl(const NvcompV5Options &o) : opts(o), mgr(CompressionConfig::from_level(o.level)) {}
+  explicit Impl(const NvcompV5Options &o) : opts(o), mgr(config_of(o)) {}
+  static CompressionConfig config_of(const NvcompV5Options &o) {  // level + checksum option
+    CompressionConfig c = CompressionConfig::from_level(o.level);
+    c.checksum = o.enable_checksum ? ChecksumPolicy::COMPUTE_NO_VERIFY : ChecksumPolicy::NO_COMPUTE_NO_VERIFY;
+    return c;
+  }
 };
 NvcompV5BatchManager::NvcompV5BatchManager(const NvcompV5Options &o) : pimpl_(new Impl(o)) {}
 NvcompV5BatchManager::~NvcompV5BatchManager() = default;

@@ -9,6 +9,7 @@
 //                  src/cuda_zstd_manager.cu:2765-3027).
 #include "zh_common.h"
 #include "zh_launch.h"
+#include "zh_xxh64.h"
 
 #include <mutex>
 #include <vector>
@@ -25,7 +26,7 @@ void entropy_launch(const ZhBlockDesc *d_descs, u32 nblocks, ZhWorkspace ws, u32
 
 extern "C" __global__ void zh_plan_kernel(const void *const *__restrict__ in_ptrs, const size_t *__restrict__ in_sizes, u32 nitems,
                                           u32 bpi, void *const *__restrict__ out_ptrs, u64 out_cap, u8 *staging, ZhBlockDesc *descs,
-                                          ZhItemDesc *items, u64 *item_size, u32 *item_status) {
+                                          ZhItemDesc *items, u64 *item_size, u32 *item_status, u32 extra_flags) {
   u32 const b = blockIdx.x * blockDim.x + threadIdx.x;
   if (b >= nitems * bpi) return;
   u32 const it = b / bpi, k = b % bpi;
@@ -36,7 +37,7 @@ extern "C" __global__ void zh_plan_kernel(const void *const *__restrict__ in_ptr
   d.frame_size = size;
   d.item = it;
   d.n = (k < nb) ? (u32)min((u64)ZH_BLOCK_MAX, size - (u64)k * ZH_BLOCK_MAX) : 0u;
-  d.flags = (k == 0 ? ZH_F_FIRST : 0u) | (k + 1 == nb ? ZH_F_LAST : 0u) | (nb == 1 ? ZH_F_DIRECT : 0u);
+  d.flags = (k == 0 ? ZH_F_FIRST : 0u) | (k + 1 == nb ? ZH_F_LAST : 0u) | (nb == 1 ? ZH_F_DIRECT : 0u) | extra_flags;
   if (nb == 1) {
     d.dst = (u8 *)out_ptrs[it];
     d.dst_cap = (u32)min(out_cap, (u64)0xFFFFFFFFu);
@@ -86,6 +87,26 @@ extern "C" __global__ __launch_bounds__(256) void zh_gather_kernel(const ZhItemD
     off += s;
   }
   (void)total_s;
+}
+
+// Content checksum (reference src/cuda_zstd_manager.cu:3037-3056): one wave per
+// finished frame appends the low 32 bits of XXH64 of the item's input (the first block
+// already set the FHD checksum flag).
+extern "C" __global__ __launch_bounds__(64) void zh_checksum_kernel(const ZhItemDesc *__restrict__ items, const ZhBlockDesc *__restrict__ descs,
+                                                                   u64 *item_size, u32 *item_status) {
+  u32 const it = blockIdx.x, lane = threadIdx.x;
+  if (item_status[it] != ZH_ST_OK) return;
+  ZhItemDesc const id = items[it];
+  ZhBlockDesc const d = descs[id.first_block];
+  u64 const h = zh_xxh64(d.src, d.frame_size);
+  u64 const size = item_size[it];
+  __syncthreads();
+  if (size + 4 > id.cap) {
+    if (lane == 0) item_status[it] = ZH_ST_TOO_SMALL;
+    return;
+  }
+  if (lane < 4) id.dst[size + lane] = (u8)(h >> (8 * lane));
+  if (lane == 0) item_size[it] = size + 4;
 }
 
 namespace zh {
@@ -146,7 +167,8 @@ int profile_collect(double *totals) {
 }
 
 hipError_t launch_compress(const ZhBlockDesc *d_descs, u32 nblocks, ZhWorkspace ws, u32 window_log, u32 cfg_block_size, u64 *d_item_size,
-                           u32 *d_item_status, u32 *d_blk_size, const ZhItemDesc *d_items, u32 nitems, bool gather, hipStream_t stream) {
+                           u32 *d_item_status, u32 *d_blk_size, const ZhItemDesc *d_items, u32 nitems, bool gather, bool checksum,
+                           hipStream_t stream) {
   if (nblocks == 0) return hipSuccess;
   std::vector<hipEvent_t> ev;
   {
@@ -159,6 +181,7 @@ hipError_t launch_compress(const ZhBlockDesc *d_descs, u32 nblocks, ZhWorkspace 
   entropy_launch(d_descs, nblocks, ws, window_log, cfg_block_size, d_item_size, d_item_status, d_blk_size, stream);
   if (!ev.empty()) (void)hipEventRecord(ev[2], stream);
   if (gather && nitems) hipLaunchKernelGGL(zh_gather_kernel, dim3(nitems), dim3(256), 0, stream, d_items, d_descs, d_blk_size, d_item_size, d_item_status);
+  if (checksum && nitems) hipLaunchKernelGGL(zh_checksum_kernel, dim3(nitems), dim3(64), 0, stream, d_items, d_descs, d_item_size, d_item_status);
   if (!ev.empty()) {
     (void)hipEventRecord(ev[3], stream);
     std::lock_guard<std::mutex> g(prof().mu);
@@ -168,11 +191,12 @@ hipError_t launch_compress(const ZhBlockDesc *d_descs, u32 nblocks, ZhWorkspace 
 }
 
 hipError_t launch_plan(const void *const *d_in_ptrs, const size_t *d_in_sizes, u32 nitems, u32 bpi, void *const *d_out_ptrs, u64 out_cap,
-                       u8 *staging, ZhBlockDesc *d_descs, ZhItemDesc *d_items, u64 *d_item_size, u32 *d_item_status, hipStream_t stream) {
+                       u8 *staging, ZhBlockDesc *d_descs, ZhItemDesc *d_items, u64 *d_item_size, u32 *d_item_status, u32 extra_flags,
+                       hipStream_t stream) {
   u32 const total = nitems * bpi;
   if (!total) return hipSuccess;
   hipLaunchKernelGGL(zh_plan_kernel, dim3((total + 255) / 256), dim3(256), 0, stream, d_in_ptrs, d_in_sizes, nitems, bpi, d_out_ptrs, out_cap,
-                     staging, d_descs, d_items, d_item_size, d_item_status);
+                     staging, d_descs, d_items, d_item_size, d_item_status, extra_flags);
   return hipGetLastError();
 }
 

@@ -251,8 +251,8 @@ class BatchedCompressor:
     """Stream-ordered batched compression of equal-capacity chunk slots
     (nvcomp_zstd_batched_compress_async_v5).  Used by bench.py."""
 
-    def __init__(self, level: int = 3, chunk_size: int = 64 * 1024):
-        self._h = lib().nvcomp_zstd_batch_create_v5(level, chunk_size, 0)
+    def __init__(self, level: int = 3, chunk_size: int = 64 * 1024, checksum: bool = False):
+        self._h = lib().nvcomp_zstd_batch_create_v5(level, chunk_size, 1 if checksum else 0)
         if not self._h:
             raise ZstdError(INVALID, "nvcomp_zstd_batch_create_v5")
         self.chunk_size = chunk_size

@@ -906,13 +906,72 @@ size_t orc_frame_header(u8 *dst, u64 content, u32 block_size, u32 window_log) {
   return o;
 }
 
+/* XXH64, seed 0 (the published xxHash algorithm, which the reference runs in
+ * src/cuda_zstd_xxhash.cu:72-228 for the frame content checksum; pinned against the
+ * python xxhash module in tests/test_oracle_stages.py). */
+static u64 xx_rotl(u64 x, int r) { return (x << r) | (x >> (64 - r)); }
+static u64 xx_round(u64 acc, u64 in) { return xx_rotl(acc + in * 0xC2B2AE3D27D4EB4Full, 31) * 0x9E3779B185EBCA87ull; }
+u64 orc_xxh64(const u8 *p, u64 n) {
+  const u64 P1 = 0x9E3779B185EBCA87ull, P2 = 0xC2B2AE3D27D4EB4Full, P3 = 0x165667B19E3779F9ull, P4 = 0x85EBCA77C2B2AE63ull,
+            P5 = 0x27D4EB2F165667C5ull;
+  u64 h, i = 0;
+  if (n >= 32) {
+    u64 v1 = P1 + P2, v2 = P2, v3 = 0, v4 = 0 - P1, w;
+    for (; i + 32 <= n; i += 32) {
+      memcpy(&w, p + i, 8); v1 = xx_round(v1, w);
+      memcpy(&w, p + i + 8, 8); v2 = xx_round(v2, w);
+      memcpy(&w, p + i + 16, 8); v3 = xx_round(v3, w);
+      memcpy(&w, p + i + 24, 8); v4 = xx_round(v4, w);
+    }
+    h = xx_rotl(v1, 1) + xx_rotl(v2, 7) + xx_rotl(v3, 12) + xx_rotl(v4, 18);
+    h = (h ^ xx_round(0, v1)) * P1 + P4;
+    h = (h ^ xx_round(0, v2)) * P1 + P4;
+    h = (h ^ xx_round(0, v3)) * P1 + P4;
+    h = (h ^ xx_round(0, v4)) * P1 + P4;
+  } else {
+    h = P5;
+  }
+  h += n;
+  for (; i + 8 <= n; i += 8) {
+    u64 w;
+    memcpy(&w, p + i, 8);
+    h ^= xx_round(0, w);
+    h = xx_rotl(h, 27) * P1 + P4;
+  }
+  if (i + 4 <= n) {
+    u32 w;
+    memcpy(&w, p + i, 4);
+    h ^= (u64)w * P1;
+    h = xx_rotl(h, 23) * P2 + P3;
+    i += 4;
+  }
+  for (; i < n; i++) {
+    h ^= (u64)p[i] * P5;
+    h = xx_rotl(h, 11) * P1;
+  }
+  h ^= h >> 33;
+  h *= P2;
+  h ^= h >> 29;
+  h *= P3;
+  h ^= h >> 32;
+  return h;
+}
+
 /* Whole frame.  block_size = reference CompressionConfig.block_size (frame
  * header single-segment rule); internal blocks are ZH_BLOCK_MAX bytes.  Blocks
  * after the first start with unknown repcodes (they are compressed
  * independently on the GPU).  Returns frame size or 0. */
+size_t orc_compress_frame_ck(u8 *dst, size_t cap, const u8 *src, u64 n, u32 block_size, u32 window_log, int checksum);
 size_t orc_compress_frame(u8 *dst, size_t cap, const u8 *src, u64 n, u32 block_size, u32 window_log) {
-  if (cap < 18) return 0;
+  return orc_compress_frame_ck(dst, cap, src, n, block_size, window_log, 0);
+}
+
+/* checksum != 0: Content_Checksum_Flag set and the low 32 bits of XXH64 of the input
+ * appended (reference src/cuda_zstd_manager.cu:3037-3056 when checksum is computed). */
+size_t orc_compress_frame_ck(u8 *dst, size_t cap, const u8 *src, u64 n, u32 block_size, u32 window_log, int checksum) {
+  if (cap < 22) return 0;
   size_t o = orc_frame_header(dst, n, block_size, window_log);
+  if (checksum) dst[4] |= 0x04;
   u64 pos = 0;
   u32 b = 0;
   do {
@@ -923,6 +982,12 @@ size_t orc_compress_frame(u8 *dst, size_t cap, const u8 *src, u64 n, u32 block_s
     if (!w) return 0;
     o += w; pos += bn; b++;
   } while (pos < n);
+  if (checksum) {
+    if (o + 4 > cap) return 0;
+    u32 h = (u32)orc_xxh64(src, n);
+    memcpy(dst + o, &h, 4);
+    o += 4;
+  }
   return o;
 }
 

@@ -178,3 +178,53 @@ def test_c3_full_batch_roundtrip(torch_cuda):
         assert host[i * slot:i * slot + sizes[i]].tobytes() == T.oracle_frame(data[i * cs:(i + 1) * cs]), f"chunk {i}"
     ratio = n * cs / sizes.sum()
     assert ratio > 2.3
+
+
+def test_checksum_frames(torch_cuda):
+    """NvcompV5 batch manager with enable_checksum: every frame equals the
+    oracle's checksum frame (FHD flag + XXH64 low 32 bits of the input), libzstd verifies
+    it, and so does the GPU decoder.  Covers the stream-ordered device-array path and the
+    host-array path with a multi-block item."""
+    import cuda_zstd
+
+    n, cs = 48, 65536
+    data = T.gen(T.DG_MIX, n, 0x5EED0003, cs, first=700)
+    dev = torch_cuda.from_numpy(data).cuda()
+    bc = cuda_zstd.BatchedCompressor(3, cs, checksum=True)
+    slot = (bc.max_out(cs) + 255) // 256 * 256
+    out = torch_cuda.empty(n * slot, dtype=torch_cuda.uint8, device="cuda")
+    ar = torch_cuda.arange(n, dtype=torch_cuda.int64, device="cuda")
+    in_sizes = torch_cuda.tensor([cs - (i % 5) * 1000 for i in range(n)], dtype=torch_cuda.int64, device="cuda")
+    out_sizes = torch_cuda.zeros(n, dtype=torch_cuda.int64, device="cuda")
+    status = torch_cuda.full((n,), -1, dtype=torch_cuda.int32, device="cuda")
+    temp = torch_cuda.empty(bc.temp_size(n, cs), dtype=torch_cuda.uint8, device="cuda")
+    bc.compress_async(dev.data_ptr() + ar * cs, in_sizes, cs, out.data_ptr() + ar * slot, out_sizes, status, temp)
+    torch_cuda.cuda.synchronize()
+    assert status.cpu().tolist() == [0] * n
+    sizes, lens, host = out_sizes.cpu().tolist(), in_sizes.cpu().tolist(), out.cpu().numpy()
+    frames = [host[i * slot:i * slot + sizes[i]].tobytes() for i in range(n)]
+    for i, f in enumerate(frames):
+        d = data[i * cs:i * cs + lens[i]]
+        assert f == T.oracle_frame(d, checksum=True), f"chunk {i}"
+        if T.zstd() is not None:
+            assert T.zstd_decompress(f, lens[i]) == d.tobytes()
+    outs, st = cuda_zstd.Manager(3).decompress_batch([out[i * slot:i * slot + sizes[i]] for i in range(n)], lens, raise_on_error=False)
+    assert st == [0] * n and all(o.cpu().numpy().tobytes() == data[i * cs:i * cs + lens[i]].tobytes() for i, o in enumerate(outs))
+    # host-array path (nvcomp_zstd_batch_compress_async_v5) with a multi-block item
+    L = cuda_zstd.lib()
+    big = T.gen(T.DG_TEXT, 1, 77, 200000)
+    items = [data[:cs], big]
+    ins = [torch_cuda.from_numpy(np.ascontiguousarray(x)).cuda() for x in items]
+    caps = [cuda_zstd.max_compressed_size(len(x)) for x in items]
+    outs2 = [torch_cuda.empty(c, dtype=torch_cuda.uint8, device="cuda") for c in caps]
+    h = L.nvcomp_zstd_batch_create_v5(3, cs, 1)
+    ip = (ctypes.c_void_p * 2)(*[t.data_ptr() for t in ins])
+    op = (ctypes.c_void_p * 2)(*[t.data_ptr() for t in outs2])
+    isz = (ctypes.c_size_t * 2)(*[len(x) for x in items])
+    osz = (ctypes.c_size_t * 2)(*caps)
+    ws = torch_cuda.empty(L.nvcomp_zstd_batch_get_compress_temp_size_v5(h, isz, 2), dtype=torch_cuda.uint8, device="cuda")
+    assert L.nvcomp_zstd_batch_compress_async_v5(h, ip, isz, 2, op, osz, ws.data_ptr(), ws.numel(), None) == 0
+    L.nvcomp_zstd_batch_destroy_v5(h)
+    for x, o, s in zip(items, outs2, osz):
+        f = o[:s].cpu().numpy().tobytes()
+        assert f == T.oracle_frame(x, checksum=True)

@@ -35,6 +35,10 @@ def oracle():
         L.orc_compress_block.restype = ctypes.c_size_t
         L.orc_max_compressed_size.restype = ctypes.c_size_t
         L.orc_fse_optimal_table_log.restype = ctypes.c_uint32
+        L.orc_compress_frame_ck.restype = ctypes.c_size_t
+        L.orc_compress_frame_ck.argtypes = [vp, ctypes.c_size_t, vp, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_int]
+        L.orc_xxh64.restype = ctypes.c_uint64
+        L.orc_xxh64.argtypes = [vp, ctypes.c_uint64]
         _o = L
     return _o
 
@@ -77,11 +81,11 @@ def gen(kind, nchunks, seed, chunk_size=65536, first=0):
     return a
 
 
-def oracle_frame(data, block_size=128 * 1024, window_log=19):
+def oracle_frame(data, block_size=128 * 1024, window_log=19, checksum=False):
     data = np.ascontiguousarray(np.frombuffer(bytes(data), np.uint8) if not isinstance(data, np.ndarray) else data)
     cap = int(oracle().orc_max_compressed_size(ctypes.c_uint64(len(data)))) + 64
     out = np.zeros(cap, np.uint8)
-    n = oracle().orc_compress_frame(out.ctypes.data_as(vp), cap, data.ctypes.data_as(vp), len(data), block_size, window_log)
+    n = oracle().orc_compress_frame_ck(out.ctypes.data_as(vp), cap, data.ctypes.data_as(vp), len(data), block_size, window_log, int(checksum))
     assert n > 0
     return out[:n].tobytes()
 
