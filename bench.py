@@ -110,6 +110,44 @@ def libzstd_roundtrip(frames, sizes, slot, host):
         return all(ex.map(lambda k: work(k, min(n, k + step)), range(0, n, step)))
 
 
+def cpu_decompress_baseline(frames, sizes, slot, threads, seconds=1.5):
+    """libzstd ZSTD_decompress (the reference's CPU decode route) over the rank-0 frames,
+    `threads` host threads, bounded wall time."""
+    import concurrent.futures as cf
+
+    import zh_testlib as T
+
+    z = T.zstd()
+    if z is None:
+        return None
+    n = len(sizes)
+
+    def work(lo, hi, dst):
+        vp = ctypes.c_void_p
+        tot = 0
+        for i in range(lo, hi):
+            tot += z.ZSTD_decompress(dst.ctypes.data_as(vp), ctypes.c_size_t(CHUNK), ctypes.c_void_p(frames.ctypes.data + i * slot),
+                                     ctypes.c_size_t(int(sizes[i])))
+        return tot
+
+    bufs = [np.zeros(CHUNK, np.uint8) for _ in range(threads)]
+    per = 64
+    done, t0 = 0, time.perf_counter()
+    with cf.ThreadPoolExecutor(threads) as ex:
+        nxt = 0
+        while time.perf_counter() - t0 < seconds:
+            futs = []
+            for t in range(threads):
+                lo = nxt % n
+                hi = min(lo + per, n)
+                futs.append(ex.submit(work, lo, hi, bufs[t]))
+                nxt = hi
+            done += sum(f.result() for f in futs)
+    el = time.perf_counter() - t0
+    return {"value": round(done / el / 1e9, 3), "unit": "GB/s (decompressed bytes)", "cores": threads, "kind": "reference",
+            "sample": f"libzstd {z.ZSTD_versionNumber()} ZSTD_decompress of {done >> 20} MiB of the same frames, {threads} threads, {el:.2f} s wall"}
+
+
 def decompress_leg(d_in, d_out, out_ptrs, out_sizes, n, dev, steps, world):
     """GPU decompression of the frames just produced, device-resident:
     zh_decode_kernel through nvcomp_zstd_batched_decompress_async_v5, timed with events on
@@ -266,10 +304,12 @@ def main():
                          "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
                          "algorithmic_bytes_per_launch": int(per_launch_bytes), "traffic_source": traffic_src},
         }
+        threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
         if dec is not None:
+            if not args.no_cpu_baseline:
+                dec["cpu_baseline"] = cpu_decompress_baseline(d_out.cpu().numpy(), out_sizes.cpu().numpy(), slot, threads)
             line["decompress"] = dec
         if not args.no_cpu_baseline:
-            threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
             line["cpu_baseline"] = cpu_baseline(host, threads)
         print(json.dumps(line), flush=True)
     if world > 1:

@@ -30,8 +30,10 @@
 #include "zh_launch.h"
 #include "zh_xxh64.h"
 
+#include <algorithm>
 #include <cstdio>
 #include <cstdlib>
+#include <mutex>
 
 typedef int64_t s64;
 
@@ -655,10 +657,15 @@ __device__ u32 decode_literals(DecLds &L, const u8 *bp, u32 bsz, const Slot &sl,
   for (;;) {
     bool need = false;
     while (i < mcnt) {
-      if (!r.ensure(stg, tlog)) { need = true; break; }
-      u32 const e = L.u.h.dt[(u32)r.bits(tlog)];
-      o[i++] = (u8)e;
-      r.pos -= (s32)(e >> 8);
+      // one container check per 4 symbols: a refill leaves >= 57 bits and 4 x 11 fit
+      if (!r.ensure(stg, 4 * tlog)) { need = true; break; }
+      u32 const k4 = min(4u, mcnt - i);
+      for (u32 u = 0; u < k4; u++) {
+        u32 const e = L.u.h.dt[(u32)r.bits(tlog)];
+        o[i + u] = (u8)e;
+        r.pos -= (s32)(e >> 8);
+      }
+      i += k4;
     }
     u64 const nm = __ballot(need);
     if (!nm) break;
@@ -914,7 +921,7 @@ __device__ __forceinline__ u32 resolve_off(u32 ofv, u32 ll, u32 &rep0, u32 &rep1
 // One workgroup (one wave) per input buffer.
 extern "C" __global__ __launch_bounds__(DEC_THREADS) void zh_decode_kernel(ZhDecArgs a) {
   __shared__ DecLds L;
-  u32 const item = blockIdx.x, lane = lane_id();
+  u32 const item = a.item0 + blockIdx.x, lane = lane_id();
   const u8 *const src = (const u8 *)(a.in_ptrs ? a.in_ptrs[item] : a.one_in);
   u64 const srcn = a.in_ptrs ? (u64)a.in_sizes[item] : a.one_in_size;
   u8 *const dst = (u8 *)(a.in_ptrs ? a.out_ptrs[item] : a.one_out);
@@ -1206,7 +1213,7 @@ extern "C" __global__ __launch_bounds__(DEC_THREADS) void zh_decode_kernel(ZhDec
 // its bit position (a worst-case sequence is 89 bits), so the six field reads of a
 // sequence are register shifts and the only memory latency per step is one round of
 // independent loads (window + three table entries).
-constexpr u32 D2_LANES = 64, SEQ_MAX_BITS = 31 + 16 + 16 + 9 + 9 + 8;
+constexpr u32 D2_LANES = 64;
 
 // 16 bytes [wb, wb + 16) of stream p (n bytes, n >= 1), bytes outside [0, n) as zeros
 // (aligned dword loads of in-stream words only) -> (hi, lo)
@@ -1218,10 +1225,15 @@ __device__ __forceinline__ void win_load(const u8 *p, s32 n, s32 wb, u64 &hi, u6
   s32 const q0 = (wb + sh) >> 2;
   s32 const qlo = 0, qhi = (n - 1 + sh) >> 2;  // words holding stream bytes
   u32 x[5];
+  if (q0 >= qlo && q0 + 4 <= qhi) {  // all five words in the stream: every step but the first / last few
 #pragma unroll
-  for (s32 k = 0; k < 5; k++) {
-    s32 const q = q0 + k;
-    x[k] = (q >= qlo && q <= qhi) ? w[q] : 0u;
+    for (s32 k = 0; k < 5; k++) x[k] = w[q0 + k];
+  } else {
+#pragma unroll
+    for (s32 k = 0; k < 5; k++) {
+      s32 const q = q0 + k;
+      x[k] = (q >= qlo && q <= qhi) ? w[q] : 0u;
+    }
   }
   u32 const o = (u32)((wb + sh) & 3);
   u32 const b0 = __builtin_amdgcn_alignbyte(x[1], x[0], o), b1 = __builtin_amdgcn_alignbyte(x[2], x[1], o),
@@ -1243,13 +1255,38 @@ __device__ __forceinline__ void win_load(const u8 *p, s32 n, s32 wb, u64 &hi, u6
   }
 }
 
-// k (<= 31) bits of the 128-bit window (hi:lo) below bit t (k <= t <= 128), branch-free
-__device__ __forceinline__ u32 win_bits(u64 hi, u64 lo, u32 t, u32 k) {
-  u32 const b = t - k;  // lowest bit
-  u64 const fromhi = hi >> ((b - 64) & 63u);
-  u64 const mixed = (lo >> (b & 63u)) | ((hi << 1) << (63u - (b & 63u)));
-  u64 const v = b >= 64 ? fromhi : mixed;
-  return (u32)v & (k ? (0xFFFFFFFFu >> (32 - k)) : 0u);
+// 64 bits of the window (hi:lo) ending at bit t (32 <= t <= 128), bit t - 1 as the MSB;
+// bits below the window read as zeros.  A step reads its fields from two of these: the
+// three extra-bit fields (<= 31 + 16 + 16 bits), then the three state updates (<= 26 bits).
+__device__ __forceinline__ u64 win_top(u64 hi, u64 lo, u32 t) {
+  s32 const b = (s32)t - 64;  // lowest bit taken
+  u32 const r = (u32)b & 63u;
+  u64 const mid = (lo >> r) | ((hi << 1) << (63u - r));
+  u64 const v = b >= 64 ? hi : b > 0 ? mid : lo;
+  return b >= 0 ? v : lo << (u32)(-b);
+}
+
+// the top k (<= 31) bits of T; T <<= k
+__device__ __forceinline__ u32 take(u64 &T, u32 k) {
+  u32 const hi32 = (u32)(T >> 32);
+  u32 const v = k ? hi32 >> (32u - k) : 0u;
+  T <<= k;
+  return v;
+}
+
+// resolve_off without branches (the lanes of a wave decode different blocks)
+__device__ __forceinline__ u32 resolve_off_bf(u32 ofv, u32 ll, u32 &r0, u32 &r1, u32 &r2) {
+  bool const lit = ofv > 3;
+  u32 const idx = ofv - 1 + (ll == 0 ? 1u : 0u);  // repeat index when !lit: 0..3
+  u32 rs = idx == 1 ? r1 : idx == 2 ? r2 : r0 - 1;
+  rs += rs == 0 ? 1u : 0u;
+  u32 const off = lit ? ofv - 3 : idx == 0 ? r0 : rs;
+  bool const upd = lit || idx != 0;
+  u32 const n2 = (!lit && idx == 1) ? r2 : r1;
+  r2 = upd ? n2 : r2;
+  r1 = upd ? r0 : r1;
+  r0 = upd ? off : r0;
+  return off;
 }
 
 extern "C" __global__ __launch_bounds__(64) void zh_dec_seq_kernel(ZhDecArgs a, u32 nitems) {
@@ -1258,8 +1295,8 @@ extern "C" __global__ __launch_bounds__(64) void zh_dec_seq_kernel(ZhDecArgs a, 
   if (lane < 36) info[0][lane] = c_LL_info[lane];
   if (lane < 53) info[1][lane] = c_ML_info[lane];
   __syncthreads();
-  u32 const it = blockIdx.x * D2_LANES + lane;
-  if (it >= nitems) return;
+  u32 const it = a.item0 + blockIdx.x * D2_LANES + lane;
+  if (it >= a.item0 + nitems) return;
   DecHandoff *const ho = handoff(a, it);
   if (ho->flag != 1) return;
   const u8 *const sp = (const u8 *)ho->sp;
@@ -1281,31 +1318,35 @@ extern "C" __global__ __launch_bounds__(64) void zh_dec_seq_kernel(ZhDecArgs a, 
       win_load(sp, n, wb, whi, wlo);
       u32 t = (u32)(pos - 8 * wb);  // bit position inside the window (121..128)
       u32 const t0 = t;
-      auto rd = [&](u32 k) -> u32 {
-        t -= k;
-        return win_bits(whi, wlo, t + k, k);
-      };
       if (i == 0) {
-        sLL = rd(lg & 0xFFu);
-        sOF = rd((lg >> 8) & 0xFFu);
-        sML = rd(lg >> 16);
+        u64 T = win_top(whi, wlo, t);
+        u32 const kL = lg & 0xFFu, kO = (lg >> 8) & 0xFFu, kM = lg >> 16;
+        sLL = take(T, kL);
+        sOF = take(T, kO);
+        sML = take(T, kM);
+        t -= kL + kO + kM;
       } else {
         u32 const eLL = TLL[sLL], eOF = TOF[sOF], eML = TML[sML];
         u32 const ofc = eOF & 0xFFu;
-        u32 const ofv = (1u << ofc) + rd(ofc);
-        u32 const mi = info[1][eML & 0xFFu];
-        u32 const ml = (mi & 0xFFFFFFu) + rd(mi >> 24);
-        u32 const li = info[0][eLL & 0xFFu];
-        u32 const ll = (li & 0xFFFFFFu) + rd(li >> 24);
-        u32 const off = resolve_off(ofv, ll, rep0, rep1, rep2);
+        u32 const mi = info[1][eML & 0xFFu], li = info[0][eLL & 0xFFu];
+        u32 const mb = mi >> 24, lb = li >> 24;
+        u64 T = win_top(whi, wlo, t);
+        u32 const ofv = (1u << ofc) + take(T, ofc);
+        u32 const ml = (mi & 0xFFFFFFu) + take(T, mb);
+        u32 const ll = (li & 0xFFFFFFu) + take(T, lb);
+        t -= ofc + mb + lb;
+        u32 const off = resolve_off_bf(ofv, ll, rep0, rep1, rep2);
         big |= off >= OFF_LIMIT;
         sumLL += ll;
         sumML += ml;
         seq[i - 1] = (u64)ll | (u64)(ml - 3) << 17 | (u64)off << 34;
         if (i < nseq) {
-          sLL = (eLL >> 16) + rd((eLL >> 8) & 0xFFu);
-          sML = (eML >> 16) + rd((eML >> 8) & 0xFFu);
-          sOF = (eOF >> 16) + rd((eOF >> 8) & 0xFFu);
+          u32 const kL = (eLL >> 8) & 0xFFu, kM = (eML >> 8) & 0xFFu, kO = (eOF >> 8) & 0xFFu;
+          u64 U = win_top(whi, wlo, t);
+          sLL = (eLL >> 16) + take(U, kL);
+          sML = (eML >> 16) + take(U, kM);
+          sOF = (eOF >> 16) + take(U, kO);
+          t -= kL + kM + kO;
         }
       }
       pos -= (s32)(t0 - t);
@@ -1316,26 +1357,80 @@ extern "C" __global__ __launch_bounds__(64) void zh_dec_seq_kernel(ZhDecArgs a, 
   ho->sbad = (bad || pos > 0 || big) ? 1u : 0u;
 }
 
+namespace {
+// Side streams and events of the pipelined decode (created on first use and kept; a call
+// holds the mutex while it enqueues its groups)
+struct DecPipe {
+  static constexpr u32 G = 4;
+  std::mutex mu;
+  hipStream_t side[G - 1] = {};
+  hipEvent_t start = nullptr, p1[G - 1] = {}, done[G - 1] = {};
+  bool ok = true;
+  DecPipe() {
+    ok = hipEventCreateWithFlags(&start, hipEventDisableTiming) == hipSuccess;
+    for (u32 k = 0; k + 1 < G; k++) {
+      ok = ok && hipStreamCreateWithFlags(&side[k], hipStreamNonBlocking) == hipSuccess;
+      ok = ok && hipEventCreateWithFlags(&p1[k], hipEventDisableTiming) == hipSuccess;
+      ok = ok && hipEventCreateWithFlags(&done[k], hipEventDisableTiming) == hipSuccess;
+    }
+  }
+};
+DecPipe &dec_pipe() {
+  static DecPipe p;
+  return p;
+}
+}  // namespace
+
 namespace zh {
 u32 dec_lds_bytes() { return (u32)sizeof(DecLds); }
 hipError_t launch_decompress(const ZhDecArgs &a0, u32 nitems, hipStream_t stream) {
   if (!nitems) return hipSuccess;
   // ZH_DEC_SYNC=1 (diagnostics only): synchronise and report after each of the three kernels
   static const bool dbg = getenv("ZH_DEC_SYNC") != nullptr;
-  auto check = [&](const char *k) {
-    if (!dbg) return;
-    hipError_t e = hipStreamSynchronize(stream);
-    fprintf(stderr, "zh_decode: %s -> %s\n", k, hipGetErrorString(e));
+  // items [first, first + cnt): phase 1, the sequence kernel, phase 3, in order on s;
+  // after_p1 (optional) is recorded once phase 1 is queued
+  auto group = [&](u32 first, u32 cnt, hipStream_t s, hipEvent_t after_p1) {
+    auto check = [&](const char *k) {
+      if (!dbg) return;
+      hipError_t e = hipStreamSynchronize(s);
+      fprintf(stderr, "zh_decode: %s -> %s\n", k, hipGetErrorString(e));
+    };
+    ZhDecArgs a = a0;
+    a.item0 = first;
+    a.phase = 1;
+    hipLaunchKernelGGL(zh_decode_kernel, dim3(cnt), dim3(DEC_THREADS), 0, s, a);
+    check("phase 1");
+    if (after_p1) (void)hipEventRecord(after_p1, s);
+    hipLaunchKernelGGL(zh_dec_seq_kernel, dim3((cnt + D2_LANES - 1) / D2_LANES), dim3(64), 0, s, a, cnt);
+    check("sequences");
+    a.phase = 3;
+    hipLaunchKernelGGL(zh_decode_kernel, dim3(cnt), dim3(DEC_THREADS), 0, s, a);
+    check("phase 3");
   };
-  ZhDecArgs a = a0;
-  a.phase = 1;
-  hipLaunchKernelGGL(zh_decode_kernel, dim3(nitems), dim3(DEC_THREADS), 0, stream, a);
-  check("phase 1");
-  hipLaunchKernelGGL(zh_dec_seq_kernel, dim3((nitems + D2_LANES - 1) / D2_LANES), dim3(64), 0, stream, a, nitems);
-  check("sequences");
-  a.phase = 3;
-  hipLaunchKernelGGL(zh_decode_kernel, dim3(nitems), dim3(DEC_THREADS), 0, stream, a);
-  check("phase 3");
+  // Large batches run as DecPipe::G groups on staggered streams: group k's phase 1 starts
+  // once group k-1's phase 1 is done, so the latency-bound sequence kernel of a group (one
+  // wave per 64 buffers) overlaps the throughput-bound phase 1 of the next groups and
+  // phase 3 of the earlier ones.
+  constexpr u32 G = DecPipe::G, MIN_GROUP = 1024;
+  DecPipe *p = (!dbg && nitems >= G * MIN_GROUP) ? &dec_pipe() : nullptr;
+  if (!p || !p->ok) {
+    group(0, nitems, stream, nullptr);
+    return hipGetLastError();
+  }
+  std::lock_guard<std::mutex> lk(p->mu);
+  u32 const per = (nitems + G - 1) / G;
+  (void)hipEventRecord(p->start, stream);
+  for (u32 k = 0; k < G; k++) {
+    hipStream_t const s = k ? p->side[k - 1] : stream;
+    if (k) {
+      (void)hipStreamWaitEvent(s, p->start, 0);
+      (void)hipStreamWaitEvent(s, p->p1[k - 1], 0);
+    }
+    u32 const first = k * per;
+    group(first, std::min(per, nitems - first), s, k + 1 < G ? p->p1[k] : nullptr);
+    if (k) (void)hipEventRecord(p->done[k - 1], s);
+  }
+  for (u32 k = 1; k < G; k++) (void)hipStreamWaitEvent(stream, p->done[k - 1], 0);
   return hipGetLastError();
 }
 }  // namespace zh

@@ -32,6 +32,7 @@ struct ZhDecArgs {
   u32 lit_bytes, block_cap, seq_cap, nvcomp_codes;
   u32 ho_off;  // offset of the item's hand-off record inside its slot (split pipeline)
   u32 phase;   // 0: whole decode in one kernel; 1 / 3: first / last kernel of the split pipeline
+  u32 item0;   // first item of this launch (launch_decompress's pipelined groups)
 };
 #define ZH_DEC_HANDOFF_BYTES 5376u  // sizeof(DecHandoff), zh_decode.hip
 
