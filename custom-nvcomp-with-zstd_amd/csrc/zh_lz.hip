@@ -387,14 +387,26 @@ extern "C" __global__ __launch_bounds__(K1_THREADS) void zh_lz_kernel(const ZhBl
       u32 const cbase = tid < NB ? SB * tid : ZH_WINDOW;  // window index of position s
       // (1) candidates, own bytes and first-8-byte prefixes; loads unconditional
       u32 cv[SB], plp = 0, psp = 0;  // prefixes packed 4 bits per position
+      // the thread's own bytes [s, s + SB + 7) from four aligned dwords, shared by its SB
+      // positions (positions past lim have cv = 0: their bytes are never compared)
+      static_assert(SB <= 5, "own[] holds 12 bytes");
+      u32 own[3];
+      {
+        u32 const w = s >> 2, sh = s & 3u;
+        u32 const w0 = in32[w], w1 = in32[w + 1], w2 = in32[w + 2], w3 = in32[w + 3];
+        own[0] = __builtin_amdgcn_alignbyte(w1, w0, sh);
+        own[1] = __builtin_amdgcn_alignbyte(w2, w1, sh);
+        own[2] = __builtin_amdgcn_alignbyte(w3, w2, sh);
+      }
 #pragma unroll
       for (u32 j = 0; j < SB; j++) {
         u32 const p = s + j;
         bool const v = p < se && p < lim;
         u32 const cw = ci[cidx(cbase + j)];
         cv[j] = v ? cw : 0u;
-        u32 olo, ohi;
-        ld64u(in32, min(p, lim), olo, ohi);
+        u32 const q = j >> 2, r = j & 3u;
+        u32 const olo = r ? __builtin_amdgcn_alignbyte(own[q + 1], own[q], r) : own[q];
+        u32 const ohi = r ? __builtin_amdgcn_alignbyte(own[q + 2], own[q + 1], r) : own[q + 1];
         u32 const cL = cv[j] & 0xFFFFu, cS = cv[j] >> 16;
         // wave-uniform skips (no lane has a candidate: rare matches), branch-free inside
         u32 xL = 0, xS = 0;
