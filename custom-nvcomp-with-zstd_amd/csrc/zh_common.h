@@ -20,6 +20,9 @@ struct ZhBlockDesc {
   u32 item;          // batch item index
   u32 dst_cap;       // bytes available at dst
   u32 flags;         // ZH_F_* below
+  const u8 *pre;     // ZH_F_DICT first block: dictionary content tail staged before the block
+  u32 pre_n;         // its length (pre_n + n <= ZH_BLOCK_MAX), 0 without a dictionary
+  u32 dict_id;       // Dictionary_ID written to the frame header (0: none)
 };
 
 enum : u32 {
@@ -27,6 +30,7 @@ enum : u32 {
   ZH_F_LAST = 2u,    // last block of its frame: Last_Block bit
   ZH_F_DIRECT = 4u,  // single-block frame written straight into the item's output
   ZH_F_CHECKSUM = 8u,  // frame carries a content checksum (first block: FHD bit; zh_checksum_kernel appends it)
+  ZH_F_DICT = 16u,     // dictionary frame: Dictionary_ID in the header, repcodes start unknown
 };
 
 // Per-block workspace carved from the caller's temp buffer.

@@ -25,7 +25,9 @@
 //              compared with the frame's checksum field
 // Error behaviour follows libzstd 1.4.9 (ZSTD_decompress): corrupt input -> ERROR_CORRUPT_DATA,
 // too little output capacity -> ERROR_BUFFER_TOO_SMALL, bad magic -> ERROR_INVALID_MAGIC,
-// checksum mismatch -> ERROR_CHECKSUM_FAILED, dictionary frames -> ERROR_DICTIONARY_MISMATCH.
+// checksum mismatch -> ERROR_CHECKSUM_FAILED, a frame naming another (or no given) dictionary ->
+// ERROR_DICTIONARY_MISMATCH.  With a dictionary (RFC 8878 §5) its content precedes every frame
+// and a formatted one's tables and repcodes seed the frame state.
 #include "zh_common.h"
 #include "zh_launch.h"
 #include "zh_xxh64.h"
@@ -724,6 +726,25 @@ __device__ s32 seq_table(DecLds &L, u32 t, u32 mode, const u8 *p, u32 avail) {
   return L.tkind[t] == TAB_NONE ? -1 : 0;  // repeat
 }
 
+// Formatted dictionary (RFC 8878 §5): its Huffman table and OF / ML / LL FSE tables become
+// the frame's previous tables (treeless literals and repeat modes use them).  Lane 0; false
+// when they do not parse.  d = the dictionary, off = its content offset.
+__device__ bool load_dict_entropy(DecLds &L, const u8 *d, u32 off) {
+  if (off < 8 + 12) return false;
+  const u8 *const p = d + 8;
+  u32 const avail = off - 8 - 12;
+  u32 o = huf_read_weights(L, p, avail);
+  if (!o) return false;
+  L.hvalid = 1;
+  u32 const order[3] = {TAB_OF, TAB_ML, TAB_LL};
+  for (u32 k = 0; k < 3; k++) {
+    s32 const u = seq_table(L, order[k], 2, p + o, avail - o);
+    if (u < 0) return false;
+    o += (u32)u;
+  }
+  return true;
+}
+
 __device__ __forceinline__ u32 to_nvcomp(u32 s) {
   switch (s) {
     case ST_OK: return 0;
@@ -744,8 +765,9 @@ __device__ __forceinline__ u32 to_nvcomp(u32 s) {
   // gathered with all loads of a round in flight.  Pass B, in sequence order, lanes =
   // bytes of one match: the match bytes whose source lies inside the window, from LDS
   // (a wave's LDS operations execute in order).  Then one coalesced flush.
-// Returns false when an offset reaches before the frame start.
-__device__ bool execute_block(DecLds &L, const Slot &sl, u8 *ob, s64 fpos, const LitSrc &lits, u32 nseq, u32 tl) {
+// Returns false when an offset reaches before the frame start and the dictionary content
+// (dlen bytes ending at dend) that precedes it.
+__device__ bool execute_block(DecLds &L, const Slot &sl, u8 *ob, s64 fpos, const LitSrc &lits, u32 nseq, u32 tl, const u8 *dend, s64 dlen) {
   u32 const lane = lane_id();
   u32 q = 0, qd = 0, opos = 0, lcur = 0;
   bool bad = false;
@@ -776,7 +798,7 @@ __device__ bool execute_block(DecLds &L, const Slot &sl, u8 *ob, s64 fpos, const
     u32 const wlen = min((u32)DEC_STAGE, tot);
     s32 const ms = vs + (s32)ll;  // window-relative match start
     // an offset reaching before the frame start is corrupt (checked before any read)
-    bool const obad = valid && ml && vs < (s32)wlen && fpos + (s64)gs + ms - (s64)off < 0;
+    bool const obad = valid && ml && vs < (s32)wlen && fpos + (s64)gs + ms - (s64)off < -dlen;
     if (__ballot(obad)) { bad = true; break; }
     L.wvs[lane] = valid && vs < (s32)wlen ? vs : 0x7FFFFFFF;
     L.wll[lane] = ll;
@@ -802,7 +824,8 @@ __device__ bool execute_block(DecLds &L, const Slot &sl, u8 *ob, s64 fpos, const
         } else {
           u32 const m = d - llj, offj = L.woff[j];
           s64 const sw = (s64)L.wvs[j] + llj - offj + (m < offj ? m : umod(m, offj));
-          ad[t] = ob + (s64)gs + sw;
+          s64 const fa = fpos + (s64)gs + sw;  // frame position of the source (< 0: dictionary)
+          ad[t] = fa >= 0 ? ob + (s64)gs + sw : dend + fa;
           w[t] = x < wlen && sw < 0;
         }
       }
@@ -873,7 +896,8 @@ struct DecHandoff {
   u32 litrle, litn;
   u64 fcs, ipc;    // frame content size (~0: absent), checksum position (~0: none)
   u64 sumLL, sumML;
-  u32 sbad, pad;
+  u32 sbad;
+  u32 rep[3];      // repcodes at the block start
 };
 static_assert(sizeof(DecHandoff) <= ZH_DEC_HANDOFF_BYTES, "hand-off record");
 
@@ -931,6 +955,9 @@ extern "C" __global__ __launch_bounds__(DEC_THREADS) void zh_decode_kernel(ZhDec
   sl.lit_cap = a.block_cap;
   sl.seq = (u64 *)(sl.lit + a.lit_bytes);
   sl.seq_cap = a.seq_cap;
+  // dictionary content precedes every frame: match sources before the frame start
+  const u8 *const dend = a.dict ? a.dict + a.dict_n : nullptr;
+  s64 const dlen = a.dict ? (s64)(a.dict_n - a.dict_off) : 0;
   if (lane < 4) L.wvs[64 + lane] = 0x7FFFFFFF;
   if (lane < 36) L.info[0][lane] = c_LL_info[lane];
   if (lane < 53) L.info[1][lane] = c_ML_info[lane];
@@ -951,7 +978,7 @@ extern "C" __global__ __launch_bounds__(DEC_THREADS) void zh_decode_kernel(ZhDec
       st = ST_CORRUPT;
     } else if (lits.n + sumML > cap) {
       st = ST_SMALL;
-    } else if (!execute_block(L, sl, dst, 0, lits, nseq, lits.n - (u32)sumLL)) {
+    } else if (!execute_block(L, sl, dst, 0, lits, nseq, lits.n - (u32)sumLL, dend, dlen)) {
       st = ST_CORRUPT;
     } else {
       produced = lits.n + sumML;
@@ -1009,17 +1036,26 @@ extern "C" __global__ __launch_bounds__(DEC_THREADS) void zh_decode_kernel(ZhDec
     else if (fcsn == 2) fcs = rd16(h) + 256ull;
     else if (fcsn == 4) fcs = rd32(h);
     else if (fcsn == 8) fcs = (u64)rd32(h) | (u64)rd32(h + 4) << 32;
-    if (did != 0) { st = ST_DICT; break; }
+    if (did != 0 && (!a.dict || did != a.dict_id)) { st = ST_DICT; break; }  // libzstd: dictionary_wrong
     ip += hsz;
     if (fcs != ~0ull && fcs > cap - produced) { st = ST_SMALL; break; }
     u64 const fstart = produced;
     // frame state: repcodes, table kinds
     u32 rep0 = 1, rep1 = 4, rep2 = 8;
+    bool const fdict = a.dict && a.dict_off;  // formatted dictionary: its tables and repcodes
     if (lane == 0) {
       L.tkind[0] = L.tkind[1] = L.tkind[2] = TAB_NONE;
       L.hvalid = 0;
+      L.err = (fdict && !load_dict_entropy(L, a.dict, a.dict_off)) ? 1u : 0u;
     }
     __syncthreads();
+    if (fdict) {
+      if (uni(L.err)) { st = ST_DICT; break; }
+      const u8 *const rp = a.dict + a.dict_off - 12;
+      rep0 = rd32(rp);
+      rep1 = rd32(rp + 4);
+      rep2 = rd32(rp + 8);
+    }
     // ---- blocks (RFC 8878 §3.1.1.2)
     for (;;) {
       if (srcn - ip < 3) { st = ST_CORRUPT; break; }
@@ -1109,6 +1145,9 @@ extern "C" __global__ __launch_bounds__(DEC_THREADS) void zh_decode_kernel(ZhDec
               ho->litn = lits.n;
               ho->fcs = fcs;
               ho->ipc = chk ? ip + bsz : ~0ull;
+              ho->rep[0] = rep0;
+              ho->rep[1] = rep1;
+              ho->rep[2] = rep2;
               ho->flag = 1;
             }
             return;  // phase 3 writes the size and status
@@ -1175,7 +1214,7 @@ extern "C" __global__ __launch_bounds__(DEC_THREADS) void zh_decode_kernel(ZhDec
         __syncthreads();
         u32 const tl = lits.n - (u32)sumLL;
         s64 const fpos = (s64)(produced - fstart);  // frame bytes before this block
-        bool const bad = !execute_block(L, sl, ob, fpos, lits, nseq, tl);
+        bool const bad = !execute_block(L, sl, ob, fpos, lits, nseq, tl, dend, dlen);
         DSTAMP(4);
         if (bad) { st = ST_CORRUPT; break; }
         produced += total;
@@ -1307,7 +1346,7 @@ extern "C" __global__ __launch_bounds__(64) void zh_dec_seq_kernel(ZhDecArgs a, 
   u32 const last = n > 0 ? sp[n - 1] : 0u;
   bool bad = last == 0;
   s32 pos = bad ? 0 : 8 * (n - 1) + (s32)hb32(last);
-  u32 rep0 = 1, rep1 = 4, rep2 = 8, sLL = 0, sOF = 0, sML = 0;
+  u32 rep0 = ho->rep[0], rep1 = ho->rep[1], rep2 = ho->rep[2], sLL = 0, sOF = 0, sML = 0;
   bool big = false;
   u64 sumLL = 0, sumML = 0;
   if (!bad) {

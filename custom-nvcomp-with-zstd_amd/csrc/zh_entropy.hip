@@ -871,15 +871,20 @@ extern "C" __global__ __launch_bounds__(K2_THREADS) void zh_entropy_kernel(const
       else if (content <= 0xFFFFFFFFull) { fcs_flag = 2; fcs_size = 4; }
       else { fcs_flag = 3; fcs_size = 8; }
     }
+    // Dictionary_ID of a formatted dictionary (raw content: none), libzstd's minimal size
+    u32 const did = (d.flags & ZH_F_DICT) ? d.dict_id : 0u;
+    u32 const didf = did == 0 ? 0u : did < 256 ? 1u : did < 65536 ? 2u : 3u;
+    u32 const didn = didf == 3 ? 4u : didf;
     if (lane == 0) {
       u32 p = 0;
       o.put(p++, 0x28); o.put(p++, 0xB5); o.put(p++, 0x2F); o.put(p++, 0xFD);
-      o.put(p++, (u8)((fcs_flag << 6) | (ss ? 0x20 : 0) | ((d.flags & ZH_F_CHECKSUM) ? 0x04 : 0)));
+      o.put(p++, (u8)((fcs_flag << 6) | (ss ? 0x20 : 0) | ((d.flags & ZH_F_CHECKSUM) ? 0x04 : 0) | didf));
       if (!ss) o.put(p++, (u8)((window_log - 10) << 3));
+      for (u32 k = 0; k < didn; k++) o.put(p++, (u8)(did >> (8 * k)));
       u64 v = fcs_size == 2 ? content - 256 : content;
       for (u32 k = 0; k < fcs_size; k++) o.put(p++, (u8)(v >> (8 * k)));
     }
-    pos = 5 + (ss ? 0 : 1) + fcs_size;
+    pos = 5 + (ss ? 0 : 1) + didn + fcs_size;
   }
   u32 const blk = pos;
   u32 const body0 = blk + 3;
@@ -1115,7 +1120,7 @@ extern "C" __global__ __launch_bounds__(K2_THREADS) void zh_entropy_kernel(const
       //    rep[1]-before-j: r2_i = r1_m for the last such m < i.
       // (oracle/zstd_oracle.c orc_resolve_repcodes is the serial form.)
       u32 cr0 = 1, cr1 = 4, cr2 = 8;  // reps before the batch's first sequence
-      if (!(d.flags & ZH_F_FIRST)) { cr0 = cr1 = cr2 = 0; }
+      if (!(d.flags & ZH_F_FIRST) || (d.flags & ZH_F_DICT)) { cr0 = cr1 = cr2 = 0; }  // dictionary frames: its repcodes never referenced
       u64 const below = (1ull << lane) - 1ull;
       CodeTabs ct;
       ct.load();

@@ -18,6 +18,7 @@
 #include "cuda_zstd_hybrid.h"
 #include "cuda_zstd_manager.h"
 #include "cuda_zstd_nvcomp.h"
+#include "zh_dict.h"
 #include "zh_launch.h"
 
 namespace cuda_zstd {
@@ -302,6 +303,66 @@ Status ensure_kernels() {
   return g_init_err == hipSuccess ? Status::SUCCESS : Status::ERROR_CUDA_ERROR;
 }
 
+// A dictionary on the device: the whole buffer (the decoder reads a formatted
+// dictionary's tables and repcodes from it) and its content offset.
+struct DevDict {
+  u8 *d = nullptr;
+  size_t cap = 0, n = 0, off = 0;
+  u32 id = 0;
+  DevDict() = default;
+  DevDict(const DevDict &) = delete;
+  DevDict &operator=(const DevDict &) = delete;
+  ~DevDict() { if (d) (void)hipFree(d); }
+  const u8 *content() const { return d + off; }
+  size_t content_n() const { return n - off; }
+  // raw content or a formatted dictionary (host or device buffer); replaces the previous one
+  Status load(const void *p, size_t bytes, hipStream_t stream) {
+    if (!p || !bytes || bytes > zh::kDictMaxBytes) return Status::ERROR_INVALID_PARAMETER;
+    std::vector<u8> h(bytes);
+    Status s = copy_any(h.data(), p, bytes, stream);
+    if (s != Status::SUCCESS) return s;
+    u32 did = 0;
+    size_t co = 0;
+    if (!zh::dict_layout(h.data(), bytes, did, co)) return Status::ERROR_DICTIONARY_FAILED;
+    if (d && hipDeviceSynchronize() != hipSuccess) return Status::ERROR_CUDA_ERROR;  // launches still reading it
+    if (bytes > cap) {
+      if (d) (void)hipFree(d);
+      d = nullptr;
+      cap = 0;
+      n = 0;
+      if (hipMalloc(&d, bytes) != hipSuccess) { d = nullptr; return Status::ERROR_OUT_OF_MEMORY; }
+      cap = bytes;
+    }
+    if (hipMemcpy(d, h.data(), bytes, hipMemcpyHostToDevice) != hipSuccess) return Status::ERROR_CUDA_ERROR;
+    n = bytes;
+    off = co;
+    id = did;
+    return Status::SUCCESS;
+  }
+  void fill(ZhDecArgs &a) const {
+    if (!n) return;
+    a.dict = d;
+    a.dict_n = n;
+    a.dict_off = (u32)off;
+    a.dict_id = id;
+  }
+};
+
+// Descriptor fields of a block: a dictionary frame's first block gets the content tail that
+// fits in front of it in K1's 64 KiB of LDS
+void set_dict_block(ZhBlockDesc &d, const DevDict *dd, bool first) {
+  d.pre = nullptr;
+  d.pre_n = 0;
+  d.dict_id = 0;
+  if (!dd || !dd->n) return;
+  d.flags |= ZH_F_DICT;
+  d.dict_id = dd->id;
+  if (!first) return;
+  size_t const cn = dd->content_n();
+  d.pre_n = (u32)std::min(cn, (size_t)ZH_BLOCK_MAX - d.n);
+  d.pre = dd->content() + cn - d.pre_n;
+}
+
 Status from_item_status(u32 s) {
   return s == ZH_ST_OK ? Status::SUCCESS : s == ZH_ST_TOO_SMALL ? Status::ERROR_BUFFER_TOO_SMALL : Status::ERROR_INVALID_PARAMETER;
 }
@@ -318,6 +379,8 @@ class ZstdBatchManager::Impl {
   std::mutex api_mutex;  // one manager serialises calls (reference src/cuda_zstd_manager.cu:1542)
   void *pinned = nullptr;
   size_t pinned_bytes = 0;
+  DevDict mgr_dict, call_dict;  // set_dictionary()'s / compress()'s per-call dictionary
+  const DevDict *active() const { return mgr_dict.n ? &mgr_dict : nullptr; }
 
   explicit Impl(const CompressionConfig &c) : config(c) {}
   ~Impl() { if (pinned) (void)hipHostFree(pinned); }
@@ -336,7 +399,7 @@ class ZstdBatchManager::Impl {
   // Run the device pipeline over a list of frames given as host arrays.
   // out_sizes: in = capacity, out = bytes; statuses out.
   Status run(const void *const *in_ptrs, const size_t *in_sizes, size_t count, void *const *out_ptrs, size_t *out_sizes, Status *statuses,
-             void *temp, size_t temp_size, hipStream_t stream) {
+             void *temp, size_t temp_size, hipStream_t stream, const DevDict *dd = nullptr) {
     Status s = ensure_kernels();
     if (s != Status::SUCCESS) return s;
     size_t nblocks = 0;
@@ -372,6 +435,7 @@ class ZstdBatchManager::Impl {
         d.item = (u32)i;
         d.flags = (k == 0 ? ZH_F_FIRST : 0u) | (k + 1 == nb ? ZH_F_LAST : 0u) | (nb == 1 ? ZH_F_DIRECT : 0u) |
                   (config.checksum != ChecksumPolicy::NO_COMPUTE_NO_VERIFY ? ZH_F_CHECKSUM : 0u);
+        set_dict_block(d, dd, k == 0);
         if (nb == 1) {
           d.dst = (u8 *)out_ptrs[i];
           d.dst_cap = (u32)std::min(out_sizes[i], (size_t)0xFFFFFFFFu);
@@ -429,6 +493,7 @@ class ZstdBatchManager::Impl {
     }
     if (hipMemcpyAsync(base, h, up, hipMemcpyHostToDevice, stream) != hipSuccess) return Status::ERROR_CUDA_ERROR;
     ZhDecArgs a = L.args(base);
+    mgr_dict.fill(a);
     a.in_ptrs = (const void *const *)(base + L.in_ptrs);
     a.in_sizes = (const size_t *)(base + L.in_sizes);
     a.out_ptrs = (void *const *)(base + L.out_ptrs);
@@ -464,6 +529,7 @@ class ZstdBatchManager::Impl {
     if (!temp || temp_size < L.total) return Status::ERROR_BUFFER_TOO_SMALL;
     u8 *base = (u8 *)(((uintptr_t)temp + 255) & ~(uintptr_t)255);
     ZhDecArgs a = L.args(base);
+    mgr_dict.fill(a);
     a.one_in = in;
     a.one_in_size = n;
     a.one_out = out;
@@ -513,10 +579,16 @@ Status ZstdBatchManager::compress(const void *in, size_t n, void *out, size_t *o
   if (!in || !out || !out_size || !temp) return Status::ERROR_INVALID_PARAMETER;
   if (n == 0) { *out_size = 0; return Status::ERROR_INVALID_PARAMETER; }
   if (temp_size < get_compress_temp_size(n)) return Status::ERROR_BUFFER_TOO_SMALL;
-  if (dict_buffer && dict_size) return Status::ERROR_NOT_IMPLEMENTED;
+  // a per-call dictionary (host or device buffer) overrides the manager's set_dictionary()
+  const DevDict *dd = pimpl_->active();
+  if (dict_buffer && dict_size) {
+    Status s = pimpl_->call_dict.load(dict_buffer, dict_size, stream);
+    if (s != Status::SUCCESS) return s;
+    dd = &pimpl_->call_dict;
+  }
   auto t0 = std::chrono::steady_clock::now();
   Status st;
-  if (select_execution_path(n, (int)pimpl_->config.cpu_threshold) == ExecutionPath::CPU) {
+  if (!dd && select_execution_path(n, (int)pimpl_->config.cpu_threshold) == ExecutionPath::CPU) {
     st = cpu_compress(in, n, out, out_size, pimpl_->config.level, stream);
     if (st == Status::SUCCESS) { pimpl_->stats.input_bytes += n; pimpl_->stats.output_bytes += *out_size; }
   } else {
@@ -524,7 +596,7 @@ Status ZstdBatchManager::compress(const void *in, size_t n, void *out, size_t *o
     const void *ip[1] = {in};
     void *opv[1] = {out};
     size_t sz[1] = {n};
-    st = pimpl_->run(ip, sz, 1, opv, out_size, &item, temp, temp_size, stream);
+    st = pimpl_->run(ip, sz, 1, opv, out_size, &item, temp, temp_size, stream, dd);
     if (st == Status::ERROR_GENERIC) st = item;
   }
   pimpl_->stats.compression_time_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
@@ -546,12 +618,25 @@ Status ZstdBatchManager::decompress(const void *in, size_t n, void *out, size_t 
   return s;
 }
 
+// Dictionary compression and decompression: raw content or a formatted RFC 8878
+// dictionary; copied to the device once (the reference keeps a shallow pointer and copies it
+// into the workspace per call, src/cuda_zstd_manager.cu:1699-1775, 3711-3764)
 Status ZstdBatchManager::set_dictionary(const dictionary::Dictionary &d) {
+  std::lock_guard<std::mutex> lock(pimpl_->api_mutex);
   if (d.raw_content.empty()) return Status::ERROR_INVALID_PARAMETER;
-  return Status::ERROR_NOT_IMPLEMENTED;
+  Status s = pimpl_->mgr_dict.load(d.raw_content.data(), d.raw_content.size(), 0);
+  if (s != Status::SUCCESS) return s;
+  pimpl_->dict = d;
+  pimpl_->dict.dict_id = pimpl_->mgr_dict.id;
+  return Status::SUCCESS;
 }
 Status ZstdBatchManager::get_dictionary(dictionary::Dictionary &d) const { d = pimpl_->dict; return Status::SUCCESS; }
-Status ZstdBatchManager::clear_dictionary() { pimpl_->dict = dictionary::Dictionary{}; return Status::SUCCESS; }
+Status ZstdBatchManager::clear_dictionary() {
+  std::lock_guard<std::mutex> lock(pimpl_->api_mutex);
+  pimpl_->dict = dictionary::Dictionary{};
+  pimpl_->mgr_dict.n = 0;
+  return Status::SUCCESS;
+}
 const CompressionStats &ZstdBatchManager::get_stats() const { return pimpl_->stats; }
 Status ZstdBatchManager::set_compression_level(int level) {
   if (!is_valid_compression_level(level)) return Status::ERROR_INVALID_PARAMETER;
@@ -601,7 +686,8 @@ Status ZstdBatchManager::compress_batch(const std::vector<BatchItem> &items, voi
   }
   auto t0 = std::chrono::steady_clock::now();
   std::vector<Status> st(idx.size());
-  Status r = idx.empty() ? Status::SUCCESS : pimpl_->run(ip.data(), isz.data(), idx.size(), op.data(), osz.data(), st.data(), temp, temp_size, stream);
+  Status r = idx.empty() ? Status::SUCCESS : pimpl_->run(ip.data(), isz.data(), idx.size(), op.data(), osz.data(), st.data(), temp, temp_size, stream,
+                                                                 pimpl_->active());
   pimpl_->stats.compression_time_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
   if (r != Status::SUCCESS && r != Status::ERROR_GENERIC) return r;
   for (size_t j = 0; j < idx.size(); j++) {
@@ -694,8 +780,10 @@ Status ZstdBatchManager::compress_batch_device(const void *const *d_in_ptrs, con
   u64 *item_size = (u64 *)d_out_sizes;
   u32 *item_status = d_statuses ? (u32 *)d_statuses : (u32 *)(base + L.item_status);
   bool const ck = pimpl_->config.checksum != ChecksumPolicy::NO_COMPUTE_NO_VERIFY;
+  const DevDict *dd = pimpl_->active();
   hipError_t e = zh::launch_plan(d_in_ptrs, d_in_sizes, (u32)count, (u32)bpi, d_out_ptrs, cap, base + L.staging, (ZhBlockDesc *)(base + L.descs),
-                                 (ZhItemDesc *)(base + L.items), item_size, item_status, ck ? ZH_F_CHECKSUM : 0u, stream);
+                                 (ZhItemDesc *)(base + L.items), item_size, item_status, ck ? ZH_F_CHECKSUM : 0u,
+                                 dd ? dd->content() : nullptr, dd ? (u32)dd->content_n() : 0u, dd ? dd->id : 0u, stream);
   if (e != hipSuccess) return Status::ERROR_CUDA_ERROR;
   ZhWorkspace ws{base + L.blocks};
   e = zh::launch_compress((const ZhBlockDesc *)(base + L.descs), (u32)nblocks, ws, pimpl_->config.window_log, pimpl_->config.block_size, item_size,
@@ -718,6 +806,7 @@ Status ZstdBatchManager::decompress_batch_device(const void *const *d_in_ptrs, c
   if (!temp || temp_size < L.total) return Status::ERROR_BUFFER_TOO_SMALL;
   u8 *base = (u8 *)(((uintptr_t)temp + 255) & ~(uintptr_t)255);
   ZhDecArgs a = L.args(base);
+  pimpl_->mgr_dict.fill(a);
   a.in_ptrs = d_in_ptrs;
   a.in_sizes = d_in_sizes;
   a.out_ptrs = d_out_ptrs;
@@ -1235,22 +1324,60 @@ size_t cuda_zstd_get_max_compressed_size(cuda_zstd_manager_t *m, size_t n) { ret
 cuda_zstd_dict_t *cuda_zstd_train_dictionary(const void **samples, const size_t *sizes, size_t num, size_t dict_size) {
   if (!samples || !sizes || num == 0 || dict_size == 0) return nullptr;
   try {
-    // raw-content dictionary from the most recent samples (COVER training is a "next" row)
+    // COVER-trained raw content (zh_dict.cpp), replacing the reference's n-gram fill
+    // (src/cuda_zstd_dictionary.cu:179-415); samples are host buffers
+    std::vector<std::pair<const u8 *, size_t>> s;
+    for (size_t i = 0; i < num; i++) {
+      if (!samples[i] && sizes[i]) return nullptr;
+      s.emplace_back((const u8 *)samples[i], sizes[i]);
+    }
+    std::vector<u8> c = zh::cover_train(s, std::min(dict_size, zh::kDictMaxBytes));
+    if (c.empty()) return nullptr;
     auto *d = new cuda_zstd_dict_t;
     d->dict.reset(new dictionary::Dictionary);
-    auto &c = d->dict->raw_content;
-    for (size_t i = num; i-- > 0 && c.size() < dict_size;) {
-      if (!samples[i] || !sizes[i]) { delete d; return nullptr; }
-      size_t take = std::min(sizes[i], dict_size - c.size());
-      const u8 *p = (const u8 *)samples[i];
-      c.insert(c.begin(), p + sizes[i] - take, p + sizes[i]);
-    }
+    d->dict->raw_content = std::move(c);
     return d;
   } catch (...) {
     return nullptr;
   }
 }
 void cuda_zstd_destroy_dictionary(cuda_zstd_dict_t *d) { delete d; }
+// reference DictionaryManager::load_dictionary (include/cuda_zstd_dictionary.h:292-310): a host
+// buffer with raw content or a formatted dictionary (e.g. ZDICT_trainFromBuffer's)
+cuda_zstd_dict_t *cuda_zstd_load_dictionary(const void *buffer, size_t size) {
+  if (!buffer || size == 0 || size > zh::kDictMaxBytes) return nullptr;
+  u32 id = 0;
+  size_t off = 0;
+  if (!zh::dict_layout((const u8 *)buffer, size, id, off)) return nullptr;
+  try {
+    auto *d = new cuda_zstd_dict_t;
+    d->dict.reset(new dictionary::Dictionary);
+    d->dict->raw_content.assign((const u8 *)buffer, (const u8 *)buffer + size);
+    d->dict->dict_id = id;
+    return d;
+  } catch (...) {
+    return nullptr;
+  }
+}
+size_t cuda_zstd_get_dictionary_content(const cuda_zstd_dict_t *d, void *out, size_t capacity) {
+  if (!d || !d->dict) return 0;
+  size_t const n = d->dict->raw_content.size();
+  if (out && capacity >= n) memcpy(out, d->dict->raw_content.data(), n);
+  return n;
+}
+int cuda_zstd_get_dictionary_layout(const cuda_zstd_dict_t *d, unsigned int *dict_id, size_t *content_offset) {
+  if (!d || !d->dict) return status_to_nvcomp_error(Status::ERROR_INVALID_PARAMETER);
+  u32 id = 0;
+  size_t off = 0;
+  if (!zh::dict_layout(d->dict->raw_content.data(), d->dict->raw_content.size(), id, off)) return status_to_nvcomp_error(Status::ERROR_DICTIONARY_FAILED);
+  if (dict_id) *dict_id = id;
+  if (content_offset) *content_offset = off;
+  return 0;
+}
+int cuda_zstd_clear_dictionary(cuda_zstd_manager_t *m) {
+  if (!m || !m->manager) return status_to_nvcomp_error(Status::ERROR_INVALID_PARAMETER);
+  return status_to_nvcomp_error(m->manager->clear_dictionary());
+}
 int cuda_zstd_set_dictionary(cuda_zstd_manager_t *m, cuda_zstd_dict_t *d) {
   if (!m || !m->manager || !d || !d->dict) return status_to_nvcomp_error(Status::ERROR_INVALID_PARAMETER);
   return status_to_nvcomp_error(m->manager->set_dictionary(*d->dict));

@@ -33,6 +33,10 @@ struct ZhDecArgs {
   u32 ho_off;  // offset of the item's hand-off record inside its slot (split pipeline)
   u32 phase;   // 0: whole decode in one kernel; 1 / 3: first / last kernel of the split pipeline
   u32 item0;   // first item of this launch (launch_decompress's pipelined groups)
+  const u8 *dict;  // dictionary (device, whole buffer) or null; its content precedes every frame
+  u64 dict_n;      // its size
+  u32 dict_off;    // content offset (formatted dictionary: after tables + repcodes; raw: 0)
+  u32 dict_id;     // Dictionary_ID (formatted), 0 for raw content
 };
 #define ZH_DEC_HANDOFF_BYTES 5376u  // sizeof(DecHandoff), zh_decode.hip
 
@@ -50,5 +54,5 @@ void profile_enable(bool on);
 int profile_collect(double *totals);
 hipError_t launch_plan(const void *const *d_in_ptrs, const size_t *d_in_sizes, u32 nitems, u32 bpi, void *const *d_out_ptrs, u64 out_cap,
                        u8 *staging, ZhBlockDesc *d_descs, ZhItemDesc *d_items, u64 *d_item_size, u32 *d_item_status, u32 extra_flags,
-                       hipStream_t stream);
+                       const u8 *dict, u32 dict_n, u32 dict_id, hipStream_t stream);
 }  // namespace zh

@@ -313,8 +313,12 @@ extern "C" __global__ __launch_bounds__(K1_THREADS) void zh_lz_kernel(const ZhBl
 
   u32 const b = blockIdx.x, tid = threadIdx.x, lane = tid & 63;
   ZhBlockDesc const d = blocks[b];
-  u32 const n = d.n;
-  if (n == 0) return;
+  if (d.n == 0) return;
+  // A dictionary frame's first block is staged behind the tail of the dictionary content
+  // (SURVEY §8f F2): positions [0, pre) are history only -- hashed and matched against,
+  // never parsed (the parse starts at pre) -- so matches reach into the dictionary.
+  u32 const pre = d.pre_n;
+  u32 const n = pre + d.n;
   u32 *meta = ws.meta(b);
 #ifdef ZH_STAMPS
   u64 const rt0 = __builtin_amdgcn_s_memrealtime();
@@ -326,7 +330,15 @@ extern "C" __global__ __launch_bounds__(K1_THREADS) void zh_lz_kernel(const ZhBl
   // ---- stage the block into LDS (16 B per lane when the source allows it) and probe RLE
   const u8 *src = d.src;
   bool same = true;
-  if ((((uintptr_t)src) & 15) == 0) {
+  if (pre) {  // dictionary tail + block, byte loads; the RLE probe looks at the block only
+    const u8 *const pp = d.pre;
+    u8 const first = src[0];
+    for (u32 i = tid; i < n; i += K1_THREADS) {
+      u8 const c = i < pre ? pp[i] : src[i - pre];
+      in[i] = c;
+      same &= i < pre || c == first;
+    }
+  } else if ((((uintptr_t)src) & 15) == 0) {
     u32 const nv = n >> 4;
     u8 const first = src[0];
     u32 const f4 = first * 0x01010101u;
@@ -345,7 +357,7 @@ extern "C" __global__ __launch_bounds__(K1_THREADS) void zh_lz_kernel(const ZhBl
   for (u32 i = tid; i < HS_SIZE; i += K1_THREADS) TS[i] = 0;
   if (tid < 2) misc[8 + tid] = 0;
   if (tid == 0) misc[MISC_ARR] = 0;
-  bool const rle = __syncthreads_and(same) && n >= 2;
+  bool const rle = __syncthreads_and(same) && d.n >= 2;
   if (rle) {
     if (tid == 0) { meta[0] = 0; meta[1] = 0; meta[2] = 1; }
     return;
@@ -355,7 +367,7 @@ extern "C" __global__ __launch_bounds__(K1_THREADS) void zh_lz_kernel(const ZhBl
   u64 *seq_out = ws.seq(b);
   u8 *lit_out = ws.lits(b);
   u32 const lim = n > ZH_HASH_READ ? n - ZH_HASH_READ : 0;
-  u32 nseq_tot = 0, nlit_tot = 0, e_in = 0;
+  u32 nseq_tot = 0, nlit_tot = 0, e_in = pre;
   // ---- inserter waves: their own loop with the same barrier sequence as the workers'
   // (separate code, so their registers never add to the workers' pressure)
   if (tid >= INS_TID) {
@@ -374,6 +386,13 @@ extern "C" __global__ __launch_bounds__(K1_THREADS) void zh_lz_kernel(const ZhBl
     u32 const lane = tid & 63;
     __syncthreads();  // P
     ZH_STAMP(st_A);
+    if (we <= pre) {  // dictionary history only: nothing to parse, keep the barrier sequence
+      for (u32 k = 0; k < WIN_BARRIERS; k++) {
+        if (lane == 0) atomicAdd(&misc[MISC_ARR], 1u);
+        __syncthreads();
+      }
+      continue;
+    }
 #ifdef ZH_STAMPS
     u64 const tP = __builtin_amdgcn_s_memtime();
 #endif

@@ -51,6 +51,13 @@ def lib() -> ctypes.CDLL:
             "cuda_zstd_compress_batch": (i, [vp, pvp, psz, sz, pvp, psz, pi, vp, sz, vp]),
             "cuda_zstd_get_error_string": (ctypes.c_char_p, [i]),
             "cuda_zstd_is_error": (i, [i]),
+            "cuda_zstd_train_dictionary": (vp, [pvp, psz, sz, sz]),
+            "cuda_zstd_load_dictionary": (vp, [vp, sz]),
+            "cuda_zstd_destroy_dictionary": (None, [vp]),
+            "cuda_zstd_set_dictionary": (i, [vp, vp]),
+            "cuda_zstd_clear_dictionary": (i, [vp]),
+            "cuda_zstd_get_dictionary_content": (sz, [vp, vp, sz]),
+            "cuda_zstd_get_dictionary_layout": (i, [vp, ctypes.POINTER(ctypes.c_uint), psz]),
             "nvcomp_zstd_batch_create_v5": (vp, [i, ctypes.c_uint, i]),
             "nvcomp_zstd_batch_destroy_v5": (None, [vp]),
             "nvcomp_zstd_batch_get_compress_temp_size_v5": (sz, [vp, psz, sz]),
@@ -171,6 +178,17 @@ class Manager:
         return res
 
 
+    def set_dictionary(self, d: "Dictionary"):
+        """ZstdManager::set_dictionary: later compress / decompress calls use `d`."""
+        rc = lib().cuda_zstd_set_dictionary(self._h, d._h)
+        if rc:
+            raise ZstdError(rc, "cuda_zstd_set_dictionary")
+
+    def clear_dictionary(self):
+        rc = lib().cuda_zstd_clear_dictionary(self._h)
+        if rc:
+            raise ZstdError(rc, "cuda_zstd_clear_dictionary")
+
     def decompress(self, frame, capacity: int, stream=None):
         """GPU-decode one device buffer (frames, concatenated) into a new device tensor of
         at most `capacity` bytes (cuda_zstd_decompress)."""
@@ -211,6 +229,58 @@ class Manager:
                     raise ZstdError(st[k], f"cuda_zstd_decompress_batch item {k}")
             return res
         return res, list(st)
+
+
+class Dictionary:
+    """Dictionary handle (reference dictionary::Dictionary, include/cuda_zstd_dictionary.h:101;
+    DictionaryTrainer::train_dictionary, DictionaryManager::load_dictionary :292).  Raw content,
+    or a formatted RFC 8878 §5 dictionary such as ZDICT_trainFromBuffer's."""
+
+    def __init__(self, handle, what: str = "dictionary"):
+        if not handle:
+            raise ZstdError(INVALID, what)
+        self._h = handle
+
+    @classmethod
+    def train(cls, samples, dict_size: int) -> "Dictionary":
+        """COVER training over host samples (bytes-like / uint8 arrays) -> raw content."""
+        raw = [bytes(s) for s in samples]
+        bufs = [ctypes.create_string_buffer(b, max(len(b), 1)) for b in raw]
+        n = len(raw)
+        ptrs = (ctypes.c_void_p * n)(*[ctypes.addressof(b) for b in bufs])
+        sizes = (ctypes.c_size_t * n)(*[len(b) for b in raw])
+        return cls(lib().cuda_zstd_train_dictionary(ptrs, sizes, n, dict_size), "cuda_zstd_train_dictionary")
+
+    @classmethod
+    def load(cls, buf) -> "Dictionary":
+        b = bytes(buf)
+        cb = ctypes.create_string_buffer(b, max(len(b), 1))
+        return cls(lib().cuda_zstd_load_dictionary(cb, len(b)), "cuda_zstd_load_dictionary")
+
+    def content(self) -> bytes:
+        n = lib().cuda_zstd_get_dictionary_content(self._h, None, 0)
+        cb = ctypes.create_string_buffer(max(n, 1))
+        lib().cuda_zstd_get_dictionary_content(self._h, cb, n)
+        return cb.raw[:n]
+
+    def layout(self):
+        """(Dictionary_ID, content offset); (0, 0) for raw content."""
+        did, off = ctypes.c_uint(), ctypes.c_size_t()
+        rc = lib().cuda_zstd_get_dictionary_layout(self._h, ctypes.byref(did), ctypes.byref(off))
+        if rc:
+            raise ZstdError(rc, "cuda_zstd_get_dictionary_layout")
+        return did.value, off.value
+
+    def close(self):
+        if self._h:
+            lib().cuda_zstd_destroy_dictionary(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:  # interpreter shutdown
+            pass
 
 
 class BatchedDecompressor:

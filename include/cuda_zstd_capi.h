@@ -42,6 +42,14 @@ size_t cuda_zstd_get_decompress_workspace_size(cuda_zstd_manager_t *manager, siz
 cuda_zstd_dict_t *cuda_zstd_train_dictionary(const void **samples, const size_t *sample_sizes, size_t num_samples, size_t dict_size);
 void cuda_zstd_destroy_dictionary(cuda_zstd_dict_t *dict);
 int cuda_zstd_set_dictionary(cuda_zstd_manager_t *manager, cuda_zstd_dict_t *dict);
+/* dictionaries: cuda_zstd_train_dictionary is COVER training (raw content);
+ * load = raw content or a formatted RFC 8878 §5 dictionary from a host buffer (reference
+ * DictionaryManager::load_dictionary, include/cuda_zstd_dictionary.h:292); content copies the
+ * bytes out (returns the size); layout gives the Dictionary_ID and content offset (0, 0 for raw) */
+cuda_zstd_dict_t *cuda_zstd_load_dictionary(const void *buffer, size_t size);
+size_t cuda_zstd_get_dictionary_content(const cuda_zstd_dict_t *dict, void *out, size_t capacity);
+int cuda_zstd_get_dictionary_layout(const cuda_zstd_dict_t *dict, unsigned int *dict_id, size_t *content_offset);
+int cuda_zstd_clear_dictionary(cuda_zstd_manager_t *manager);
 const char *cuda_zstd_get_error_string(int error_code);
 int cuda_zstd_is_error(int code);
 

@@ -20,9 +20,9 @@
 namespace cuda_zstd {
 
 namespace dictionary {
-// Raw-content dictionary (reference include/cuda_zstd_dictionary.h).  Dictionary
-// compression is a "next" row: set_dictionary() reports
-// ERROR_NOT_IMPLEMENTED until then, instead of emitting frames libzstd cannot decode.
+// Dictionary bytes (reference include/cuda_zstd_dictionary.h): raw content or a formatted
+// RFC 8878 §5 dictionary.  dict_id is filled in by set_dictionary (the
+// formatted dictionary's ID; 0 for raw content).
 struct Dictionary {
   std::vector<u8> raw_content;
   u32 dict_id = 0;

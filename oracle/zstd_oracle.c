@@ -829,13 +829,15 @@ void orc_lz_match_info(const u8 *src, u32 n, u8 *len, u16 *off) {
   }
 }
 
-/* Parse + merge.  Returns number of sequences; *last_lits = trailing literals. */
-size_t orc_lz_parse(const u8 *src, u32 n, orc_seq_t *seq, u32 *last_lits) {
+/* Parse + merge over src[0, n).  Positions [0, pre) are dictionary history:
+ * hashed and matched against like any other, but the parse starts at pre.
+ * Returns number of sequences; *last_lits = trailing literals. */
+size_t orc_lz_parse_pre(const u8 *src, u32 pre, u32 n, orc_seq_t *seq, u32 *last_lits) {
   u8 *len = malloc(n + 1);
   u16 *off = malloc(sizeof(u16) * (n + 1));
   orc_lz_match_info(src, n, len, off);
   size_t ns = 0;
-  u32 p = 0, anchor = 0, lim = n > ZH_HASH_READ ? n - ZH_HASH_READ : 0;
+  u32 p = pre, anchor = pre, lim = n > ZH_HASH_READ ? n - ZH_HASH_READ : 0;
   while (p < lim) {
     if (len[p] == 0 || len[p + 1] > len[p]) { p++; continue; }
     u32 ll = p - anchor;
@@ -848,6 +850,7 @@ size_t orc_lz_parse(const u8 *src, u32 n, orc_seq_t *seq, u32 *last_lits) {
   free(len); free(off);
   return ns;
 }
+size_t orc_lz_parse(const u8 *src, u32 n, orc_seq_t *seq, u32 *last_lits) { return orc_lz_parse_pre(src, 0, n, seq, last_lits); }
 
 /* ------------------------------------------------------------------------ */
 /* Block + frame                                                            */
@@ -859,7 +862,8 @@ static int is_rle(const u8 *src, size_t n) {
 
 /* Compress one block (<= ZH_BLOCK_MAX) with its block header.  rep[] in/out.
  * Returns bytes written or 0 on insufficient capacity. */
-size_t orc_compress_block(u8 *dst, size_t cap, const u8 *src, u32 n, int last, u32 rep[3]) {
+size_t orc_compress_block_pre(u8 *dst, size_t cap, const u8 *buf, u32 pre, u32 n, int last, u32 rep[3]) {
+  const u8 *src = buf + pre;  /* the block; buf[0, pre) = dictionary history staged before it */
   u32 hdr;
   if (n >= 2 && is_rle(src, n)) {
     if (cap < 4) return 0;
@@ -869,7 +873,7 @@ size_t orc_compress_block(u8 *dst, size_t cap, const u8 *src, u32 n, int last, u
   }
   orc_seq_t *seq = malloc(sizeof(orc_seq_t) * (n / ZH_MIN_MATCH_SHORT + 2));
   u32 lastLits;
-  size_t ns = orc_lz_parse(src, n, seq, &lastLits);
+  size_t ns = orc_lz_parse_pre(buf, pre, pre + n, seq, &lastLits);
   u32 repSave[3] = {rep[0], rep[1], rep[2]};
   size_t body = (cap > 3) ? orc_encode_block_body(dst + 3, cap - 3, src, n, seq, ns, rep) : (size_t)-1;
   free(seq);
@@ -886,19 +890,28 @@ size_t orc_compress_block(u8 *dst, size_t cap, const u8 *src, u32 n, int last, u
   dst[0] = (u8)hdr; dst[1] = (u8)(hdr >> 8); dst[2] = (u8)(hdr >> 16);
   return 3 + body;
 }
+size_t orc_compress_block(u8 *dst, size_t cap, const u8 *src, u32 n, int last, u32 rep[3]) {
+  return orc_compress_block_pre(dst, cap, src, 0, n, last, rep);
+}
 
 /* Frame header (reference write_frame_header, src/cuda_zstd_manager.cu:3998-4106,
  * without dictionary / checksum).  Returns header size. */
-size_t orc_frame_header(u8 *dst, u64 content, u32 block_size, u32 window_log) {
+size_t orc_frame_header_dict(u8 *dst, u64 content, u32 block_size, u32 window_log, u32 dict_id);
+size_t orc_frame_header(u8 *dst, u64 content, u32 block_size, u32 window_log) { return orc_frame_header_dict(dst, content, block_size, window_log, 0); }
+/* dict_id != 0: Dictionary_ID field of libzstd's minimal size (the reference writes a 1-byte
+ * XXH32 of the buffer, :4020-4026, which libzstd rejects). */
+size_t orc_frame_header_dict(u8 *dst, u64 content, u32 block_size, u32 window_log, u32 dict_id) {
   size_t o = 0;
+  u32 const didf = dict_id == 0 ? 0 : dict_id < 256 ? 1 : dict_id < 65536 ? 2 : 3;
   u32 magic = 0xFD2FB528u;
   memcpy(dst, &magic, 4); o = 4;
   int ss = content <= block_size;
   u32 fcs_flag, fcs_size;
   if (ss) { if (content < 256) { fcs_flag = 0; fcs_size = 1; } else if (content < 65536 + 256) { fcs_flag = 1; fcs_size = 2; } else if (content <= 0xFFFFFFFFull) { fcs_flag = 2; fcs_size = 4; } else { fcs_flag = 3; fcs_size = 8; } }
   else { if (content >= 256 && content < 65536 + 256) { fcs_flag = 1; fcs_size = 2; } else if (content <= 0xFFFFFFFFull) { fcs_flag = 2; fcs_size = 4; } else { fcs_flag = 3; fcs_size = 8; } }
-  dst[o++] = (u8)((fcs_flag << 6) | (ss ? 0x20 : 0));
+  dst[o++] = (u8)((fcs_flag << 6) | (ss ? 0x20 : 0) | didf);
   if (!ss) dst[o++] = (u8)((window_log - 10) << 3);
+  for (u32 k = 0; k < (didf == 3 ? 4u : didf); k++) dst[o++] = (u8)(dict_id >> (8 * k));
   if (fcs_size == 1) dst[o++] = (u8)content;
   else if (fcs_size == 2) { u32 v = (u32)content - 256; dst[o++] = (u8)v; dst[o++] = (u8)(v >> 8); }
   else if (fcs_size == 4) { u32 v = (u32)content; memcpy(dst + o, &v, 4); o += 4; }
@@ -968,17 +981,96 @@ size_t orc_compress_frame(u8 *dst, size_t cap, const u8 *src, u64 n, u32 block_s
 
 /* checksum != 0: Content_Checksum_Flag set and the low 32 bits of XXH64 of the input
  * appended (reference src/cuda_zstd_manager.cu:3037-3056 when checksum is computed). */
-size_t orc_compress_frame_ck(u8 *dst, size_t cap, const u8 *src, u64 n, u32 block_size, u32 window_log, int checksum) {
-  if (cap < 22) return 0;
-  size_t o = orc_frame_header(dst, n, block_size, window_log);
+/* ------------------------------------------------------------------------ */
+/* Dictionaries (RFC 8878 §5)                                */
+/* ------------------------------------------------------------------------ */
+static u32 dict_fwd32(const u8 *p, size_t avail, size_t bitpos) {
+  size_t b = bitpos >> 3; u64 v = 0;
+  for (size_t i = 0; i < 5; i++) if (b + i < avail) v |= (u64)p[b + i] << (8 * i);
+  return (u32)(v >> (bitpos & 7));
+}
+/* bytes of an FSE table description (FSE_readNCount restated for sizing); 0 if malformed */
+static size_t dict_ncount_size(const u8 *p, size_t avail, u32 maxSV, u32 maxLog) {
+  if (!avail) return 0;
+  u32 nb = (dict_fwd32(p, avail, 0) & 15u) + 5u;
+  if (nb > maxLog) return 0;
+  size_t bp = 4; int rem = (1 << nb) + 1, thr = 1 << nb; nb++;
+  u32 sym = 0; int prev0 = 0;
+  while (rem > 1 && sym <= maxSV) {
+    if (prev0) {
+      u32 n0 = sym, r;
+      do { r = dict_fwd32(p, avail, bp) & 3u; bp += 2; n0 += r; } while (r == 3 && bp < 8 * avail + 32);
+      if (n0 > maxSV) return 0;
+      sym = n0;
+    }
+    u32 bs = dict_fwd32(p, avail, bp); int mx = (2 * thr - 1) - rem, c;
+    if ((int)(bs & (u32)(thr - 1)) < mx) { c = (int)(bs & (u32)(thr - 1)); bp += nb - 1; }
+    else { c = (int)(bs & (u32)(2 * thr - 1)); if (c >= thr) c -= mx; bp += nb; }
+    c--; rem -= c < 0 ? -c : c; sym++; prev0 = c == 0;
+    while (rem < thr) { nb--; thr >>= 1; }
+  }
+  if (rem != 1) return 0;
+  size_t used = (bp + 7) >> 3;
+  return used <= avail ? used : 0;
+}
+/* Raw content (no 0xEC30A437 magic): *id = 0, content at 0.  Formatted: Dictionary_ID, Huffman
+ * table description, OF / ML / LL FSE table descriptions, three repcodes (each in [1, content
+ * size], libzstd ZSTD_loadDEntropy), content.  Returns 0, or -1 if malformed. */
+int orc_dict_layout(const u8 *d, size_t n, u32 *id, size_t *content_off) {
+  u32 magic = 0;
+  *id = 0; *content_off = 0;
+  if (n >= 4) memcpy(&magic, d, 4);
+  if (n < 8 || magic != 0xEC30A437u) return 0;
+  memcpy(id, d + 4, 4);
+  size_t o = 8;
+  u32 hb = d[o];
+  size_t hsz = hb >= 128 ? 1 + ((size_t)(hb - 127) + 1) / 2 : 1 + (size_t)hb;
+  if (hb == 0 || o + hsz > n) return -1;
+  o += hsz;
+  static const u32 msv[3] = {31, 52, 35}, mlg[3] = {8, 9, 9};
+  for (int t = 0; t < 3; t++) {
+    size_t u = o < n ? dict_ncount_size(d + o, n - o, msv[t], mlg[t]) : 0;
+    if (!u) return -1;
+    o += u;
+  }
+  if (o + 12 > n) return -1;
+  for (int k = 0; k < 3; k++) {
+    u32 r; memcpy(&r, d + o + 4 * k, 4);
+    if (r == 0 || r > n - o - 12) return -1;
+  }
+  *content_off = o + 12;
+  return 0;
+}
+
+/* Whole frame with an optional dictionary (dict_n == 0: none).  The first block is compressed
+ * behind the last min(content, ZH_BLOCK_MAX - block) bytes of the dictionary content; blocks of
+ * a dictionary frame start with unknown repcodes (the dictionary's are never referenced). */
+size_t orc_compress_frame_dict(u8 *dst, size_t cap, const u8 *src, u64 n, u32 block_size, u32 window_log, int checksum, const u8 *dict,
+                               size_t dict_n) {
+  u32 did = 0;
+  size_t co = 0;
+  if (dict_n && orc_dict_layout(dict, dict_n, &did, &co)) return 0;
+  if (cap < (dict_n ? 26u : 22u)) return 0;
+  size_t o = orc_frame_header_dict(dst, n, block_size, window_log, did);
   if (checksum) dst[4] |= 0x04;
   u64 pos = 0;
   u32 b = 0;
   do {
     u32 bn = (u32)((n - pos) < ZH_BLOCK_MAX ? (n - pos) : ZH_BLOCK_MAX);
     u32 rep[3] = {1, 4, 8};
-    if (b > 0) { rep[0] = rep[1] = rep[2] = 0; }
-    size_t w = orc_compress_block(dst + o, cap - o, src + pos, bn, pos + bn >= n, rep);
+    if (b > 0 || dict_n) { rep[0] = rep[1] = rep[2] = 0; }
+    size_t w;
+    if (b == 0 && dict_n) {
+      size_t cn = dict_n - co;
+      u32 pre = (u32)(cn < (size_t)(ZH_BLOCK_MAX - bn) ? cn : (size_t)(ZH_BLOCK_MAX - bn));
+      u8 *buf = malloc((size_t)pre + bn + 16);
+      memcpy(buf, dict + dict_n - pre, pre);
+      memcpy(buf + pre, src, bn);
+      w = orc_compress_block_pre(dst + o, cap - o, buf, pre, bn, pos + bn >= n, rep);
+      free(buf);
+    } else {
+      w = orc_compress_block(dst + o, cap - o, src + pos, bn, pos + bn >= n, rep);
+    }
     if (!w) return 0;
     o += w; pos += bn; b++;
   } while (pos < n);
@@ -989,6 +1081,9 @@ size_t orc_compress_frame_ck(u8 *dst, size_t cap, const u8 *src, u64 n, u32 bloc
     o += 4;
   }
   return o;
+}
+size_t orc_compress_frame_ck(u8 *dst, size_t cap, const u8 *src, u64 n, u32 block_size, u32 window_log, int checksum) {
+  return orc_compress_frame_dict(dst, cap, src, n, block_size, window_log, checksum, NULL, 0);
 }
 
 size_t orc_max_compressed_size(u64 n) {

@@ -1,0 +1,120 @@
+"""Dictionaries on the GPU: frames compressed with a dictionary are
+byte-identical to the oracle's and decode with libzstd ZSTD_decompress_usingDict; the GPU decoder
+reads them and libzstd's own dictionary frames at levels 1-19 (the dictionary's entropy tables,
+repcodes and content).  Mirrors the reference's tests/test_dictionary.cu (train, compress with and
+without, round trip) and tests/test_dictionary_compression.cu (set_dictionary, compress,
+decompress)."""
+import numpy as np
+import pytest
+
+import zh_testlib as T
+
+pytestmark = pytest.mark.gpu
+
+SIZES = [1, 7, 100, 4095, 16384, 50000, 65536, 70000, 200000]
+
+
+@pytest.fixture(scope="module")
+def torch_cuda():
+    import torch
+
+    assert torch.cuda.is_available(), "gpu tests need a GPU"
+    return torch
+
+
+@pytest.fixture(scope="module")
+def dicts():
+    import cuda_zstd
+
+    a = T.gen(T.DG_JSON, 512, 0x5EED0005, 4096)
+    samples = [a[i:i + 4096] for i in range(0, len(a), 4096)]
+    return {"zdict": T.zdict_train(samples, 16384), "cover": cuda_zstd.Dictionary.train(samples, 16384).content()}
+
+
+def _dev(torch, b):
+    a = np.frombuffer(bytes(b), np.uint8).copy()
+    return torch.from_numpy(a if a.size else np.zeros(1, np.uint8)).cuda()[: len(a)]
+
+
+def _mgr(level, d=None):
+    import cuda_zstd
+
+    m = cuda_zstd.Manager(level)
+    if d is not None:
+        m.set_dictionary(cuda_zstd.Dictionary.load(d))
+    return m
+
+
+@pytest.mark.parametrize("kind", ["zdict", "cover"])
+def test_compress_with_dictionary_matches_oracle(torch_cuda, dicts, kind):
+    d = dicts[kind]
+    m = _mgr(3, d)
+    src = T.gen(T.DG_JSON, 1, 0x5EED0305, 200000)
+    for n in SIZES:
+        data = src[:n]
+        f = m.compress(_dev(torch_cuda, data)).cpu().numpy().tobytes()
+        assert f == T.oracle_frame(data, dictionary=d), (kind, n)
+        assert T.zstd_decompress(f, n, dictionary=d) == data.tobytes(), (kind, n)
+        assert m.decompress(_dev(torch_cuda, f), n).cpu().numpy().tobytes() == data.tobytes(), (kind, n)
+
+
+@pytest.mark.parametrize("level", [1, 3, 9, 19])
+def test_gpu_decodes_libzstd_dictionary_frames(torch_cuda, dicts, level):
+    src = T.gen(T.DG_JSON, 1, 0x5EED0405, 150000)
+    sizes = [100, 4096, 30000, 65536, 150000]
+    for kind in ("zdict", "cover"):
+        d = dicts[kind]
+        frames = [T.zstd_compress_dict(src[:n], d, level) for n in sizes]
+        outs, st = _mgr(3, d).decompress_batch([_dev(torch_cuda, f) for f in frames], sizes, raise_on_error=False)
+        for o, s, n in zip(outs, st, sizes):
+            assert s == 0, (kind, level, n, s)
+            assert o.cpu().numpy().tobytes() == src[:n].tobytes(), (kind, level, n)
+
+
+def test_batch_with_dictionary(torch_cuda, dicts):
+    d = dicts["zdict"]
+    m = _mgr(3, d)
+    a = T.gen(T.DG_JSON, 96, 0x5EED0505, 16384)
+    recs = [a[i:i + 16384] for i in range(0, len(a), 16384)]
+    frames = m.compress_batch([_dev(torch_cuda, r) for r in recs])
+    for r, f in zip(recs, frames):
+        assert f.cpu().numpy().tobytes() == T.oracle_frame(r, dictionary=d)
+    outs = m.decompress_batch(frames, [16384] * len(recs))
+    assert all(o.cpu().numpy().tobytes() == r.tobytes() for o, r in zip(outs, recs))
+
+
+def test_dictionary_mismatch(torch_cuda, dicts):
+    import cuda_zstd
+
+    data = T.gen(T.DG_JSON, 1, 0x5EED0605, 8000)
+    f = T.zstd_compress_dict(data, dicts["zdict"], 3)  # names the dictionary's ID
+    for m in (_mgr(3), _mgr(3, dicts["cover"])):
+        with pytest.raises(cuda_zstd.ZstdError):
+            m.decompress(_dev(torch_cuda, f), 8000)
+    assert _mgr(3, dicts["zdict"]).decompress(_dev(torch_cuda, f), 8000).cpu().numpy().tobytes() == data.tobytes()
+
+
+def _create_sample(size, prefix):  # reference tests/test_dictionary.cu:17-28
+    p = np.frombuffer(prefix.encode(), np.uint8)
+    i = np.arange(size)
+    out = (i % 256).astype(np.uint8)
+    m = (i % 100) < len(p)
+    out[m] = p[i[m] % len(p)]
+    return out
+
+
+def test_reference_dictionary_scenario(torch_cuda):
+    """reference tests/test_dictionary.cu: train 32 KB on three samples, compress 128 KiB without
+    and with the dictionary (level 5); both succeed and the dictionary frame round-trips."""
+    import cuda_zstd
+
+    pfx = "COMMON_HEADER_PATTERN_"
+    samples = [_create_sample(64 * 1024, pfx), _create_sample(32 * 1024, pfx), _create_sample(48 * 1024, pfx)]
+    dd = cuda_zstd.Dictionary.train(samples, 32 * 1024)
+    data = _create_sample(128 * 1024, pfx)
+    m = cuda_zstd.Manager(5)
+    assert m.compress(_dev(torch_cuda, data)).numel() > 0
+    m.set_dictionary(dd)
+    withd = m.compress(_dev(torch_cuda, data)).cpu().numpy().tobytes()
+    assert T.zstd_decompress(withd, len(data), dictionary=dd.content()) == data.tobytes()
+    assert m.decompress(_dev(torch_cuda, withd), len(data)).cpu().numpy().tobytes() == data.tobytes()

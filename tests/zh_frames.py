@@ -22,6 +22,8 @@ def walk(frame: bytes):
         fhd = b[ip + 4]
         single, chk, did, fcsf = (fhd >> 5) & 1, (fhd >> 2) & 1, fhd & 3, fhd >> 6
         hs = 1 + (0 if single else 1) + (0, 1, 2, 4)[did] + ((1 if single else 0), 2, 4, 8)[fcsf]
+        dp = ip + 5 + (0 if single else 1)
+        dict_id = int.from_bytes(b[dp:dp + (0, 1, 2, 4)[did]], "little")
         ip += 4 + hs
         first = True
         while True:
@@ -29,7 +31,7 @@ def walk(frame: bytes):
             last, bt, bsz = bh & 1, (bh >> 1) & 3, bh >> 3
             ip += 3
             d = {"type": ("raw", "rle", "compressed", "reserved")[bt], "size": bsz, "first_in_frame": first, "checksum": bool(chk),
-                 "single_segment": bool(single), "fcs": fcsf != 0 or bool(single)}
+                 "single_segment": bool(single), "fcs": fcsf != 0 or bool(single), "dict_id": dict_id}
             first = False
             if bt == 2:
                 p = b[ip:ip + bsz]

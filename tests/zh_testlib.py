@@ -37,6 +37,11 @@ def oracle():
         L.orc_fse_optimal_table_log.restype = ctypes.c_uint32
         L.orc_compress_frame_ck.restype = ctypes.c_size_t
         L.orc_compress_frame_ck.argtypes = [vp, ctypes.c_size_t, vp, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_int]
+        L.orc_compress_frame_dict.restype = ctypes.c_size_t
+        L.orc_compress_frame_dict.argtypes = [vp, ctypes.c_size_t, vp, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_int, vp,
+                                              ctypes.c_size_t]
+        L.orc_dict_layout.restype = ctypes.c_int
+        L.orc_dict_layout.argtypes = [vp, ctypes.c_size_t, ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(ctypes.c_size_t)]
         L.orc_xxh64.restype = ctypes.c_uint64
         L.orc_xxh64.argtypes = [vp, ctypes.c_uint64]
         _o = L
@@ -81,21 +86,33 @@ def gen(kind, nchunks, seed, chunk_size=65536, first=0):
     return a
 
 
-def oracle_frame(data, block_size=128 * 1024, window_log=19, checksum=False):
+def oracle_frame(data, block_size=128 * 1024, window_log=19, checksum=False, dictionary=None):
     data = np.ascontiguousarray(np.frombuffer(bytes(data), np.uint8) if not isinstance(data, np.ndarray) else data)
     cap = int(oracle().orc_max_compressed_size(ctypes.c_uint64(len(data)))) + 64
     out = np.zeros(cap, np.uint8)
-    n = oracle().orc_compress_frame_ck(out.ctypes.data_as(vp), cap, data.ctypes.data_as(vp), len(data), block_size, window_log, int(checksum))
+    d = np.frombuffer(bytes(dictionary), np.uint8).copy() if dictionary else None
+    n = oracle().orc_compress_frame_dict(out.ctypes.data_as(vp), cap, data.ctypes.data_as(vp), len(data), block_size, window_log, int(checksum),
+                                         d.ctypes.data_as(vp) if d is not None else None, 0 if d is None else len(d))
     assert n > 0
     return out[:n].tobytes()
 
 
-def zstd_decompress(frame, size):
+def zstd_decompress(frame, size, dictionary=None):
     z = zstd()
     assert z is not None, "libzstd not available"
     src = np.frombuffer(frame, np.uint8).copy()
     dst = np.zeros(max(size, 1), np.uint8)
-    r = z.ZSTD_decompress(dst.ctypes.data_as(vp), ctypes.c_size_t(len(dst)), src.ctypes.data_as(vp), ctypes.c_size_t(len(src)))
+    if dictionary is None:
+        r = z.ZSTD_decompress(dst.ctypes.data_as(vp), ctypes.c_size_t(len(dst)), src.ctypes.data_as(vp), ctypes.c_size_t(len(src)))
+    else:  # ZSTD_decompress_usingDict: raw content or a formatted dictionary
+        z.ZSTD_createDCtx.restype = vp
+        z.ZSTD_freeDCtx.argtypes = [vp]
+        z.ZSTD_decompress_usingDict.restype = ctypes.c_size_t
+        z.ZSTD_decompress_usingDict.argtypes = [vp, vp, ctypes.c_size_t, vp, ctypes.c_size_t, vp, ctypes.c_size_t]
+        dct = np.frombuffer(bytes(dictionary), np.uint8).copy()
+        dctx = z.ZSTD_createDCtx()
+        r = z.ZSTD_decompress_usingDict(dctx, dst.ctypes.data, len(dst), src.ctypes.data, len(src), dct.ctypes.data, len(dct))
+        z.ZSTD_freeDCtx(dctx)
     if z.ZSTD_isError(r):
         raise AssertionError("libzstd: " + z.ZSTD_getErrorName(r).decode())
     return dst[:r].tobytes()
@@ -152,3 +169,47 @@ def special_inputs():
         "runs": np.repeat(rng.integers(0, 4, 700, dtype=np.uint8), 97)[:65536].copy(),
     }
     return out
+
+
+def dict_layout(buf):
+    """(Dictionary_ID, content offset) by the oracle's RFC 8878 §5 parser; None if malformed."""
+    b = np.frombuffer(bytes(buf), np.uint8).copy()
+    did, off = ctypes.c_uint32(), ctypes.c_size_t()
+    r = oracle().orc_dict_layout(b.ctypes.data_as(vp), len(b), ctypes.byref(did), ctypes.byref(off))
+    return None if r else (did.value, off.value)
+
+
+def zdict_train(samples, capacity):
+    """libzstd ZDICT_trainFromBuffer (a formatted dictionary) over host samples."""
+    z = zstd()
+    assert z is not None, "libzstd not available"
+    z.ZDICT_trainFromBuffer.restype = ctypes.c_size_t
+    z.ZDICT_trainFromBuffer.argtypes = [vp, ctypes.c_size_t, vp, ctypes.POINTER(ctypes.c_size_t), ctypes.c_uint]
+    z.ZDICT_isError.restype = ctypes.c_uint
+    raw = [bytes(s) for s in samples]
+    buf = np.frombuffer(b"".join(raw), np.uint8).copy()
+    sizes = (ctypes.c_size_t * len(raw))(*[len(r) for r in raw])
+    out = np.zeros(capacity, np.uint8)
+    r = z.ZDICT_trainFromBuffer(out.ctypes.data_as(vp), capacity, buf.ctypes.data_as(vp), sizes, len(raw))
+    assert not z.ZDICT_isError(r), "ZDICT_trainFromBuffer failed"
+    return out[:r].tobytes()
+
+
+def zstd_compress_dict(data, dictionary, level=3):
+    """libzstd ZSTD_compress_usingDict frame of `data`."""
+    z = zstd()
+    assert z is not None, "libzstd not available"
+    z.ZSTD_createCCtx.restype = vp
+    z.ZSTD_freeCCtx.argtypes = [vp]
+    z.ZSTD_compressBound.restype = ctypes.c_size_t
+    z.ZSTD_compress_usingDict.restype = ctypes.c_size_t
+    z.ZSTD_compress_usingDict.argtypes = [vp, vp, ctypes.c_size_t, vp, ctypes.c_size_t, vp, ctypes.c_size_t, ctypes.c_int]
+    src = np.ascontiguousarray(np.frombuffer(bytes(data), np.uint8))
+    dct = np.frombuffer(bytes(dictionary), np.uint8).copy()
+    cap = int(z.ZSTD_compressBound(ctypes.c_size_t(len(src)))) + 64
+    out = np.zeros(cap, np.uint8)
+    cctx = z.ZSTD_createCCtx()
+    r = z.ZSTD_compress_usingDict(cctx, out.ctypes.data, cap, src.ctypes.data if len(src) else None, len(src), dct.ctypes.data, len(dct), level)
+    z.ZSTD_freeCCtx(cctx)
+    assert not z.ZSTD_isError(r), z.ZSTD_getErrorName(r)
+    return out[:r].tobytes()
