@@ -1,0 +1,93 @@
+"""C5: 4,096 x 16 KiB JSON-like records (tools/datagen.c kind json, seed
+0x5EED0005), level 9, with a 64 KiB dictionary trained on every fourth record by libzstd's
+ZDICT_trainFromBuffer and by this library's COVER trainer.  GPU: ZstdBatchManager::
+compress_batch with the dictionary set (device-resident records; blocking call including its
+host-side pointer arrays; median of 3 after a warm-up).  CPU reference: libzstd
+ZSTD_compress_usingCDict(level 9) with the same dictionary, one thread.  libzstd decodes every
+GPU frame with the dictionary.  Prints one JSON line."""
+import ctypes
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+sys.path.insert(0, os.path.join(ROOT, "custom-nvcomp-with-zstd_amd"))
+import cuda_zstd  # noqa: E402
+import zh_testlib as T  # noqa: E402
+
+REC, N, SEED, LEVEL, DICT = 16384, 4096, 0x5EED0005, 9, 65536
+vp = ctypes.c_void_p
+
+
+def libzstd_cdict(recs, d, level):
+    z = T.zstd()
+    z.ZSTD_createCCtx.restype = vp
+    z.ZSTD_freeCCtx.argtypes = [vp]
+    z.ZSTD_createCDict.restype = vp
+    z.ZSTD_createCDict.argtypes = [vp, ctypes.c_size_t, ctypes.c_int]
+    z.ZSTD_freeCDict.argtypes = [vp]
+    z.ZSTD_compress_usingCDict.restype = ctypes.c_size_t
+    z.ZSTD_compress_usingCDict.argtypes = [vp, vp, ctypes.c_size_t, vp, ctypes.c_size_t, vp]
+    db = np.frombuffer(d or b"\0", np.uint8).copy()
+    cd = z.ZSTD_createCDict(db.ctypes.data, len(d) if d else 0, level)
+    cctx = z.ZSTD_createCCtx()
+    out = np.zeros(2 * REC, np.uint8)
+    total, t0 = 0, time.perf_counter()
+    for r in recs:
+        s = z.ZSTD_compress_usingCDict(cctx, out.ctypes.data, out.size, r.ctypes.data, r.size, cd)
+        assert not z.ZSTD_isError(s)
+        total += s
+    el = time.perf_counter() - t0
+    z.ZSTD_freeCCtx(cctx)
+    z.ZSTD_freeCDict(cd)
+    return total, el
+
+
+def gpu_run(recs_dev, d):
+    m = cuda_zstd.Manager(LEVEL)
+    if d:
+        m.set_dictionary(cuda_zstd.Dictionary.load(d))
+    frames = m.compress_batch(recs_dev)
+    torch.cuda.synchronize()
+    ts = []
+    for _ in range(3):
+        t0 = time.perf_counter()
+        frames = m.compress_batch(recs_dev)
+        torch.cuda.synchronize()
+        ts.append(time.perf_counter() - t0)
+    return frames, sorted(ts)[1]
+
+
+def main():
+    host = T.gen(T.DG_JSON, N, SEED, REC)
+    recs = [host[i * REC:(i + 1) * REC] for i in range(N)]
+    train = recs[::4]
+    dicts = {"none": None, "zdict": T.zdict_train(train, DICT), "cover": cuda_zstd.Dictionary.train(train, DICT).content()}
+    dev = torch.from_numpy(host).cuda()
+    recs_dev = [dev[i * REC:(i + 1) * REC] for i in range(N)]
+    total = N * REC
+    res = {"workload": "C5: 4096 x 16 KiB JSON-like records, level 9, 64 KiB dictionary (trained on every 4th record)",
+           "dict_bytes": {k: len(v) for k, v in dicts.items() if v}, "ratio": {}, "gpu_GBps": {}, "libzstd_l9_1thread_MBps": {}}
+    verified = True
+    for name, d in dicts.items():
+        frames, t = gpu_run(recs_dev, d)
+        res["ratio"][f"gpu_{name}"] = round(total / sum(f.numel() for f in frames), 4)
+        res["gpu_GBps"][name] = round(total / t / 1e9, 3)
+        for r, f in zip(recs, frames):
+            if T.zstd_decompress(f.cpu().numpy().tobytes(), REC, dictionary=d) != r.tobytes():
+                verified = False
+                break
+        lz, el = libzstd_cdict(recs, d, LEVEL)
+        res["ratio"][f"libzstd_l9_{name}"] = round(total / lz, 4)
+        res["libzstd_l9_1thread_MBps"][name] = round(total / el / 1e6, 1)
+    res["libzstd_verified"] = verified
+    print(json.dumps(res), flush=True)
+
+
+if __name__ == "__main__":
+    main()
