@@ -1,25 +1,34 @@
 """Benchmark: BASELINE.json metric "compress GB/s + ratio, 1 GB @ level 3, 64 KB chunks;
 libzstd round-trip OK" on MI355X.
 
-Workload (config C3): every rank compresses 16384 x 64 KiB chunks
-(1 GiB, Silesia-like synthetic mix, seed 0x5EED0003) that are already resident in
-HBM, through the stream-ordered C-ABI entry nvcomp_zstd_batched_compress_async_v5
-(K1 zh_lz_kernel -> K2 zh_entropy_kernel -> zh_fse_chain_kernel -> zh_seq_pack_kernel).
-Multi-GPU (C4): one process per GPU,
-chunks sharded by rank with no data-path collective (weak scaling); the only
-collective is the RCCL all-gather of per-chunk compressed sizes that gives every
-rank the global output offsets, inside the timed step.
+Workload (config C3): 16384 x 64 KiB chunks (1 GiB, Silesia-like
+synthetic mix, seed 0x5EED0003) already resident in HBM, compressed through the
+stream-ordered C-ABI entry nvcomp_zstd_batched_compress_async_v5 (K1 zh_lz_kernel ->
+K2 zh_entropy_kernel -> zh_fse_chain_kernel -> zh_seq_pack_kernel).
 
-Prints one JSON line (driver contract).  Roofline = the dominant kernel's
-algorithmic bytes (input + compressed output) per launch / its
-average HIP-event duration on the launch stream.  cpu_baseline = libzstd level 3
-(the reference's own CPU route for <1 MiB items, src/cuda_zstd_manager.cu:1604-1668)
-over a bounded sample of the same chunks on the host cores.
+Multi-GPU (C4): one process per GPU; the SAME 16384-chunk batch is split
+into contiguous ranges of ceil(B/G) chunks (shard.ShardPlan) -- strong scaling -- with no
+data-path collective.  The only exchange is the RCCL all-gather of the per-chunk
+compressed sizes that gives every rank the global frame offsets; it is inside the timed
+step, and the step time is the max over ranks.  --weak keeps 16384 chunks per rank.
+An optional payload gather (every rank's frames into one contiguous image on rank 0,
+RCCL all-gather of the padded frame slots) is timed separately (--payload-gather).
+
+Prints one JSON line (driver contract).  roofline = the dominant kernel's algorithmic
+bytes (input + compressed output) per launch / its average HIP-event
+duration on the launch stream, plus the measured issue-rate fraction of that kernel from
+the committed rocprofv3 SQ summary (profiles/*_sq_summary.json): K1 is bound by VALU
+issue, not by HBM.  cpu_baseline = libzstd level 3 (the reference's own CPU route,
+src/cuda_zstd_manager.cu:1604-1668) through tools/libcpubench.so: one ZSTD_CCtx per
+POSIX thread, ZSTD_compressCCtx over the same chunks, 1 thread and the box's host share.
+Extra legs at N=1 (not `value`): C3 on uniform random bytes, C2 (one 64 MiB frame through
+ZstdManager::compress), and GPU decompression of the C3 frames.
 """
 import argparse
 import ctypes
 import json
 import os
+import statistics
 import sys
 import time
 
@@ -32,10 +41,13 @@ sys.path.insert(0, os.path.join(ROOT, "custom-nvcomp-with-zstd_amd"))
 sys.path.insert(0, os.path.join(ROOT, "tests"))
 
 CHUNK = 64 * 1024
-CHUNKS_PER_GPU = 16384
+CHUNKS = 16384
 HBM_PEAK_GBS = 8000.0
+N_SIMD = 1024          # 256 CUs x 4 SIMDs
+VALU_CYCLES = 4        # a wave64 VALU instruction occupies its 16-lane SIMD for 4 cycles
 METRIC = "compress GB/s + ratio, 1 GB @ level 3, 64 KB chunks; libzstd round-trip OK"
 SEEDS = {"mix": 0x5EED0003, "random": 0x5EED0004}
+C2_BYTES, C2_SEED = 64 << 20, 0x5EED0002
 
 
 def gen_chunks(kind, n, first):
@@ -44,44 +56,77 @@ def gen_chunks(kind, n, first):
     return T.gen(T.KINDS[kind], n, SEEDS[kind], CHUNK, first=first)
 
 
-def cpu_baseline(data, threads, seconds=1.5):
-    """libzstd ZSTD_compress(level 3) over the rank-0 chunks, one CCtx per call,
-    `threads` host threads, bounded wall time."""
-    import concurrent.futures as cf
+# ----------------------------------------------------------------------------- host CPU
+def host_info():
+    model, phys = None, set()
+    try:
+        cur = {}
+        for line in open("/proc/cpuinfo"):
+            if not line.strip():
+                if "physical id" in cur and "core id" in cur:
+                    phys.add((cur["physical id"], cur["core id"]))
+                cur = {}
+                continue
+            k, _, v = line.partition(":")
+            cur[k.strip()] = v.strip()
+            if k.strip() == "model name" and model is None:
+                model = v.strip()
+    except OSError:
+        pass
+    return {"cpu_model": model, "physical_cores": len(phys) or None, "hw_threads": os.cpu_count(),
+            "affinity_threads": len(os.sched_getaffinity(0))}
 
-    import zh_testlib as T
 
-    z = T.zstd()
-    if z is None:
+def _cpubench():
+    so = os.path.join(ROOT, "tools", "libcpubench.so")
+    if not os.path.exists(so):
         return None
-    n = len(data) // CHUNK
-    cap = 80000
+    L = ctypes.CDLL(so)
+    L.cpub_run.restype = ctypes.c_int
+    L.cpub_run.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_size_t, ctypes.c_size_t, ctypes.c_int,
+                           ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_size_t)]
+    L.cpub_zstd_version.restype = ctypes.c_uint
+    return L
 
-    def work(lo, hi, out):
-        tot = 0
-        vp = ctypes.c_void_p
-        for i in range(lo, hi):
-            tot += z.ZSTD_compress(out.ctypes.data_as(vp), ctypes.c_size_t(cap), ctypes.c_void_p(data.ctypes.data + i * CHUNK), ctypes.c_size_t(CHUNK), 3)
-        return tot
 
-    bufs = [np.zeros(cap, np.uint8) for _ in range(threads)]
-    per = 64  # chunks per task
-    done_bytes, comp_bytes, t0 = 0, 0, time.perf_counter()
-    with cf.ThreadPoolExecutor(threads) as ex:
-        nxt = 0
-        while time.perf_counter() - t0 < seconds:
-            futs = []
-            for t in range(threads):
-                lo = nxt % n
-                hi = min(lo + per, n)
-                futs.append(ex.submit(work, lo, hi, bufs[t]))
-                done_bytes += (hi - lo) * CHUNK
-                nxt = hi
-            comp_bytes += sum(f.result() for f in futs)
-    el = time.perf_counter() - t0
-    return {"value": round(done_bytes / el / 1e9, 3), "unit": "GB/s", "cores": threads, "kind": "reference",
-            "sample": f"libzstd {z.ZSTD_versionNumber()} ZSTD_compress level 3 (the reference's CPU route) on {done_bytes >> 20} MiB "
-                      f"of the same 64 KiB chunks, {threads} threads, {el:.2f} s wall; ratio {done_bytes / max(comp_bytes, 1):.3f}"}
+def cpu_run(mode, data, nchunks, threads, passes=5, sizes=None, slot=0):
+    """Median wall time of `passes` sweeps over nchunks chunks (after one warm-up sweep)."""
+    L = _cpubench()
+    if L is None:
+        return None
+    secs = (ctypes.c_double * (passes + 1))()
+    outb = ctypes.c_size_t()
+    sz = sizes.ctypes.data if sizes is not None else None
+    rc = L.cpub_run(mode, data.ctypes.data, sz, nchunks, CHUNK, slot, 3, threads, passes + 1, secs, ctypes.byref(outb))
+    if rc:
+        return None
+    t = statistics.median(list(secs)[1:])
+    return {"seconds": t, "out_bytes": outb.value, "version": L.cpub_zstd_version()}
+
+
+def cpu_baseline(host, threads, gpu_gbs):
+    """libzstd level 3 over the same chunks: 1 thread on a 1024-chunk (64 MiB) sample and
+    `threads` threads on the whole rank-0 batch; median of 5 sweeps after a warm-up."""
+    n = len(host) // CHUNK
+    n1 = min(n, 1024)
+    one = cpu_run(0, host, n1, 1)
+    many = cpu_run(0, host, n, threads)
+    if one is None or many is None:
+        return None
+    info = host_info()
+    g1 = n1 * CHUNK / one["seconds"] / 1e9
+    gm = n * CHUNK / many["seconds"] / 1e9
+    cores = info["physical_cores"] or threads
+    model_all = g1 * cores  # linear model: every physical core at the 1-thread rate (upper bound for the CPU)
+    return {"value": round(gm, 3), "unit": "GB/s", "cores": threads, "kind": "reference",
+            "sample": f"libzstd {one['version']} ZSTD_compressCCtx level 3 (one CCtx per POSIX thread, tools/cpubench.c) over the same 64 KiB "
+                      f"chunks: {threads} threads x {n} chunks ({n * CHUNK >> 20} MiB), median of 5 sweeps; ratio {n * CHUNK / many['out_bytes']:.4f}",
+            "single_thread": {"value": round(g1, 4), "unit": "GB/s", "sample": f"{n1} chunks, median of 5 sweeps"},
+            "host": info,
+            "all_core_model": {"value": round(model_all, 2), "unit": "GB/s",
+                               "how": f"1-thread rate x {cores} physical cores (linear, no SMT gain); the box grants {threads} threads per GPU"},
+            "gpu_speedup": {"vs_measured_threads": round(gpu_gbs / gm, 2), "vs_single_thread": round(gpu_gbs / g1, 1),
+                            "vs_all_core_model": round(gpu_gbs / model_all, 2)}}
 
 
 def libzstd_roundtrip(frames, sizes, slot, host):
@@ -110,105 +155,184 @@ def libzstd_roundtrip(frames, sizes, slot, host):
         return all(ex.map(lambda k: work(k, min(n, k + step)), range(0, n, step)))
 
 
-def cpu_decompress_baseline(frames, sizes, slot, threads, seconds=1.5):
-    """libzstd ZSTD_decompress (the reference's CPU decode route) over the rank-0 frames,
-    `threads` host threads, bounded wall time."""
-    import concurrent.futures as cf
+# ----------------------------------------------------------------------------- GPU legs
+class Batch:
+    """Device-resident chunk slots + the stream-ordered batched compressor."""
 
+    def __init__(self, host, dev, level=3):
+        import cuda_zstd
+
+        self.n = n = len(host) // CHUNK
+        self.dev = dev
+        self.host = host
+        self.d_in = torch.from_numpy(host).to(dev)
+        self.bc = cuda_zstd.BatchedCompressor(level, CHUNK)
+        self.slot = (self.bc.max_out(CHUNK) + 255) // 256 * 256
+        self.d_out = torch.empty(max(n, 1) * self.slot, dtype=torch.uint8, device=dev)
+        ar = torch.arange(n, dtype=torch.int64, device=dev)
+        self.in_ptrs = self.d_in.data_ptr() + ar * CHUNK
+        self.out_ptrs = self.d_out.data_ptr() + ar * self.slot
+        self.in_sizes = torch.full((n,), CHUNK, dtype=torch.int64, device=dev)
+        self.out_sizes = torch.zeros(n, dtype=torch.int64, device=dev)
+        self.status = torch.zeros(n, dtype=torch.int32, device=dev)
+        self.temp = torch.empty(max(self.bc.temp_size(max(n, 1), CHUNK), 256), dtype=torch.uint8, device=dev)
+        self.stream = torch.cuda.current_stream(dev)
+
+    def compress(self):
+        if self.n:
+            self.bc.compress_async(self.in_ptrs, self.in_sizes, CHUNK, self.out_ptrs, self.out_sizes, self.status, self.temp, self.stream)
+
+
+def timed_events(fn, steps):
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(steps):
+        fn()
+    e1.record()
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) / steps
+
+
+def random_leg(dev, steps):
+    """C3 on uniform random bytes (seed 0x5EED0004): raw-block fallbacks everywhere."""
+    b = Batch(gen_chunks("random", CHUNKS, 0), dev)
+    b.compress()
+    torch.cuda.synchronize()
+    ms = timed_events(b.compress, steps)
+    ok = int((b.status != 0).sum().item()) == 0
+    comp = int(b.out_sizes.sum().item())
+    res = {"value": round(CHUNKS * CHUNK / (ms / 1e3) / 1e9, 3), "unit": "GB/s", "ms_per_step": round(ms, 3), "ratio": round(CHUNKS * CHUNK / comp, 4),
+           "status_ok": ok, "workload": "C3-random: 16384 x 64 KiB uniform random chunks, level 3"}
+    del b
+    torch.cuda.empty_cache()
+    return res
+
+
+def c2_leg(dev, steps):
+    """C2: one 64 MiB buffer (iid over a seeded 16-symbol alphabet) -> one frame through
+    ZstdManager::compress (cuda_zstd_compress); libzstd decodes the frame; libzstd level-3
+    ratio of the same buffer beside ours."""
+    import cuda_zstd
     import zh_testlib as T
 
+    host = T.gen(T.DG_SYM16, 1, C2_SEED, C2_BYTES)
+    d = torch.from_numpy(host).to(dev)
+    m = cuda_zstd.Manager(3)
+    f = m.compress(d)
+    torch.cuda.synchronize()
+    ms = timed_events(lambda: m.compress(d), steps)
+    frame = f.cpu().numpy().tobytes()
+    res = {"value": round(C2_BYTES / (ms / 1e3) / 1e9, 3), "unit": "GB/s", "ms_per_call": round(ms, 3), "ratio": round(C2_BYTES / len(frame), 4),
+           "workload": "C2: 64 MiB iid 16-symbol buffer, one frame (1024 x 64 KiB blocks), ZstdManager::compress incl. its host sync"}
     z = T.zstd()
-    if z is None:
-        return None
-    n = len(sizes)
-
-    def work(lo, hi, dst):
-        vp = ctypes.c_void_p
-        tot = 0
-        for i in range(lo, hi):
-            tot += z.ZSTD_decompress(dst.ctypes.data_as(vp), ctypes.c_size_t(CHUNK), ctypes.c_void_p(frames.ctypes.data + i * slot),
-                                     ctypes.c_size_t(int(sizes[i])))
-        return tot
-
-    bufs = [np.zeros(CHUNK, np.uint8) for _ in range(threads)]
-    per = 64
-    done, t0 = 0, time.perf_counter()
-    with cf.ThreadPoolExecutor(threads) as ex:
-        nxt = 0
-        while time.perf_counter() - t0 < seconds:
-            futs = []
-            for t in range(threads):
-                lo = nxt % n
-                hi = min(lo + per, n)
-                futs.append(ex.submit(work, lo, hi, bufs[t]))
-                nxt = hi
-            done += sum(f.result() for f in futs)
-    el = time.perf_counter() - t0
-    return {"value": round(done / el / 1e9, 3), "unit": "GB/s (decompressed bytes)", "cores": threads, "kind": "reference",
-            "sample": f"libzstd {z.ZSTD_versionNumber()} ZSTD_decompress of {done >> 20} MiB of the same frames, {threads} threads, {el:.2f} s wall"}
+    if z is not None:
+        res["libzstd_verified"] = T.zstd_decompress(frame, C2_BYTES) == host.tobytes()
+        res["libzstd_l3_ratio"] = round(C2_BYTES / len(T.zstd_compress(host.tobytes(), 3)), 4)
+    m.close()
+    return res
 
 
-def decompress_leg(d_in, d_out, out_ptrs, out_sizes, n, dev, steps, world):
+def decompress_leg(b, steps, world):
     """GPU decompression of the frames just produced, device-resident:
     zh_decode_kernel through nvcomp_zstd_batched_decompress_async_v5, timed with events on
     the launch stream after one warm-up; output compared with the input on the device."""
     import cuda_zstd
 
+    n, dev = b.n, b.dev
     bd = cuda_zstd.BatchedDecompressor()
-    back = torch.empty(n * CHUNK, dtype=torch.uint8, device=dev)
+    back = torch.empty(max(n, 1) * CHUNK, dtype=torch.uint8, device=dev)
     ar = torch.arange(n, dtype=torch.int64, device=dev)
     back_ptrs = back.data_ptr() + ar * CHUNK
     dsizes = torch.zeros(n, dtype=torch.int64, device=dev)
     status = torch.full((n,), -1, dtype=torch.int32, device=dev)
-    temp = torch.empty(bd.temp_size(n, CHUNK), dtype=torch.uint8, device=dev)
-    run = lambda: bd.decompress_async(out_ptrs, out_sizes, None, CHUNK, back_ptrs, dsizes, status, temp)
+    temp = torch.empty(max(bd.temp_size(max(n, 1), CHUNK), 256), dtype=torch.uint8, device=dev)
+
+    def run():
+        if n:
+            bd.decompress_async(b.out_ptrs, b.out_sizes, None, CHUNK, back_ptrs, dsizes, status, temp)
+
     run()
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    e0.record()
-    for _ in range(steps):
-        run()
-    e1.record()
-    torch.cuda.synchronize(dev)
-    ms = e0.elapsed_time(e1) / steps
-    ok = bool((status == 0).all().item()) and bool((dsizes == CHUNK).all().item()) and torch.equal(back, d_in)
-    t = torch.tensor([ms], dtype=torch.float64, device=dev)
+    ms = timed_events(run, steps)
+    ok = bool((status == 0).all().item()) and bool((dsizes == CHUNK).all().item()) and torch.equal(back[: n * CHUNK], b.d_in)
+    t = torch.tensor([ms, float(n), float(b.out_sizes.sum().item())], dtype=torch.float64, device=dev)
+    okt = torch.tensor([0 if ok else 1], dtype=torch.int64, device=dev)
     if world > 1:
+        tot = t.clone()
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    ms = t.item()
-    comp = float(out_sizes.sum().item())
+        dist.all_reduce(tot, op=dist.ReduceOp.SUM)
+        dist.all_reduce(okt, op=dist.ReduceOp.SUM)
+        n_all, comp = tot[1].item(), tot[2].item()
+    else:
+        n_all, comp = float(n), t[2].item()
+    ms = t[0].item()
     del back, temp
-    return {"value": round(world * n * CHUNK / (ms / 1e3) / 1e9, 3), "unit": "GB/s (decompressed bytes)", "kernel": "zh_decode_kernel",
-            "ms_per_step": round(ms, 3), "steps": steps, "roundtrip_equal": ok,
-            "hbm_GBps_algorithmic": round((n * CHUNK + comp) / (ms / 1e3) / 1e9, 2)}
+    return {"value": round(n_all * CHUNK / (ms / 1e3) / 1e9, 3), "unit": "GB/s (decompressed bytes)", "kernel": "zh_decode_kernel",
+            "ms_per_step": round(ms, 3), "steps": steps, "roundtrip_equal": okt.item() == 0,
+            "hbm_GBps_algorithmic": round((n_all * CHUNK + comp) / (ms / 1e3) / 1e9, 2)}
+
+
+def cpu_decompress_baseline(b, threads):
+    """libzstd ZSTD_decompressDCtx (the reference's CPU decode route) over the rank-0 frames."""
+    frames = b.d_out.cpu().numpy()
+    sizes = b.out_sizes.cpu().numpy().astype(np.uint64)
+    r = cpu_run(1, frames, b.n, threads, sizes=sizes, slot=b.slot)
+    if r is None:
+        return None
+    return {"value": round(b.n * CHUNK / r["seconds"] / 1e9, 3), "unit": "GB/s (decompressed bytes)", "cores": threads, "kind": "reference",
+            "sample": f"libzstd {r['version']} ZSTD_decompressDCtx of the {b.n} frames, {threads} threads, median of 5 sweeps"}
+
+
+# ----------------------------------------------------------------------------- profiles
+def _newest(pattern):
+    import glob
+
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", pattern)))
+    return files[-1] if files else None
 
 
 def pmc_traffic(kernel):
     """HBM bytes per launch of `kernel` from the newest committed rocprofv3 PMC summary
     (profiles/*_rocprof_summary.json, written by tools/prof_summary.py: 2 x FETCH_SIZE +
     WRITE_SIZE, the gfx950 correction of the microarchitecture guide)."""
-    import glob
-
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_rocprof_summary.json")))
-    if not files:
+    f = _newest("*_rocprof_summary.json")
+    if not f:
         return None, None
-    k = json.load(open(files[-1])).get("kernels", {}).get(kernel, {})
-    b = k.get("hbm_bytes")
-    return (int(b) if b else None), os.path.relpath(files[-1], ROOT)
+    b = json.load(open(f)).get("kernels", {}).get(kernel, {}).get("hbm_bytes")
+    return (int(b) if b else None), os.path.relpath(f, ROOT)
 
 
+def issue_fraction(kernel):
+    """VALU issue fraction of `kernel` from the newest committed SQ summary
+    (profiles/*_sq_summary.json, tools/sq_summary.py): SQ_INSTS_VALU x 4 cycles over
+    1024 SIMDs x the kernel's cycles (GRBM_GUI_ACTIVE / 8 XCDs)."""
+    f = _newest("*_sq_summary.json")
+    if not f:
+        return None
+    k = json.load(open(f)).get("kernels", {}).get(kernel)
+    if not k:
+        return None
+    return {"valu_issue_frac": k.get("valu_issue_frac"), "salu_per_valu": k.get("salu_per_valu"),
+            "lds_bank_conflict_frac": k.get("lds_bank_conflict_frac"), "valu_insts_per_input_byte": k.get("valu_insts_per_input_byte"),
+            "source": os.path.relpath(f, ROOT)}
+
+
+# ----------------------------------------------------------------------------- main
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--dataset", default="mix", choices=sorted(SEEDS))
-    ap.add_argument("--chunks", type=int, default=CHUNKS_PER_GPU, help="chunks per GPU")
+    ap.add_argument("--chunks", type=int, default=CHUNKS, help="chunks in the batch (per GPU with --weak)")
+    ap.add_argument("--weak", action="store_true", help="weak scaling: every rank compresses --chunks chunks of its own")
+    ap.add_argument("--payload-gather", action="store_true", help="also time an RCCL gather of every rank's frames (N>1)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-verify", action="store_true", help="skip the libzstd decode of every rank-0 frame after timing")
     ap.add_argument("--no-decompress", action="store_true", help="skip the GPU decompression leg")
+    ap.add_argument("--no-legs", action="store_true", help="skip the C3-random and C2 legs (N=1)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -222,29 +346,23 @@ def main():
         dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
 
     import cuda_zstd
-
-    n = args.chunks
     from cuda_zstd import shard
 
-    host = gen_chunks(args.dataset, n, first=shard.weak_range(rank, n)[0])
-    d_in = torch.from_numpy(host).to(dev)
-    bc = cuda_zstd.BatchedCompressor(3, CHUNK)
-    slot = (bc.max_out(CHUNK) + 255) // 256 * 256
-    d_out = torch.empty(n * slot, dtype=torch.uint8, device=dev)
-    ar = torch.arange(n, dtype=torch.int64, device=dev)
-    in_ptrs = d_in.data_ptr() + ar * CHUNK
-    out_ptrs = d_out.data_ptr() + ar * slot
-    in_sizes = torch.full((n,), CHUNK, dtype=torch.int64, device=dev)
-    out_sizes = torch.zeros(n, dtype=torch.int64, device=dev)
-    status = torch.zeros(n, dtype=torch.int32, device=dev)
-    temp = torch.empty(bc.temp_size(n, CHUNK), dtype=torch.uint8, device=dev)
-    stream = torch.cuda.current_stream(dev)
-    from cuda_zstd import shard
+    if args.weak:
+        n_total = args.chunks * world
+        lo, hi = shard.weak_range(rank, args.chunks)
+        plan = shard.ShardPlan(world, n_total)  # equal slices: q = chunks
+    else:
+        n_total = args.chunks
+        plan = shard.ShardPlan(world, n_total)
+        lo, hi = plan.range(rank)
+    host = gen_chunks(args.dataset, hi - lo, first=lo)
+    b = Batch(host, dev)
 
     def step():
-        bc.compress_async(in_ptrs, in_sizes, CHUNK, out_ptrs, out_sizes, status, temp, stream)
+        b.compress()
         # RCCL all-gather of the per-chunk sizes -> global frame offsets (the only exchange)
-        return shard.gather_offsets(out_sizes, world)[1]
+        return plan.gather_offsets(b.out_sizes)
 
     for _ in range(args.warmup):
         step()
@@ -255,7 +373,7 @@ def main():
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        step()
+        all_sizes, offs = step()
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
@@ -263,8 +381,8 @@ def main():
     cuda_zstd.profile_enable(False)
     launches, kms = cuda_zstd.profile_collect()
 
-    assert int((status != 0).sum().item()) == 0, "compression failed on some chunks"
-    comp = int(out_sizes.sum().item())
+    assert int((b.status != 0).sum().item()) == 0, "compression failed on some chunks"
+    comp = int(b.out_sizes.sum().item())
     stats = torch.tensor([el, float(comp), kms[0] / max(launches, 1), kms[1] / max(launches, 1)], dtype=torch.float64, device=dev)
     if world > 1:
         mx = stats.clone()
@@ -275,42 +393,77 @@ def main():
         k1, k2 = mx[2].item(), mx[3].item()
     else:
         comp_all, k1, k2 = float(comp), stats[2].item(), stats[3].item()
+    gathered_total = int(all_sizes.sum().item())  # == sum of every rank's frame bytes
+
+    gather = None
+    if args.payload_gather and world > 1:
+        # frames of every rank into one image: all-gather of the padded slot array (q slots per rank)
+        q = plan.q
+        pad = torch.zeros(q * b.slot, dtype=torch.uint8, device=dev)
+        pad[: b.n * b.slot] = b.d_out[: b.n * b.slot]
+        img = torch.empty(world * q * b.slot, dtype=torch.uint8, device=dev)
+        dist.barrier()
+        torch.cuda.synchronize(dev)
+        g0 = time.perf_counter()
+        dist.all_gather_into_tensor(img, pad)
+        torch.cuda.synchronize(dev)
+        gt = torch.tensor([time.perf_counter() - g0], dtype=torch.float64, device=dev)
+        dist.all_reduce(gt, op=dist.ReduceOp.MAX)
+        gather = {"ms": round(gt.item() * 1e3, 3), "bytes_per_rank": int(q * b.slot),
+                  "how": "RCCL all_gather_into_tensor of the padded frame slots (not part of value)"}
+        del pad, img
 
     verified = None
     if not args.no_verify and rank == 0:
-        verified = libzstd_roundtrip(d_out.cpu().numpy(), out_sizes.cpu().numpy(), slot, host)
+        verified = libzstd_roundtrip(b.d_out.cpu().numpy(), b.out_sizes.cpu().numpy(), b.slot, host)
 
     dec = None
     if not args.no_decompress:
-        dec = decompress_leg(d_in, d_out, out_ptrs, out_sizes, n, dev, min(args.steps, 5), world)
+        dec = decompress_leg(b, min(args.steps, 5), world)
+
+    legs = {}
+    if world == 1 and not args.no_legs and args.dataset == "mix" and args.chunks == CHUNKS:
+        legs["c3_random"] = random_leg(dev, 5)
+        legs["c2_64mib"] = c2_leg(dev, 5)
 
     if rank == 0:
-        total_in = float(world * n * CHUNK)
+        total_in = float(n_total * CHUNK)
         gbs = total_in * args.steps / el / 1e9
         # dominant kernel roofline: algorithmic bytes per launch = sum over its chunks of (input + compressed)
-        per_launch_bytes = n * CHUNK + comp_all / world
+        per_launch_bytes = b.n * CHUNK + comp
         dom, dom_ms = ("zh_lz_kernel", k1) if k1 >= k2 else ("entropy_stage", k2)
         achieved = per_launch_bytes / (dom_ms / 1e3) / 1e9 if dom_ms > 0 else 0.0
-        traffic, traffic_src = pmc_traffic(dom) if args.dataset == "mix" and n == CHUNKS_PER_GPU else (None, None)
+        full = args.dataset == "mix" and b.n == CHUNKS
+        traffic, traffic_src = pmc_traffic(dom) if full else (None, None)
+        issue = issue_fraction(dom) if full else None
         line = {
             "metric": METRIC, "value": round(gbs, 3), "unit": "GB/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
-            "ms_per_step": round(el / args.steps * 1e3, 3), "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+            "ms_per_step": round(el / args.steps * 1e3, 3), "higher_is_better": True, "scaling": "weak" if args.weak else "strong",
+            "vs_baseline": None,
             "dtype": "u8", "data": f"synthetic {args.dataset} corpus (tools/datagen.c, seed {SEEDS[args.dataset]:#x}), device-resident",
-            "config": {"workload": f"C3: {n} x 64 KiB chunks ({n * CHUNK / 2**30:.2f} GiB) per GPU, level 3, independent frames",
-                       "chunk_bytes": CHUNK, "chunks_per_gpu": n, "level": 3, "ratio": round(total_in / comp_all, 4),
+            "config": {"workload": f"C3{'' if world == 1 else '/C4'}: {n_total} x 64 KiB chunks ({total_in / 2**30:.2f} GiB), level 3, independent frames"
+                                   + ("" if world == 1 else f", {'weak: per rank' if args.weak else 'strong: one batch split'} over {world} GPUs"),
+                       "chunk_bytes": CHUNK, "chunks_total": n_total, "chunks_rank0": b.n, "level": 3, "ratio": round(total_in / comp_all, 4),
                        "kernel_ms": {"zh_lz_kernel": round(k1, 3), "entropy_stage": round(k2, 3)},
-                       "parallelism": f"dp{world} (chunk shards, RCCL all-gather of sizes)", "libzstd_verified": verified},
+                       "parallelism": f"dp{world} (contiguous chunk shards, RCCL all-gather of sizes inside the step)",
+                       "libzstd_verified": verified, "gathered_frame_bytes": gathered_total},
             "roofline": {"kernel": dom, "bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
-                         "algorithmic_bytes_per_launch": int(per_launch_bytes), "traffic_source": traffic_src},
+                         "algorithmic_bytes_per_launch": int(per_launch_bytes), "traffic_source": traffic_src,
+                         "limiter": "VALU/SALU instruction issue (not HBM): see issue" if dom == "zh_lz_kernel" else "latency (serial FSE chains)",
+                         "issue": issue},
         }
-        threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
+        if gather:
+            line["payload_gather"] = gather
+        threads = min(len(os.sched_getaffinity(0)), int(os.environ.get("OMP_NUM_THREADS", "0")) or 16)
         if dec is not None:
-            if not args.no_cpu_baseline:
-                dec["cpu_baseline"] = cpu_decompress_baseline(d_out.cpu().numpy(), out_sizes.cpu().numpy(), slot, threads)
+            if not args.no_cpu_baseline and world == 1:
+                dec["cpu_baseline"] = cpu_decompress_baseline(b, threads)
             line["decompress"] = dec
-        if not args.no_cpu_baseline:
-            line["cpu_baseline"] = cpu_baseline(host, threads)
+        if legs:
+            line["legs"] = legs
+        if not args.no_cpu_baseline and world == 1:
+            line["cpu_baseline"] = cpu_baseline(host, threads, gbs)
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()

@@ -35,6 +35,8 @@
 #include <algorithm>
 #include <cstdio>
 #include <cstdlib>
+#include <map>
+#include <memory>
 #include <mutex>
 
 typedef int64_t s64;
@@ -974,7 +976,7 @@ extern "C" __global__ __launch_bounds__(DEC_THREADS) void zh_decode_kernel(ZhDec
     u64 const sumLL = uni64(ho->sumLL), sumML = uni64(ho->sumML), fcs = uni64(ho->fcs), ipc = uni64(ho->ipc);
     u32 st = ST_OK;
     u64 produced = 0;
-    if (uni(ho->sbad) || sumLL > lits.n) {
+    if (uni(ho->sbad) || sumLL > lits.n || lits.n + sumML > BLOCKSIZE_MAX) {
       st = ST_CORRUPT;
     } else if (lits.n + sumML > cap) {
       st = ST_SMALL;
@@ -1209,6 +1211,9 @@ extern "C" __global__ __launch_bounds__(DEC_THREADS) void zh_decode_kernel(ZhDec
         }
         if (sumLL > lits.n) { st = ST_CORRUPT; break; }
         u64 const total = lits.n + sumML;
+        // RFC 8878 §3.1.1.2.4: a block regenerates at most Block_Maximum_Size (128 KiB), which
+        // also keeps execute_block's u32 window arithmetic in range
+        if (total > BLOCKSIZE_MAX) { st = ST_CORRUPT; break; }
         if (total > cap - produced) { st = ST_SMALL; break; }
         __threadfence_block();  // the records (and Huffman literals) are read back below
         __syncthreads();
@@ -1397,26 +1402,44 @@ extern "C" __global__ __launch_bounds__(64) void zh_dec_seq_kernel(ZhDecArgs a, 
 }
 
 namespace {
-// Side streams and events of the pipelined decode (created on first use and kept; a call
-// holds the mutex while it enqueues its groups)
+// Side streams and events of the pipelined decode, one set per device (created on the
+// device of the caller's stream at its first large decode and kept; a call holds the
+// set's mutex while it enqueues its groups)
 struct DecPipe {
   static constexpr u32 G = 4;
   std::mutex mu;
+  int device = -1;
   hipStream_t side[G - 1] = {};
   hipEvent_t start = nullptr, p1[G - 1] = {}, done[G - 1] = {};
   bool ok = true;
-  DecPipe() {
-    ok = hipEventCreateWithFlags(&start, hipEventDisableTiming) == hipSuccess;
+  explicit DecPipe(int dev) : device(dev) {
+    int cur = -1;
+    ok = hipGetDevice(&cur) == hipSuccess && hipSetDevice(dev) == hipSuccess;
+    ok = ok && hipEventCreateWithFlags(&start, hipEventDisableTiming) == hipSuccess;
     for (u32 k = 0; k + 1 < G; k++) {
       ok = ok && hipStreamCreateWithFlags(&side[k], hipStreamNonBlocking) == hipSuccess;
       ok = ok && hipEventCreateWithFlags(&p1[k], hipEventDisableTiming) == hipSuccess;
       ok = ok && hipEventCreateWithFlags(&done[k], hipEventDisableTiming) == hipSuccess;
     }
+    if (cur >= 0) (void)hipSetDevice(cur);
   }
 };
-DecPipe &dec_pipe() {
-  static DecPipe p;
-  return p;
+// The device a stream belongs to (the null stream: the current device)
+int stream_device(hipStream_t s) {
+  int dev = -1;
+  if (s && hipStreamGetDevice(s, &dev) == hipSuccess) return dev;
+  (void)hipGetLastError();
+  if (hipGetDevice(&dev) != hipSuccess) dev = 0;
+  return dev;
+}
+DecPipe *dec_pipe(hipStream_t s) {
+  static std::mutex mu;
+  static std::map<int, std::unique_ptr<DecPipe>> pipes;
+  int const dev = stream_device(s);
+  std::lock_guard<std::mutex> lk(mu);
+  auto &p = pipes[dev];
+  if (!p) p.reset(new DecPipe(dev));
+  return p.get();
 }
 }  // namespace
 
@@ -1451,7 +1474,7 @@ hipError_t launch_decompress(const ZhDecArgs &a0, u32 nitems, hipStream_t stream
   // wave per 64 buffers) overlaps the throughput-bound phase 1 of the next groups and
   // phase 3 of the earlier ones.
   constexpr u32 G = DecPipe::G, MIN_GROUP = 1024;
-  DecPipe *p = (!dbg && nitems >= G * MIN_GROUP) ? &dec_pipe() : nullptr;
+  DecPipe *p = (!dbg && nitems >= G * MIN_GROUP) ? dec_pipe(stream) : nullptr;
   if (!p || !p->ok) {
     group(0, nitems, stream, nullptr);
     return hipGetLastError();

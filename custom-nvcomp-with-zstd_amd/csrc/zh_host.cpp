@@ -608,7 +608,9 @@ Status ZstdBatchManager::compress(const void *in, size_t n, void *out, size_t *o
 Status ZstdBatchManager::decompress(const void *in, size_t n, void *out, size_t *out_size, void *temp, size_t temp_size, hipStream_t stream) {
   std::lock_guard<std::mutex> lock(pimpl_->api_mutex);
   if (!in || !out || !out_size || !temp || n < 4) return Status::ERROR_INVALID_PARAMETER;
-  if (temp_size < get_decompress_temp_size(n)) return Status::ERROR_BUFFER_TOO_SMALL;
+  // the slot the decode actually uses: sized by the output capacity, so a workspace from
+  // allocate_inference_workspace(max_out) is enough (reference tests/test_inference_api.cu:398-410)
+  if (temp_size < DecLayout::make(1, *out_size).total) return Status::ERROR_BUFFER_TOO_SMALL;
   if (!is_device_ptr(in) || !is_device_ptr(out)) return Status::ERROR_INVALID_PARAMETER;  // device-resident API
   auto t0 = std::chrono::steady_clock::now();
   size_t got = 0;
@@ -749,7 +751,7 @@ Status ZstdBatchManager::decompress_async_no_sync(const void *in, size_t n, void
                                                   hipStream_t stream) {
   std::lock_guard<std::mutex> lock(pimpl_->api_mutex);
   if (!in || !out || !d_actual || !temp || n < 4) return Status::ERROR_INVALID_PARAMETER;
-  if (temp_size < get_decompress_temp_size(n)) return Status::ERROR_BUFFER_TOO_SMALL;
+  if (temp_size < DecLayout::make(1, cap).total) return Status::ERROR_BUFFER_TOO_SMALL;
   return pimpl_->run_decompress_one(in, n, out, cap, nullptr, d_actual, temp, temp_size, stream);
 }
 size_t ZstdBatchManager::get_inference_workspace_size(size_t, size_t max_out) const { return DecLayout::make(1, max_out).total; }

@@ -1,0 +1,122 @@
+"""The reference's own call shapes on the drop-in boundary (§8f F1
+inference API), on the GPU:
+
+* NvcompV5BatchManager::compress_async with device pointer arrays, host input sizes and a
+  device size array (reference tests/test_nvcomp_batch.cu:132-134), then decompress_async
+  with device arrays -- through the C++ API (tests/cpp/boundary.cpp);
+* CompressionConfig::cpu_threshold routing (reference src/cuda_zstd_manager.cu:1604-1668):
+  a 64 KiB device item below a 1 MiB threshold takes the libzstd route, a 2 MiB one the GPU;
+* the single-buffer C entry nvcomp_zstd_compress_async_v5 / nvcomp_zstd_decompress_async_v5;
+* the inference flow (allocate_inference_workspace + decompress_to_preallocated, reference
+  tests/test_inference_api.cu:398-410) with outputs below 128 KiB.
+GPU frames must equal the oracle's; every frame must decode with libzstd."""
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+import zh_testlib as T
+
+pytestmark = pytest.mark.gpu
+DRIVER = os.path.join(T.ROOT, "tests", "cpp", "boundary")
+
+
+def _chunks():
+    sizes = [65536, 65536, 40001, 1000, 65536, 12345, 9]
+    return [T.gen(k, 1, 900 + i, s) for i, (k, s) in enumerate(zip([T.DG_MIX, T.DG_TEXT, T.DG_JSON, T.DG_EXE, T.DG_RANDOM, T.DG_CSV, T.DG_MIX], sizes))]
+
+
+def _run(mode, datas, tmp_path, *extra):
+    assert os.path.exists(DRIVER), "tests/cpp/boundary not built (__graft_entry__.build())"
+    (tmp_path / "in.bin").write_bytes(b"".join(d.tobytes() for d in datas))
+    (tmp_path / "sizes.bin").write_bytes(np.array([len(d) for d in datas], np.uint64).tobytes())
+    r = subprocess.run([DRIVER, mode, str(tmp_path), *extra], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, f"boundary {mode}: rc {r.returncode}\n{r.stdout}\n{r.stderr}"
+    fs = np.frombuffer((tmp_path / "fsizes.bin").read_bytes(), np.uint64)
+    blob = (tmp_path / "frames.bin").read_bytes()
+    offs = np.concatenate([[0], np.cumsum(fs)]).astype(np.int64)
+    return [blob[offs[i]:offs[i + 1]] for i in range(len(fs))]
+
+
+def test_nvcomp_batch_device_arrays(tmp_path, libzstd):
+    datas = _chunks()
+    frames = _run("nvcomp", datas, tmp_path)
+    for k, (f, d) in enumerate(zip(frames, datas)):
+        assert f == T.oracle_frame(d), f"item {k}"
+        assert T.zstd_decompress(f, len(d)) == d.tobytes()
+    assert (tmp_path / "back.bin").read_bytes() == b"".join(d.tobytes() for d in datas)
+
+
+def test_cpu_threshold_routing(tmp_path, libzstd):
+    small = T.gen(T.DG_MIX, 1, 0x5EED0003, 65536)
+    big = T.gen(T.DG_MIX, 32, 0x5EED0003, 65536)  # 2 MiB: at/above the threshold -> GPU
+    frames = _run("threshold", [small, big], tmp_path, str(1 << 20))
+    # below the threshold: libzstd's own frame (the reference's CPU route), not the GPU's
+    assert frames[0] != T.oracle_frame(small)
+    cands = set()
+    for p in ("/opt/conda/lib/libzstd.so.1", "libzstd.so.1", "/usr/lib/x86_64-linux-gnu/libzstd.so.1"):
+        try:
+            L = ctypes.CDLL(p)
+        except OSError:
+            continue
+        L.ZSTD_compress.restype = ctypes.c_size_t
+        L.ZSTD_compress.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int]
+        out = np.zeros(70000, np.uint8)
+        r = L.ZSTD_compress(out.ctypes.data, 70000, small.ctypes.data, len(small), 3)
+        cands.add(out[:r].tobytes())
+    assert frames[0] in cands, "CPU-routed frame is not libzstd ZSTD_compress(level 3)"
+    assert T.zstd_decompress(frames[0], len(small)) == small.tobytes()
+    assert frames[1] == T.oracle_frame(big)
+    assert T.zstd_decompress(frames[1], len(big)) == big.tobytes()
+    # threshold 0 (the default): the 64 KiB item goes to the GPU
+    frames0 = _run("threshold", [small], tmp_path, "0")
+    assert frames0[0] == T.oracle_frame(small)
+
+
+def test_inference_workspace(tmp_path, libzstd):
+    datas = [T.gen(T.DG_TEXT, 1, 77, 65536), T.gen(T.DG_JSON, 1, 78, 5000), T.gen(T.DG_MIX, 1, 79, 65536 * 3 + 17)]
+    frames = _run("inference", datas, tmp_path)
+    for f, d in zip(frames, datas):
+        assert f == T.oracle_frame(d)
+    assert (tmp_path / "back.bin").read_bytes() == b"".join(d.tobytes() for d in datas)
+
+
+def test_nvcomp_single_buffer_c_api(libzstd):
+    import torch
+
+    import cuda_zstd
+
+    L = cuda_zstd.lib()
+    vp, sz = ctypes.c_void_p, ctypes.c_size_t
+    L.nvcomp_zstd_create_manager_v5.restype = vp
+    L.nvcomp_zstd_create_manager_v5.argtypes = [ctypes.c_int]
+    L.nvcomp_zstd_destroy_manager_v5.argtypes = [vp]
+    L.nvcomp_zstd_get_compress_temp_size_v5.restype = sz
+    L.nvcomp_zstd_get_compress_temp_size_v5.argtypes = [vp, sz]
+    L.nvcomp_zstd_get_decompress_temp_size_v5.restype = sz
+    L.nvcomp_zstd_get_decompress_temp_size_v5.argtypes = [vp, sz]
+    L.nvcomp_zstd_compress_async_v5.argtypes = [vp, vp, sz, vp, ctypes.POINTER(sz), vp, sz, vp]
+    L.nvcomp_zstd_decompress_async_v5.argtypes = [vp, vp, sz, vp, ctypes.POINTER(sz), vp, sz, vp]
+    h = L.nvcomp_zstd_create_manager_v5(3)
+    assert h
+    try:
+        for n in (65536, 1 << 20, 777):
+            d = T.gen(T.DG_MIX, 1, 4242, n)
+            din = torch.from_numpy(d).cuda()
+            out = torch.empty(cuda_zstd.max_compressed_size(n), dtype=torch.uint8, device="cuda")
+            tmp = torch.empty(L.nvcomp_zstd_get_compress_temp_size_v5(h, n), dtype=torch.uint8, device="cuda")
+            cs = sz(out.numel())
+            s = torch.cuda.current_stream().cuda_stream
+            assert L.nvcomp_zstd_compress_async_v5(h, din.data_ptr(), n, out.data_ptr(), ctypes.byref(cs), tmp.data_ptr(), tmp.numel(), s) == 0
+            frame = out[: cs.value].cpu().numpy().tobytes()  # output valid on return (reference semantics)
+            assert frame == T.oracle_frame(d)
+            assert T.zstd_decompress(frame, n) == d.tobytes()
+            back = torch.empty(n, dtype=torch.uint8, device="cuda")
+            dt = torch.empty(L.nvcomp_zstd_get_decompress_temp_size_v5(h, cs.value), dtype=torch.uint8, device="cuda")
+            us = sz(n)
+            assert L.nvcomp_zstd_decompress_async_v5(h, out.data_ptr(), cs.value, back.data_ptr(), ctypes.byref(us), dt.data_ptr(), dt.numel(), s) == 0
+            assert us.value == n and torch.equal(back, din)
+    finally:
+        L.nvcomp_zstd_destroy_manager_v5(h)

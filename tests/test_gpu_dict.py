@@ -118,3 +118,31 @@ def test_reference_dictionary_scenario(torch_cuda):
     withd = m.compress(_dev(torch_cuda, data)).cpu().numpy().tobytes()
     assert T.zstd_decompress(withd, len(data), dictionary=dd.content()) == data.tobytes()
     assert m.decompress(_dev(torch_cuda, withd), len(data)).cpu().numpy().tobytes() == data.tobytes()
+
+
+def test_c5_level9_cover_64k(torch_cuda, libzstd):
+    """Config C5 at test size: level 9, a 64 KiB COVER dictionary trained by
+    cuda_zstd_train_dictionary on 256 JSON-like records of 16 KiB (seed 0x5EED0005); 256 other
+    records compressed in one batch.  GPU frames == the oracle's, libzstd decodes them with
+    the dictionary, and the ratio gains over no dictionary."""
+    import cuda_zstd
+
+    recs = T.gen(T.DG_JSON, 512, 0x5EED0005, 16384)
+    train = [recs[i * 16384:(i + 1) * 16384] for i in range(0, 512, 2)]
+    test = [recs[i * 16384:(i + 1) * 16384] for i in range(1, 512, 2)]
+    d = cuda_zstd.Dictionary.train(train, 65536)
+    content = d.content()
+    assert len(content) == 65536
+    m = cuda_zstd.Manager(9)
+    plain = m.compress_batch([torch_cuda.from_numpy(r.copy()).cuda() for r in test])
+    m.set_dictionary(d)
+    outs = m.compress_batch([torch_cuda.from_numpy(r.copy()).cuda() for r in test])
+    total = sum(len(r) for r in test)
+    for k, (o, r) in enumerate(zip(outs, test)):
+        f = o.cpu().numpy().tobytes()
+        assert f == T.oracle_frame(r, dictionary=content, level=9), k
+        assert T.zstd_decompress(f, len(r), dictionary=content) == r.tobytes(), k
+    ratio = total / sum(o.numel() for o in outs)
+    ratio0 = total / sum(o.numel() for o in plain)
+    print(f"C5 (256 x 16 KiB, level 9): ratio {ratio0:.3f} without -> {ratio:.3f} with the 64 KiB COVER dictionary")
+    assert ratio > 1.15 * ratio0

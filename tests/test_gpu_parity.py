@@ -228,3 +228,19 @@ def test_checksum_frames(torch_cuda):
     for x, o, s in zip(items, outs2, osz):
         f = o[:s].cpu().numpy().tobytes()
         assert f == T.oracle_frame(x, checksum=True)
+
+
+def test_reference_ratio_floors_on_gpu(torch_cuda, mgr):
+    """The reference's ratio floors for 64 KiB inputs (tests/test_compressible_data.cu:272,
+    311, 325, 363: JSON > 1.3, period-8 > 1.5, zeros > 10, 0xFF > 500) on GPU frames."""
+    import json
+    import os
+
+    floors = json.load(open(os.path.join(T.GOLDEN, "reference_vectors.json")))["ratio_floors_64k"]
+    s = T.special_inputs()
+    cases = {"json": T.gen(T.DG_JSON, 1, 3, 65536), "period8": s["period8_64k"], "zeros": s["zeros_64k"], "ff": s["ff_64k"]}
+    names = sorted(cases)
+    outs = mgr.compress_batch([torch_cuda.from_numpy(cases[k].copy()).cuda() for k in names])
+    _check(outs, [cases[k] for k in names])
+    for k, o in zip(names, outs):
+        assert 65536 / o.numel() > floors[k], (k, 65536 / o.numel(), floors[k])

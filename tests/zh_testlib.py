@@ -86,7 +86,7 @@ def gen(kind, nchunks, seed, chunk_size=65536, first=0):
     return a
 
 
-def oracle_frame(data, block_size=128 * 1024, window_log=19, checksum=False, dictionary=None):
+def oracle_frame(data, block_size=128 * 1024, window_log=19, checksum=False, dictionary=None, level=3):
     data = np.ascontiguousarray(np.frombuffer(bytes(data), np.uint8) if not isinstance(data, np.ndarray) else data)
     cap = int(oracle().orc_max_compressed_size(ctypes.c_uint64(len(data)))) + 64
     out = np.zeros(cap, np.uint8)
