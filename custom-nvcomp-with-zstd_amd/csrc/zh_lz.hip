@@ -9,16 +9,18 @@
 // One workgroup of 1024 threads (16 wave64, one workgroup per CU) per block,
 // everything in LDS:
 //   in[]   the block, staged once with 16-B loads (64 KiB)
-//   TL/TS  2 x 2^13 u32 hash tables, entry = (position+1) << 16 | content tag
+//   TL/TS  2 x 2^14 u16 hash tables, entry = position + 1 (0 = empty)
 //   cinfo  one 4096-position window: candidates -> match info (off<<8|len) in place
 //   exb    per-position exits of the 64-position parse segments
 // Wave roles (wave specialisation, all synchronised with workgroup barriers):
 //   waves 14, 15  inserters: one wave per hash table walks the next window's
-//                 tiles of 256 positions (4 per lane).  A single wave needs no
-//                 barrier between a tile's lookups and its inserts because LDS
-//                 executes one wave's operations in order.  Candidates are held
-//                 in registers and dumped into cinfo at the window switch, so
-//                 the next window's insertion overlaps this window's lengths.
+//                 tiles of ZH_TILE positions.  A single wave needs no barrier
+//                 between a tile's lookups and its inserts because LDS executes
+//                 one wave's operations in order; lanes of one store that hit the
+//                 same slot are resolved to the latest position by a read-back.
+//                 Candidates are held in registers and dumped into cinfo at the
+//                 window switch, so the next window's insertion overlaps this
+//                 window's lengths.
 //   waves 0..13   match lengths of the window, 5 positions per thread, with
 //                 same-offset chains resolved in registers.
 //   waves 0..13   the serial greedy/lazy-1 parse, lanes = positions: pointer
@@ -37,15 +39,17 @@ constexpr u32 SB = 5;                       // positions per thread in the lengt
 constexpr u32 NB = (ZH_WINDOW + SB - 1) / SB;  // length-phase threads (thread NB takes position `we`)
 constexpr u32 TILES = ZH_WINDOW / ZH_TILE;  // 16 tiles per window
 constexpr u32 TPL = ZH_TILE / 64;           // positions per inserter lane per tile
+constexpr u32 NCR = TILES * TPL / 2;        // candidate registers per inserter lane (u16 pairs)
 static_assert(NPSEG == 64 && NB + 1 <= INS_TID, "thread roles");
-static_assert(ZH_WINDOW % ZH_TILE == 0 && TPL == 4, "tiles tile windows");
+static_assert(ZH_WINDOW % ZH_TILE == 0 && ZH_TILE % 64 == 0 && TILES * TPL % 2 == 0, "tiles tile windows");
 
 constexpr u32 HL_SIZE = 1u << ZH_HASH_LOG_LONG;
 constexpr u32 HS_SIZE = 1u << ZH_HASH_LOG_SHORT;
+constexpr u32 T_PAD = 8;                    // + a junk slot (index HL/HS_SIZE) for lanes past lim
 constexpr u32 OFF_IN = 0;
 constexpr u32 OFF_TL = OFF_IN + ZH_BLOCK_MAX + 16;
-constexpr u32 OFF_TS = OFF_TL + 4 * HL_SIZE;
-constexpr u32 OFF_CI = OFF_TS + 4 * HS_SIZE;
+constexpr u32 OFF_TS = OFF_TL + 2 * (HL_SIZE + T_PAD);
+constexpr u32 OFF_CI = OFF_TS + 2 * (HS_SIZE + T_PAD);
 constexpr u32 CI_WORDS = ZH_WINDOW + 8;  // + the lookahead slot of position `we`
 __device__ __forceinline__ u32 cidx(u32 i) { return i; }
 constexpr u32 OFF_EXB = OFF_CI + 4 * CI_WORDS;      // u8 per position: its parse segment exit (relative)
@@ -120,27 +124,37 @@ __device__ __forceinline__ u32 ext_head(const u32 *in32, u32 p, u32 q, u32 n) {
   return min(l, n - p);
 }
 
-// Table entries: (position+1) << 16 | 16-bit content tag.  ds_max keeps the latest
-// position (the tag only rides along); a tag mismatch proves the common prefix is
-// below the table's minimum match, so the candidate is dropped without touching
-// the input (same result as the oracle, fewer LDS reads).
-__device__ __forceinline__ u32 tag_long(u32 lo, u32 hi) { (void)lo; return hi >> 16; }               // bytes 6..7
-__device__ __forceinline__ u32 tag_short(u32 lo, u32 hi) { return (lo >> 24) | ((hi & 0xFFu) << 8); }  // bytes 3..4
-
 template <bool LONG>
-__device__ __forceinline__ void hash_tag(u32 lo, u32 hi, u32 &h, u32 &tag) {
+__device__ __forceinline__ u32 hash_of(u32 lo, u32 hi) {
   u64 const v = ((u64)hi << 32) | lo;
-  if (LONG) { h = hash_long(v); tag = tag_long(lo, hi); }
-  else { h = hash_short(v); tag = tag_short(lo, hi); }
+  return LONG ? hash_long(v) : hash_short(v);
 }
 
-// Inserter wave: the 16 tiles of window [wsb, we) against one table.  Lane l handles
-// positions tb + l + 64k of each tile; all lookups of a tile are issued before its
-// inserts and after the previous tile's inserts (program order = LDS order within a
-// wave).  Candidates (position+1, tag-filtered, 0 = none) go to creg as u16 pairs.
+// Inserter wave: the tiles of window [wsb, we) against one table (u16 entries = position
+// + 1).  Lane l handles positions tb + l + 64k of each tile; all lookups of a tile are
+// issued before its stores and after the previous tile's stores (program order = LDS
+// order within a wave).  Stores of later k carry later positions and land later; lanes
+// of ONE store that hit the same slot leave one of their values, so every lane reads its
+// slot back and lanes that find an earlier position rewrite theirs until none does: the
+// slot ends with the latest position, as in the oracle's serial loop.  Candidates
+// (position + 1, 0 = none) go to creg as u16 pairs.
 template <bool LONG, typename Hook>
-__device__ __forceinline__ void insert_window(const u32 *in32, u32 *T, u32 wsb, u32 we, u32 lim, u32 lane, u32 (&creg)[TILES * TPL / 2], u32 &cwe,
-                                              Hook &&between_tiles) {
+__device__ __forceinline__ void insert_window(const u32 *in32, u16 *T, u32 wsb, u32 we, u32 lim, u32 lane, u32 (&creg)[NCR], u32 &cwe,
+                                              const u32 *arrivals, Hook &&between_tiles) {
+  constexpr u32 JUNK = LONG ? HL_SIZE : HS_SIZE;
+  // Software pipeline: the input dwords of tile t+1 and the workers' arrival counter are
+  // read together with tile t's table read-back, so a tile costs one LDS round trip.
+  u32 wv[TPL][3];
+  auto load_in = [&](u32 tb, u32 lim_t, u32 (&w)[TPL][3]) {
+#pragma unroll
+    for (u32 k = 0; k < TPL; k++) {
+      u32 const q = min(tb + 64 * k + lane, lim_t) >> 2;
+      w[k][0] = in32[q];
+      w[k][1] = in32[q + 1];
+      w[k][2] = in32[q + 2];
+    }
+  };
+  load_in(wsb, lim, wv);
 #pragma unroll
   for (u32 t = 0; t < TILES; t++) {
     // opaque per-tile copy of lim: keeps the compiler from hoisting every tile's
@@ -148,49 +162,61 @@ __device__ __forceinline__ void insert_window(const u32 *in32, u32 *T, u32 wsb, 
     u32 lim_t;
     __asm__ volatile("v_mov_b32 %0, %1" : "=v"(lim_t) : "v"(lim));
     u32 const tb = wsb + t * ZH_TILE;
-    u32 h[TPL], tg[TPL], e[TPL];
+    u32 h[TPL], e[TPL];
 #pragma unroll
     for (u32 k = 0; k < TPL; k++) {
-      u32 const p = tb + 64 * k + lane;
-      u32 lo, hi;
-      ld64u(in32, min(p, lim_t), lo, hi);
-      hash_tag<LONG>(lo, hi, h[k], tg[k]);
-      e[k] = T[h[k]];
+      u32 const p = tb + 64 * k + lane, sh = min(p, lim_t) & 3u;
+      u32 const lo = __builtin_amdgcn_alignbyte(wv[k][1], wv[k][0], sh), hi = __builtin_amdgcn_alignbyte(wv[k][2], wv[k][1], sh);
+      u32 const hh = hash_of<LONG>(lo, hi);
+      e[k] = T[hh];
+      h[k] = p < lim_t ? hh : JUNK;
     }
 #pragma unroll
-    for (u32 k = 0; k < TPL; k++) {
-      u32 const p = tb + 64 * k + lane;
-      atomicMax(&T[h[k]], p < lim_t ? (((p + 1) << 16) | tg[k]) : 0u);  // max with 0: no-op
-    }
-    u32 c[TPL];
+    for (u32 k = 0; k < TPL; k++) T[h[k]] = (u16)(tb + 64 * k + lane + 1);
+    u32 r[TPL];
 #pragma unroll
-    for (u32 k = 0; k < TPL; k++) {
-      u32 const p = tb + 64 * k + lane;
-      c[k] = (p < lim_t && e[k] && (e[k] & 0xFFFFu) == tg[k]) ? (e[k] >> 16) : 0u;
+    for (u32 k = 0; k < TPL; k++) r[k] = T[h[k]];
+    if (t + 1 < TILES) load_in(tb + ZH_TILE, lim_t, wv);
+    u32 const arr = __atomic_load_n(arrivals, __ATOMIC_RELAXED);
+    for (;;) {  // (branch-free body: losers rewrite, everyone else writes the junk slot)
+      bool need = false;
+      u32 w[TPL];
+#pragma unroll
+      for (u32 k = 0; k < TPL; k++) {
+        bool const nk = h[k] != JUNK && r[k] < tb + 64 * k + lane + 1;
+        w[k] = nk ? h[k] : JUNK;
+        need |= nk;
+      }
+      if (!__ballot(need)) break;
+#pragma unroll
+      for (u32 k = 0; k < TPL; k++) T[w[k]] = (u16)(tb + 64 * k + lane + 1);
+#pragma unroll
+      for (u32 k = 0; k < TPL; k++) r[k] = T[h[k]];
     }
-    creg[2 * t] = c[0] | (c[1] << 16);
-    creg[2 * t + 1] = c[2] | (c[3] << 16);
-    // materialise this tile's candidates now (otherwise the compiler sinks their
-    // computation to the dump and keeps every tile's temporaries alive)
-    __asm__ volatile("" : "+v"(creg[2 * t]), "+v"(creg[2 * t + 1]) :: "memory");
-    between_tiles();
+#pragma unroll
+    for (u32 k = 0; k < TPL; k += 2) {
+      u32 const c0 = h[k] != JUNK ? e[k] : 0u, c1 = h[k + 1] != JUNK ? e[k + 1] : 0u;
+      creg[(t * TPL + k) / 2] = c0 | (c1 << 16);
+      // materialise this tile's candidates now (otherwise the compiler sinks their
+      // computation to the dump and keeps every tile's temporaries alive)
+      __asm__ volatile("" : "+v"(creg[(t * TPL + k) / 2]) :: "memory");
+    }
+    between_tiles(arr);
   }
   // the next window's first position (lazy rule at this window's end): looked up
   // after all of this window's tiles, before any of the next window's
   cwe = 0;
   if (lane == 0 && we < lim) {
-    u32 lo, hi, hh, tt;
+    u32 lo, hi;
     ld64u(in32, we, lo, hi);
-    hash_tag<LONG>(lo, hi, hh, tt);
-    u32 const ee = T[hh];
-    cwe = (ee && (ee & 0xFFFFu) == tt) ? (ee >> 16) : 0u;
+    cwe = T[hash_of<LONG>(lo, hi)];
   }
   __asm__ volatile("" ::: "memory");
 }
 
 // Dump an inserter's candidates into its half of the cinfo words (LONG: low half).
 template <bool LONG>
-__device__ __forceinline__ void dump_window(u8 *ci8, u32 lane_, const u32 (&creg)[TILES * TPL / 2], u32 cwe) {
+__device__ __forceinline__ void dump_window(u8 *ci8, u32 lane_, const u32 (&creg)[NCR], u32 cwe) {
   // opaque lane copy: stops the 64 addresses from being hoisted out of the window loop
   u32 lane;
   __asm__ volatile("v_mov_b32 %0, %1" : "=v"(lane) : "v"(lane_));
@@ -198,8 +224,8 @@ __device__ __forceinline__ void dump_window(u8 *ci8, u32 lane_, const u32 (&creg
   for (u32 t = 0; t < TILES; t++) {
 #pragma unroll
     for (u32 k = 0; k < TPL; k++) {
-      u32 const i = t * ZH_TILE + 64 * k + lane;
-      u16 const v = (u16)(creg[2 * t + (k >> 1)] >> (16 * (k & 1)));
+      u32 const i = t * ZH_TILE + 64 * k + lane, j = t * TPL + k;
+      u16 const v = (u16)(creg[j / 2] >> (16 * (j & 1)));
       *(u16 *)(ci8 + 4 * cidx(i) + (LONG ? 0 : 2)) = v;
     }
   }
@@ -248,10 +274,10 @@ __device__ __forceinline__ u32 parse_steps(const u32 *ci, u32 i, u32 wn, u32 la,
 // so the next window's insertion spreads over the whole window step.
 constexpr u32 WIN_BARRIERS = 5;  // R, X, J, E1, E2
 template <bool LONG>
-__device__ __forceinline__ void inserter_loop(const u32 *in32, u32 *T, u8 *ci8, u32 *misc_, u32 n, u32 lim, u32 lane, u32 *dbg) {
-  u32 creg[TILES * TPL / 2];
+__device__ __forceinline__ void inserter_loop(const u32 *in32, u16 *T, u8 *ci8, u32 *misc_, u32 n, u32 lim, u32 lane, u32 *dbg) {
+  u32 creg[NCR];
   u32 cwe = 0;
-  insert_window<LONG>(in32, T, 0, min((u32)ZH_WINDOW, n), lim, lane, creg, cwe, [] {});
+  insert_window<LONG>(in32, T, 0, min((u32)ZH_WINDOW, n), lim, lane, creg, cwe, &misc_[MISC_ARR], [](u32) {});
 #ifdef ZH_STAMPS
   u32 st_ins = 0;
 #endif
@@ -261,16 +287,19 @@ __device__ __forceinline__ void inserter_loop(const u32 *in32, u32 *T, u8 *ci8, 
     dump_window<LONG>(ci8, lane, creg, cwe);
     __syncthreads();  // P: candidates of this window in cinfo
     u32 const done = passed + WIN_BARRIERS;
-    auto take_ready = [&] {
-      while (passed < done && __atomic_load_n(&misc_[MISC_ARR], __ATOMIC_RELAXED) >= (INS_TID / 64) * (passed + 1)) {
+    // arr: the arrival counter as read with the last tile's read-back; a barrier taken
+    // here means the counter is re-read for the next one
+    auto take_ready = [&](u32 arr) {
+      while (passed < done && arr >= (INS_TID / 64) * (passed + 1)) {
         __syncthreads();
         passed++;
+        arr = __atomic_load_n(&misc_[MISC_ARR], __ATOMIC_RELAXED);
       }
     };
 #ifdef ZH_STAMPS
     u64 const ti0 = __builtin_amdgcn_s_memtime();
 #endif
-    if (we < n) insert_window<LONG>(in32, T, we, min(we + ZH_WINDOW, n), lim, lane, creg, cwe, take_ready);
+    if (we < n) insert_window<LONG>(in32, T, we, min(we + ZH_WINDOW, n), lim, lane, creg, cwe, &misc_[MISC_ARR], take_ready);
 #ifdef ZH_STAMPS
     u32 const dti = (u32)(__builtin_amdgcn_s_memtime() - ti0);
     st_ins += dti;
@@ -302,7 +331,7 @@ extern "C" __global__ __launch_bounds__(K1_THREADS) void zh_lz_kernel(const ZhBl
   extern __shared__ __attribute__((aligned(16))) u8 smem[];
   u8 *in = smem + OFF_IN;
   u32 *in32 = (u32 *)in;
-  u32 *TL = (u32 *)(smem + OFF_TL), *TS = (u32 *)(smem + OFF_TS);
+  u16 *TL = (u16 *)(smem + OFF_TL), *TS = (u16 *)(smem + OFF_TS);
   u32 *ci = (u32 *)(smem + OFF_CI);
   u8 *ci8 = smem + OFF_CI;
   u8 *exb = smem + OFF_EXB;
@@ -353,8 +382,7 @@ extern "C" __global__ __launch_bounds__(K1_THREADS) void zh_lz_kernel(const ZhBl
     for (u32 i = tid; i < n; i += K1_THREADS) { u8 c = src[i]; in[i] = c; same &= c == first; }
   }
   if (tid < 16) in[n + tid] = 0;
-  for (u32 i = tid; i < HL_SIZE; i += K1_THREADS) TL[i] = 0;
-  for (u32 i = tid; i < HS_SIZE; i += K1_THREADS) TS[i] = 0;
+  for (u32 i = tid; i < (HL_SIZE + HS_SIZE + 2 * T_PAD) / 2; i += K1_THREADS) ((u32 *)TL)[i] = 0;  // both tables (adjacent)
   if (tid < 2) misc[8 + tid] = 0;
   if (tid == 0) misc[MISC_ARR] = 0;
   bool const rle = __syncthreads_and(same) && d.n >= 2;
@@ -371,6 +399,11 @@ extern "C" __global__ __launch_bounds__(K1_THREADS) void zh_lz_kernel(const ZhBl
   // ---- inserter waves: their own loop with the same barrier sequence as the workers'
   // (separate code, so their registers never add to the workers' pressure)
   if (tid >= INS_TID) {
+    // The inserters are the youngest waves of the workgroup and would lose every VALU
+    // issue arbitration to the 3 worker waves sharing their SIMD; the next window's tables
+    // gate the workers' next window, so they take priority (MI355X_MICROARCH.md, "VALU issue
+    // is arbitrated ... by priority, then age").
+    __builtin_amdgcn_s_setprio(2);
     if (tid < INS_TID + 64) inserter_loop<true>(in32, TL, ci8, misc, n, lim, lane, ws.dbg(b));
     else inserter_loop<false>(in32, TS, ci8, misc, n, lim, lane, ws.dbg(b));
     return;

@@ -69,36 +69,49 @@ extern "C" __global__ void zh_plan_kernel(const void *const *__restrict__ in_ptr
   }
 }
 
-// one workgroup per item; only items with more than one block do work
+// One workgroup per block: a block of a multi-block frame sums the staged sizes of its
+// frame's blocks (its output offset and the frame's total), the frame's first block sets the
+// item's size and status, and every block copies its own staged bytes (a 64 MiB frame is
+// 1024 workgroups, not one).
 extern "C" __global__ __launch_bounds__(256) void zh_gather_kernel(const ZhItemDesc *__restrict__ items, const ZhBlockDesc *__restrict__ descs,
                                                                     const u32 *__restrict__ blk_size, u64 *item_size, u32 *item_status) {
-  ZhItemDesc const id = items[blockIdx.x];
+  u32 const b = blockIdx.x, tid = threadIdx.x;
+  ZhBlockDesc const d = descs[b];
+  if (d.n == 0) return;
+  ZhItemDesc const id = items[d.item];
   if (id.nblocks <= 1) return;
-  __shared__ u64 total_s;
-  __shared__ u32 bad_s;
-  if (threadIdx.x == 0) {
-    u64 t = 0;
-    u32 bad = 0;
-    for (u32 k = 0; k < id.nblocks; k++) {
-      u32 const s = blk_size[id.first_block + k];
-      if (s == 0xFFFFFFFFu) bad = 1; else t += s;
-    }
-    total_s = t;
-    bad_s = bad || t > id.cap;
-    item_size[blockIdx.x] = t;
-    item_status[blockIdx.x] = (bad || t > id.cap) ? ZH_ST_TOO_SMALL : ZH_ST_OK;
+  u32 const k = b - id.first_block;
+  __shared__ u64 part[2][4];
+  __shared__ u32 badp[4];
+  u64 pre = 0, tot = 0;
+  u32 bad = 0;
+  for (u32 j = tid; j < id.nblocks; j += 256) {
+    u32 const s = blk_size[id.first_block + j];
+    bad |= s == 0xFFFFFFFFu;
+    u64 const v = s == 0xFFFFFFFFu ? 0u : s;
+    tot += v;
+    pre += j < k ? v : 0u;
   }
+  for (u32 o = 32; o; o >>= 1) {
+    pre += __shfl_down(pre, o, 64);
+    tot += __shfl_down(tot, o, 64);
+    bad |= __shfl_down(bad, o, 64);
+  }
+  if ((tid & 63) == 0) { part[0][tid >> 6] = pre; part[1][tid >> 6] = tot; badp[tid >> 6] = bad; }
   __syncthreads();
-  if (bad_s) return;
-  u64 off = 0;
-  for (u32 k = 0; k < id.nblocks; k++) {
-    u32 const s = blk_size[id.first_block + k];
-    const u8 *src = descs[id.first_block + k].dst;
-    u8 *dst = id.dst + off;
-    for (u32 i = threadIdx.x; i < s; i += blockDim.x) dst[i] = src[i];
-    off += s;
+  pre = part[0][0] + part[0][1] + part[0][2] + part[0][3];
+  tot = part[1][0] + part[1][1] + part[1][2] + part[1][3];
+  bad = badp[0] | badp[1] | badp[2] | badp[3];
+  bool const fail = bad || tot > id.cap;
+  if (k == 0 && tid == 0) {
+    item_size[d.item] = tot;
+    item_status[d.item] = fail ? ZH_ST_TOO_SMALL : ZH_ST_OK;
   }
-  (void)total_s;
+  if (fail) return;
+  u32 const s = blk_size[b];
+  const u8 *src = d.dst;
+  u8 *dst = id.dst + pre;
+  for (u32 i = tid; i < s; i += 256) dst[i] = src[i];
 }
 
 // Content checksum (reference src/cuda_zstd_manager.cu:3037-3056): one wave per
@@ -192,7 +205,7 @@ hipError_t launch_compress(const ZhBlockDesc *d_descs, u32 nblocks, ZhWorkspace 
   if (!ev.empty()) (void)hipEventRecord(ev[1], stream);
   entropy_launch(d_descs, nblocks, ws, window_log, cfg_block_size, d_item_size, d_item_status, d_blk_size, stream);
   if (!ev.empty()) (void)hipEventRecord(ev[2], stream);
-  if (gather && nitems) hipLaunchKernelGGL(zh_gather_kernel, dim3(nitems), dim3(256), 0, stream, d_items, d_descs, d_blk_size, d_item_size, d_item_status);
+  if (gather && nitems) hipLaunchKernelGGL(zh_gather_kernel, dim3(nblocks), dim3(256), 0, stream, d_items, d_descs, d_blk_size, d_item_size, d_item_status);
   if (checksum && nitems) hipLaunchKernelGGL(zh_checksum_kernel, dim3(nitems), dim3(64), 0, stream, d_items, d_descs, d_item_size, d_item_status);
   if (!ev.empty()) {
     (void)hipEventRecord(ev[3], stream);

@@ -13,11 +13,11 @@
 #define ZSTD_HIP_PARAMS_H_
 
 #define ZH_BLOCK_MAX 65536          /* bytes per device block (one workgroup) */
-#define ZH_TILE 256                 /* hash insertion granularity (positions) */
+#define ZH_TILE 128                 /* hash insertion granularity (positions) */
 #define ZH_WINDOW 4096              /* parse window (positions) */
 #define ZH_SEG 16                   /* positions per thread in the parse */
-#define ZH_HASH_LOG_LONG 13         /* 8-byte hash table: 2^13 u32 entries */
-#define ZH_HASH_LOG_SHORT 13        /* 5-byte hash table: 2^13 u32 entries */
+#define ZH_HASH_LOG_LONG 14         /* 8-byte hash table: 2^14 u16 entries */
+#define ZH_HASH_LOG_SHORT 14        /* 5-byte hash table: 2^14 u16 entries */
 #define ZH_HASH_READ 8              /* bytes read per hashed position */
 #define ZH_MIN_MATCH_LONG 8
 #define ZH_MIN_MATCH_SHORT 5

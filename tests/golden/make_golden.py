@@ -94,42 +94,64 @@ class ZS(ctypes.Structure):
     _fields_ = [("offset", ctypes.c_uint), ("litLength", ctypes.c_uint), ("matchLength", ctypes.c_uint), ("rep", ctypes.c_uint)]
 
 
+def _block_case(o, cc, name, src, full):
+    size = len(src)
+    seqbuf = np.zeros((size // 5 + 2, 3), np.uint32)
+    last = ctypes.c_uint32()
+    ns = o.orc_lz_parse(src.ctypes.data_as(vp), ctypes.c_uint32(size), seqbuf.ctypes.data_as(vp), ctypes.byref(last))
+    zs = (ZS * max(ns, 1))()
+    for k in range(ns):
+        zs[k].offset, zs[k].litLength, zs[k].matchLength = int(seqbuf[k, 2]), int(seqbuf[k, 0]), int(seqbuf[k, 1])
+    z.ZSTD_CCtx_reset(vp(cc), 3)
+    z.ZSTD_CCtx_setParameter(vp(cc), 100, 3)
+    z.ZSTD_CCtx_setParameter(vp(cc), 1011, 0)
+    buf = np.zeros(size * 2 + 512, np.uint8)
+    r = z.ZSTD_compressSequences(vp(cc), buf.ctypes.data_as(vp), ctypes.c_size_t(len(buf)), zs, ctypes.c_size_t(ns),
+                                 src.ctypes.data_as(vp), ctypes.c_size_t(size))
+    assert not is_err(r)
+    fr = bytes(buf[:r])
+    fhd = fr[4]
+    hs = 5 + (0 if (fhd >> 5) & 1 else 1) + [0, 1, 2, 4][fhd & 3] + [1 if (fhd >> 5) & 1 else 0, 2, 4, 8][fhd >> 6]
+    c = {"name": name, "last_literals": last.value, "libzstd_block": fr[hs:].hex()}
+    if full:  # 64 KiB: the input is regenerated from its generator, the parse pinned by its digest
+        import hashlib
+        c["nseq"] = int(ns)
+        c["sequences_sha256"] = hashlib.sha256(seqbuf[:ns].astype("<u4").tobytes()).hexdigest()
+    else:
+        c["input"] = src.tobytes().hex()
+        c["sequences"] = seqbuf[:ns].tolist()
+    return c
+
+
 def block_cases():
     """libzstd ZSTD_compressSequences (noBlockDelimiters) on the oracle's own parse:
-    pins the oracle's entropy stage byte-for-byte.  Inputs kept small (<= 8 KiB)."""
+    pins the oracle's entropy stage byte-for-byte.  Small inputs (<= 8 KiB) carry their
+    bytes; the 64 KiB blocks of the metric's chunk size (4-stream Huffman, FSE-compressed
+    weights, large-nbSeq FSE tables) are named by their tools/datagen.c generator."""
     o = T.oracle()
     cc = z.ZSTD_createCCtx()
     out = []
-    seqbuf = np.zeros((4000, 3), np.uint32)
     for name, kind, size, seed in [("text", T.DG_TEXT, 8192, 1), ("csv", T.DG_CSV, 6000, 2), ("json", T.DG_JSON, 8192, 3),
                                    ("exe", T.DG_EXE, 5000, 4), ("sensor", T.DG_SENSOR, 8192, 5), ("source", T.DG_SOURCE, 7000, 6),
                                    ("sym16", T.DG_SYM16, 4096, 7), ("text_small", T.DG_TEXT, 700, 8)]:
-        src = T.gen(kind, 1, seed, size)
-        last = ctypes.c_uint32()
-        ns = o.orc_lz_parse(src.ctypes.data_as(vp), ctypes.c_uint32(size), seqbuf.ctypes.data_as(vp), ctypes.byref(last))
-        zs = (ZS * max(ns, 1))()
-        for k in range(ns):
-            zs[k].offset, zs[k].litLength, zs[k].matchLength = int(seqbuf[k, 2]), int(seqbuf[k, 0]), int(seqbuf[k, 1])
-        z.ZSTD_CCtx_reset(vp(cc), 3)
-        z.ZSTD_CCtx_setParameter(vp(cc), 100, 3)
-        z.ZSTD_CCtx_setParameter(vp(cc), 1011, 0)
-        buf = np.zeros(size * 2 + 512, np.uint8)
-        r = z.ZSTD_compressSequences(vp(cc), buf.ctypes.data_as(vp), ctypes.c_size_t(len(buf)), zs, ctypes.c_size_t(ns),
-                                     src.ctypes.data_as(vp), ctypes.c_size_t(size))
-        assert not is_err(r)
-        fr = bytes(buf[:r])
-        fhd = fr[4]
-        hs = 5 + (0 if (fhd >> 5) & 1 else 1) + [0, 1, 2, 4][fhd & 3] + [1 if (fhd >> 5) & 1 else 0, 2, 4, 8][fhd >> 6]
-        out.append({"name": name, "input": src.tobytes().hex(), "sequences": seqbuf[:ns].tolist(), "last_literals": last.value,
-                    "libzstd_block": fr[hs:].hex()})
+        out.append(_block_case(o, cc, name, T.gen(kind, 1, seed, size), False))
+    for kname in ("mix", "text", "exe", "sensor", "json", "csv", "source", "sym16"):
+        for first in (0, 5):
+            c = _block_case(o, cc, f"{kname}_64k_{first}", T.gen(T.KINDS[kname], 1, 0x5EED0003, 65536, first=first), True)
+            c["gen"] = {"kind": kname, "seed": 0x5EED0003, "size": 65536, "first": first}
+            out.append(c)
     return out
 
 
 def main():
     ver = int(z.ZSTD_versionNumber())
-    json.dump({"libzstd_version": ver, "cases": fse_cases()}, open(os.path.join(HERE, "fse_normalize_ncount.json"), "w"))
-    json.dump({"libzstd_version": ver, "cases": huf_cases()}, open(os.path.join(HERE, "huf_ctable.json"), "w"))
-    json.dump({"libzstd_version": ver, "cases": block_cases()}, open(os.path.join(HERE, "entropy_blocks.json"), "w"))
+    only = sys.argv[1:]  # e.g. "blocks": regenerate only the entropy-block fixtures (they follow the LZ parameters)
+    if not only or "fse" in only:
+        json.dump({"libzstd_version": ver, "cases": fse_cases()}, open(os.path.join(HERE, "fse_normalize_ncount.json"), "w"))
+    if not only or "huf" in only:
+        json.dump({"libzstd_version": ver, "cases": huf_cases()}, open(os.path.join(HERE, "huf_ctable.json"), "w"))
+    if not only or "blocks" in only:
+        json.dump({"libzstd_version": ver, "cases": block_cases()}, open(os.path.join(HERE, "entropy_blocks.json"), "w"))
     ref = {
         "source": "reference tests/test_fse_header.cu:57-66,100-115; tests/test_fse_encoding.cu:15-60; tests/test_compressible_data.cu:272,311,325,363",
         "ncount": [{"norm": [16, 16], "maxsv": 1, "tablelog": 5, "bytes": "103f"},

@@ -244,3 +244,22 @@ def test_reference_ratio_floors_on_gpu(torch_cuda, mgr):
     _check(outs, [cases[k] for k in names])
     for k, o in zip(names, outs):
         assert 65536 / o.numel() > floors[k], (k, 65536 / o.numel(), floors[k])
+
+
+def test_full_size_blocks_match_libzstd(torch_cuda, mgr):
+    """64 KiB chunks (the metric's size): the GPU frame's block equals libzstd 1.4.9
+    ZSTD_compressSequences' block for the same sequences (tests/golden/entropy_blocks.json,
+    made by tests/golden/make_golden.py): 4-stream Huffman literals, FSE-compressed weights
+    and full-size FSE sequence tables pinned to libzstd, not only to the oracle."""
+    import json
+    import os
+
+    cases = [c for c in json.load(open(os.path.join(T.GOLDEN, "entropy_blocks.json")))["cases"] if "gen" in c]
+    assert len(cases) >= 10
+    datas = [T.gen(T.KINDS[c["gen"]["kind"]], 1, c["gen"]["seed"], c["gen"]["size"], first=c["gen"]["first"]) for c in cases]
+    outs = mgr.compress_batch([torch_cuda.from_numpy(d).cuda() for d in datas])
+    for c, o in zip(cases, outs):
+        fr = o.cpu().numpy().tobytes()
+        fhd = fr[4]
+        hs = 5 + (0 if (fhd >> 5) & 1 else 1) + [0, 1, 2, 4][fhd & 3] + [1 if (fhd >> 5) & 1 else 0, 2, 4, 8][fhd >> 6]
+        assert fr[hs:].hex() == c["libzstd_block"], c["name"]

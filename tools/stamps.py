@@ -28,7 +28,7 @@ bc.compress_async(*args, temp)
 torch.cuda.synchronize()
 a256 = lambda v: (v + 255) // 256 * 256
 base = a256(temp.data_ptr()) - temp.data_ptr()
-off = a256(n * 40)
+off = a256(n * 56)  # sizeof(ZhBlockDesc)
 off = a256(off + n * 24)
 off = a256(off + n * 4)
 off = a256(off + n * 8)
