@@ -223,7 +223,7 @@ def c2_leg(dev, steps):
     ms = timed_events(lambda: m.compress(d), steps)
     frame = f.cpu().numpy().tobytes()
     res = {"value": round(C2_BYTES / (ms / 1e3) / 1e9, 3), "unit": "GB/s", "ms_per_call": round(ms, 3), "ratio": round(C2_BYTES / len(frame), 4),
-           "workload": "C2: 64 MiB iid 16-symbol buffer, one frame (1024 x 64 KiB blocks), ZstdManager::compress incl. its host sync"}
+           "workload": "C2: 64 MiB iid 16-symbol buffer, one frame (2048 x 32 KiB blocks, each matched against the 32 KiB before it), ZstdManager::compress incl. its host sync"}
     z = T.zstd()
     if z is not None:
         res["libzstd_verified"] = T.zstd_decompress(frame, C2_BYTES) == host.tobytes()

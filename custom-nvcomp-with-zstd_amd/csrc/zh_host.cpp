@@ -136,6 +136,9 @@ ZstdManager::ExecutionPath ZstdManager::select_execution_path(size_t size, int c
 // host libzstd bridge (the reference's CPU route; FORCE_CPU + decompress)
 // ============================================================================
 namespace {
+constexpr u32 kSkippableMagic = 0x184D2A50u;  // RFC 8878 skippable frames 0x184D2A50..5F
+constexpr u32 kMetadataMagic = 0x444D5A43u;   // "CZMD": this library's metadata frame
+constexpr size_t kMetadataFrameBytes = 16;
 struct LibZstd {
   size_t (*compress)(void *, size_t, const void *, size_t, int) = nullptr;
   size_t (*decompress)(void *, size_t, const void *, size_t) = nullptr;
@@ -242,7 +245,13 @@ struct WsLayout {
   }
 };
 
-inline size_t blocks_of(size_t n) { return (n + ZH_BLOCK_MAX - 1) / ZH_BLOCK_MAX; }
+// Device blocks of a frame of n bytes (ZH_FRAME_BLOCK: 64 KiB, or 32 KiB history blocks for
+// larger frames and for dictionary frames over 32 KiB)
+inline size_t block_size_of(size_t n, bool dict) { return ZH_FRAME_BLOCK(n, dict); }
+inline size_t blocks_of(size_t n, bool dict = false) {
+  size_t const bs = block_size_of(n, dict);
+  return (n + bs - 1) / bs;
+}
 
 // Decoder workspace (zh_decode.hip): per-item arrays (host-array entry points upload
 // them), then one slot per item holding the literals and sequence records of the block
@@ -309,10 +318,19 @@ struct DevDict {
   u8 *d = nullptr;
   size_t cap = 0, n = 0, off = 0;
   u32 id = 0;
+  bool owned = true;  // false: a view of caller memory (streaming history)
   DevDict() = default;
   DevDict(const DevDict &) = delete;
   DevDict &operator=(const DevDict &) = delete;
-  ~DevDict() { if (d) (void)hipFree(d); }
+  ~DevDict() { if (d && owned) (void)hipFree(d); }
+  // raw-content view of device-resident history (never freed here)
+  static void view(DevDict &v, const void *p, size_t bytes) {
+    v.owned = false;
+    v.d = (u8 *)p;
+    v.cap = v.n = bytes;
+    v.off = 0;
+    v.id = 0;
+  }
   const u8 *content() const { return d + off; }
   size_t content_n() const { return n - off; }
   // raw content or a formatted dictionary (host or device buffer); replaces the previous one
@@ -349,11 +367,16 @@ struct DevDict {
 };
 
 // Descriptor fields of a block: a dictionary frame's first block gets the content tail that
-// fits in front of it in K1's 64 KiB of LDS
-void set_dict_block(ZhBlockDesc &d, const DevDict *dd, bool first) {
+// fits in front of it in K1's 64 KiB of LDS; a later block of a history frame gets the 32 KiB
+// of input before it (when the window reaches that far)
+void set_dict_block(ZhBlockDesc &d, const DevDict *dd, bool first, bool hist) {
   d.pre = nullptr;
   d.pre_n = 0;
   d.dict_id = 0;
+  if (!first && hist) {
+    d.pre = d.src - ZH_HIST_BLOCK;
+    d.pre_n = ZH_HIST_BLOCK;
+  }
   if (!dd || !dd->n) return;
   d.flags |= ZH_F_DICT;
   d.dict_id = dd->id;
@@ -404,8 +427,10 @@ class ZstdBatchManager::Impl {
     if (s != Status::SUCCESS) return s;
     size_t nblocks = 0;
     bool staged = false;
+    bool const has_dict = dd && dd->n;
+    bool const hist = config.window_log >= ZH_HIST_WINDOW_LOG;
     for (size_t i = 0; i < count; i++) {
-      size_t nb = blocks_of(in_sizes[i]);
+      size_t nb = blocks_of(in_sizes[i], has_dict);
       nblocks += nb;
       staged |= nb > 1;
     }
@@ -422,20 +447,20 @@ class ZstdBatchManager::Impl {
     u8 *staging = base + L.staging;
     size_t b = 0;
     for (size_t i = 0; i < count; i++) {
-      size_t const n = in_sizes[i], nb = blocks_of(n);
+      size_t const n = in_sizes[i], nb = blocks_of(n, has_dict), bs = block_size_of(n, has_dict);
       hi[i].dst = (u8 *)out_ptrs[i];
       hi[i].cap = out_sizes[i];
       hi[i].first_block = (u32)b;
       hi[i].nblocks = (u32)nb;
       for (size_t k = 0; k < nb; k++, b++) {
         ZhBlockDesc &d = hd[b];
-        d.src = (const u8 *)in_ptrs[i] + k * ZH_BLOCK_MAX;
+        d.src = (const u8 *)in_ptrs[i] + k * bs;
         d.frame_size = n;
-        d.n = (u32)std::min((size_t)ZH_BLOCK_MAX, n - k * ZH_BLOCK_MAX);
+        d.n = (u32)std::min(bs, n - k * bs);
         d.item = (u32)i;
         d.flags = (k == 0 ? ZH_F_FIRST : 0u) | (k + 1 == nb ? ZH_F_LAST : 0u) | (nb == 1 ? ZH_F_DIRECT : 0u) |
                   (config.checksum != ChecksumPolicy::NO_COMPUTE_NO_VERIFY ? ZH_F_CHECKSUM : 0u);
-        set_dict_block(d, dd, k == 0);
+        set_dict_block(d, dd, k == 0, hist);
         if (nb == 1) {
           d.dst = (u8 *)out_ptrs[i];
           d.dst_cap = (u32)std::min(out_sizes[i], (size_t)0xFFFFFFFFu);
@@ -522,14 +547,14 @@ class ZstdBatchManager::Impl {
   // One buffer, no pointer-array upload (ZhDecArgs single-item fields).  Synchronous
   // unless d_actual is given (then the size lands there, stream-ordered, 0 on error).
   Status run_decompress_one(const void *in, size_t n, void *out, size_t cap, size_t *h_actual, size_t *d_actual, void *temp, size_t temp_size,
-                            hipStream_t stream) {
+                            hipStream_t stream, const DevDict *dd = nullptr) {
     Status s = ensure_kernels();
     if (s != Status::SUCCESS) return s;
     DecLayout L = DecLayout::make(1, cap);
     if (!temp || temp_size < L.total) return Status::ERROR_BUFFER_TOO_SMALL;
     u8 *base = (u8 *)(((uintptr_t)temp + 255) & ~(uintptr_t)255);
     ZhDecArgs a = L.args(base);
-    mgr_dict.fill(a);
+    (dd ? *dd : mgr_dict).fill(a);
     a.one_in = in;
     a.one_in_size = n;
     a.one_out = out;
@@ -564,8 +589,9 @@ Status ZstdBatchManager::configure(const CompressionConfig &c) {
 }
 CompressionConfig ZstdBatchManager::get_config() const { return pimpl_->config; }
 
+// sized for the dictionary layout as well (a per-call dictionary is only known at compress())
 size_t ZstdBatchManager::get_compress_temp_size(size_t n) const {
-  size_t nb = std::max<size_t>(1, blocks_of(n));
+  size_t nb = std::max<size_t>(1, blocks_of(n, true));
   return WsLayout::make(nb, 1, nb > 1).total;
 }
 // one slot for 128 KiB blocks (reference src/cuda_zstd_manager.cu:1373-1408 also sizes for one block)
@@ -620,6 +646,37 @@ Status ZstdBatchManager::decompress(const void *in, size_t n, void *out, size_t 
   return s;
 }
 
+Status ZstdBatchManager::compress_with_history(const void *in, size_t n, void *out, size_t *out_size, void *temp, size_t temp_size,
+                                               const void *hist, size_t hist_n, hipStream_t stream) {
+  std::lock_guard<std::mutex> lock(pimpl_->api_mutex);
+  if (!in || !out || !out_size || !temp || (hist_n && !hist)) return Status::ERROR_INVALID_PARAMETER;
+  if (n == 0) { *out_size = 0; return Status::ERROR_INVALID_PARAMETER; }
+  if (temp_size < get_compress_temp_size(n)) return Status::ERROR_BUFFER_TOO_SMALL;
+  DevDict view;
+  if (hist_n) DevDict::view(view, hist, hist_n);
+  Status item;
+  const void *ip[1] = {in};
+  void *opv[1] = {out};
+  size_t sz[1] = {n};
+  auto t0 = std::chrono::steady_clock::now();
+  Status st = pimpl_->run(ip, sz, 1, opv, out_size, &item, temp, temp_size, stream, hist_n ? &view : pimpl_->active());
+  if (st == Status::ERROR_GENERIC) st = item;
+  pimpl_->stats.compression_time_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  return st;
+}
+Status ZstdBatchManager::decompress_with_history(const void *in, size_t n, void *out, size_t *out_size, void *temp, size_t temp_size,
+                                                 const void *hist, size_t hist_n, hipStream_t stream) {
+  std::lock_guard<std::mutex> lock(pimpl_->api_mutex);
+  if (!in || !out || !out_size || !temp || n < 4 || (hist_n && !hist)) return Status::ERROR_INVALID_PARAMETER;
+  if (temp_size < DecLayout::make(1, *out_size).total) return Status::ERROR_BUFFER_TOO_SMALL;
+  DevDict view;
+  if (hist_n) DevDict::view(view, hist, hist_n);
+  size_t got = 0;
+  Status s = pimpl_->run_decompress_one(in, n, out, *out_size, &got, nullptr, temp, temp_size, stream, hist_n ? &view : nullptr);
+  if (s == Status::SUCCESS) *out_size = got;
+  return s;
+}
+
 // Dictionary compression and decompression: raw content or a formatted RFC 8878
 // dictionary; copied to the device once (the reference keeps a shallow pointer and copies it
 // into the workspace per call, src/cuda_zstd_manager.cu:1699-1775, 3711-3764)
@@ -654,7 +711,8 @@ void ZstdBatchManager::reset_stats() { pimpl_->stats = CompressionStats{}; }
 size_t ZstdBatchManager::get_batch_compress_temp_size(const std::vector<size_t> &sizes) const {
   size_t nb = 0;
   bool staged = false;
-  for (size_t s : sizes) { size_t k = blocks_of(s); nb += k; staged |= k > 1; }
+  bool const dict = pimpl_->active() != nullptr;  // the manager's dictionary, if set before this query
+  for (size_t s : sizes) { size_t k = blocks_of(s, dict); nb += k; staged |= k > 1; }
   return WsLayout::make(nb, sizes.size(), staged).total;
 }
 size_t ZstdBatchManager::get_batch_decompress_temp_size(const std::vector<size_t> &sizes) const {
@@ -774,7 +832,10 @@ Status ZstdBatchManager::compress_batch_device(const void *const *d_in_ptrs, con
   if (s != Status::SUCCESS) return s;
   if (!count) return Status::SUCCESS;
   if (!d_in_ptrs || !d_in_sizes || !d_out_ptrs || !d_out_sizes || max_chunk == 0) return Status::ERROR_INVALID_PARAMETER;
-  size_t const bpi = blocks_of(max_chunk), nblocks = count * bpi;
+  const DevDict *dd = pimpl_->active();
+  // (with a dictionary set, chunks over 32 KiB take two history blocks: a larger workspace
+  // than get_batch_device_temp_size's, from nvcomp_zstd_batch_get_compress_temp_size_v5)
+  size_t const bpi = blocks_of(max_chunk, dd != nullptr), nblocks = count * bpi;
   WsLayout L = WsLayout::make(nblocks, count, bpi > 1);
   if (!temp || temp_size < L.total) return Status::ERROR_BUFFER_TOO_SMALL;
   u8 *base = (u8 *)(((uintptr_t)temp + 255) & ~(uintptr_t)255);
@@ -782,10 +843,10 @@ Status ZstdBatchManager::compress_batch_device(const void *const *d_in_ptrs, con
   u64 *item_size = (u64 *)d_out_sizes;
   u32 *item_status = d_statuses ? (u32 *)d_statuses : (u32 *)(base + L.item_status);
   bool const ck = pimpl_->config.checksum != ChecksumPolicy::NO_COMPUTE_NO_VERIFY;
-  const DevDict *dd = pimpl_->active();
+  u32 const hist = pimpl_->config.window_log >= ZH_HIST_WINDOW_LOG ? 1u : 0u;
   hipError_t e = zh::launch_plan(d_in_ptrs, d_in_sizes, (u32)count, (u32)bpi, d_out_ptrs, cap, base + L.staging, (ZhBlockDesc *)(base + L.descs),
                                  (ZhItemDesc *)(base + L.items), item_size, item_status, ck ? ZH_F_CHECKSUM : 0u,
-                                 dd ? dd->content() : nullptr, dd ? (u32)dd->content_n() : 0u, dd ? dd->id : 0u, stream);
+                                 dd ? dd->content() : nullptr, dd ? (u32)dd->content_n() : 0u, dd ? dd->id : 0u, hist, stream);
   if (e != hipSuccess) return Status::ERROR_CUDA_ERROR;
   ZhWorkspace ws{base + L.blocks};
   e = zh::launch_compress((const ZhBlockDesc *)(base + L.descs), (u32)nblocks, ws, pimpl_->config.window_log, pimpl_->config.block_size, item_size,
@@ -821,8 +882,45 @@ Status ZstdBatchManager::decompress_batch_device(const void *const *d_in_ptrs, c
 }
 
 // ============================================================================
-// Streaming manager: each chunk an independent frame (reference :6306-6310)
+// Streaming manager (reference src/cuda_zstd_manager.cu:6043-6455).  compress_chunk: each chunk
+// an independent frame (:6306-6310).  compress_chunk_with_history: the chunk is compressed with
+// the preceding stream bytes (a 64 KiB device window, the most K1 can stage) as raw-content
+// history, as the reference passes its window to compress() as a dictionary (:6327-6418).
+// decompress_chunk keeps the same window of decoded bytes and hands it to the decoder, so
+// chunks of either kind decode in stream order.
 // ============================================================================
+namespace {
+constexpr size_t kStreamWindow = 64 * 1024;
+// a device window of the last kStreamWindow stream bytes (double-buffered: no overlapping copies)
+struct HistWindow {
+  u8 *buf[2] = {nullptr, nullptr};
+  int cur = 0;
+  size_t n = 0;
+  ~HistWindow() {
+    for (u8 *b : buf)
+      if (b) (void)hipFree(b);
+  }
+  Status ensure() {
+    for (u8 *&b : buf)
+      if (!b && hipMalloc(&b, kStreamWindow) != hipSuccess) { b = nullptr; return Status::ERROR_OUT_OF_MEMORY; }
+    return Status::SUCCESS;
+  }
+  const u8 *data() const { return buf[cur]; }
+  Status append(const void *src, size_t len, hipStream_t stream) {
+    Status s = ensure();
+    if (s != Status::SUCCESS) return s;
+    u8 *const dst = buf[cur ^ 1];
+    size_t const take = std::min(len, kStreamWindow), keep = std::min(n, kStreamWindow - take);
+    if (keep && hipMemcpyAsync(dst, buf[cur] + n - keep, keep, hipMemcpyDeviceToDevice, stream) != hipSuccess) return Status::ERROR_CUDA_ERROR;
+    if (hipMemcpyAsync(dst + keep, (const u8 *)src + len - take, take, hipMemcpyDefault, stream) != hipSuccess) return Status::ERROR_CUDA_ERROR;
+    cur ^= 1;
+    n = keep + take;
+    return Status::SUCCESS;
+  }
+  void clear() { n = 0; }
+};
+}  // namespace
+
 class ZstdStreamingManager::Impl {
  public:
   CompressionConfig config;
@@ -830,56 +928,85 @@ class ZstdStreamingManager::Impl {
   void *ws = nullptr;
   size_t ws_size = 0;
   bool comp = false, decomp = false;
+  HistWindow chist, dhist;  // compressor's and decompressor's stream windows
   explicit Impl(const CompressionConfig &c) : config(c), mgr(c) {}
   ~Impl() { if (ws) (void)hipFree(ws); }
+  Status ensure_ws(size_t need) {
+    if (need <= ws_size) return Status::SUCCESS;
+    if (ws) (void)hipFree(ws);
+    ws = nullptr;
+    ws_size = 0;
+    if (hipMalloc(&ws, need) != hipSuccess) return Status::ERROR_OUT_OF_MEMORY;
+    ws_size = need;
+    return Status::SUCCESS;
+  }
 };
 ZstdStreamingManager::ZstdStreamingManager() : pimpl_(new Impl(CompressionConfig::from_level(3))) {}
 ZstdStreamingManager::ZstdStreamingManager(const CompressionConfig &c) : pimpl_(new Impl(c)) {}
 ZstdStreamingManager::~ZstdStreamingManager() = default;
 Status ZstdStreamingManager::init_compression(hipStream_t, size_t max_chunk) {
-  size_t need = pimpl_->mgr.get_compress_temp_size(max_chunk ? max_chunk : (size_t)ZH_BLOCK_MAX);
-  if (need > pimpl_->ws_size) {
-    if (pimpl_->ws) (void)hipFree(pimpl_->ws);
-    pimpl_->ws = nullptr;
-    pimpl_->ws_size = 0;
-    if (hipMalloc(&pimpl_->ws, need) != hipSuccess) return Status::ERROR_OUT_OF_MEMORY;
-    pimpl_->ws_size = need;
-  }
+  Status s = pimpl_->ensure_ws(pimpl_->mgr.get_compress_temp_size(max_chunk ? max_chunk : (size_t)ZH_BLOCK_MAX));
+  if (s != Status::SUCCESS) return s;
   pimpl_->comp = true;
   return Status::SUCCESS;
 }
-Status ZstdStreamingManager::init_compression_with_history(hipStream_t s, size_t m) { return init_compression(s, m); }
+Status ZstdStreamingManager::init_compression_with_history(hipStream_t st, size_t m) {
+  Status s = init_compression(st, m);
+  if (s == Status::SUCCESS) s = pimpl_->chist.ensure();
+  return s;
+}
 Status ZstdStreamingManager::init_decompression(hipStream_t) {
-  size_t need = pimpl_->mgr.get_decompress_temp_size(0);
-  if (need > pimpl_->ws_size) {
-    if (pimpl_->ws) (void)hipFree(pimpl_->ws);
-    pimpl_->ws = nullptr;
-    pimpl_->ws_size = 0;
-    if (hipMalloc(&pimpl_->ws, need) != hipSuccess) return Status::ERROR_OUT_OF_MEMORY;
-    pimpl_->ws_size = need;
-  }
+  Status s = pimpl_->ensure_ws(pimpl_->mgr.get_decompress_temp_size(0));
+  if (s == Status::SUCCESS) s = pimpl_->dhist.ensure();
+  if (s != Status::SUCCESS) return s;
   pimpl_->decomp = true;
   return Status::SUCCESS;
 }
 Status ZstdStreamingManager::compress_chunk(const void *in, size_t n, void *out, size_t *out_size, bool, hipStream_t stream) {
   if (!pimpl_->comp) return Status::ERROR_NOT_INITIALIZED;
-  size_t need = pimpl_->mgr.get_compress_temp_size(n);
-  if (need > pimpl_->ws_size) {
-    Status s = init_compression(stream, n);
+  Status s = pimpl_->ensure_ws(pimpl_->mgr.get_compress_temp_size(n));
+  if (s != Status::SUCCESS) return s;
+  s = pimpl_->mgr.compress(in, n, out, out_size, pimpl_->ws, pimpl_->ws_size, nullptr, 0, stream);
+  // the stream window follows every chunk, so a later chunk_with_history sees these bytes
+  if (s == Status::SUCCESS && pimpl_->chist.buf[0]) s = pimpl_->chist.append(in, n, stream);
+  return s;
+}
+Status ZstdStreamingManager::compress_chunk_with_history(const void *in, size_t n, void *out, size_t *out_size, bool, hipStream_t stream) {
+  if (!in || !out || !out_size) return Status::ERROR_INVALID_PARAMETER;
+  if (!pimpl_->comp || !pimpl_->chist.buf[0]) {  // auto-initialise, as the reference does
+    Status s = init_compression_with_history(stream, n);
     if (s != Status::SUCCESS) return s;
   }
-  return pimpl_->mgr.compress(in, n, out, out_size, pimpl_->ws, pimpl_->ws_size, nullptr, 0, stream);
-}
-Status ZstdStreamingManager::compress_chunk_with_history(const void *in, size_t n, void *out, size_t *out_size, bool last, hipStream_t stream) {
-  return compress_chunk(in, n, out, out_size, last, stream);
+  Status s = pimpl_->ensure_ws(pimpl_->mgr.get_compress_temp_size(n));
+  if (s != Status::SUCCESS) return s;
+  s = pimpl_->mgr.compress_with_history(in, n, out, out_size, pimpl_->ws, pimpl_->ws_size, pimpl_->chist.data(), pimpl_->chist.n, stream);
+  if (s == Status::SUCCESS) s = pimpl_->chist.append(in, n, stream);
+  return s;
 }
 Status ZstdStreamingManager::decompress_chunk(const void *in, size_t n, void *out, size_t *out_size, bool *is_last, hipStream_t stream) {
-  if (!pimpl_->decomp) return Status::ERROR_NOT_INITIALIZED;
-  if (is_last) *is_last = true;
-  return pimpl_->mgr.decompress(in, n, out, out_size, pimpl_->ws, pimpl_->ws_size, stream);
+  if (!in || !out || !out_size) return Status::ERROR_INVALID_PARAMETER;
+  if (!pimpl_->decomp) {
+    Status s = init_decompression(stream);
+    if (s != Status::SUCCESS) return s;
+  }
+  if (is_last) *is_last = true;  // every chunk is a complete frame
+  Status s = pimpl_->ensure_ws(pimpl_->mgr.get_decompress_temp_size(n));
+  if (s != Status::SUCCESS) return s;
+  s = pimpl_->mgr.decompress_with_history(in, n, out, out_size, pimpl_->ws, pimpl_->ws_size, pimpl_->dhist.data(), pimpl_->dhist.n, stream);
+  if (s == Status::SUCCESS) s = pimpl_->dhist.append(out, *out_size, stream);
+  return s;
 }
-Status ZstdStreamingManager::reset() { pimpl_->comp = pimpl_->decomp = false; return Status::SUCCESS; }
-Status ZstdStreamingManager::reset_streaming() { return Status::SUCCESS; }
+Status ZstdStreamingManager::reset() {
+  pimpl_->comp = pimpl_->decomp = false;
+  pimpl_->chist.clear();
+  pimpl_->dhist.clear();
+  return Status::SUCCESS;
+}
+Status ZstdStreamingManager::reset_streaming() {
+  pimpl_->chist.clear();
+  pimpl_->dhist.clear();
+  return Status::SUCCESS;
+}
 Status ZstdStreamingManager::flush(hipStream_t s) { return hipStreamSynchronize(s) == hipSuccess ? Status::SUCCESS : Status::ERROR_CUDA_ERROR; }
 Status ZstdStreamingManager::flush_streaming(hipStream_t s) { return flush(s); }
 Status ZstdStreamingManager::set_config(const CompressionConfig &c) { pimpl_->config = c; return pimpl_->mgr.configure(c); }
@@ -922,28 +1049,113 @@ Status decompress_simple(const void *in, size_t n, void *out, size_t *out_size, 
   return s;
 }
 
+// Frame header fields of the first zstd frame in a buffer, after any skippable frames (the
+// reference parse_zstd_frame_header skips them the same way, src/cuda_zstd_manager.cu:875-900);
+// *meta_level = the level of a metadata frame written by write_metadata_frame, else -1.
+namespace {
+struct FrameProbe {
+  u64 content = 0;
+  bool has_content = false, checksum = false;
+  u32 dict_id = 0, window_log = 0;
+  int meta_level = -1;
+  size_t frame_offset = 0;
+};
+Status probe_frame(const void *data, size_t n, FrameProbe &f) {
+  if (!data || n < 4) return Status::ERROR_INVALID_PARAMETER;
+  size_t off = 0;
+  for (int guard = 0; guard < 64; guard++) {  // (bounded number of leading skippable frames)
+    u8 h[18] = {0};
+    size_t const take = std::min<size_t>(n - off, sizeof(h));
+    if (take < 4) return Status::ERROR_CORRUPT_DATA;
+    if (copy_any(h, (const u8 *)data + off, take, 0) != Status::SUCCESS) return Status::ERROR_CUDA_ERROR;
+    u32 magic;
+    memcpy(&magic, h, 4);
+    if ((magic & 0xFFFFFFF0u) == kSkippableMagic) {
+      if (take < 8) return Status::ERROR_CORRUPT_DATA;
+      u32 fs;
+      memcpy(&fs, h + 4, 4);
+      if (fs == 8 && take >= 16) {
+        u32 cm, lv;
+        memcpy(&cm, h + 8, 4);
+        memcpy(&lv, h + 12, 4);
+        if (cm == kMetadataMagic) f.meta_level = (int)lv;
+      }
+      if (n - off < 8 + (size_t)fs) return Status::ERROR_CORRUPT_DATA;
+      off += 8 + (size_t)fs;
+      continue;
+    }
+    if (magic != ZSTD_MAGIC) return Status::ERROR_INVALID_MAGIC;
+    if (take < 5) return Status::ERROR_CORRUPT_DATA;
+    u8 const fhd = h[4];
+    u32 const fcs_flag = fhd >> 6, ss = (fhd >> 5) & 1, did = fhd & 3;
+    size_t o = 5;
+    if (!ss) f.window_log = 10 + (h[o++] >> 3);
+    u32 const dsz = did == 0 ? 0 : did == 1 ? 1 : did == 2 ? 2 : 4;
+    if (o + dsz > take) return Status::ERROR_CORRUPT_DATA;
+    for (u32 k = 0; k < dsz; k++) f.dict_id |= (u32)h[o + k] << (8 * k);
+    o += dsz;
+    u32 const fsz = fcs_flag == 0 ? (ss ? 1 : 0) : fcs_flag == 1 ? 2 : fcs_flag == 2 ? 4 : 8;
+    if (o + fsz > take) return Status::ERROR_CORRUPT_DATA;
+    u64 v = 0;
+    for (u32 k = 0; k < fsz; k++) v |= (u64)h[o + k] << (8 * k);
+    if (fsz == 2) v += 256;
+    f.content = v;
+    f.has_content = fsz != 0;
+    f.checksum = (fhd >> 2) & 1;
+    f.frame_offset = off;
+    return Status::SUCCESS;
+  }
+  return Status::ERROR_CORRUPT_DATA;
+}
+}  // namespace
+
 Status get_decompressed_size(const void *data, size_t n, size_t *out) {
   if (!data || !out || n < 4) return Status::ERROR_INVALID_PARAMETER;
-  u8 h[18] = {0};
-  if (copy_any(h, data, std::min<size_t>(n, sizeof(h)), 0) != Status::SUCCESS) return Status::ERROR_CUDA_ERROR;
-  u32 magic;
-  memcpy(&magic, h, 4);
-  if (magic != ZSTD_MAGIC) return Status::ERROR_INVALID_MAGIC;
-  u8 const fhd = h[4];
-  u32 const fcs_flag = fhd >> 6, ss = (fhd >> 5) & 1, did = fhd & 3;
-  size_t o = 5 + (ss ? 0 : 1) + (did == 0 ? 0 : did == 1 ? 1 : did == 2 ? 2 : 4);
-  u32 const fsz = fcs_flag == 0 ? (ss ? 1 : 0) : fcs_flag == 1 ? 2 : fcs_flag == 2 ? 4 : 8;
-  if (!fsz) return Status::ERROR_UNSUPPORTED_FORMAT;
-  if (o + fsz > n) return Status::ERROR_CORRUPT_DATA;
-  u64 v = 0;
-  for (u32 k = 0; k < fsz; k++) v |= (u64)h[o + k] << (8 * k);
-  if (fsz == 2) v += 256;
-  *out = (size_t)v;
+  FrameProbe f;
+  Status s = probe_frame(data, n, f);
+  if (s != Status::SUCCESS) return s;
+  if (!f.has_content) return Status::ERROR_UNSUPPORTED_FORMAT;
+  *out = (size_t)f.content;
   return Status::SUCCESS;
 }
 Status validate_compressed_data(const void *data, size_t n, bool) {
-  size_t s;
-  return get_decompressed_size(data, n, &s);
+  FrameProbe f;
+  return probe_frame(data, n, f);
+}
+
+// Skippable metadata frame (RFC 8878 §3.1.2): the reference declares SkippableFrameHeader +
+// CustomMetadataFrame {custom magic, compression level} and a device writer
+// (src/cuda_zstd_manager.cu:309-318, 391-412) but never calls it.  Here it is a utility: 16
+// bytes [0x184D2A50][8][kMetadataMagic][level] in front of frames; every zstd decoder (libzstd,
+// zh_decode.hip) skips it, extract_metadata reads the level back.
+Status write_metadata_frame(void *out, size_t capacity, int level, size_t *written, hipStream_t stream) {
+  if (!out || !written) return Status::ERROR_INVALID_PARAMETER;
+  if (capacity < kMetadataFrameBytes) return Status::ERROR_BUFFER_TOO_SMALL;
+  u32 const w[4] = {kSkippableMagic, 8u, kMetadataMagic, (u32)level};
+  Status s = copy_any(out, w, sizeof(w), stream);
+  if (s == Status::SUCCESS) *written = kMetadataFrameBytes;
+  return s;
+}
+
+// reference is_nvcomp_zstd_format / extract_metadata (include/cuda_zstd_manager.h:415-419,
+// src/cuda_zstd_manager.cu:992-1030): frame header fields after any skippable frames; the
+// level comes from a metadata frame (3 when there is none, as the reference reports)
+bool is_nvcomp_zstd_format(const void *data, size_t n) {
+  FrameProbe f;
+  return probe_frame(data, n, f) == Status::SUCCESS;
+}
+Status extract_metadata(const void *data, size_t n, NvcompMetadata &m) {
+  FrameProbe f;
+  Status s = probe_frame(data, n, f);
+  if (s != Status::SUCCESS) return s;
+  m.format_version = get_format_version();
+  m.compression_level = f.meta_level >= 0 ? (u32)f.meta_level : 3u;
+  m.uncompressed_size = f.has_content ? f.content : 0;
+  m.dictionary_id = f.dict_id;
+  m.checksum_policy = f.checksum ? ChecksumPolicy::COMPUTE_AND_VERIFY : ChecksumPolicy::NO_COMPUTE_NO_VERIFY;
+  m.chunk_size = 128 * 1024;
+  m.num_chunks = f.has_content ? (u32)((f.content + m.chunk_size - 1) / m.chunk_size) : 0;
+  return Status::SUCCESS;
 }
 
 // ============================================================================
@@ -1565,7 +1777,56 @@ unsigned int cuda_zstd_hybrid_query_routing(cuda_zstd_hybrid_engine_t *e, size_t
 void cuda_zstd_hip_profile_enable(int on) { zh::profile_enable(on != 0); }
 int cuda_zstd_hip_profile_collect(double *ms3) { return zh::profile_collect(ms3); }
 
-const char *cuda_zstd_hip_version(void) { return "cuda_zstd_hip 0.1.0 (gfx950)"; }
+struct cuda_zstd_stream_t {
+  std::unique_ptr<ZstdStreamingManager> m;
+};
+cuda_zstd_stream_t *cuda_zstd_stream_create(int level) {
+  if (!is_valid_compression_level(level)) return nullptr;
+  try {
+    auto *h = new cuda_zstd_stream_t;
+    h->m.reset(new ZstdStreamingManager(CompressionConfig::from_level(level)));
+    return h;
+  } catch (...) {
+    return nullptr;
+  }
+}
+void cuda_zstd_stream_destroy(cuda_zstd_stream_t *s) { delete s; }
+int cuda_zstd_stream_compress_chunk(cuda_zstd_stream_t *s, const void *src, size_t n, void *dst, size_t *dst_size, int with_history, int last,
+                                    hipStream_t stream) {
+  if (!s || !s->m) return status_to_nvcomp_error(Status::ERROR_INVALID_PARAMETER);
+  if (!with_history && !s->m->is_compression_initialized()) {
+    Status st = s->m->init_compression(stream, n);
+    if (st != Status::SUCCESS) return status_to_nvcomp_error(st);
+  }
+  return status_to_nvcomp_error(with_history ? s->m->compress_chunk_with_history(src, n, dst, dst_size, last != 0, stream)
+                                             : s->m->compress_chunk(src, n, dst, dst_size, last != 0, stream));
+}
+int cuda_zstd_stream_decompress_chunk(cuda_zstd_stream_t *s, const void *src, size_t n, void *dst, size_t *dst_size, int *is_last,
+                                      hipStream_t stream) {
+  if (!s || !s->m) return status_to_nvcomp_error(Status::ERROR_INVALID_PARAMETER);
+  bool l = false;
+  Status st = s->m->decompress_chunk(src, n, dst, dst_size, &l, stream);
+  if (is_last) *is_last = l ? 1 : 0;
+  return status_to_nvcomp_error(st);
+}
+int cuda_zstd_stream_reset(cuda_zstd_stream_t *s) { return s && s->m ? status_to_nvcomp_error(s->m->reset()) : 2; }
+
+int cuda_zstd_write_metadata_frame(void *dst, size_t capacity, int level, size_t *written, hipStream_t stream) {
+  return status_to_nvcomp_error(write_metadata_frame(dst, capacity, level, written, stream));
+}
+int cuda_zstd_extract_metadata(const void *src, size_t size, unsigned int *level, unsigned long long *usize, unsigned int *dict_id, int *has_ck) {
+  NvcompMetadata m;
+  Status s = extract_metadata(src, size, m);
+  if (s == Status::SUCCESS) {
+    if (level) *level = m.compression_level;
+    if (usize) *usize = m.uncompressed_size;
+    if (dict_id) *dict_id = m.dictionary_id;
+    if (has_ck) *has_ck = m.checksum_policy != ChecksumPolicy::NO_COMPUTE_NO_VERIFY;
+  }
+  return status_to_nvcomp_error(s);
+}
+
+const char *cuda_zstd_hip_version(void) { return "cuda_zstd_hip 0.2.0 (gfx950)"; }
 unsigned int cuda_zstd_hip_kernel_lds_bytes(int which) { return which == 0 ? zh::lz_lds_bytes() : zh::entropy_lds_bytes(); }
 
 }  // extern "C"

@@ -54,5 +54,5 @@ void profile_enable(bool on);
 int profile_collect(double *totals);
 hipError_t launch_plan(const void *const *d_in_ptrs, const size_t *d_in_sizes, u32 nitems, u32 bpi, void *const *d_out_ptrs, u64 out_cap,
                        u8 *staging, ZhBlockDesc *d_descs, ZhItemDesc *d_items, u64 *d_item_size, u32 *d_item_status, u32 extra_flags,
-                       const u8 *dict, u32 dict_n, u32 dict_id, hipStream_t stream);
+                       const u8 *dict, u32 dict_n, u32 dict_id, u32 hist, hipStream_t stream);
 }  // namespace zh

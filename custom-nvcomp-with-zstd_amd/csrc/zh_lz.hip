@@ -357,9 +357,22 @@ extern "C" __global__ __launch_bounds__(K1_THREADS) void zh_lz_kernel(const ZhBl
 #endif
 
   // ---- stage the block into LDS (16 B per lane when the source allows it) and probe RLE
+  // (the probe looks at the block only, never at the history in front of it)
   const u8 *src = d.src;
   bool same = true;
-  if (pre) {  // dictionary tail + block, byte loads; the RLE probe looks at the block only
+  // a history block's prefix is the input right before it: one contiguous region
+  const u8 *const gsrc = (pre && d.pre + pre == src) ? d.pre : (pre ? nullptr : src);
+  if (gsrc && (((uintptr_t)gsrc) & 15) == 0 && (pre & 15) == 0) {
+    u32 const nv = n >> 4, pv = pre >> 4;
+    u8 const first = src[0];
+    u32 const f4 = first * 0x01010101u;
+    for (u32 i = tid; i < nv; i += K1_THREADS) {
+      uint4 v = ((const uint4 *)gsrc)[i];
+      ((uint4 *)in)[i] = v;
+      same &= i < pv || ((v.x == f4) & (v.y == f4) & (v.z == f4) & (v.w == f4));
+    }
+    for (u32 i = (nv << 4) + tid; i < n; i += K1_THREADS) { u8 c = gsrc[i]; in[i] = c; same &= c == first; }
+  } else if (pre) {  // dictionary tail + block, byte loads
     const u8 *const pp = d.pre;
     u8 const first = src[0];
     for (u32 i = tid; i < n; i += K1_THREADS) {
@@ -367,16 +380,6 @@ extern "C" __global__ __launch_bounds__(K1_THREADS) void zh_lz_kernel(const ZhBl
       in[i] = c;
       same &= i < pre || c == first;
     }
-  } else if ((((uintptr_t)src) & 15) == 0) {
-    u32 const nv = n >> 4;
-    u8 const first = src[0];
-    u32 const f4 = first * 0x01010101u;
-    for (u32 i = tid; i < nv; i += K1_THREADS) {
-      uint4 v = ((const uint4 *)src)[i];
-      ((uint4 *)in)[i] = v;
-      same &= (v.x == f4) & (v.y == f4) & (v.z == f4) & (v.w == f4);
-    }
-    for (u32 i = (nv << 4) + tid; i < n; i += K1_THREADS) { u8 c = src[i]; in[i] = c; same &= c == first; }
   } else {
     u8 const first = src[0];
     for (u32 i = tid; i < n; i += K1_THREADS) { u8 c = src[i]; in[i] = c; same &= c == first; }

@@ -27,21 +27,26 @@ void entropy_launch(const ZhBlockDesc *d_descs, u32 nblocks, ZhWorkspace ws, u32
 extern "C" __global__ void zh_plan_kernel(const void *const *__restrict__ in_ptrs, const size_t *__restrict__ in_sizes, u32 nitems,
                                           u32 bpi, void *const *__restrict__ out_ptrs, u64 out_cap, u8 *staging, ZhBlockDesc *descs,
                                           ZhItemDesc *items, u64 *item_size, u32 *item_status, u32 extra_flags,
-                                          const u8 *dict, u32 dict_n, u32 dict_id) {
+                                          const u8 *dict, u32 dict_n, u32 dict_id, u32 hist) {
   u32 const b = blockIdx.x * blockDim.x + threadIdx.x;
   if (b >= nitems * bpi) return;
   u32 const it = b / bpi, k = b % bpi;
   u64 const size = in_sizes[it];
-  u64 const nb = (size + ZH_BLOCK_MAX - 1) / ZH_BLOCK_MAX;
+  u64 const bs = ZH_FRAME_BLOCK(size, dict != nullptr);
+  u64 const nb = (size + bs - 1) / bs;
   ZhBlockDesc d;
-  d.src = (const u8 *)in_ptrs[it] + (u64)k * ZH_BLOCK_MAX;
+  d.src = (const u8 *)in_ptrs[it] + (u64)k * bs;
   d.frame_size = size;
   d.item = it;
-  d.n = (k < nb) ? (u32)min((u64)ZH_BLOCK_MAX, size - (u64)k * ZH_BLOCK_MAX) : 0u;
+  d.n = (k < nb) ? (u32)min(bs, size - (u64)k * bs) : 0u;
   d.flags = (k == 0 ? ZH_F_FIRST : 0u) | (k + 1 == nb ? ZH_F_LAST : 0u) | (nb == 1 ? ZH_F_DIRECT : 0u) | extra_flags;
   d.pre = nullptr;
   d.pre_n = 0;
   d.dict_id = 0;
+  if (k > 0 && hist) {  // history frame: the previous 32 KiB block is staged in front
+    d.pre = d.src - ZH_HIST_BLOCK;
+    d.pre_n = ZH_HIST_BLOCK;
+  }
   if (dict) {  // dictionary frame: the first block is compressed behind the content's tail
     d.flags |= ZH_F_DICT;
     d.dict_id = dict_id;
@@ -217,11 +222,11 @@ hipError_t launch_compress(const ZhBlockDesc *d_descs, u32 nblocks, ZhWorkspace 
 
 hipError_t launch_plan(const void *const *d_in_ptrs, const size_t *d_in_sizes, u32 nitems, u32 bpi, void *const *d_out_ptrs, u64 out_cap,
                        u8 *staging, ZhBlockDesc *d_descs, ZhItemDesc *d_items, u64 *d_item_size, u32 *d_item_status, u32 extra_flags,
-                       const u8 *dict, u32 dict_n, u32 dict_id, hipStream_t stream) {
+                       const u8 *dict, u32 dict_n, u32 dict_id, u32 hist, hipStream_t stream) {
   u32 const total = nitems * bpi;
   if (!total) return hipSuccess;
   hipLaunchKernelGGL(zh_plan_kernel, dim3((total + 255) / 256), dim3(256), 0, stream, d_in_ptrs, d_in_sizes, nitems, bpi, d_out_ptrs, out_cap,
-                     staging, d_descs, d_items, d_item_size, d_item_status, extra_flags, dict, dict_n, dict_id);
+                     staging, d_descs, d_items, d_item_size, d_item_status, extra_flags, dict, dict_n, dict_id, hist);
   return hipGetLastError();
 }
 

@@ -162,14 +162,40 @@ size_t cuda_zstd_hybrid_max_compressed_size(cuda_zstd_hybrid_engine_t *engine, s
 unsigned int cuda_zstd_hybrid_query_routing(cuda_zstd_hybrid_engine_t *engine, size_t data_size, unsigned int input_loc,
                                             unsigned int output_loc, int is_compression);
 
+/* ---------------- streaming (reference ZstdStreamingManager, include/cuda_zstd_manager.h:300-352) ----
+ * No C binding in the reference; added so the streaming path is reachable from C/ctypes.  Every
+ * chunk is a complete frame; with_history = compress_chunk_with_history (the preceding <= 64 KiB
+ * of the stream as raw-content history); decompress_chunk keeps the decoded window, so chunks
+ * decode in stream order.  Device buffers; blocking on return. */
+typedef struct cuda_zstd_stream_t cuda_zstd_stream_t;
+cuda_zstd_stream_t *cuda_zstd_stream_create(int compression_level);
+void cuda_zstd_stream_destroy(cuda_zstd_stream_t *s);
+int cuda_zstd_stream_compress_chunk(cuda_zstd_stream_t *s, const void *src, size_t src_size, void *dst, size_t *dst_size, int with_history,
+                                    int is_last_chunk, hipStream_t stream);
+int cuda_zstd_stream_decompress_chunk(cuda_zstd_stream_t *s, const void *src, size_t src_size, void *dst, size_t *dst_size,
+                                      int *is_last_chunk, hipStream_t stream);
+int cuda_zstd_stream_reset(cuda_zstd_stream_t *s);
+
+/* ---------------- frame metadata (skippable frames) ----------------
+ * A 16-byte skippable frame [0x184D2A50][8][0x444D5A43 "CZMD"][level] in front of frames: the
+ * reference's SkippableFrameHeader + CustomMetadataFrame (src/cuda_zstd_manager.cu:309-318,
+ * writer :391-412).  dst: host or device.  extract: the first zstd frame's header fields after
+ * any skippable frames (reference extract_metadata, src/cuda_zstd_manager.cu:992-1030); level 3
+ * when no metadata frame is present.  Return nvcomp-style codes. */
+int cuda_zstd_write_metadata_frame(void *dst, size_t capacity, int compression_level, size_t *written, hipStream_t stream);
+int cuda_zstd_extract_metadata(const void *src, size_t size, unsigned int *compression_level, unsigned long long *uncompressed_size,
+                               unsigned int *dictionary_id, int *has_checksum);
+
 /* ---------------- library info ---------------- */
 const char *cuda_zstd_hip_version(void);
 /* Per-kernel timing with HIP events recorded on the launch stream (bench.py roofline).
  * collect() waits for the recorded launches and returns their count; ms3[0..2] = summed
- * milliseconds of zh_lz_kernel, zh_entropy_kernel, zh_gather_kernel. */
+ * milliseconds of K1 (zh_lz_kernel), the entropy stage (zh_entropy_kernel +
+ * zh_fse_chain_kernel + zh_seq_pack_kernel) and the frame tail (zh_gather_kernel +
+ * zh_checksum_kernel). */
 void cuda_zstd_hip_profile_enable(int on);
 int cuda_zstd_hip_profile_collect(double *ms3);
-/* LDS bytes requested by the two device kernels (for launch-bound checks in tests). */
+/* LDS bytes requested by K1 (which = 0) and the entropy kernel (1), for launch-bound checks. */
 unsigned int cuda_zstd_hip_kernel_lds_bytes(int which);
 
 #ifdef __cplusplus

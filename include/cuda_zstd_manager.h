@@ -115,6 +115,15 @@ class ZstdBatchManager : public ZstdManager {
                                  int *d_statuses, void *temp_workspace, size_t temp_size, hipStream_t stream);
   static size_t get_batch_device_decompress_temp_size(size_t count, size_t max_uncompressed_chunk_bytes);
 
+  // Streaming history (what the reference's compress_chunk_with_history does by
+  // passing its device window as a raw-content dictionary, src/cuda_zstd_manager.cu:6327-6418):
+  // d_history = device-resident preceding bytes (no copy), used as the frame's history; frames
+  // decode with that history as a raw-content dictionary (libzstd ZSTD_decompress_usingDict too).
+  Status compress_with_history(const void *uncompressed_data, size_t uncompressed_size, void *compressed_data, size_t *compressed_size,
+                               void *temp_workspace, size_t temp_size, const void *d_history, size_t history_size, hipStream_t stream = 0);
+  Status decompress_with_history(const void *compressed_data, size_t compressed_size, void *uncompressed_data, size_t *uncompressed_size,
+                                 void *temp_workspace, size_t temp_size, const void *d_history, size_t history_size, hipStream_t stream = 0);
+
  private:
   class Impl;
   std::unique_ptr<Impl> pimpl_;
@@ -168,6 +177,12 @@ u32 get_optimal_block_size(u32 input_size, u32 compression_level);
 
 constexpr const char *get_format_name() { return "cuda_zstd"; }
 constexpr u32 get_format_version() { return 0x00010000; }
+// reference include/cuda_zstd_manager.h:415-419 (skips leading skippable frames)
+bool is_nvcomp_zstd_format(const void *compressed_data, size_t compressed_size);
+Status extract_metadata(const void *compressed_data, size_t compressed_size, NvcompMetadata &metadata);
+// 16-byte skippable metadata frame (reference SkippableFrameHeader + CustomMetadataFrame,
+// src/cuda_zstd_manager.cu:309-318, 391-412) written to a host or device buffer
+Status write_metadata_frame(void *output, size_t capacity, int compression_level, size_t *written, hipStream_t stream = 0);
 
 }  // namespace cuda_zstd
 #endif  // __cplusplus

@@ -101,6 +101,17 @@ struct CompressionConfig {
   static CompressionConfig get_default();
 };
 
+// reference include/cuda_zstd_types.h:290-298
+struct NvcompMetadata {
+  u32 format_version = 0;
+  u32 compression_level = 0;
+  u64 uncompressed_size = 0;
+  u32 num_chunks = 0;
+  u32 chunk_size = 0;
+  u32 dictionary_id = 0;
+  ChecksumPolicy checksum_policy = ChecksumPolicy::NO_COMPUTE_NO_VERIFY;
+};
+
 struct CompressionStats {
   uint64_t input_bytes = 0;
   uint64_t output_bytes = 0;

@@ -13,6 +13,13 @@
 #define ZSTD_HIP_PARAMS_H_
 
 #define ZH_BLOCK_MAX 65536          /* bytes per device block (one workgroup) */
+#define ZH_HIST_BLOCK 32768         /* device block of a history frame (below) */
+#define ZH_HIST_WINDOW_LOG 16       /* history needs a window of >= 64 KiB */
+/* Device block size of a frame of n bytes: frames up to 64 KiB are one
+ * block; larger frames, and dictionary frames over 32 KiB, are cut into 32 KiB blocks that are
+ * each staged behind the 32 KiB before them (the previous block, or the dictionary's tail for
+ * the first), so matches reach across block boundaries within the 64 KiB of LDS. */
+#define ZH_FRAME_BLOCK(n, dict) ((((n) <= ZH_BLOCK_MAX) && !((dict) && (n) > ZH_HIST_BLOCK)) ? ZH_BLOCK_MAX : ZH_HIST_BLOCK)
 #define ZH_TILE 128                 /* hash insertion granularity (positions) */
 #define ZH_WINDOW 4096              /* parse window (positions) */
 #define ZH_SEG 16                   /* positions per thread in the parse */

@@ -1055,8 +1055,9 @@ size_t orc_compress_frame_dict(u8 *dst, size_t cap, const u8 *src, u64 n, u32 bl
   if (checksum) dst[4] |= 0x04;
   u64 pos = 0;
   u32 b = 0;
+  u32 const bs = ZH_FRAME_BLOCK(n, dict_n != 0);
   do {
-    u32 bn = (u32)((n - pos) < ZH_BLOCK_MAX ? (n - pos) : ZH_BLOCK_MAX);
+    u32 bn = (u32)((n - pos) < bs ? (n - pos) : bs);
     u32 rep[3] = {1, 4, 8};
     if (b > 0 || dict_n) { rep[0] = rep[1] = rep[2] = 0; }
     size_t w;
@@ -1068,6 +1069,9 @@ size_t orc_compress_frame_dict(u8 *dst, size_t cap, const u8 *src, u64 n, u32 bl
       memcpy(buf + pre, src, bn);
       w = orc_compress_block_pre(dst + o, cap - o, buf, pre, bn, pos + bn >= n, rep);
       free(buf);
+    } else if (b > 0 && window_log >= ZH_HIST_WINDOW_LOG) {
+      /* history: the previous 32 KiB block is hashed and matched against, never parsed */
+      w = orc_compress_block_pre(dst + o, cap - o, src + pos - ZH_HIST_BLOCK, ZH_HIST_BLOCK, bn, pos + bn >= n, rep);
     } else {
       w = orc_compress_block(dst + o, cap - o, src + pos, bn, pos + bn >= n, rep);
     }

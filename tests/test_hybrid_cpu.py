@@ -61,3 +61,21 @@ def test_c1_force_cpu_roundtrip(libzstd):
         assert rc == 0 and bsz.value == data.size and np.array_equal(back, data)
     finally:
         L.cuda_zstd_hybrid_destroy(e)
+
+
+def test_metadata_frame_host():
+    """Skippable metadata frame (reference SkippableFrameHeader + CustomMetadataFrame,
+    src/cuda_zstd_manager.cu:309-318, 391-412): libzstd skips it, extract_metadata reads the
+    level and the following frame's header (host buffers, no GPU)."""
+    import cuda_zstd
+
+    data = T.gen(T.DG_TEXT, 1, 5, 100000)
+    meta = cuda_zstd.metadata_frame(9)
+    assert len(meta) == 16 and meta[:4] == bytes.fromhex("502a4d18")
+    frame = T.oracle_frame(data, checksum=True)
+    blob = meta + frame
+    if T.zstd() is not None:
+        assert T.zstd_decompress(blob, len(data)) == data.tobytes()
+    m = cuda_zstd.extract_metadata(blob)
+    assert m == {"level": 9, "uncompressed_size": len(data), "dictionary_id": 0, "checksum": True}
+    assert cuda_zstd.extract_metadata(frame)["level"] == 3
