@@ -139,6 +139,7 @@ namespace {
 constexpr u32 kSkippableMagic = 0x184D2A50u;  // RFC 8878 skippable frames 0x184D2A50..5F
 constexpr u32 kMetadataMagic = 0x444D5A43u;   // "CZMD": this library's metadata frame
 constexpr size_t kMetadataFrameBytes = 16;
+constexpr int kLazy2Level = 9;  // levels >= 9 (LAZY and up, reference src/cuda_zstd_types.cpp:172-182) parse LAZY2 on the device
 struct LibZstd {
   size_t (*compress)(void *, size_t, const void *, size_t, int) = nullptr;
   size_t (*decompress)(void *, size_t, const void *, size_t) = nullptr;
@@ -475,7 +476,7 @@ class ZstdBatchManager::Impl {
     hipError_t e = zh::launch_compress((const ZhBlockDesc *)(base + L.descs), (u32)nblocks, ws, config.window_log, config.block_size,
                                        (u64 *)(base + L.item_size), (u32 *)(base + L.item_status), (u32 *)(base + L.blk_size),
                                        (const ZhItemDesc *)(base + L.items), (u32)count, staged,
-                                       config.checksum != ChecksumPolicy::NO_COMPUTE_NO_VERIFY, stream);
+                                       config.checksum != ChecksumPolicy::NO_COMPUTE_NO_VERIFY, config.level >= kLazy2Level, stream);
     if (e != hipSuccess) return Status::ERROR_CUDA_ERROR;
     u64 *h_size = (u64 *)(h + up_bytes);
     u32 *h_status = (u32 *)(h_size + count);
@@ -850,7 +851,8 @@ Status ZstdBatchManager::compress_batch_device(const void *const *d_in_ptrs, con
   if (e != hipSuccess) return Status::ERROR_CUDA_ERROR;
   ZhWorkspace ws{base + L.blocks};
   e = zh::launch_compress((const ZhBlockDesc *)(base + L.descs), (u32)nblocks, ws, pimpl_->config.window_log, pimpl_->config.block_size, item_size,
-                          item_status, (u32 *)(base + L.blk_size), (const ZhItemDesc *)(base + L.items), (u32)count, bpi > 1, ck, stream);
+                          item_status, (u32 *)(base + L.blk_size), (const ZhItemDesc *)(base + L.items), (u32)count, bpi > 1, ck,
+                          pimpl_->config.level >= kLazy2Level, stream);
   return e == hipSuccess ? Status::SUCCESS : Status::ERROR_CUDA_ERROR;
 }
 

@@ -48,7 +48,7 @@ hipError_t init_kernels();
 u32 lz_lds_bytes();
 u32 entropy_lds_bytes();
 hipError_t launch_compress(const ZhBlockDesc *d_descs, u32 nblocks, ZhWorkspace ws, u32 window_log, u32 cfg_block_size, u64 *d_item_size,
-                           u32 *d_item_status, u32 *d_blk_size, const ZhItemDesc *d_items, u32 nitems, bool gather, bool checksum,
+                           u32 *d_item_status, u32 *d_blk_size, const ZhItemDesc *d_items, u32 nitems, bool gather, bool checksum, bool lazy2,
                            hipStream_t stream);
 void profile_enable(bool on);
 int profile_collect(double *totals);

@@ -206,9 +206,9 @@ __device__ __forceinline__ void insert_window(const u32 *in32, u16 *T, u32 wsb, 
   // the next window's first position (lazy rule at this window's end): looked up
   // after all of this window's tiles, before any of the next window's
   cwe = 0;
-  if (lane == 0 && we < lim) {
+  if (lane < 2 && we + lane < lim) {  // (lane 1: we + 1, the second lookahead of LAZY2)
     u32 lo, hi;
-    ld64u(in32, we, lo, hi);
+    ld64u(in32, we + lane, lo, hi);
     cwe = T[hash_of<LONG>(lo, hi)];
   }
   __asm__ volatile("" ::: "memory");
@@ -229,7 +229,7 @@ __device__ __forceinline__ void dump_window(u8 *ci8, u32 lane_, const u32 (&creg
       *(u16 *)(ci8 + 4 * cidx(i) + (LONG ? 0 : 2)) = v;
     }
   }
-  if (lane == 0) *(u16 *)(ci8 + 4 * cidx(ZH_WINDOW) + (LONG ? 0 : 2)) = (u16)cwe;
+  if (lane < 2) *(u16 *)(ci8 + 4 * cidx(ZH_WINDOW + lane) + (LONG ? 0 : 2)) = (u16)cwe;
 }
 
 // Lane-per-position parse steps for window index i (a wave's 64 lanes = one parse
@@ -240,7 +240,17 @@ __device__ __forceinline__ void dump_window(u8 *ci8, u32 lane_, const u32 (&creg
 // v from lane `src` (< 64) of the wave: ds_bpermute on a byte address, no lane-base math
 __device__ __forceinline__ u32 bperm(u32 v, u32 src) { return (u32)__builtin_amdgcn_ds_bpermute((int)(src << 2), (int)v); }
 
-__device__ __forceinline__ u32 parse_steps(const u32 *ci, u32 i, u32 wn, u32 la, u32 lane, u32 (&X)[7]) {
+// Parse cost of a match: libzstd's lazy "gain" (4 per byte, minus the offset's bit length)
+__device__ __forceinline__ int match_gain(u32 inf) {
+  return inf ? 4 * (int)(inf & 255u) - (31 - (int)__builtin_clz((inf >> 8) + 1u)) : -1000;
+}
+
+// LAZY2 (levels >= 9): a match at i is deferred when the match at i+1 gains
+// more than 4 over it or the one at i+2 more than 7 (libzstd ZSTD_compressBlock_lazy_generic,
+// depth 2); otherwise (levels < 9) when the match at i+1 is longer.  la / la2: the match info
+// of the next window's first two positions.
+template <bool LAZY2>
+__device__ __forceinline__ u32 parse_steps(const u32 *ci, u32 i, u32 wn, u32 la, u32 la2, u32 lane, u32 (&X)[7]) {
   u32 const sb = i & ~63u;
   u32 const slen = wn > sb ? min(64u, wn - sb) : 0u;
   // unconditional (clamped) loads, then selects: no exec-mask branches
@@ -248,7 +258,15 @@ __device__ __forceinline__ u32 parse_steps(const u32 *ci, u32 i, u32 wn, u32 la,
   u32 const inf = i < wn ? r0 : 0u;
   u32 const inf1 = i + 1 < wn ? r1 : la;
   u32 const l = inf & 255u;
-  bool const tk = l != 0 && (inf1 & 255u) <= l;
+  bool tk;
+  if (LAZY2) {
+    u32 const r2 = ci[min(i + 2, (u32)ZH_WINDOW + 1)];
+    u32 const inf2 = i + 2 < wn ? r2 : (i + 2 == wn ? la : la2);
+    int const g0 = match_gain(inf);
+    tk = l != 0 && match_gain(inf1) <= g0 + 4 && match_gain(inf2) <= g0 + 7;
+  } else {
+    tk = l != 0 && (inf1 & 255u) <= l;
+  }
   u32 x = lane + (tk ? l : 1u);
   if (__ballot(tk)) {
 #pragma unroll
@@ -327,7 +345,8 @@ __device__ __forceinline__ void inserter_loop(const u32 *in32, u16 *T, u8 *ci8, 
 #define ZH_STAMP(acc) do { } while (0)
 #endif
 
-extern "C" __global__ __launch_bounds__(K1_THREADS) void zh_lz_kernel(const ZhBlockDesc *__restrict__ blocks, ZhWorkspace ws) {
+template <bool LAZY2>
+__device__ __forceinline__ void lz_block(const ZhBlockDesc *__restrict__ blocks, ZhWorkspace ws) {
   extern __shared__ __attribute__((aligned(16))) u8 smem[];
   u8 *in = smem + OFF_IN;
   u32 *in32 = (u32 *)in;
@@ -438,7 +457,7 @@ extern "C" __global__ __launch_bounds__(K1_THREADS) void zh_lz_kernel(const ZhBl
       // thread tid < NB: positions [s, se) of the window; thread NB: position `we`;
       // threads above NB take part in the wave-level steps with no positions
       u32 const s = tid < NB ? wsb + SB * tid : we;
-      u32 const se = tid < NB ? min(s + SB, we) : (tid == NB ? min(we + 1, n) : s);
+      u32 const se = tid < NB ? min(s + SB, we) : (tid == NB ? min(we + 2, n) : s);  // (we, we+1: lookahead)
       u32 const cbase = tid < NB ? SB * tid : ZH_WINDOW;  // window index of position s
       // (1) candidates, own bytes and first-8-byte prefixes; loads unconditional
       u32 cv[SB], plp = 0, psp = 0;  // prefixes packed 4 bits per position
@@ -565,9 +584,10 @@ extern "C" __global__ __launch_bounds__(K1_THREADS) void zh_lz_kernel(const ZhBl
         u32 v = 0;
         if (lL && lL >= lS) v = ((p - (cL - 1)) << 8) | lL;
         else if (lS) v = ((p - (cS - 1)) << 8) | lS;
-        ci[p < se ? cidx(cbase + j) : ZH_WINDOW + 1 + j] = v;  // (past the run: junk slots)
+        ci[p < se ? cidx(cbase + j) : ZH_WINDOW + 2 + j] = v;  // (past the run: junk slots)
       }
-      if (tid == NB && we >= n) ci[cidx(ZH_WINDOW)] = 0;  // no position after the block
+      if (tid == NB && we >= n) ci[cidx(ZH_WINDOW)] = 0;          // no position after the block
+      if (tid == NB && we + 1 >= n) ci[cidx(ZH_WINDOW + 1)] = 0;
 #undef PL
 #undef PS
     }
@@ -582,6 +602,7 @@ extern "C" __global__ __launch_bounds__(K1_THREADS) void zh_lz_kernel(const ZhBl
     if (tid == 0) { st_Bmax += misc[8]; st_Imax += misc[9]; misc[8] = 0; misc[9] = 0; }
 #endif
     u32 const info_ahead = __builtin_amdgcn_readfirstlane(ci[cidx(ZH_WINDOW)]);
+    u32 const info_ahead2 = LAZY2 ? __builtin_amdgcn_readfirstlane(ci[cidx(ZH_WINDOW + 1)]) : 0u;
 
     // ---- parse.  Lanes = positions (PR rounds of the 896 worker lanes); each wave's 64
     // lanes are one parse segment of 64 positions.  step(p) = next position the greedy /
@@ -595,7 +616,7 @@ extern "C" __global__ __launch_bounds__(K1_THREADS) void zh_lz_kernel(const ZhBl
     for (u32 rr = 0; rr < PR; rr++) {
       u32 const i = INS_TID * rr + tid;
       u32 X[7];
-      infr[rr] = parse_steps(ci, i, wn, la, lane, X);
+      infr[rr] = parse_steps<LAZY2>(ci, i, wn, la, info_ahead2, lane, X);
 #pragma unroll
       for (u32 k = 0; k < 6; k++) xk[rr][k] = X[k];
       exb[i < wn ? i : (u32)ZH_WINDOW] = (u8)X[6];  // (past the window: junk byte)
@@ -708,11 +729,24 @@ extern "C" __global__ __launch_bounds__(K1_THREADS) void zh_lz_kernel(const ZhBl
 #endif
 }
 
+// level < 9: greedy + lazy-1; level >= 9: LAZY2 (the same kernel body, one instantiation each)
+extern "C" __global__ __launch_bounds__(K1_THREADS) void zh_lz_kernel(const ZhBlockDesc *__restrict__ blocks, ZhWorkspace ws) {
+  lz_block<false>(blocks, ws);
+}
+extern "C" __global__ __launch_bounds__(K1_THREADS) void zh_lz_lazy2_kernel(const ZhBlockDesc *__restrict__ blocks, ZhWorkspace ws) {
+  lz_block<true>(blocks, ws);
+}
+
 extern "C" u32 zh_lz_lds_bytes() { return K1_LDS; }
 
 namespace zh {
-hipError_t lz_init() { return hipFuncSetAttribute((const void *)zh_lz_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)K1_LDS); }
-void lz_launch(const ZhBlockDesc *d_descs, u32 nblocks, ZhWorkspace ws, hipStream_t stream) {
-  hipLaunchKernelGGL(zh_lz_kernel, dim3(nblocks), dim3(K1_THREADS), K1_LDS, stream, d_descs, ws);
+hipError_t lz_init() {
+  hipError_t e = hipFuncSetAttribute((const void *)zh_lz_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)K1_LDS);
+  if (e != hipSuccess) return e;
+  return hipFuncSetAttribute((const void *)zh_lz_lazy2_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)K1_LDS);
+}
+void lz_launch(const ZhBlockDesc *d_descs, u32 nblocks, ZhWorkspace ws, bool lazy2, hipStream_t stream) {
+  if (lazy2) hipLaunchKernelGGL(zh_lz_lazy2_kernel, dim3(nblocks), dim3(K1_THREADS), K1_LDS, stream, d_descs, ws);
+  else hipLaunchKernelGGL(zh_lz_kernel, dim3(nblocks), dim3(K1_THREADS), K1_LDS, stream, d_descs, ws);
 }
 }  // namespace zh

@@ -18,7 +18,7 @@ extern "C" u32 zh_lz_lds_bytes();
 extern "C" u32 zh_entropy_lds_bytes();
 namespace zh {
 hipError_t lz_init();
-void lz_launch(const ZhBlockDesc *d_descs, u32 nblocks, ZhWorkspace ws, hipStream_t stream);
+void lz_launch(const ZhBlockDesc *d_descs, u32 nblocks, ZhWorkspace ws, bool lazy2, hipStream_t stream);
 hipError_t entropy_init();
 void entropy_launch(const ZhBlockDesc *d_descs, u32 nblocks, ZhWorkspace ws, u32 window_log, u32 cfg_block_size, u64 *d_item_size,
                     u32 *d_item_status, u32 *d_blk_size, hipStream_t stream);
@@ -197,7 +197,7 @@ int profile_collect(double *totals) {
 }
 
 hipError_t launch_compress(const ZhBlockDesc *d_descs, u32 nblocks, ZhWorkspace ws, u32 window_log, u32 cfg_block_size, u64 *d_item_size,
-                           u32 *d_item_status, u32 *d_blk_size, const ZhItemDesc *d_items, u32 nitems, bool gather, bool checksum,
+                           u32 *d_item_status, u32 *d_blk_size, const ZhItemDesc *d_items, u32 nitems, bool gather, bool checksum, bool lazy2,
                            hipStream_t stream) {
   if (nblocks == 0) return hipSuccess;
   std::vector<hipEvent_t> ev;
@@ -206,7 +206,7 @@ hipError_t launch_compress(const ZhBlockDesc *d_descs, u32 nblocks, ZhWorkspace 
     if (prof().on) for (int k = 0; k < 4; k++) ev.push_back(prof_event());
   }
   if (!ev.empty()) (void)hipEventRecord(ev[0], stream);
-  lz_launch(d_descs, nblocks, ws, stream);
+  lz_launch(d_descs, nblocks, ws, lazy2, stream);
   if (!ev.empty()) (void)hipEventRecord(ev[1], stream);
   entropy_launch(d_descs, nblocks, ws, window_log, cfg_block_size, d_item_size, d_item_status, d_blk_size, stream);
   if (!ev.empty()) (void)hipEventRecord(ev[2], stream);

@@ -832,14 +832,30 @@ void orc_lz_match_info(const u8 *src, u32 n, u8 *len, u16 *off) {
 /* Parse + merge over src[0, n).  Positions [0, pre) are dictionary history:
  * hashed and matched against like any other, but the parse starts at pre.
  * Returns number of sequences; *last_lits = trailing literals. */
+/* Parse strategy: 0 = greedy with a one-position lazy check (levels < 9); 1 = LAZY2 (levels
+ * >= 9; the reference maps level 9 to LAZY, src/cuda_zstd_types.cpp:172-182):
+ * libzstd ZSTD_compressBlock_lazy_generic's depth-2 rule on this matcher's candidates -- the
+ * match at p is deferred when the match at p+1 gains more than 4, or the one at p+2 more than 7,
+ * with gain = 4 x length - bit length of (offset + 1).  Set by orc_compress_frame_lv. */
+static int orc_parse_lazy2 = 0;
+static int match_gain(const u8 *len, const u16 *off, u32 p) {
+  return len[p] ? 4 * (int)len[p] - (31 - __builtin_clz((u32)off[p] + 1u)) : -1000;
+}
 size_t orc_lz_parse_pre(const u8 *src, u32 pre, u32 n, orc_seq_t *seq, u32 *last_lits) {
-  u8 *len = malloc(n + 1);
-  u16 *off = malloc(sizeof(u16) * (n + 1));
+  u8 *len = malloc(n + 2);
+  u16 *off = malloc(sizeof(u16) * (n + 2));
   orc_lz_match_info(src, n, len, off);
+  len[n + 1] = 0; off[n + 1] = 0;
   size_t ns = 0;
   u32 p = pre, anchor = pre, lim = n > ZH_HASH_READ ? n - ZH_HASH_READ : 0;
   while (p < lim) {
-    if (len[p] == 0 || len[p + 1] > len[p]) { p++; continue; }
+    int defer;
+    if (len[p] == 0) defer = 1;
+    else if (orc_parse_lazy2) {
+      int const g0 = match_gain(len, off, p);
+      defer = match_gain(len, off, p + 1) > g0 + 4 || match_gain(len, off, p + 2) > g0 + 7;
+    } else defer = len[p + 1] > len[p];
+    if (defer) { p++; continue; }
     u32 ll = p - anchor;
     if (ns && ll == 0 && seq[ns - 1].off == off[p]) seq[ns - 1].ml += len[p]; /* continuation merge */
     else { seq[ns].ll = ll; seq[ns].ml = len[p]; seq[ns].off = off[p]; ns++; }
@@ -1088,6 +1104,15 @@ size_t orc_compress_frame_dict(u8 *dst, size_t cap, const u8 *src, u64 n, u32 bl
 }
 size_t orc_compress_frame_ck(u8 *dst, size_t cap, const u8 *src, u64 n, u32 block_size, u32 window_log, int checksum) {
   return orc_compress_frame_dict(dst, cap, src, n, block_size, window_log, checksum, NULL, 0);
+}
+/* The frame at a compression level: levels >= 9 parse LAZY2 (the device's zh_lz_lazy2_kernel). */
+size_t orc_compress_frame_lv(u8 *dst, size_t cap, const u8 *src, u64 n, u32 block_size, u32 window_log, int checksum, const u8 *dict,
+                             size_t dict_n, int level) {
+  int const save = orc_parse_lazy2;
+  orc_parse_lazy2 = level >= 9;
+  size_t const r = orc_compress_frame_dict(dst, cap, src, n, block_size, window_log, checksum, dict, dict_n);
+  orc_parse_lazy2 = save;
+  return r;
 }
 
 size_t orc_max_compressed_size(u64 n) {

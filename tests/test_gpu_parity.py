@@ -263,3 +263,19 @@ def test_full_size_blocks_match_libzstd(torch_cuda, mgr):
         fhd = fr[4]
         hs = 5 + (0 if (fhd >> 5) & 1 else 1) + [0, 1, 2, 4][fhd & 3] + [1 if (fhd >> 5) & 1 else 0, 2, 4, 8][fhd >> 6]
         assert fr[hs:].hex() == c["libzstd_block"], c["name"]
+
+
+@pytest.mark.parametrize("level", [9, 19])
+def test_lazy2_levels_match_oracle(torch_cuda, level):
+    """Levels >= 9 run the LAZY2 parse (zh_lz_lazy2_kernel): frames equal the
+    oracle's at that level and decode with libzstd; ragged and multi-block sizes included."""
+    import cuda_zstd
+
+    m = cuda_zstd.Manager(level)
+    datas = [T.gen(k, 1, 40 + k, s) for k, s in ((T.DG_JSON, 65536), (T.DG_TEXT, 65536), (T.DG_MIX, 65536), (T.DG_SOURCE, 40000),
+                                                (T.DG_CSV, 300000), (T.DG_EXE, 777), (T.DG_SENSOR, 65535))]
+    outs = m.compress_batch([torch_cuda.from_numpy(d).cuda() for d in datas])
+    for k, (o, d) in enumerate(zip(outs, datas)):
+        got = o.cpu().numpy().tobytes()
+        assert got == T.oracle_frame(d, level=level), k
+        assert T.zstd_decompress(got, len(d)) == d.tobytes(), k

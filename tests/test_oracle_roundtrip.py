@@ -52,3 +52,16 @@ def test_ratio_vs_libzstd_level3(libzstd):
         src = np.ascontiguousarray(data[i * 65536:(i + 1) * 65536])
         ref += libzstd.ZSTD_compress(out.ctypes.data_as(ctypes.c_void_p), ctypes.c_size_t(80000), src.ctypes.data_as(ctypes.c_void_p), ctypes.c_size_t(65536), 3)
     assert ref / ours > 0.90
+
+
+def test_lazy2_parse_roundtrip_and_gain(libzstd):
+    """Level >= 9 (LAZY2 parse): frames decode with libzstd and the parse gains on JSON records."""
+    data = T.gen(T.DG_JSON, 8, 0x5EED0005, 16384)
+    l3 = l9 = 0
+    for i in range(8):
+        c = data[i * 16384:(i + 1) * 16384]
+        f9 = T.oracle_frame(c, level=9)
+        assert T.zstd_decompress(f9, len(c)) == c.tobytes()
+        l9 += len(f9)
+        l3 += len(T.oracle_frame(c))
+    assert l9 < l3

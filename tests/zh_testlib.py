@@ -40,6 +40,9 @@ def oracle():
         L.orc_compress_frame_dict.restype = ctypes.c_size_t
         L.orc_compress_frame_dict.argtypes = [vp, ctypes.c_size_t, vp, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_int, vp,
                                               ctypes.c_size_t]
+        L.orc_compress_frame_lv.restype = ctypes.c_size_t
+        L.orc_compress_frame_lv.argtypes = [vp, ctypes.c_size_t, vp, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_int, vp,
+                                            ctypes.c_size_t, ctypes.c_int]
         L.orc_dict_layout.restype = ctypes.c_int
         L.orc_dict_layout.argtypes = [vp, ctypes.c_size_t, ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(ctypes.c_size_t)]
         L.orc_xxh64.restype = ctypes.c_uint64
@@ -86,13 +89,20 @@ def gen(kind, nchunks, seed, chunk_size=65536, first=0):
     return a
 
 
-def oracle_frame(data, block_size=128 * 1024, window_log=19, checksum=False, dictionary=None, level=3):
+def level_window_log(level):
+    """Window log of a level (apply_level_parameters, zh_host.cpp; reference src/cuda_zstd_types.cpp:860-950)."""
+    return 18 if level <= 1 else 19 if level <= 3 else 20 if level <= 6 else 22 if level <= 9 else 23
+
+
+def oracle_frame(data, block_size=128 * 1024, window_log=None, checksum=False, dictionary=None, level=3):
+    if window_log is None:
+        window_log = level_window_log(level)
     data = np.ascontiguousarray(np.frombuffer(bytes(data), np.uint8) if not isinstance(data, np.ndarray) else data)
     cap = int(oracle().orc_max_compressed_size(ctypes.c_uint64(len(data)))) + 64
     out = np.zeros(cap, np.uint8)
     d = np.frombuffer(bytes(dictionary), np.uint8).copy() if dictionary else None
-    n = oracle().orc_compress_frame_dict(out.ctypes.data_as(vp), cap, data.ctypes.data_as(vp), len(data), block_size, window_log, int(checksum),
-                                         d.ctypes.data_as(vp) if d is not None else None, 0 if d is None else len(d))
+    n = oracle().orc_compress_frame_lv(out.ctypes.data_as(vp), cap, data.ctypes.data_as(vp), len(data), block_size, window_log, int(checksum),
+                                       d.ctypes.data_as(vp) if d is not None else None, 0 if d is None else len(d), level)
     assert n > 0
     return out[:n].tobytes()
 
