@@ -109,6 +109,8 @@ __device__ __forceinline__ u32 ext_head(const u32 *in32, u32 p, u32 q, u32 n) {
   u32 l = EXT_SPAN;
 #pragma unroll
   for (u32 h0 = 0; h0 < NW; h0 += H) {
+    // the second half only when some lane's match reaches past the first one
+    if (h0 && !__ballot(l == EXT_SPAN)) break;
     u32 A[H + 1], B[H + 1];
 #pragma unroll
     for (u32 k = 0; k <= H; k++) { A[k] = in32[wp + h0 + k]; B[k] = in32[wq + h0 + k]; }
@@ -453,7 +455,8 @@ __device__ __forceinline__ void lz_block(const ZhBlockDesc *__restrict__ blocks,
 #endif
 
     // ---- match lengths (threads 0..NB), while the inserter waves build the next window
-    {
+    // (a worker wave without positions skips the phase: wave-uniform)
+    if ((tid & ~63u) <= NB) {
       // thread tid < NB: positions [s, se) of the window; thread NB: position `we`;
       // threads above NB take part in the wave-level steps with no positions
       u32 const s = tid < NB ? wsb + SB * tid : we;
