@@ -1696,6 +1696,10 @@ int nvcomp_zstd_batch_compress_async_v5(nvcomp_zstd_batch_manager_t *m, const vo
   return status_to_nvcomp_error(m->mgr->compress_async(in, in_sizes, n, out, out_sizes, t, tb, s));
 }
 size_t nvcomp_zstd_batched_compress_get_temp_size_v5(size_t n, size_t max_chunk) { return ZstdBatchManager::get_batch_device_temp_size(n, max_chunk); }
+int nvcomp_zstd_batch_set_dictionary_v5(nvcomp_zstd_batch_manager_t *m, cuda_zstd_dict_t *d) {
+  if (!m || !m->mgr || !d || !d->dict) return status_to_nvcomp_error(Status::ERROR_INVALID_PARAMETER);
+  return status_to_nvcomp_error(m->mgr->batch_manager().set_dictionary(*d->dict));
+}
 int nvcomp_zstd_batched_compress_async_v5(nvcomp_zstd_batch_manager_t *m, const void *const *d_in, const size_t *d_in_sizes, size_t max_chunk,
                                           size_t n, void *const *d_out, size_t *d_out_sizes, int *d_statuses, void *t, size_t tb, hipStream_t s) {
   if (!m || !m->mgr) return status_to_nvcomp_error(Status::ERROR_INVALID_PARAMETER);
