@@ -30,6 +30,18 @@
 //                 the marks place literals and sequence records.
 #include "zh_common.h"
 
+#ifdef ZH_STAMPS
+__device__ u32 g_fixups;  // diagnostic: inserter read-back fix-up rounds (all blocks)
+extern "C" __global__ void zh_read_fixups(u32 *out) { *out = g_fixups; g_fixups = 0; }
+extern "C" u32 zh_fixups_host() {
+  u32 *d = nullptr, h = 0;
+  if (hipMalloc(&d, 4) != hipSuccess) return ~0u;
+  hipLaunchKernelGGL(zh_read_fixups, dim3(1), dim3(1), 0, 0, d);
+  (void)hipMemcpy(&h, d, 4, hipMemcpyDeviceToHost);
+  (void)hipFree(d);
+  return h;
+}
+#endif
 namespace {
 
 constexpr u32 K1_THREADS = 1024;
@@ -140,69 +152,118 @@ __device__ __forceinline__ u32 hash_of(u32 lo, u32 hi) {
 // slot back and lanes that find an earlier position rewrite theirs until none does: the
 // slot ends with the latest position, as in the oracle's serial loop.  Candidates
 // (position + 1, 0 = none) go to creg as u16 pairs.
+// Repair path of insert_window for a batch in which some lane of a ds_write_b16 lost its
+// slot to a LOWER position of the same store (never observed on gfx950, where the highest
+// lane of a store wins, but kept so the table semantics never depend on it).  The batch's
+// lookups of tile b >= 1 were issued after the earlier tiles' unrepaired stores: the correct
+// value is the max of that and every earlier-tile position of the batch hashing to the same
+// slot.  Then every lost store is rewritten while its slot holds an older position (slots only
+// ever move forward, so later tiles' stores are never undone).
+template <bool LONG, u32 BT>
+__device__ __forceinline__ void insert_repair(u16 *T, u32 tb0, u32 lane, const u32 (&h)[BT][TPL], u32 (&e)[BT][TPL]) {
+  constexpr u32 JUNK = LONG ? HL_SIZE : HS_SIZE;
+  for (u32 b = 1; b < BT; b++)
+    for (u32 bb = 0; bb < b; bb++)
+      for (u32 kk = 0; kk < TPL; kk++)
+        for (u32 j = 0; j < 64; j++) {
+          u32 const hj = __builtin_amdgcn_readlane(h[bb][kk], j);
+          u32 const pj = tb0 + bb * ZH_TILE + 64 * kk + j + 1;
+#pragma unroll
+          for (u32 k = 0; k < TPL; k++)
+            if (hj != JUNK && h[b][k] == hj && e[b][k] < pj) e[b][k] = pj;
+        }
+  for (;;) {
+    bool need = false;
+#pragma unroll
+    for (u32 b = 0; b < BT; b++)
+#pragma unroll
+      for (u32 k = 0; k < TPL; k++) {
+        u32 const v = tb0 + b * ZH_TILE + 64 * k + lane + 1;
+        if (h[b][k] != JUNK && (u32)T[h[b][k]] < v) {
+          T[h[b][k]] = (u16)v;
+          need = true;
+        }
+      }
+    if (!__ballot(need)) break;
+  }
+}
+
+// Inserter wave: the tiles of window [wsb, we) against one table (u16 entries = position
+// + 1).  Lane l handles positions tb + l + 64k of each tile; a tile's lookups are issued
+// before its stores and after the previous tile's stores (program order = LDS order within a
+// wave).  Stores of later k / later tiles carry later positions and land later; lanes of ONE
+// store that hit the same slot leave one of their values (on gfx950 the highest lane's, i.e.
+// the latest position, as in the oracle's serial loop), which a read-back of every lane's
+// slot verifies (insert_repair otherwise).  BT tiles are issued per LDS round trip together
+// with the next batch's input dwords and the workers' arrival counter.  Candidates
+// (position + 1, 0 = none) go to creg as u16 pairs.
 template <bool LONG, typename Hook>
 __device__ __forceinline__ void insert_window(const u32 *in32, u16 *T, u32 wsb, u32 we, u32 lim, u32 lane, u32 (&creg)[NCR], u32 &cwe,
                                               const u32 *arrivals, Hook &&between_tiles) {
   constexpr u32 JUNK = LONG ? HL_SIZE : HS_SIZE;
-  // Software pipeline: the input dwords of tile t+1 and the workers' arrival counter are
-  // read together with tile t's table read-back, so a tile costs one LDS round trip.
-  u32 wv[TPL][3];
-  auto load_in = [&](u32 tb, u32 lim_t, u32 (&w)[TPL][3]) {
+  constexpr u32 BT = 2;  // tiles per LDS round trip
+  static_assert(TILES % BT == 0, "batches tile windows");
+  u32 wv[BT][TPL][3];
+  auto load_in = [&](u32 tb0, u32 lim_t) {
 #pragma unroll
-    for (u32 k = 0; k < TPL; k++) {
-      u32 const q = min(tb + 64 * k + lane, lim_t) >> 2;
-      w[k][0] = in32[q];
-      w[k][1] = in32[q + 1];
-      w[k][2] = in32[q + 2];
-    }
+    for (u32 b = 0; b < BT; b++)
+#pragma unroll
+      for (u32 k = 0; k < TPL; k++) {
+        u32 const q = min(tb0 + b * ZH_TILE + 64 * k + lane, lim_t) >> 2;
+        wv[b][k][0] = in32[q];
+        wv[b][k][1] = in32[q + 1];
+        wv[b][k][2] = in32[q + 2];
+      }
   };
-  load_in(wsb, lim, wv);
+  load_in(wsb, lim);
 #pragma unroll
-  for (u32 t = 0; t < TILES; t++) {
-    // opaque per-tile copy of lim: keeps the compiler from hoisting every tile's
+  for (u32 t0 = 0; t0 < TILES; t0 += BT) {
+    // opaque per-batch copy of lim: keeps the compiler from hoisting every tile's
     // bounds checks (64 masks) to the top of the unrolled loop
     u32 lim_t;
     __asm__ volatile("v_mov_b32 %0, %1" : "=v"(lim_t) : "v"(lim));
-    u32 const tb = wsb + t * ZH_TILE;
-    u32 h[TPL], e[TPL];
+    u32 const tb0 = wsb + t0 * ZH_TILE;
+    u32 h[BT][TPL], e[BT][TPL], r[BT][TPL];
 #pragma unroll
-    for (u32 k = 0; k < TPL; k++) {
-      u32 const p = tb + 64 * k + lane, sh = min(p, lim_t) & 3u;
-      u32 const lo = __builtin_amdgcn_alignbyte(wv[k][1], wv[k][0], sh), hi = __builtin_amdgcn_alignbyte(wv[k][2], wv[k][1], sh);
-      u32 const hh = hash_of<LONG>(lo, hi);
-      e[k] = T[hh];
-      h[k] = p < lim_t ? hh : JUNK;
-    }
-#pragma unroll
-    for (u32 k = 0; k < TPL; k++) T[h[k]] = (u16)(tb + 64 * k + lane + 1);
-    u32 r[TPL];
-#pragma unroll
-    for (u32 k = 0; k < TPL; k++) r[k] = T[h[k]];
-    if (t + 1 < TILES) load_in(tb + ZH_TILE, lim_t, wv);
-    u32 const arr = __atomic_load_n(arrivals, __ATOMIC_RELAXED);
-    for (;;) {  // (branch-free body: losers rewrite, everyone else writes the junk slot)
-      bool need = false;
-      u32 w[TPL];
+    for (u32 b = 0; b < BT; b++) {
+      u32 const tb = tb0 + b * ZH_TILE;
 #pragma unroll
       for (u32 k = 0; k < TPL; k++) {
-        bool const nk = h[k] != JUNK && r[k] < tb + 64 * k + lane + 1;
-        w[k] = nk ? h[k] : JUNK;
-        need |= nk;
+        u32 const p = tb + 64 * k + lane, sh = min(p, lim_t) & 3u;
+        u32 const lo = __builtin_amdgcn_alignbyte(wv[b][k][1], wv[b][k][0], sh), hi = __builtin_amdgcn_alignbyte(wv[b][k][2], wv[b][k][1], sh);
+        u32 const hh = hash_of<LONG>(lo, hi);
+        e[b][k] = T[hh];
+        h[b][k] = p < lim_t ? hh : JUNK;
       }
-      if (!__ballot(need)) break;
 #pragma unroll
-      for (u32 k = 0; k < TPL; k++) T[w[k]] = (u16)(tb + 64 * k + lane + 1);
+      for (u32 k = 0; k < TPL; k++) T[h[b][k]] = (u16)(tb + 64 * k + lane + 1);
 #pragma unroll
-      for (u32 k = 0; k < TPL; k++) r[k] = T[h[k]];
+      for (u32 k = 0; k < TPL; k++) r[b][k] = T[h[b][k]];
+    }
+    if (t0 + BT < TILES) load_in(tb0 + BT * ZH_TILE, lim_t);
+    u32 const arr = __atomic_load_n(arrivals, __ATOMIC_RELAXED);
+    bool lost = false;
+#pragma unroll
+    for (u32 b = 0; b < BT; b++)
+#pragma unroll
+      for (u32 k = 0; k < TPL; k++) lost |= h[b][k] != JUNK && r[b][k] < tb0 + b * ZH_TILE + 64 * k + lane + 1;
+    if (__ballot(lost)) {
+#ifdef ZH_STAMPS
+      if (lane == 0) atomicAdd(&g_fixups, 1u);
+#endif
+      insert_repair<LONG, BT>(T, tb0, lane, h, e);
     }
 #pragma unroll
-    for (u32 k = 0; k < TPL; k += 2) {
-      u32 const c0 = h[k] != JUNK ? e[k] : 0u, c1 = h[k + 1] != JUNK ? e[k + 1] : 0u;
-      creg[(t * TPL + k) / 2] = c0 | (c1 << 16);
-      // materialise this tile's candidates now (otherwise the compiler sinks their
-      // computation to the dump and keeps every tile's temporaries alive)
-      __asm__ volatile("" : "+v"(creg[(t * TPL + k) / 2]) :: "memory");
-    }
+    for (u32 b = 0; b < BT; b++)
+#pragma unroll
+      for (u32 k = 0; k < TPL; k += 2) {
+        u32 const c0 = h[b][k] != JUNK ? e[b][k] : 0u, c1 = h[b][k + 1] != JUNK ? e[b][k + 1] : 0u;
+        u32 const ri = ((t0 + b) * TPL + k) / 2;
+        creg[ri] = c0 | (c1 << 16);
+        // materialise this batch's candidates now (otherwise the compiler sinks their
+        // computation to the dump and keeps every tile's temporaries alive)
+        __asm__ volatile("" : "+v"(creg[ri]) :: "memory");
+      }
     between_tiles(arr);
   }
   // the next window's first position (lazy rule at this window's end): looked up
@@ -241,6 +302,21 @@ __device__ __forceinline__ void dump_window(u8 *ci8, u32 lane_, const u32 (&creg
 // takes a match there, else 0.
 // v from lane `src` (< 64) of the wave: ds_bpermute on a byte address, no lane-base math
 __device__ __forceinline__ u32 bperm(u32 v, u32 src) { return (u32)__builtin_amdgcn_ds_bpermute((int)(src << 2), (int)v); }
+
+// Inclusive wave64 prefix sum with DPP (row_shr 1/2/4/8 inside 16-lane rows, then
+// row_bcast:15 / row_bcast:31 across rows): VALU only, no LDS round trip (a __shfl_up
+// scan is 6 dependent ds_bpermutes).  Lanes whose DPP source is outside the row read 0.
+__device__ __forceinline__ u32 wave_scan_incl(u32 v) {
+  v += (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xf, 0xf, false);  // row_shr:1
+  v += (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xf, 0xf, false);  // row_shr:2
+  v += (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xf, 0xf, false);  // row_shr:4
+  v += (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xf, 0xf, false);  // row_shr:8
+  v += (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xa, 0xf, false);  // row_bcast:15 into rows 1, 3
+  v += (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xc, 0xf, false);  // row_bcast:31 into rows 2, 3
+  return v;
+}
+// value of lane - 1 (lane 0: 0), DPP wave_shr:1
+__device__ __forceinline__ u32 wave_shr1(u32 v) { return (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x138, 0xf, 0xf, false); }
 
 // Parse cost of a match: libzstd's lazy "gain" (4 per byte, minus the offset's bit length)
 __device__ __forceinline__ int match_gain(u32 inf) {
@@ -535,13 +611,8 @@ __device__ __forceinline__ void lz_block(const ZhBlockDesc *__restrict__ blocks,
       //     byte 2 for S: the half that was just consumed), read back in (4).
       {
         u32 const nh = __builtin_popcount(heads);
-        u32 inc = nh;
-#pragma unroll
-        for (u32 dd = 1; dd < 64; dd <<= 1) {
-          u32 const t = __shfl_up(inc, dd, 64);
-          if (lane >= dd) inc += t;
-        }
-        u32 const hbase = inc - nh, htot = __shfl(inc, 63, 64);
+        u32 const inc = wave_scan_incl(nh);
+        u32 const hbase = inc - nh, htot = __builtin_amdgcn_readlane(inc, 63);
         u32 *hb = hbuf + (tid >> 6) * HB_STRIDE;
         for (u32 c0 = 0; c0 < htot; c0 += 64) {
           // branch-free scatter: slots not in this pass (or not heads) write the junk slot
@@ -637,7 +708,7 @@ __device__ __forceinline__ void lz_block(const ZhBlockDesc *__restrict__ blocks,
       u32 ex = entry;
       for (;;) {
         ex = entry < SE ? S + exb[64 * lane + (entry - S)] : entry;
-        u32 const pe = __shfl_up(ex, 1, 64);
+        u32 const pe = wave_shr1(ex);
         u32 const ne = lane == 0 ? max(wsb, e_in) : max(S, pe);
         bool const ch = ne != entry;
         entry = ne;
@@ -691,14 +762,9 @@ __device__ __forceinline__ void lz_block(const ZhBlockDesc *__restrict__ blocks,
 #pragma unroll
       for (u32 c0 = 0; c0 < PR * NWW; c0 += 64) {
         u32 const v = c0 + lane < PR * NWW ? wpart[c0 + lane] : 0u;
-        u32 inc = v;
-#pragma unroll
-        for (u32 dd = 1; dd < 64; dd <<= 1) {
-          u32 const t = __shfl_up(inc, dd, 64);
-          if (lane >= dd) inc += t;
-        }
+        u32 const inc = wave_scan_incl(v);
         if (c0 + lane < PR * NWW) wpart[WP_OFF + c0 + lane] = carry + inc - v;
-        carry += __shfl(inc, 63, 64);
+        carry += __builtin_amdgcn_readlane(inc, 63);
       }
       if (tid == 0) wpart[WP_TOT] = carry;
     }
