@@ -73,3 +73,31 @@ struct ZhWorkspace {
 
 // Status codes written per item (values of cuda_zstd::Status).
 enum : u32 { ZH_ST_OK = 0, ZH_ST_INVALID = 2, ZH_ST_TOO_SMALL = 7 };
+
+// ---------------- wave64 cross-lane helpers on DPP (VALU only, no LDS round trip) ----------------
+// Inclusive prefix with row_shr 1/2/4/8 inside 16-lane rows, then row_bcast:15 / row_bcast:31
+// across rows (GFX9 DPP); a __shfl_up scan is 6 dependent ds_bpermutes.  Lanes whose DPP
+// source is outside the row read 0 (the identity of add and unsigned max).
+#define ZH_DPP(v, ctrl, rmask) ((u32)__builtin_amdgcn_update_dpp(0, (int)(v), (ctrl), (rmask), 0xf, false))
+__device__ __forceinline__ u32 wave_scan_incl(u32 v) {
+  v += ZH_DPP(v, 0x111, 0xf);  // row_shr:1
+  v += ZH_DPP(v, 0x112, 0xf);  // row_shr:2
+  v += ZH_DPP(v, 0x114, 0xf);  // row_shr:4
+  v += ZH_DPP(v, 0x118, 0xf);  // row_shr:8
+  v += ZH_DPP(v, 0x142, 0xa);  // row_bcast:15 into rows 1, 3
+  v += ZH_DPP(v, 0x143, 0xc);  // row_bcast:31 into rows 2, 3
+  return v;
+}
+__device__ __forceinline__ u32 wave_scan_max_incl(u32 v) {
+  v = max(v, ZH_DPP(v, 0x111, 0xf));
+  v = max(v, ZH_DPP(v, 0x112, 0xf));
+  v = max(v, ZH_DPP(v, 0x114, 0xf));
+  v = max(v, ZH_DPP(v, 0x118, 0xf));
+  v = max(v, ZH_DPP(v, 0x142, 0xa));
+  v = max(v, ZH_DPP(v, 0x143, 0xc));
+  return v;
+}
+// value of lane - 1 (lane 0 reads 0): DPP wave_shr:1
+__device__ __forceinline__ u32 wave_shr1(u32 v) { return ZH_DPP(v, 0x138, 0xf); }
+// v of a wave-uniform lane (v_readlane into an SGPR)
+__device__ __forceinline__ u32 lane_value(u32 v, u32 uniform_lane) { return (u32)__builtin_amdgcn_readlane((int)v, (int)uniform_lane); }

@@ -787,12 +787,7 @@ __device__ bool execute_block(DecLds &L, const Slot &sl, u8 *ob, s64 fpos, const
       ll = tl;
     }
     u32 const span = ll + ml;
-    u32 incl = span, linc = ll;
-#pragma unroll
-    for (u32 dd = 1; dd < 64; dd <<= 1) {
-      u32 const t = __shfl_up(incl, dd, 64), tl2 = __shfl_up(linc, dd, 64);
-      if (lane >= dd) { incl += t; linc += tl2; }
-    }
+    u32 const incl = wave_scan_incl(span), linc = wave_scan_incl(ll);  // DPP (zh_common.h)
     s32 const vs = (s32)(incl - span) - (s32)qd;  // window-relative start (q: qd bytes done)
     s32 const ve = (s32)incl - (s32)qd;
     u32 const lit0 = lcur + linc - ll;

@@ -101,26 +101,12 @@ struct CodeTabs {
 __device__ __forceinline__ void wave_sync() { __syncthreads(); }  // one wave per workgroup
 
 __device__ __forceinline__ u32 wave_excl_scan(u32 v, u32 &total) {
-  u32 const lane = lane_id();
-  u32 incl = v;
-#pragma unroll
-  for (u32 d = 1; d < 64; d <<= 1) {
-    u32 t = __shfl_up(incl, d, 64);
-    if (lane >= d) incl += t;
-  }
-  total = __shfl(incl, 63, 64);
+  u32 const incl = wave_scan_incl(v);  // DPP (zh_common.h)
+  total = lane_value(incl, 63);
   return incl - v;
 }
-__device__ __forceinline__ u32 wave_sum(u32 v) {
-#pragma unroll
-  for (u32 d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d, 64);
-  return v;
-}
-__device__ __forceinline__ u32 wave_max(u32 v) {
-#pragma unroll
-  for (u32 d = 32; d >= 1; d >>= 1) v = max(v, (u32)__shfl_xor(v, d, 64));
-  return v;
-}
+__device__ __forceinline__ u32 wave_sum(u32 v) { return lane_value(wave_scan_incl(v), 63); }
+__device__ __forceinline__ u32 wave_max(u32 v) { return lane_value(wave_scan_max_incl(v), 63); }
 
 // ---------------- output: bytes at dst[pos..] guarded by cap ----------------
 struct Out {
@@ -1050,7 +1036,7 @@ extern "C" __global__ __launch_bounds__(K2_THREADS) void zh_entropy_kernel(const
         u64 const rec = nrec;
         nrec = i + 64 < nseq_raw ? seq[i + 64] : 0;  // (this chunk writes only indices <= i)
         u32 const cum = (u32)(rec & 0x1FFFFu), ml = (u32)((rec >> 17) & 255u), off = (u32)((rec >> 25) & 0xFFFFu);
-        u32 pc = __shfl_up(cum, 1, 64), po = __shfl_up(off, 1, 64);
+        u32 pc = wave_shr1(cum), po = wave_shr1(off);
         if (lane == 0) { pc = carryCum; po = carryOff; }
         u32 const ll = cum - pc;
         bool const flag = valid && i > 0 && ll == 0 && off == po;
@@ -1086,15 +1072,15 @@ extern "C" __global__ __launch_bounds__(K2_THREADS) void zh_entropy_kernel(const
         if (hcount) {
           int const lastH = 63 - __builtin_clzll(hm);
           openIdx = nbSeq + hcount - 1;
-          openLL = __shfl(ll, lastH, 64);
-          openOff = __shfl(off, lastH, 64);
-          openMl = __shfl(misc[lane], lastH, 64);
+          openLL = lane_value(ll, (u32)lastH);
+          openOff = lane_value(off, (u32)lastH);
+          openMl = lane_value(misc[lane], (u32)lastH);
           open = true;
         }
         nbSeq += hcount;
         u32 const lastLane = min(63u, nseq_raw - 1 - base);
-        carryCum = __shfl(cum, lastLane, 64);
-        carryOff = __shfl(off, lastLane, 64);
+        carryCum = lane_value(cum, lastLane);
+        carryOff = lane_value(off, lastLane);
         wave_sync();
       }
       if (open && lane == 0) seq[openIdx] = (u64)openLL | ((u64)openMl << 17) | ((u64)openOff << 34);
@@ -1133,7 +1119,7 @@ extern "C" __global__ __launch_bounds__(K2_THREADS) void zh_entropy_kernel(const
         u64 const rec = nrec;
         nrec = i + 64 < nbSeq ? seq[i + 64] : 0;
         u32 const ll = (u32)(rec & 0x1FFFFu), ml = (u32)((rec >> 17) & 0x1FFFFu), off = (u32)(rec >> 34);
-        u32 r0 = __shfl_up(off, 1, 64);
+        u32 r0 = wave_shr1(off);
         if (lane == 0) r0 = cr0;
         bool const keep1 = ll > 0 && off == r0;
         u64 const nk1 = __ballot(valid && !keep1);
@@ -1153,9 +1139,9 @@ extern "C" __global__ __launch_bounds__(K2_THREADS) void zh_entropy_kernel(const
         // reps after the batch's last sequence
         u32 const lastLane = min(63u, nbSeq - 1 - base);
         u32 const n1 = keep1 ? r1 : r0, n2 = keep2 ? r2 : r1;
-        cr0 = __shfl(off, lastLane, 64);
-        cr1 = __shfl(n1, lastLane, 64);
-        cr2 = __shfl(n2, lastLane, 64);
+        cr0 = lane_value(off, lastLane);
+        cr1 = lane_value(n1, lastLane);
+        cr2 = lane_value(n2, lastLane);
         u32 const mlb = ml - 3;
         u32 const llc = ct.ll_code(ll), mlc = ct.ml_code(mlb);
         if (valid) {

@@ -303,20 +303,7 @@ __device__ __forceinline__ void dump_window(u8 *ci8, u32 lane_, const u32 (&creg
 // v from lane `src` (< 64) of the wave: ds_bpermute on a byte address, no lane-base math
 __device__ __forceinline__ u32 bperm(u32 v, u32 src) { return (u32)__builtin_amdgcn_ds_bpermute((int)(src << 2), (int)v); }
 
-// Inclusive wave64 prefix sum with DPP (row_shr 1/2/4/8 inside 16-lane rows, then
-// row_bcast:15 / row_bcast:31 across rows): VALU only, no LDS round trip (a __shfl_up
-// scan is 6 dependent ds_bpermutes).  Lanes whose DPP source is outside the row read 0.
-__device__ __forceinline__ u32 wave_scan_incl(u32 v) {
-  v += (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xf, 0xf, false);  // row_shr:1
-  v += (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xf, 0xf, false);  // row_shr:2
-  v += (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xf, 0xf, false);  // row_shr:4
-  v += (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xf, 0xf, false);  // row_shr:8
-  v += (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xa, 0xf, false);  // row_bcast:15 into rows 1, 3
-  v += (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xc, 0xf, false);  // row_bcast:31 into rows 2, 3
-  return v;
-}
-// value of lane - 1 (lane 0: 0), DPP wave_shr:1
-__device__ __forceinline__ u32 wave_shr1(u32 v) { return (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x138, 0xf, 0xf, false); }
+// (wave_scan_incl, wave_shr1: DPP helpers in zh_common.h)
 
 // Parse cost of a match: libzstd's lazy "gain" (4 per byte, minus the offset's bit length)
 __device__ __forceinline__ int match_gain(u32 inf) {
