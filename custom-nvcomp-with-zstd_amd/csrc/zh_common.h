@@ -63,6 +63,7 @@ enum : u32 {
 
 struct ZhWorkspace {
   u8 *base;          // nblocks * ZH_WS_BLOCK_BYTES
+  u32 *ctr;          // K1's block counter (persistent workgroups take the next block from it)
   __device__ u64 *seq(u32 b) const { return (u64 *)(base + (size_t)b * ZH_WS_BLOCK_BYTES); }
   __device__ u8 *lits(u32 b) const { return base + (size_t)b * ZH_WS_BLOCK_BYTES + ZH_SEQ_BYTES; }
   __device__ u32 *meta(u32 b) const { return (u32 *)(base + (size_t)b * ZH_WS_BLOCK_BYTES + ZH_SEQ_BYTES + ZH_LIT_BYTES); }

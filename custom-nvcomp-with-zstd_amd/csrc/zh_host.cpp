@@ -230,7 +230,7 @@ inline size_t align256(size_t v) { return (v + 255) & ~(size_t)255; }
 
 // Workspace layout inside the caller's temp buffer
 struct WsLayout {
-  size_t descs, items, blk_size, item_size, item_status, staging, blocks, total;
+  size_t descs, items, blk_size, item_size, item_status, staging, counter, blocks, total;
   static WsLayout make(size_t nblocks, size_t nitems, bool staged) {
     WsLayout L{};
     size_t o = 0;
@@ -240,6 +240,7 @@ struct WsLayout {
     L.item_size = o; o = align256(o + nitems * 8);
     L.item_status = o; o = align256(o + nitems * 4);
     L.staging = o; o = align256(o + (staged ? nblocks * (size_t)ZH_STAGE_SLOT : 0));
+    L.counter = o; o = align256(o + 4);
     L.blocks = o; o = align256(o + nblocks * (size_t)ZH_WS_BLOCK_BYTES);
     L.total = o + 256;  // slack for base alignment
     return L;
@@ -472,7 +473,7 @@ class ZstdBatchManager::Impl {
       }
     }
     if (hipMemcpyAsync(base, h, up_bytes, hipMemcpyHostToDevice, stream) != hipSuccess) return Status::ERROR_CUDA_ERROR;
-    ZhWorkspace ws{base + L.blocks};
+    ZhWorkspace ws{base + L.blocks, (u32 *)(base + L.counter)};
     hipError_t e = zh::launch_compress((const ZhBlockDesc *)(base + L.descs), (u32)nblocks, ws, config.window_log, config.block_size,
                                        (u64 *)(base + L.item_size), (u32 *)(base + L.item_status), (u32 *)(base + L.blk_size),
                                        (const ZhItemDesc *)(base + L.items), (u32)count, staged,
@@ -849,7 +850,7 @@ Status ZstdBatchManager::compress_batch_device(const void *const *d_in_ptrs, con
                                  (ZhItemDesc *)(base + L.items), item_size, item_status, ck ? ZH_F_CHECKSUM : 0u,
                                  dd ? dd->content() : nullptr, dd ? (u32)dd->content_n() : 0u, dd ? dd->id : 0u, hist, stream);
   if (e != hipSuccess) return Status::ERROR_CUDA_ERROR;
-  ZhWorkspace ws{base + L.blocks};
+  ZhWorkspace ws{base + L.blocks, (u32 *)(base + L.counter)};
   e = zh::launch_compress((const ZhBlockDesc *)(base + L.descs), (u32)nblocks, ws, pimpl_->config.window_log, pimpl_->config.block_size, item_size,
                           item_status, (u32 *)(base + L.blk_size), (const ZhItemDesc *)(base + L.items), (u32)count, bpi > 1, ck,
                           pimpl_->config.level >= kLazy2Level, stream);

@@ -30,6 +30,8 @@
 //                 the marks place literals and sequence records.
 #include "zh_common.h"
 
+#include <algorithm>
+
 #ifdef ZH_STAMPS
 __device__ u32 g_fixups;  // diagnostic: inserter read-back fix-up rounds (all blocks)
 extern "C" __global__ void zh_read_fixups(u32 *out) { *out = g_fixups; g_fixups = 0; }
@@ -410,8 +412,38 @@ __device__ __forceinline__ void inserter_loop(const u32 *in32, u16 *T, u8 *ci8, 
 #define ZH_STAMP(acc) do { } while (0)
 #endif
 
+// The next block's input is loaded into registers while the current one is processed
+// (persistent workgroups, one per CU): 64 KiB / 1024 threads = four 16-B vectors per thread.
+// Only for blocks whose staged region (history prefix + block) is one 16-B aligned run of a
+// multiple of 16 bytes -- every 64 KiB chunk and every history block; others stage directly.
+struct Prefetch {
+  uint4 v[4];
+  bool ok;
+};
+__device__ __forceinline__ const u8 *staged_region(const ZhBlockDesc &d, u32 &n) {
+  u32 const pre = d.pre_n;
+  n = pre + d.n;
+  // a history block's prefix is the input right before it: one contiguous region
+  const u8 *const g = (pre && d.pre + pre == d.src) ? d.pre : (pre ? nullptr : d.src);
+  return (d.n && g && (((uintptr_t)g) & 15) == 0 && (pre & 15) == 0 && (n & 15) == 0) ? g : nullptr;
+}
+__device__ __forceinline__ void prefetch_block(const ZhBlockDesc *__restrict__ blocks, u32 b, u32 nblocks, u32 tid, Prefetch &pf) {
+  pf.ok = false;
+  if (b >= nblocks) return;
+  ZhBlockDesc const d = blocks[b];
+  u32 n;
+  const u8 *const g = staged_region(d, n);
+  if (!g) return;
+  pf.ok = true;
+#pragma unroll
+  for (u32 k = 0; k < 4; k++) {
+    u32 const i = tid + K1_THREADS * k;
+    pf.v[k] = i < (n >> 4) ? ((const uint4 *)g)[i] : make_uint4(0, 0, 0, 0);
+  }
+}
+
 template <bool LAZY2>
-__device__ __forceinline__ void lz_block(const ZhBlockDesc *__restrict__ blocks, ZhWorkspace ws) {
+__device__ __forceinline__ u32 lz_block(const ZhBlockDesc *__restrict__ blocks, ZhWorkspace ws, u32 b, u32 nblocks, u32 *s_take, Prefetch &pf) {
   extern __shared__ __attribute__((aligned(16))) u8 smem[];
   u8 *in = smem + OFF_IN;
   u32 *in32 = (u32 *)in;
@@ -424,9 +456,20 @@ __device__ __forceinline__ void lz_block(const ZhBlockDesc *__restrict__ blocks,
   u32 *segx = (u32 *)(smem + OFF_SEG);
   u32 *misc = (u32 *)(smem + OFF_MISC);
 
-  u32 const b = blockIdx.x, tid = threadIdx.x, lane = tid & 63;
+  // opaque per-block thread index: stops the compiler from hoisting LDS addresses derived
+  // from it out of the persistent block loop (they would stay live, and spill, across it)
+  u32 tid;
+  __asm__ volatile("v_mov_b32 %0, %1" : "=v"(tid) : "v"((u32)threadIdx.x));
+  u32 const lane = tid & 63;
   ZhBlockDesc const d = blocks[b];
-  if (d.n == 0) return;
+  // the next block for this workgroup (dynamic: a slow block does not hold up a fixed share)
+  if (tid == 0) *s_take = atomicAdd(ws.ctr, 1u);
+  if (d.n == 0) {
+    __syncthreads();
+    u32 const next_b = *s_take;
+    prefetch_block(blocks, next_b, nblocks, tid, pf);
+    return next_b;
+  }
   // A dictionary frame's first block is staged behind the tail of the dictionary content
   // (SURVEY §8f F2): positions [0, pre) are history only -- hashed and matched against,
   // never parsed (the parse starts at pre) -- so matches reach into the dictionary.
@@ -444,9 +487,21 @@ __device__ __forceinline__ void lz_block(const ZhBlockDesc *__restrict__ blocks,
   // (the probe looks at the block only, never at the history in front of it)
   const u8 *src = d.src;
   bool same = true;
-  // a history block's prefix is the input right before it: one contiguous region
-  const u8 *const gsrc = (pre && d.pre + pre == src) ? d.pre : (pre ? nullptr : src);
-  if (gsrc && (((uintptr_t)gsrc) & 15) == 0 && (pre & 15) == 0) {
+  u32 nst;
+  if (pf.ok && staged_region(d, nst)) {  // prefetched during the previous block
+    u32 const nv = n >> 4, pv = pre >> 4;
+    u32 const f4 = src[0] * 0x01010101u;
+#pragma unroll
+    for (u32 k = 0; k < 4; k++) {
+      u32 const i = tid + K1_THREADS * k;
+      uint4 const v = pf.v[k];
+      if (i < nv) {
+        ((uint4 *)in)[i] = v;
+        same &= i < pv || ((v.x == f4) & (v.y == f4) & (v.z == f4) & (v.w == f4));
+      }
+    }
+  } else if (const u8 *const gsrc = (pre && d.pre + pre == src) ? d.pre : (pre ? nullptr : src);
+             gsrc && (((uintptr_t)gsrc) & 15) == 0 && (pre & 15) == 0) {
     u32 const nv = n >> 4, pv = pre >> 4;
     u8 const first = src[0];
     u32 const f4 = first * 0x01010101u;
@@ -473,9 +528,11 @@ __device__ __forceinline__ void lz_block(const ZhBlockDesc *__restrict__ blocks,
   if (tid < 2) misc[8 + tid] = 0;
   if (tid == 0) misc[MISC_ARR] = 0;
   bool const rle = __syncthreads_and(same) && d.n >= 2;
+  u32 const next_b = *s_take;  // (written before the barrier above)
+  prefetch_block(blocks, next_b, nblocks, tid, pf);  // the next block's input, in flight from here
   if (rle) {
     if (tid == 0) { meta[0] = 0; meta[1] = 0; meta[2] = 1; }
-    return;
+    return next_b;
   }
 
   ZH_STAMP(st_stage);
@@ -493,7 +550,8 @@ __device__ __forceinline__ void lz_block(const ZhBlockDesc *__restrict__ blocks,
     __builtin_amdgcn_s_setprio(2);
     if (tid < INS_TID + 64) inserter_loop<true>(in32, TL, ci8, misc, n, lim, lane, ws.dbg(b));
     else inserter_loop<false>(in32, TS, ci8, misc, n, lim, lane, ws.dbg(b));
-    return;
+    __builtin_amdgcn_s_setprio(0);
+    return next_b;
   }
 
   u32 const tid_ = tid;
@@ -783,14 +841,31 @@ __device__ __forceinline__ void lz_block(const ZhBlockDesc *__restrict__ blocks,
     dbg[0] = st_stage; dbg[1] = st_A; dbg[2] = st_B; dbg[3] = st_J; dbg[4] = st_E; dbg[5] = st_rounds; dbg[20] = st_Bw; dbg[21] = st_X; dbg[22] = st_E1;
   }
 #endif
+  return next_b;
 }
 
-// level < 9: greedy + lazy-1; level >= 9: LAZY2 (the same kernel body, one instantiation each)
-extern "C" __global__ __launch_bounds__(K1_THREADS) void zh_lz_kernel(const ZhBlockDesc *__restrict__ blocks, ZhWorkspace ws) {
-  lz_block<false>(blocks, ws);
+// Persistent workgroups (grid = one per CU, the LDS footprint allows no second): workgroup g
+// takes blocks g, g + grid, ... and stages each block from registers loaded while the previous
+// one was processed, so the HBM latency of staging and the per-block launch gap overlap work.
+template <bool LAZY2>
+__device__ __forceinline__ void lz_blocks(const ZhBlockDesc *__restrict__ blocks, u32 nblocks, ZhWorkspace ws) {
+  __shared__ u32 s_take;  // block index taken from the counter, broadcast to the workgroup
+  if (threadIdx.x == 0) s_take = atomicAdd(ws.ctr, 1u);
+  __syncthreads();
+  u32 b = s_take;
+  Prefetch pf;
+  prefetch_block(blocks, b, nblocks, threadIdx.x, pf);
+  while (b < nblocks) {
+    b = lz_block<LAZY2>(blocks, ws, b, nblocks, &s_take, pf);  // returns the next block taken
+    __syncthreads();  // every wave is done with this block's LDS before the next is staged
+  }
 }
-extern "C" __global__ __launch_bounds__(K1_THREADS) void zh_lz_lazy2_kernel(const ZhBlockDesc *__restrict__ blocks, ZhWorkspace ws) {
-  lz_block<true>(blocks, ws);
+// level < 9: greedy + lazy-1; level >= 9: LAZY2 (the same kernel body, one instantiation each)
+extern "C" __global__ __launch_bounds__(K1_THREADS) void zh_lz_kernel(const ZhBlockDesc *__restrict__ blocks, u32 nblocks, ZhWorkspace ws) {
+  lz_blocks<false>(blocks, nblocks, ws);
+}
+extern "C" __global__ __launch_bounds__(K1_THREADS) void zh_lz_lazy2_kernel(const ZhBlockDesc *__restrict__ blocks, u32 nblocks, ZhWorkspace ws) {
+  lz_blocks<true>(blocks, nblocks, ws);
 }
 
 extern "C" u32 zh_lz_lds_bytes() { return K1_LDS; }
@@ -802,7 +877,13 @@ hipError_t lz_init() {
   return hipFuncSetAttribute((const void *)zh_lz_lazy2_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)K1_LDS);
 }
 void lz_launch(const ZhBlockDesc *d_descs, u32 nblocks, ZhWorkspace ws, bool lazy2, hipStream_t stream) {
-  if (lazy2) hipLaunchKernelGGL(zh_lz_lazy2_kernel, dim3(nblocks), dim3(K1_THREADS), K1_LDS, stream, d_descs, ws);
-  else hipLaunchKernelGGL(zh_lz_kernel, dim3(nblocks), dim3(K1_THREADS), K1_LDS, stream, d_descs, ws);
+  // one persistent workgroup per CU of the stream's device
+  int dev = 0, cus = 0;
+  if (stream) (void)hipStreamGetDevice(stream, &dev);
+  else (void)hipGetDevice(&dev);
+  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) cus = 256;
+  u32 const grid = std::min(nblocks, (u32)cus);
+  if (lazy2) hipLaunchKernelGGL(zh_lz_lazy2_kernel, dim3(grid), dim3(K1_THREADS), K1_LDS, stream, d_descs, nblocks, ws);
+  else hipLaunchKernelGGL(zh_lz_kernel, dim3(grid), dim3(K1_THREADS), K1_LDS, stream, d_descs, nblocks, ws);
 }
 }  // namespace zh

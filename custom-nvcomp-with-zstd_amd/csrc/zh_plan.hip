@@ -206,6 +206,7 @@ hipError_t launch_compress(const ZhBlockDesc *d_descs, u32 nblocks, ZhWorkspace 
     if (prof().on) for (int k = 0; k < 4; k++) ev.push_back(prof_event());
   }
   if (!ev.empty()) (void)hipEventRecord(ev[0], stream);
+  (void)hipMemsetAsync(ws.ctr, 0, 4, stream);  // K1's block counter
   lz_launch(d_descs, nblocks, ws, lazy2, stream);
   if (!ev.empty()) (void)hipEventRecord(ev[1], stream);
   entropy_launch(d_descs, nblocks, ws, window_log, cfg_block_size, d_item_size, d_item_status, d_blk_size, stream);

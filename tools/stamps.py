@@ -34,6 +34,7 @@ off = a256(off + n * 4)
 off = a256(off + n * 8)
 off = a256(off + n * 4)
 off = a256(off + 0)
+off = a256(off + 4)  # K1 block counter
 blocks = base + off
 WS = 13120 * 8 + 118080 + 256 + 4096
 h = temp.cpu().numpy()
