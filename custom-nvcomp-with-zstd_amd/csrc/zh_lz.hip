@@ -164,9 +164,15 @@ __device__ __forceinline__ u32 hash_of(u32 lo, u32 hi) {
 template <bool LONG, u32 BT>
 __device__ __forceinline__ void insert_repair(u16 *T, u32 tb0, u32 lane, const u32 (&h)[BT][TPL], u32 (&e)[BT][TPL]) {
   constexpr u32 JUNK = LONG ? HL_SIZE : HS_SIZE;
+  // (compile-time slot loops unrolled, the lane loop kept rolled: this code never runs on
+  // gfx950 and must not bloat the inserter's instruction stream)
+#pragma unroll
   for (u32 b = 1; b < BT; b++)
+#pragma unroll
     for (u32 bb = 0; bb < b; bb++)
+#pragma unroll
       for (u32 kk = 0; kk < TPL; kk++)
+#pragma unroll 1
         for (u32 j = 0; j < 64; j++) {
           u32 const hj = __builtin_amdgcn_readlane(h[bb][kk], j);
           u32 const pj = tb0 + bb * ZH_TILE + 64 * kk + j + 1;
