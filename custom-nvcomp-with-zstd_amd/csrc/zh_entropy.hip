@@ -306,6 +306,97 @@ __device__ u32 fse_write_ncount(u8 *out, const s16 *norm, u32 maxSV, u32 tableLo
   return (u32)(out - ostart);
 }
 
+// ---------------- FSE normalisation + NCount, wave-parallel (lane = symbol, maxSV < 64) ----------------
+// FSE_normalizeCount (libzstd v1.4.9) with the per-symbol probabilities on the lanes and the
+// two reductions (sum, first-maximum) on DPP; the rare "m2" redistribution falls back to the
+// serial code above on lane 0.  c = this lane's count (0 past maxSV).  The result is
+// returned per lane (lane s: norm[s]) and stored to norm[] in LDS.
+__device__ int fse_normalize_wave(s16 *norm, u32 tableLog, u32 c, u32 total, u32 maxSV, bool useLowProbCount, u32 lane, u32 *cnt_scratch) {
+  s16 const lowProbCount = useLowProbCount ? -1 : 1;
+  u32 const scale = 62 - tableLog;
+  u64 const step = (1ull << 62) / total;
+  u64 const vStep = 1ull << (scale - 20);
+  u32 const lowThreshold = total >> tableLog;
+  int n = 0, contrib = 0;
+  u32 key = 0;  // proba * 256 + (255 - s): the first symbol of maximal probability wins, as in the serial loop
+  if (lane <= maxSV && c != 0) {
+    if (c <= lowThreshold) {
+      n = lowProbCount;
+      contrib = 1;
+    } else {
+      u64 const cs = (u64)c * step;
+      int proba = (int)(cs >> scale);
+      if (proba < 8) proba += cs - ((u64)proba << scale) > vStep * c_rtb[proba];
+      n = proba;
+      contrib = proba;
+      key = ((u32)proba << 8) | (255u - lane);
+    }
+  }
+  int const still = (int)(1u << tableLog) - (int)wave_sum((u32)contrib);
+  u32 const kmax = wave_max(key);
+  u32 const largest = kmax ? 255u - (kmax & 255u) : 0u;
+  int const nl = (int)lane_value((u32)n, largest);
+  if (-still >= (nl >> 1)) {  // libzstd's FSE_normalizeM2 (rare): serial, from LDS
+    if (lane <= maxSV) cnt_scratch[lane] = c;
+    __syncthreads();
+    if (lane == 0) fse_normalize_m2(norm, tableLog, cnt_scratch, total, maxSV, lowProbCount);
+    __syncthreads();
+    return lane <= maxSV ? norm[lane] : 0;
+  }
+  if (lane == largest) n += still;
+  if (lane <= maxSV) norm[lane] = (s16)n;
+  return n;
+}
+
+// FSE_writeNCount with every lane running the same (wave-uniform, scalar) loop; the counts
+// come from the lanes of normv (v_readlane), lane 0 stores the bytes.  Returns the size.
+__device__ u32 fse_write_ncount_wave(u8 *out, int normv, u32 maxSV, u32 tableLog, u32 lane) {
+  u32 o = 0;
+  auto put2 = [&](u32 bs) {
+    if (lane == 0) { out[o] = (u8)bs; out[o + 1] = (u8)(bs >> 8); }
+    o += 2;
+  };
+  int const tableSize = 1 << tableLog;
+  int remaining = tableSize + 1, threshold = tableSize, nbBits = (int)tableLog + 1;
+  u32 bitStream = tableLog - 5;
+  int bitCount = 4;
+  u32 symbol = 0;
+  u32 const alphabetSize = maxSV + 1;
+  bool previousIs0 = false;
+  while (symbol < alphabetSize && remaining > 1) {
+    if (previousIs0) {
+      u32 start = symbol;
+      while (symbol < alphabetSize && !lane_value((u32)normv, symbol)) symbol++;
+      if (symbol == alphabetSize) break;
+      while (symbol >= start + 24) {
+        start += 24;
+        bitStream += 0xFFFFu << bitCount;
+        put2(bitStream);
+        bitStream >>= 16;
+      }
+      while (symbol >= start + 3) { start += 3; bitStream += 3u << bitCount; bitCount += 2; }
+      bitStream += (symbol - start) << bitCount;
+      bitCount += 2;
+      if (bitCount > 16) { put2(bitStream); bitStream >>= 16; bitCount -= 16; }
+    }
+    int count = (int)lane_value((u32)normv, symbol++);
+    int const max = (2 * threshold - 1) - remaining;
+    remaining -= count < 0 ? -count : count;
+    count++;
+    if (count >= threshold) count += max;
+    bitStream += (u32)count << bitCount;
+    bitCount += nbBits;
+    bitCount -= (count < max);
+    previousIs0 = (count == 1);
+    if (remaining < 1) return 0;
+    while (remaining < threshold) { nbBits--; threshold >>= 1; }
+    if (bitCount > 16) { put2(bitStream); bitStream >>= 16; bitCount -= 16; }
+  }
+  if (remaining != 1) return 0;
+  if (lane == 0) { out[o] = (u8)bitStream; out[o + 1] = (u8)(bitStream >> 8); }
+  return o + (u32)(bitCount + 7) / 8;
+}
+
 struct FseSym { u32 dNb; s32 dFS; };
 
 // FSE_buildCTable_wksp into LDS (stateTable + symbol transforms)
@@ -1160,63 +1251,64 @@ extern "C" __global__ __launch_bounds__(K2_THREADS) void zh_entropy_kernel(const
       u32 const seqHead = op;
       op += 1;
       u64 const rec0 = seq[0], recL = seq[nbSeq - 1];
+      u32 hposw = 0, typesw = 0, logsw[3];
       {
-        u32 *first_code = scr->wcount, *last_code = scr->wcount + 4, *types = scr->wcount + 8, *logs = scr->wcount + 12;
-        if (lane == 0) {
-          first_code[0] = ll_code((u32)(rec0 & 0x1FFFFu)); first_code[1] = highbit32((u32)(rec0 >> 34) & 0x1FFFFu); first_code[2] = ml_code((u32)((rec0 >> 17) & 0x1FFFFu));
-          last_code[0] = ll_code((u32)(recL & 0x1FFFFu)); last_code[1] = highbit32((u32)(recL >> 34) & 0x1FFFFu); last_code[2] = ml_code((u32)((recL >> 17) & 0x1FFFFu));
-          misc[0] = 0;
-        }
+        // ZSTD_selectEncodingType (dfast) + normalisation + NCount header, wave-parallel
+        // (lane = symbol; every value below is wave-uniform)
+        u32 const first_code[3] = {ll_code((u32)(rec0 & 0x1FFFFu)), highbit32((u32)(rec0 >> 34) & 0x1FFFFu), ml_code((u32)((rec0 >> 17) & 0x1FFFFu))};
+        u32 const last_code[3] = {ll_code((u32)(recL & 0x1FFFFu)), highbit32((u32)(recL >> 34) & 0x1FFFFu), ml_code((u32)((recL >> 17) & 0x1FFFFu))};
         for (int t = 0; t < 3; t++) {
           u16 *st = t == 0 ? stLL : t == 1 ? stOF : stML;
           FseSym *sy = t == 0 ? symLL : t == 1 ? symOF : symML;
-          if (lane == 0) {  // ZSTD_selectEncodingType (dfast) + normalisation + NCount header
-            u32 hpos = misc[0];
-            u32 *cnt = hist + 64 * t;
-            u32 const maxSym = t == 0 ? 35 : t == 1 ? 31 : 52;
-            u32 const fseLog = t == 1 ? 8 : 9, defLog = t == 1 ? 5 : 6, defMax = t == 0 ? 35 : t == 1 ? 28 : 52;
-            const s16 *defNorm = t == 0 ? c_LL_def : t == 1 ? c_OF_def : c_ML_def;
-            u32 mx = maxSym;
-            while (mx && !cnt[mx]) mx--;
-            u32 mostFrequent = 0;
-            for (u32 s = 0; s <= mx; s++) mostFrequent = max(mostFrequent, cnt[s]);
-            bool const defAllowed = (t == 1) ? (mx <= 28) : true;
-            u32 type;
-            if (mostFrequent == nbSeq) type = (defAllowed && nbSeq <= 2) ? 0 : 1;
-            else if (defAllowed && ((nbSeq < (1u << defLog)) || (mostFrequent < (nbSeq >> (defLog - 1))))) type = 0;
-            else type = 2;
-            u32 bmax = 0, blog = 0;
-            if (type == 1) {
+          u32 *cnt = hist + 64 * t;
+          u32 const maxSym = t == 0 ? 35 : t == 1 ? 31 : 52;
+          u32 const fseLog = t == 1 ? 8 : 9, defLog = t == 1 ? 5 : 6, defMax = t == 0 ? 35 : t == 1 ? 28 : 52;
+          const s16 *defNorm = t == 0 ? c_LL_def : t == 1 ? c_OF_def : c_ML_def;
+          u32 c = lane <= maxSym ? cnt[lane] : 0u;
+          u64 const nz = __ballot(c != 0);
+          u32 const mx = nz ? 63u - (u32)__builtin_clzll(nz) : 0u;
+          u32 const mostFrequent = wave_max(c);
+          bool const defAllowed = (t == 1) ? (mx <= 28) : true;
+          u32 type;
+          if (mostFrequent == nbSeq) type = (defAllowed && nbSeq <= 2) ? 0 : 1;
+          else if (defAllowed && ((nbSeq < (1u << defLog)) || (mostFrequent < (nbSeq >> (defLog - 1))))) type = 0;
+          else type = 2;
+          u32 bmax = 0, blog = 0;
+          if (type == 1) {
+            u32 const fc = first_code[t];
+            if (lane == 0) {
               st[0] = 0; st[1] = 0;
-              u32 const c = first_code[t];
-              sy[c].dNb = 0; sy[c].dFS = 0;
-              hbuf[hpos++] = (u8)c;
-              logs[t] = 0;
-            } else if (type == 0) {
-              for (u32 s = 0; s <= defMax; s++) norm[s] = defNorm[s];
-              bmax = defMax; blog = defLog;
-              logs[t] = defLog;
-            } else {
-              u32 nb1 = nbSeq;
-              u32 const tl = fse_optimal_table_log(fseLog, nbSeq, mx, 2);
-              if (cnt[last_code[t]] > 1) { cnt[last_code[t]]--; nb1--; }
-              fse_normalize(norm, tl, cnt, nb1, mx, nb1 >= 2048);
-              u32 h = fse_write_ncount(hbuf + hpos, norm, mx, tl);
-              hpos += h;
-              bmax = mx; blog = tl;
-              logs[t] = tl;
+              sy[fc].dNb = 0; sy[fc].dFS = 0;
+              hbuf[hposw] = (u8)fc;
             }
-            types[t] = type;
-            misc[0] = hpos;
-            misc[20] = type; misc[21] = bmax; misc[22] = blog;
+            hposw++;
+            logsw[t] = 0;
+          } else if (type == 0) {
+            if (lane <= defMax) norm[lane] = defNorm[lane];
+            bmax = defMax; blog = defLog;
+            logsw[t] = defLog;
+          } else {
+            u32 nb1 = nbSeq;
+            u32 const tl = fse_optimal_table_log(fseLog, nbSeq, mx, 2);
+            u32 const lc = last_code[t];
+            if (lane_value(c, lc) > 1) {
+              if (lane == lc) c--;
+              nb1--;
+            }
+            int const nv = fse_normalize_wave(norm, tl, c, nb1, mx, nb1 >= 2048, lane, scr->cumul);
+            hposw += fse_write_ncount_wave(hbuf + hposw, nv, mx, tl, lane);
+            bmax = mx; blog = tl;
+            logsw[t] = tl;
           }
+          typesw |= type << (6 - 2 * t);
           wave_sync();
-          if (misc[20] != 1) fse_build_ctable_par(st, sy, tsym, norm, misc[21], misc[22], scr);
+          if (type != 1) fse_build_ctable_par(st, sy, tsym, norm, bmax, blog, scr);
           wave_sync();
         }
         if (lane == 0) {
-          misc[1] = (types[0] << 6) + (types[1] << 4) + (types[2] << 2);
-          misc[2] = logs[0]; misc[3] = logs[1]; misc[4] = logs[2];
+          misc[0] = hposw;
+          misc[1] = typesw;
+          misc[2] = logsw[0]; misc[3] = logsw[1]; misc[4] = logsw[2];
         }
       }
       wave_sync();
