@@ -30,6 +30,7 @@
 // and a formatted one's tables and repcodes seed the frame state.
 #include "zh_common.h"
 #include "zh_launch.h"
+#include "zh_pipe.h"
 #include "zh_xxh64.h"
 
 #include <algorithm>
@@ -1397,45 +1398,7 @@ extern "C" __global__ __launch_bounds__(64) void zh_dec_seq_kernel(ZhDecArgs a, 
 }
 
 namespace {
-// Side streams and events of the pipelined decode, one set per device (created on the
-// device of the caller's stream at its first large decode and kept; a call holds the
-// set's mutex while it enqueues its groups)
-struct DecPipe {
-  static constexpr u32 G = 4;
-  std::mutex mu;
-  int device = -1;
-  hipStream_t side[G - 1] = {};
-  hipEvent_t start = nullptr, p1[G - 1] = {}, done[G - 1] = {};
-  bool ok = true;
-  explicit DecPipe(int dev) : device(dev) {
-    int cur = -1;
-    ok = hipGetDevice(&cur) == hipSuccess && hipSetDevice(dev) == hipSuccess;
-    ok = ok && hipEventCreateWithFlags(&start, hipEventDisableTiming) == hipSuccess;
-    for (u32 k = 0; k + 1 < G; k++) {
-      ok = ok && hipStreamCreateWithFlags(&side[k], hipStreamNonBlocking) == hipSuccess;
-      ok = ok && hipEventCreateWithFlags(&p1[k], hipEventDisableTiming) == hipSuccess;
-      ok = ok && hipEventCreateWithFlags(&done[k], hipEventDisableTiming) == hipSuccess;
-    }
-    if (cur >= 0) (void)hipSetDevice(cur);
-  }
-};
-// The device a stream belongs to (the null stream: the current device)
-int stream_device(hipStream_t s) {
-  int dev = -1;
-  if (s && hipStreamGetDevice(s, &dev) == hipSuccess) return dev;
-  (void)hipGetLastError();
-  if (hipGetDevice(&dev) != hipSuccess) dev = 0;
-  return dev;
-}
-DecPipe *dec_pipe(hipStream_t s) {
-  static std::mutex mu;
-  static std::map<int, std::unique_ptr<DecPipe>> pipes;
-  int const dev = stream_device(s);
-  std::lock_guard<std::mutex> lk(mu);
-  auto &p = pipes[dev];
-  if (!p) p.reset(new DecPipe(dev));
-  return p.get();
-}
+struct DecPipeTag {};
 }  // namespace
 
 namespace zh {
@@ -1464,30 +1427,21 @@ hipError_t launch_decompress(const ZhDecArgs &a0, u32 nitems, hipStream_t stream
     hipLaunchKernelGGL(zh_decode_kernel, dim3(cnt), dim3(DEC_THREADS), 0, s, a);
     check("phase 3");
   };
-  // Large batches run as DecPipe::G groups on staggered streams: group k's phase 1 starts
+  // Large batches run as G groups on staggered streams (zh_pipe.h): group k's phase 1 starts
   // once group k-1's phase 1 is done, so the latency-bound sequence kernel of a group (one
   // wave per 64 buffers) overlaps the throughput-bound phase 1 of the next groups and
   // phase 3 of the earlier ones.
-  constexpr u32 G = DecPipe::G, MIN_GROUP = 1024;
-  DecPipe *p = (!dbg && nitems >= G * MIN_GROUP) ? dec_pipe(stream) : nullptr;
-  if (!p || !p->ok) {
+  constexpr u32 G = 4, MIN_GROUP = 1024;
+  StreamPipe<G> *p = (!dbg && nitems >= G * MIN_GROUP) ? stream_pipe<DecPipeTag, G>(stream) : nullptr;
+  if (!p) {
     group(0, nitems, stream, nullptr);
     return hipGetLastError();
   }
-  std::lock_guard<std::mutex> lk(p->mu);
   u32 const per = (nitems + G - 1) / G;
-  (void)hipEventRecord(p->start, stream);
-  for (u32 k = 0; k < G; k++) {
-    hipStream_t const s = k ? p->side[k - 1] : stream;
-    if (k) {
-      (void)hipStreamWaitEvent(s, p->start, 0);
-      (void)hipStreamWaitEvent(s, p->p1[k - 1], 0);
-    }
+  p->run(stream, [&](u32 k, hipStream_t s, hipEvent_t after_first) {
     u32 const first = k * per;
-    group(first, std::min(per, nitems - first), s, k + 1 < G ? p->p1[k] : nullptr);
-    if (k) (void)hipEventRecord(p->done[k - 1], s);
-  }
-  for (u32 k = 1; k < G; k++) (void)hipStreamWaitEvent(stream, p->done[k - 1], 0);
+    group(first, std::min(per, nitems - first), s, after_first);
+  });
   return hipGetLastError();
 }
 }  // namespace zh
