@@ -36,13 +36,24 @@ enum : u32 {
 // Per-block workspace carved from the caller's temp buffer.
 //   seq   : ZH_SEQ_CAP u64 records (K1: cumLit | ml<<17 | off<<25; K2 rewrites in place)
 //   lits  : ZH_BLOCK_MAX literal bytes; once the literals section is written, the
-//           sequences' FSE codes and states in encoding order, per table (LL, OF, ML),
-//           NS = nbSeq rounded up to 32 entries each: states u16 [0, 6 NS), codes u8 [6 NS, 9 NS)
+//           sequences' FSE states and codes in encoding order in the segment-interleaved
+//           layout of the chain kernel (below): states u16 [0, 128 L), codes u8 [128 L, 192 L),
+//           L = zh_k3_seglen(nbSeq)
 //   meta  : u32[4] = {nseq, nlit, rle, 0}
 #define ZH_SEQ_CAP 13120u
 #define ZH_SEQ_BYTES (ZH_SEQ_CAP * 8u)
-#define ZH_LIT_BYTES (9u * ZH_SEQ_CAP > (u32)ZH_BLOCK_MAX ? 9u * ZH_SEQ_CAP : (u32)ZH_BLOCK_MAX)
-static_assert(ZH_SEQ_CAP % 32 == 0, "state / code arrays are padded to 32 entries");
+// FSE chain segments (zh_entropy.hip K3): each of the three tables' chains is cut into
+// ZH_K3_SEGS segments of L steps (L a multiple of 16); lane t * ZH_K3_SEGS + g of the chain
+// wave runs segment g of table t.  Step e of table t is element
+//   ((r / 16) * 64 + t * ZH_K3_SEGS + g) * 16 + r % 16,   g = e / L, r = e % L
+// of the state (u16) and code (u8) arrays: every 16-step batch of the 63 lanes is one
+// contiguous run (1 KiB of codes, 2 KiB of states), so the chain kernel's loads and stores
+// are whole cache lines.
+#define ZH_K3_SEGS 21u
+#define ZH_K3_SEGLEN(nbseq) ((((nbseq) + ZH_K3_SEGS - 1u) / ZH_K3_SEGS + 15u) & ~15u)
+#define ZH_K3_BYTES(nbseq) (192u * ZH_K3_SEGLEN(nbseq))
+#define ZH_LIT_BYTES (ZH_K3_BYTES(ZH_SEQ_CAP) > (u32)ZH_BLOCK_MAX ? ZH_K3_BYTES(ZH_SEQ_CAP) : (u32)ZH_BLOCK_MAX)
+static_assert(3u * ZH_K3_SEGS <= 64u, "one lane per (table, segment)");
 #define ZH_META_BYTES 256u  // u32[4] counters + u32[60] diagnostic stamps (-DZH_STAMPS builds)
 //   fse   : hand-off from the entropy kernel to the FSE chain and packing kernels:
 //           the block's three FSE tables (state tables + symbol transforms, ZH_FSE_TAB_BYTES)
@@ -71,6 +82,14 @@ struct ZhWorkspace {
   __device__ u8 *fse(u32 b) const { return base + (size_t)b * ZH_WS_BLOCK_BYTES + ZH_SEQ_BYTES + ZH_LIT_BYTES + ZH_META_BYTES; }
   __device__ u32 *fsef(u32 b) const { return (u32 *)(fse(b) + ZH_FSE_FIELDS); }
 };
+
+// Element index of step e of table t in the chain layout (see ZH_K3_SEGS); m = zh_k3_magic(L)
+// gives e / L as umulhi(e << 8, m) exactly for e < 2^14, L <= 1024
+__host__ __device__ __forceinline__ u32 zh_k3_magic(u32 L) { return ((1u << 24) + L - 1u) / L; }
+__device__ __forceinline__ u32 zh_k3_index(u32 e, u32 t, u32 L, u32 m) {
+  u32 const g = __umulhi(e << 8, m), r = e - g * L;
+  return (((r >> 4) * 64u + t * ZH_K3_SEGS + g) << 4) + (r & 15u);
+}
 
 // Status codes written per item (values of cuda_zstd::Status).
 enum : u32 { ZH_ST_OK = 0, ZH_ST_INVALID = 2, ZH_ST_TOO_SMALL = 7 };

@@ -1201,8 +1201,8 @@ extern "C" __global__ __launch_bounds__(K2_THREADS) void zh_entropy_kernel(const
       u64 const below = (1ull << lane) - 1ull;
       CodeTabs ct;
       ct.load();
-      u32 const NS = (nbSeq + 31) & ~31u;
-      u8 *const cb = ws.lits(b) + 6 * NS;  // codes in encoding order (step nbSeq-1-i), per table
+      u32 const k3L = ZH_K3_SEGLEN(nbSeq), k3m = zh_k3_magic(k3L);
+      u8 *const cb = ws.lits(b) + 128u * k3L;  // codes in encoding order (step nbSeq-1-i), chain layout (zh_common.h)
       u64 nrec = lane < nbSeq ? seq[lane] : 0;
       for (u32 base = 0; base < nbSeq; base += 64) {
         u32 const i = base + lane;
@@ -1242,7 +1242,8 @@ extern "C" __global__ __launch_bounds__(K2_THREADS) void zh_entropy_kernel(const
           // + the LL / ML codes in the spare top bits (ob < 2^17: offsets stay inside the block)
           seq[i] = (u64)ll | ((u64)mlb << 17) | ((u64)ob << 34) | ((u64)llc << 51) | ((u64)mlc << 57);
           u32 const k = nbSeq - 1 - i;
-          cb[k] = (u8)llc; cb[NS + k] = (u8)highbit32(ob); cb[2 * NS + k] = (u8)mlc;
+          u32 const x0 = zh_k3_index(k, 0, k3L, k3m);
+          cb[x0] = (u8)llc; cb[x0 + 16u * ZH_K3_SEGS] = (u8)highbit32(ob); cb[x0 + 32u * ZH_K3_SEGS] = (u8)mlc;
         }
       }
       wave_sync();
@@ -1352,117 +1353,158 @@ extern "C" __global__ __launch_bounds__(K2_THREADS) void zh_entropy_kernel(const
 }
 
 // ======================= FSE state chains (K3) =======================
-// Lanes = (block, table): lane 3j + t runs table t (LL, OF, ML) of the workgroup's
-// block j; 11 blocks per wave, so 33 serial chains advance together instead of 3.
-// Encoding step e (e >= 1) encodes sequence nbSeq-1-e from the state the previous step
-// left (step 0 is FSE_initCState2 with the last sequence's code).  The state before
-// each step goes to the block's literal area (free by now) as u16 (table t at
-// [t * NS, t * NS + nbSeq), NS = nbSeq rounded up to 32); the codes come from pass B of
-// the entropy kernel (u8 arrays after the states); the final states go to the fse fields.
-constexpr u32 K3_BLOCKS = 11;  // 39 KB of LDS: 4 workgroups (one per SIMD) per CU
-constexpr u32 K3_CODES = 192;  // LDS: c_LL_code (64) + c_ML_code (128)
-constexpr u32 K3_LDS = K3_CODES + K3_BLOCKS * ZH_FSE_TAB_BYTES;
-constexpr u32 K3_BATCH = 16;   // records loaded ahead per lane
+// One wave per block (K3_WAVES per workgroup).  Lane t * K3_SEGS + g runs segment g of table
+// t's (LL, OF, ML) chain: encoding step e (e >= 1) encodes sequence nbSeq-1-e from the state
+// the previous step left (step 0 is FSE_initCState2 with the last sequence's code).  The state
+// before each step goes to the block's literal area (free by now) as u16, the codes come from
+// pass B of the entropy kernel, both in the segment-interleaved chain layout (zh_common.h:
+// each 16-step batch of the 63 segments is one contiguous run); the final states go to the
+// fse fields.
+//
+// A chain is serial, but its step map s -> stT[(s >> nb) + dFS] is many-to-one (a symbol with
+// normalised count c leaves at most c states), so two trajectories that start apart merge
+// within a few dozen steps and then never part.  Segment g > 0 therefore starts from a guess
+// (its first state after K3_WARM warm-up steps from an arbitrary state) and the segments run
+// in parallel; then, in Jacobi rounds, every segment whose entry differs from its left
+// neighbour's exit reruns from the right entry until its new trajectory meets the stored one
+// (from there on every state is already right).  The states written are exactly the serial
+// chain's.  The kernel's time is a block's longest segment, not its whole chain.
+constexpr u32 K3_SEGS = ZH_K3_SEGS;  // 3 x 21 = 63 lanes
+constexpr u32 K3_WARM = 64;    // warm-up steps before a segment's first step
+constexpr u32 K3_WAVES = 4;    // blocks (one per wave) per workgroup: the CU holds at most 16 workgroups
+constexpr u32 K3_TAB_STRIDE = (ZH_FSE_TAB_BYTES + 15) & ~15u;
+constexpr u32 K3_LDS = K3_WAVES * K3_TAB_STRIDE;
+constexpr u32 K3_BATCH = 16;   // steps per code load / state store
 constexpr u32 K3_TABW = ZH_FSE_TAB_BYTES / 4;
 
-extern "C" __global__ __launch_bounds__(64) void zh_fse_chain_kernel(const ZhBlockDesc *__restrict__ blocks, u32 nblocks, ZhWorkspace ws) {
-  extern __shared__ __attribute__((aligned(16))) u8 smem[];
-  u32 const lane = lane_id();
-  u32 const b0 = blockIdx.x * K3_BLOCKS;
-  u8 *codes = smem;
-  codes[lane] = c_LL_code[lane];
-  codes[64 + lane] = c_ML_code[lane];
-  codes[128 + lane] = c_ML_code[64 + lane];
-  // which of the workgroup's blocks have chains (lane j looks at block b0 + j)
-  bool const mine = lane < K3_BLOCKS && b0 + lane < nblocks && blocks[b0 + lane].n != 0 && ws.fsef(b0 + lane)[ZH_FF_NEED] != 0;
-  u64 const needm = __ballot(mine);
-  // stage the needed tables: 8 independent loads per lane in flight
-  u32 const nw = K3_BLOCKS * K3_TABW;
-  for (u32 w0 = 0; w0 < nw; w0 += 64 * 8) {
-    u32 v[8];
-#pragma unroll
-    for (u32 q = 0; q < 8; q++) {
-      u32 const w = w0 + 64 * q + lane, jj = w / K3_TABW;
-      v[q] = (w < nw && ((needm >> jj) & 1u)) ? ((const u32 *)ws.fse(b0 + jj))[w - jj * K3_TABW] : 0u;
-    }
-#pragma unroll
-    for (u32 q = 0; q < 8; q++) {
-      u32 const w = w0 + 64 * q + lane;
-      if (w < nw) ((u32 *)(smem + K3_CODES))[w] = v[q];
-    }
-  }
-  __syncthreads();
-  u32 const j = lane / 3, t = lane - 3 * j;
-  if (j >= K3_BLOCKS || !((needm >> j) & 1u)) return;
-  u32 const bb = b0 + j;
+extern "C" __global__ __launch_bounds__(64 * K3_WAVES) __attribute__((amdgpu_waves_per_eu(8, 8))) void zh_fse_chain_kernel(const ZhBlockDesc *__restrict__ blocks, u32 nblocks, ZhWorkspace ws) {
+  extern __shared__ __attribute__((aligned(16))) u8 smem_all[];
+  u32 const lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;  // (lane_id() is threadIdx.x: one-wave kernels)
+  u32 const bb = blockIdx.x * K3_WAVES + wv;
+  u8 *const smem = smem_all + wv * K3_TAB_STRIDE;  // this wave's block tables
+#ifdef ZH_STAMPS
+  u64 const k3pre = __builtin_amdgcn_s_memtime();
+  u64 const k3rt0 = __builtin_amdgcn_s_memrealtime();
+#endif
+  if (bb >= nblocks || blocks[bb].n == 0) return;
   u32 *ff = ws.fsef(bb);
-  u32 const nbSeq = ff[ZH_FF_NBSEQ];
-  const u8 *tb = smem + K3_CODES + j * ZH_FSE_TAB_BYTES;
-  const u16 *stT = (const u16 *)(tb + (t == 0 ? ZH_FT_STLL : t == 1 ? ZH_FT_STOF : ZH_FT_STML));
-  const FseSym *syT = (const FseSym *)(tb + (t == 0 ? ZH_FT_SYLL : t == 1 ? ZH_FT_SYOF : ZH_FT_SYML));
-  u32 const NS = (nbSeq + 31) & ~31u;
-  u16 *gst = (u16 *)ws.lits(bb) + t * NS;              // states (64-B aligned per table)
-  const u8 *cb = ws.lits(bb) + 6 * NS + t * NS;        // codes in encoding order
-  u32 s;
+  if (ff[ZH_FF_NEED] == 0) return;
   {
-    FseSym const tr = syT[cb[0]];  // FSE_initCState2 with the last sequence's code
-    u32 const nb = (tr.dNb + (1u << 15)) >> 16;
-    s = stT[(((nb << 16) - tr.dNb) >> nb) + tr.dFS];
+    const u32 *src = (const u32 *)ws.fse(bb);
+    u32 v[(K3_TABW + 63) / 64];
+#pragma unroll
+    for (u32 q = 0; q < (K3_TABW + 63) / 64; q++) v[q] = 64 * q + lane < K3_TABW ? src[64 * q + lane] : 0u;
+#pragma unroll
+    for (u32 q = 0; q < (K3_TABW + 63) / 64; q++)
+      if (64 * q + lane < K3_TABW) ((u32 *)smem)[64 * q + lane] = v[q];
   }
-  // Batches of 16 steps: one 16-byte load of codes per lane (loaded two batches ahead,
-  // ping-pong buffers: no copies of loads in flight), symbol transforms, the dependent
-  // chain (one LDS round trip per step), two 16-byte stores of the states.  Steps
-  // outside [1, nbSeq) are dead (predicated; padding entries of both arrays).
+  // the tables are this wave's own: LDS executes one wave's operations in order
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  u32 const t = min(lane / K3_SEGS, 2u), g = lane - K3_SEGS * t;  // lane 63: an empty segment
+  u32 const nbSeq = ff[ZH_FF_NBSEQ];
+  const u16 *stT = (const u16 *)(smem + (t == 0 ? ZH_FT_STLL : t == 1 ? ZH_FT_STOF : ZH_FT_STML));
+  const FseSym *syT = (const FseSym *)(smem + (t == 0 ? ZH_FT_SYLL : t == 1 ? ZH_FT_SYOF : ZH_FT_SYML));
+  // chain layout (zh_common.h): batch k of this lane's segment at element (64 k + lane) * 16
+  u32 const seglen = ZH_K3_SEGLEN(nbSeq), nk = seglen / K3_BATCH;
+  u16 *const gst = (u16 *)ws.lits(bb);                 // states
+  const u8 *const cbase = ws.lits(bb) + 128u * seglen;  // codes
+  u32 const ln = lane;  // (slot 63 exists in the layout and is never read by the packing kernel)
+  auto codes_at = [&](u32 k, u32 slot) { return *(const uint4 *)(cbase + ((64u * k + slot) << 4)); };  // batch k's 16 codes
+  u32 const a = lane < 3 * K3_SEGS ? g * seglen : 3u * K3_SEGS * seglen;  // first step (lane 63: none)
+  auto init_state = [&](u32 code) {  // FSE_initCState2
+    FseSym const tr = syT[code];
+    u32 const nb = (tr.dNb + (1u << 15)) >> 16;
+    return (u32)stT[(((nb << 16) - tr.dNb) >> nb) + tr.dFS];
+  };
+  auto step = [&](u32 s, u32 code, bool live) {
+    FseSym const tr = syT[code];
+    u32 const nb = (s + tr.dNb) >> 16;
+    u32 const nx = stT[min((s >> nb) + (u32)tr.dFS, 1023u)];
+    return live ? nx : s;
+  };
+  // entry guess: segment 0 the exact initial state, others the state after the last K3_WARM
+  // steps of the segment before, run from an arbitrary state (their codes: K3_WARM / 16
+  // 16-byte loads issued together)
+  u32 entry;
+  if (a == 0) {
+    entry = init_state(codes_at(0, ln).x & 63u);
+  } else {
+    constexpr u32 NW = K3_WARM / K3_BATCH;
+    u32 const kw = nk > NW ? nk - NW : 0u, ep = a - seglen;  // first warm-up batch, first step of segment g-1
+    uint4 cw[NW];
+#pragma unroll
+    for (u32 j = 0; j < NW; j++) cw[j] = kw + j < nk ? codes_at(kw + j, ln - 1) : make_uint4(0, 0, 0, 0);
+    u32 s = stT[0];
+#pragma unroll
+    for (u32 j = 0; j < NW; j++) {
+      u32 const w[4] = {cw[j].x, cw[j].y, cw[j].z, cw[j].w};
+#pragma unroll
+      for (u32 q = 0; q < K3_BATCH; q++) {
+        u32 const e = ep + K3_BATCH * (kw + j) + q;
+        s = step(s, (w[q >> 2] >> (8 * (q & 3))) & 63u, kw + j < nk && e >= 1 && e < nbSeq);
+      }
+    }
+    entry = s;
+  }
 #ifdef ZH_STAMPS
   u64 const k3t0 = __builtin_amdgcn_s_memtime();
-  u64 k3chain = 0, k3codes = 0, k3wait = 0;
+  u32 k3rounds = 0, k3rerun = 0;
 #endif
-  uint4 ca = ((const uint4 *)cb)[0], cc = ((const uint4 *)cb)[1];
-  auto batch = [&](u32 k0, uint4 &c4) {
-#ifdef ZH_STAMPS
-    u64 const kt0 = __builtin_amdgcn_s_memtime();
-#endif
-    u32 const w[4] = {c4.x, c4.y, c4.z, c4.w};
-    u32 dnb[K3_BATCH];
-    s32 dfs[K3_BATCH];
+  // A pass over the segment from state s: batches of K3_BATCH steps, the next batch's codes
+  // (and, with check, its first stored state) loaded while this one runs; with check, stops
+  // at the first batch whose stored first state equals the new trajectory's (returns true:
+  // merged, everything from there on and the exit are already right).  s ends as the exit
+  // state when the pass runs to the end.
+  auto pass = [&](u32 &s, bool check) {
+    uint4 cn = codes_at(0, ln);
+    u32 on = check ? (u32)gst[ln << 4] : 0u;
+    for (u32 k = 0; k < nk; k++) {
+      uint4 const c4 = cn;
+      u32 const o = on;
+      if (k + 1 < nk) {
+        cn = codes_at(k + 1, ln);
+        if (check) on = gst[(64u * (k + 1) + ln) << 4];
+      }
+      if (check && s == o) return true;  // met the stored trajectory: the rest is stored
+      u32 const w[4] = {c4.x, c4.y, c4.z, c4.w};
+      u32 sv[K3_BATCH];
 #pragma unroll
-    for (u32 q = 0; q < K3_BATCH; q++) {
-      FseSym const tr = syT[(w[q >> 2] >> (8 * (q & 3))) & 63u];
-      bool const live = k0 + q >= 1 && k0 + q < nbSeq;
-      dnb[q] = live ? tr.dNb : 0u;  // a dead step maps s to stT[s] ...
-      dfs[q] = live ? tr.dFS : 0;
+      for (u32 q = 0; q < K3_BATCH; q++) {
+        sv[q] = s;
+        u32 const e = a + K3_BATCH * k + q;
+        s = step(s, (w[q >> 2] >> (8 * (q & 3))) & 63u, e >= 1 && e < nbSeq);
+      }
+      uint4 *dst = (uint4 *)(gst + ((64u * k + ln) << 4));
+      dst[0] = make_uint4(sv[0] | (sv[1] << 16), sv[2] | (sv[3] << 16), sv[4] | (sv[5] << 16), sv[6] | (sv[7] << 16));
+      dst[1] = make_uint4(sv[8] | (sv[9] << 16), sv[10] | (sv[11] << 16), sv[12] | (sv[13] << 16), sv[14] | (sv[15] << 16));
     }
-    u32 const kn = k0 + 2 * K3_BATCH;
-    if (kn < NS) c4 = *(const uint4 *)(cb + kn);
-#ifdef ZH_STAMPS
-    __asm__ volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    u64 const kt1 = __builtin_amdgcn_s_memtime();
-    k3codes += kt1 - kt0;
-#endif
-    u32 sv[K3_BATCH];
-#pragma unroll
-    for (u32 q = 0; q < K3_BATCH; q++) {
-      sv[q] = s;
-      u32 const nb = (s + dnb[q]) >> 16;
-      u32 const nx2 = stT[min((s >> nb) + (u32)dfs[q], 1023u)];
-      bool const live = k0 + q >= 1 && k0 + q < nbSeq;
-      s = live ? nx2 : s;  // ... and is discarded
-    }
-#ifdef ZH_STAMPS
-    __asm__ volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    k3chain += __builtin_amdgcn_s_memtime() - kt1;
-#endif
-    uint4 *dst = (uint4 *)(gst + k0);
-    dst[0] = make_uint4(sv[0] | (sv[1] << 16), sv[2] | (sv[3] << 16), sv[4] | (sv[5] << 16), sv[6] | (sv[7] << 16));
-    dst[1] = make_uint4(sv[8] | (sv[9] << 16), sv[10] | (sv[11] << 16), sv[12] | (sv[13] << 16), sv[14] | (sv[15] << 16));
+    return false;
   };
-  for (u32 k0 = 0; k0 < nbSeq; k0 += 2 * K3_BATCH) {  // NS is a multiple of 32
-    batch(k0, ca);
-    batch(k0 + K3_BATCH, cc);
-  }
-  ff[ZH_FF_SLL + t] = s;
+  // first pass: every segment from its entry guess
+  u32 x = entry;
+  (void)pass(x, false);
+  // Jacobi rounds: entry(g) = exit(g - 1); a changed entry reruns its segment until the new
+  // trajectory merges with the stored one (exit then unchanged) or the segment ends
+  for (;;) {
+    u32 const pe = wave_shr1(x);
+    u32 const ne = (g == 0 || lane >= 3 * K3_SEGS) ? entry : pe;
+    bool const active = ne != entry;
+    if (!__ballot(active)) break;
 #ifdef ZH_STAMPS
-  if (t == 0) { u32 *dbg = ws.dbg(bb); dbg[46] = (u32)(__builtin_amdgcn_s_memtime() - k3t0); dbg[47] = (u32)k3codes; dbg[48] = (u32)k3chain; dbg[49] = nbSeq; }
+    k3rounds++;
+    k3rerun += __builtin_popcountll(__ballot(active));
+#endif
+    if (active) {
+      entry = ne;
+      u32 s = ne;
+      if (!pass(s, true)) x = s;  // ran to the segment's end without merging: a new exit
+    }
+  }
+  if (g == K3_SEGS - 1 && lane < 3 * K3_SEGS) ff[ZH_FF_SLL + t] = x;
+#ifdef ZH_STAMPS
+  if (lane == 0) { u32 *dbg = ws.dbg(bb); dbg[46] = (u32)(__builtin_amdgcn_s_memtime() - k3t0); dbg[47] = k3rounds; dbg[48] = k3rerun; dbg[49] = nbSeq;
+                   dbg[50] = (u32)(k3t0 - k3pre); dbg[51] = (u32)k3rt0; dbg[52] = (u32)__builtin_amdgcn_s_memrealtime(); }
 #endif
 }
 
@@ -1492,14 +1534,18 @@ extern "C" __global__ __launch_bounds__(64) void zh_seq_pack_kernel(const ZhBloc
   u32 const sLL = ff[ZH_FF_SLL], sOF = ff[ZH_FF_SOF], sML = ff[ZH_FF_SML];
   Out const o{d.dst, d.dst_cap};
   const u64 *seq = ws.seq(b);
-  u32 const NS = (nbSeq + 31) & ~31u;
-  const u16 *gLL = (const u16 *)ws.lits(b), *gOF = gLL + NS, *gML = gOF + NS;
+  u32 const k3L = ZH_K3_SEGLEN(nbSeq), k3m = zh_k3_magic(k3L);
+  const u16 *gLL = (const u16 *)ws.lits(b), *gOF = gLL + 16u * ZH_K3_SEGS, *gML = gOF + 16u * ZH_K3_SEGS;  // chain layout
   CodeTabs ct;
   ct.load();
   wave_sync();
   BitSink bs{ff[ZH_FF_OP], 0};
   u64 nrec = lane < nbSeq ? seq[nbSeq - 1 - lane] : 0;
-  u32 nL = 0 < lane && lane < nbSeq ? gLL[lane] : 0u, nM = 0 < lane && lane < nbSeq ? gML[lane] : 0u, nO = 0 < lane && lane < nbSeq ? gOF[lane] : 0u;
+  u32 nL = 0, nM = 0, nO = 0;
+  if (0 < lane && lane < nbSeq) {
+    u32 const x = zh_k3_index(lane, 0, k3L, k3m);
+    nL = gLL[x]; nM = gML[x]; nO = gOF[x];
+  }
   for (u32 e0 = 0; e0 < nbSeq; e0 += 64) {
     u32 const e = e0 + lane;
     bool const valid = e < nbSeq;
@@ -1507,7 +1553,12 @@ extern "C" __global__ __launch_bounds__(64) void zh_seq_pack_kernel(const ZhBloc
     u32 const s_L = nL, s_M = nM, s_O = nO;
     u32 const en = e + 64;
     nrec = en < nbSeq ? seq[nbSeq - 1 - en] : 0;  // next chunk in flight
-    nL = en < nbSeq ? gLL[en] : 0u; nM = en < nbSeq ? gML[en] : 0u; nO = en < nbSeq ? gOF[en] : 0u;
+    if (en < nbSeq) {
+      u32 const x = zh_k3_index(en, 0, k3L, k3m);
+      nL = gLL[x]; nM = gML[x]; nO = gOF[x];
+    } else {
+      nL = nM = nO = 0;
+    }
     u32 const ll = (u32)(rec & 0x1FFFFu), mlb = (u32)((rec >> 17) & 0x1FFFFu), ob = (u32)(rec >> 34) & 0x1FFFFu;
     u32 const llc = valid ? (u32)(rec >> 51) & 63u : 0, mlc = valid ? (u32)(rec >> 57) & 63u : 0, ofc = valid ? highbit32(ob) : 0;
     u32 const llbits = ct.ll_bits(llc), mlbits = ct.ml_bits(mlc);
@@ -1543,7 +1594,7 @@ void entropy_launch(const ZhBlockDesc *d_descs, u32 nblocks, ZhWorkspace ws, u32
                     u32 *d_item_status, u32 *d_blk_size, hipStream_t stream) {
   hipLaunchKernelGGL(zh_entropy_kernel, dim3(nblocks), dim3(K2_THREADS), K2_LDS, stream, d_descs, ws, window_log, cfg_block_size, d_item_size,
                      d_item_status, d_blk_size);
-  hipLaunchKernelGGL(zh_fse_chain_kernel, dim3((nblocks + K3_BLOCKS - 1) / K3_BLOCKS), dim3(64), K3_LDS, stream, d_descs, nblocks, ws);
+  hipLaunchKernelGGL(zh_fse_chain_kernel, dim3((nblocks + K3_WAVES - 1) / K3_WAVES), dim3(64 * K3_WAVES), K3_LDS, stream, d_descs, nblocks, ws);
   hipLaunchKernelGGL(zh_seq_pack_kernel, dim3(nblocks), dim3(64), KP_LDS, stream, d_descs, ws, d_item_size, d_item_status, d_blk_size);
 }
 }  // namespace zh

@@ -14,7 +14,7 @@ import cuda_zstd
 import zh_testlib as T
 
 kind = sys.argv[1] if len(sys.argv) > 1 else "mix"
-n, cs = 2048, 65536
+n, cs = (int(sys.argv[2]) if len(sys.argv) > 2 else 2048), 65536
 data = T.gen(T.KINDS[kind], n, 0x5EED0003, cs)
 dev = torch.from_numpy(data).cuda()
 bc = cuda_zstd.BatchedCompressor(3, cs)
@@ -36,11 +36,11 @@ off = a256(off + n * 4)
 off = a256(off + 0)
 off = a256(off + 4)  # K1 block counter
 blocks = base + off
-WS = 13120 * 8 + 118080 + 256 + 4096
+WS = 13120 * 8 + 122880 + 256 + 4096
 h = temp.cpu().numpy()
-m0 = h[blocks + 13120 * 8 + 118080: blocks + 13120 * 8 + 118080 + 16].view(np.uint32)
+m0 = h[blocks + 13120 * 8 + 122880: blocks + 13120 * 8 + 122880 + 16].view(np.uint32)
 print('block 0 meta (nseq, nlit, rle):', m0[:3].tolist(), 'temp', temp.numel(), 'blocks off', blocks, 'n*WS', n * WS)
-raw = np.array([h[blocks + b * WS + 13120 * 8 + 118080 + 16: blocks + b * WS + 13120 * 8 + 118080 + 16 + 52 * 4].view(np.uint32) for b in range(n)])
+raw = np.array([h[blocks + b * WS + 13120 * 8 + 122880 + 16: blocks + b * WS + 13120 * 8 + 122880 + 16 + 56 * 4].view(np.uint32) for b in range(n)])
 st = raw[:, :6]
 k2 = raw[:, 6:15].astype(np.float64)
 names = ["stage", "A(insert)", "B(lengths+exit)", "J(jacobi)", "E(emit)", "rounds"]
@@ -56,11 +56,28 @@ t2 = k2.sum(1).mean()
 print(kind, "K2 mean cycles/block", int(t2))
 for k, nm in enumerate(k2n):
     print(f"  {nm:20s} mean {k2[:, k].mean():12.0f}  share {k2[:, k].mean() / t2 * 100:5.1f}%")
-print(f"  of huf_build: parallel tree {np.array([h[blocks + b * WS + 13120 * 8 + 118080 + 16 + 42 * 4: blocks + b * WS + 13120 * 8 + 118080 + 16 + 43 * 4].view(np.uint32)[0] for b in range(n)]).mean():.0f}")
-print(f"  K3 per block: total {raw[:, 46].mean():.0f}  codes+loads {raw[:, 47].mean():.0f}  chain {raw[:, 48].mean():.0f}  (record wait {raw[:, 50].mean():.0f})  nbSeq {raw[:, 49].mean():.0f}")
+print(f"  of huf_build: parallel tree {np.array([h[blocks + b * WS + 13120 * 8 + 122880 + 16 + 42 * 4: blocks + b * WS + 13120 * 8 + 122880 + 16 + 43 * 4].view(np.uint32)[0] for b in range(n)]).mean():.0f}")
+print(f"  K3 per block: cycles mean {raw[:, 46].mean():.0f} max {raw[:, 46].max()}  Jacobi rounds mean {raw[:, 47].mean():.2f} max {raw[:, 47].max()}"
+      f"  reruns mean {raw[:, 48].mean():.1f}  nbSeq mean {raw[:, 49].mean():.0f} p99 {np.percentile(raw[:, 49], 99):.0f} max {raw[:, 49].max()}")
+print(f"  K3 staging+warm-up cycles mean {raw[:, 50].mean():.0f} max {raw[:, 50].max()}")
+t0, t1 = raw[:, 51].astype(np.int64), raw[:, 52].astype(np.int64)
+ok = (t1 >= t0) & (raw[:, 49] > 0)
+if ok.any():
+    base_t = t0[ok].min()
+    ev = sorted([(int(a - base_t), 1) for a in t0[ok]] + [(int(b - base_t), -1) for b in t1[ok]])
+    cur = peak = 0
+    for _, d in ev:
+        cur += d
+        peak = max(peak, cur)
+    span = (t1[ok].max() - base_t)
+    print(f"  K3 span {span / 100:.1f} us (100 MHz ticks), peak concurrent waves {peak}, mean concurrent {(t1[ok] - t0[ok]).sum() / span:.0f}, mean wave {(t1[ok] - t0[ok]).mean() / 100:.1f} us")
+    st_ = np.sort(t0[ok] - base_t)
+    print("  K3 wave start times (us) at 10/50/90/100 %:", [round(float(st_[int(q * (len(st_) - 1))]) / 100, 1) for q in (0.1, 0.5, 0.9, 1.0)])
+slow = np.argsort(raw[:, 46])[-5:]
+print("  slowest K3 blocks (cycles, rounds, reruns, nbSeq):", [(int(raw[b, 46]), int(raw[b, 47]), int(raw[b, 48]), int(raw[b, 49])) for b in slow])
 print(f"  of fse_chains: serial chain steps only {raw[:, 18].mean():.0f}  raw seqs mean {raw[:, 19].mean():.0f}")
 # wall clock per block (s_memrealtime, 100 MHz) and placement
-rt = np.array([h[blocks + b * WS + 13120 * 8 + 118080 + 16 + 23 * 4: blocks + b * WS + 13120 * 8 + 118080 + 16 + 28 * 4].view(np.uint32) for b in range(n)]).astype(np.int64)
+rt = np.array([h[blocks + b * WS + 13120 * 8 + 122880 + 16 + 23 * 4: blocks + b * WS + 13120 * 8 + 122880 + 16 + 28 * 4].view(np.uint32) for b in range(n)]).astype(np.int64)
 dur = (rt[:, 1] - rt[:, 0]) & 0xFFFFFFFF
 print(f"  block wall (realtime 100MHz ticks) mean {dur.mean():.0f} = {dur.mean() * 10:.0f} ns; memtime mean {rt[:, 4].mean():.0f} -> clock {rt[:, 4].mean() / (dur.mean() * 10):.2f} GHz")
 cu = (rt[:, 3] & 0xFFFFFFFF).astype(np.int64) * 1000 + ((rt[:, 2] >> 8) & 0xF) + 16 * ((rt[:, 2] >> 12) & 0x1) + 32 * ((rt[:, 2] >> 13) & 0x7)
@@ -70,6 +87,6 @@ busy = {}
 for c, d in zip(cu.tolist(), dur.tolist()):
     busy[c] = busy.get(c, 0) + d
 print(f"  per-CU busy fraction of span: mean {np.mean(list(busy.values())) / (t1 - t0):.3f}")
-mx = np.array([h[blocks + b * WS + 13120 * 8 + 118080 + 16 + 40 * 4: blocks + b * WS + 13120 * 8 + 118080 + 16 + 42 * 4].view(np.uint32) for b in range(n)])
+mx = np.array([h[blocks + b * WS + 13120 * 8 + 122880 + 16 + 40 * 4: blocks + b * WS + 13120 * 8 + 122880 + 16 + 42 * 4].view(np.uint32) for b in range(n)])
 if kind:
     print(f"  B-work max over worker waves {mx[:, 0].mean():.0f}   inserter busy max {mx[:, 1].mean():.0f}  (per block)")
