@@ -77,7 +77,7 @@ static_assert(sizeof(SerialScratch) <= 1024, "scratch");
 __device__ __forceinline__ u32 highbit32(u32 v) { return 31u - (u32)__builtin_clz(v); }
 __device__ __forceinline__ u32 ll_code(u32 ll) { return ll > 63 ? highbit32(ll) + 19 : c_LL_code[ll]; }
 __device__ __forceinline__ u32 ml_code(u32 mlBase) { return mlBase > 127 ? highbit32(mlBase) + 36 : c_ML_code[mlBase]; }
-__device__ __forceinline__ u32 lane_id() { return threadIdx.x; }
+__device__ __forceinline__ u32 lane_id() { return threadIdx.x & 63u; }
 // Code tables held across the wave (lane x holds entry x), looked up with ds_bpermute
 // instead of a constant-memory load per lookup.  All lanes must execute the lookups.
 struct CodeTabs {
@@ -98,7 +98,13 @@ struct CodeTabs {
   __device__ __forceinline__ u32 ll_bits(u32 c) const { return (u32)__shfl((int)llb, (int)(c & 63u), 64); }
   __device__ __forceinline__ u32 ml_bits(u32 c) const { return (u32)__shfl((int)mlb, (int)(c & 63u), 64); }
 };
-__device__ __forceinline__ void wave_sync() { __syncthreads(); }  // one wave per workgroup
+// Orders a wave's LDS accesses around it (the data is the wave's own: LDS executes one wave's
+// operations in order, so a compiler fence is all that is needed; kernels with several waves
+// per workgroup give each wave its own LDS slice)
+__device__ __forceinline__ void wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+}
 
 __device__ __forceinline__ u32 wave_excl_scan(u32 v, u32 &total) {
   u32 const incl = wave_scan_incl(v);  // DPP (zh_common.h)
@@ -338,9 +344,9 @@ __device__ int fse_normalize_wave(s16 *norm, u32 tableLog, u32 c, u32 total, u32
   int const nl = (int)lane_value((u32)n, largest);
   if (-still >= (nl >> 1)) {  // libzstd's FSE_normalizeM2 (rare): serial, from LDS
     if (lane <= maxSV) cnt_scratch[lane] = c;
-    __syncthreads();
+    wave_sync();
     if (lane == 0) fse_normalize_m2(norm, tableLog, cnt_scratch, total, maxSV, lowProbCount);
-    __syncthreads();
+    wave_sync();
     return lane <= maxSV ? norm[lane] : 0;
   }
   if (lane == largest) n += still;
@@ -1379,7 +1385,7 @@ constexpr u32 K3_TABW = ZH_FSE_TAB_BYTES / 4;
 
 extern "C" __global__ __launch_bounds__(64 * K3_WAVES) __attribute__((amdgpu_waves_per_eu(8, 8))) void zh_fse_chain_kernel(const ZhBlockDesc *__restrict__ blocks, u32 nblocks, ZhWorkspace ws) {
   extern __shared__ __attribute__((aligned(16))) u8 smem_all[];
-  u32 const lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;  // (lane_id() is threadIdx.x: one-wave kernels)
+  u32 const lane = lane_id(), wv = threadIdx.x >> 6;
   u32 const bb = blockIdx.x * K3_WAVES + wv;
   u8 *const smem = smem_all + wv * K3_TAB_STRIDE;  // this wave's block tables
 #ifdef ZH_STAMPS
@@ -1512,12 +1518,18 @@ extern "C" __global__ __launch_bounds__(64 * K3_WAVES) __attribute__((amdgpu_wav
 // One wave per block left by the entropy kernel: FSE state bits and extra bits of 64
 // encode steps per bit-sink append, final state flush, then the block is finished
 // (raw fallback, header, status) exactly as the entropy kernel does for other blocks.
-constexpr u32 KP_SW = 0, KP_DNB = 4 * SW_WORDS, KP_LDS = KP_DNB + 4 * 128;
+// K4_WAVES blocks (one per wave, each with its own LDS slice) per workgroup: a CU holds at
+// most 16 workgroups.
+constexpr u32 KP_SW = 0, KP_DNB = 4 * SW_WORDS, KP_LDS = (KP_DNB + 4 * 128 + 15) & ~15u;
+constexpr u32 K4_WAVES = 4;
 
-extern "C" __global__ __launch_bounds__(64) void zh_seq_pack_kernel(const ZhBlockDesc *__restrict__ blocks, ZhWorkspace ws, u64 *__restrict__ item_size,
-                                                                     u32 *__restrict__ item_status, u32 *__restrict__ blk_size) {
-  extern __shared__ __attribute__((aligned(16))) u8 smem[];
-  u32 const b = blockIdx.x, lane = lane_id();
+extern "C" __global__ __launch_bounds__(64 * K4_WAVES) void zh_seq_pack_kernel(const ZhBlockDesc *__restrict__ blocks, u32 nblocks, ZhWorkspace ws,
+                                                                               u64 *__restrict__ item_size, u32 *__restrict__ item_status,
+                                                                               u32 *__restrict__ blk_size) {
+  extern __shared__ __attribute__((aligned(16))) u8 smem_all[];
+  u32 const wv = threadIdx.x >> 6, b = blockIdx.x * K4_WAVES + wv, lane = lane_id();
+  u8 *const smem = smem_all + wv * KP_LDS;
+  if (b >= nblocks) return;
   ZhBlockDesc const d = blocks[b];
   if (d.n == 0) return;
   const u32 *ff = ws.fsef(b);
@@ -1595,6 +1607,7 @@ void entropy_launch(const ZhBlockDesc *d_descs, u32 nblocks, ZhWorkspace ws, u32
   hipLaunchKernelGGL(zh_entropy_kernel, dim3(nblocks), dim3(K2_THREADS), K2_LDS, stream, d_descs, ws, window_log, cfg_block_size, d_item_size,
                      d_item_status, d_blk_size);
   hipLaunchKernelGGL(zh_fse_chain_kernel, dim3((nblocks + K3_WAVES - 1) / K3_WAVES), dim3(64 * K3_WAVES), K3_LDS, stream, d_descs, nblocks, ws);
-  hipLaunchKernelGGL(zh_seq_pack_kernel, dim3(nblocks), dim3(64), KP_LDS, stream, d_descs, ws, d_item_size, d_item_status, d_blk_size);
+  hipLaunchKernelGGL(zh_seq_pack_kernel, dim3((nblocks + K4_WAVES - 1) / K4_WAVES), dim3(64 * K4_WAVES), K4_WAVES * KP_LDS, stream, d_descs, nblocks, ws, d_item_size,
+                     d_item_status, d_blk_size);
 }
 }  // namespace zh
