@@ -879,6 +879,25 @@ __device__ __forceinline__ void copy_bytes(const Out &o, u32 pos, const u8 *src,
 // ============================================================================
 // Raw fallback (ZSTD_compressBlock_internal: a compressed body of >= n - minGain bytes is
 // replaced by the raw block) and the block header; returns the block's end offset.
+// A 64-lane sweep over u64 records: lane l of chunk c gets record 64 c + l, loaded
+// RING_DEPTH chunks ahead (global-memory latency at 4 waves per SIMD is several chunks' work)
+constexpr u32 RING_DEPTH = 4;
+struct RecRing {
+  u64 r[RING_DEPTH];
+  __device__ __forceinline__ void init(const u64 *seq, u32 n, u32 lane) {
+#pragma unroll
+    for (u32 k = 0; k < RING_DEPTH; k++) r[k] = lane + 64 * k < n ? seq[lane + 64 * k] : 0;
+  }
+  __device__ __forceinline__ u64 next(const u64 *seq, u32 n, u32 i) {
+    u64 const v = r[0];
+#pragma unroll
+    for (u32 k = 0; k + 1 < RING_DEPTH; k++) r[k] = r[k + 1];
+    u32 const j = i + 64 * RING_DEPTH;
+    r[RING_DEPTH - 1] = j < n ? seq[j] : 0;
+    return v;
+  }
+};
+
 __device__ u32 finish_block(const ZhBlockDesc &d, const Out &o, u32 blk, u32 op, bool early_raw) {
   u32 const lane = lane_id(), n = d.n, last = (d.flags & ZH_F_LAST) ? 1u : 0u, body0 = blk + 3;
   u32 const body = op - body0;
@@ -1097,15 +1116,34 @@ extern "C" __global__ __launch_bounds__(K2_THREADS) void zh_entropy_kernel(const
         for (u32 k = 0; k < ns; k++) {
           u32 a = single ? 0 : k * seg, e = single ? nl : (k < 3 ? (k + 1) * seg : nl);
           BitSink bs{op, 0};
-          // symbols from e-1 down to a, 8 per lane per append (codes paired into <= 22-bit fields)
+          // symbols from e-1 down to a, 8 per lane per append (codes paired into <= 22-bit fields);
+          // a lane's 8 symbols are the bytes [A, A + 8), A = e - 8 - base - 8 lane, read as three
+          // aligned dwords, the next append's in flight while this one is encoded
+          const u32 *l32 = (const u32 *)lits;
+          auto ld3 = [&](u32 base_, u32 (&dw)[3]) {
+            int const A = (int)e - 8 - (int)base_ - 8 * (int)lane;
+            u32 const w0 = A > (int)a ? (u32)A >> 2 : a >> 2;
+            dw[0] = l32[w0]; dw[1] = l32[w0 + 1]; dw[2] = l32[w0 + 2];
+          };
+          u32 dn[3];
+          ld3(0, dn);
           for (u32 base = 0; base < e - a; base += 512) {
+            u32 const dw[3] = {dn[0], dn[1], dn[2]};
+            if (base + 512 < e - a) ld3(base + 512, dn);
+            int const A = (int)e - 8 - (int)base - 8 * (int)lane;
+            u32 const sh = (u32)A & 3u;
+            u32 const lo = __builtin_amdgcn_alignbyte(dw[1], dw[0], sh), hi = __builtin_amdgcn_alignbyte(dw[2], dw[1], sh);
+            bool const full = A >= (int)a;  // all 8 bytes inside the stream (else: byte loads)
             u32 v[4], nb[4];
 #pragma unroll
             for (u32 f = 0; f < 4; f++) {
               u32 const j0 = base + 8 * lane + 2 * f, j1 = j0 + 1;
               u32 c0 = 0, n0 = 0, c1 = 0, n1 = 0;
-              if (j0 < e - a) { u8 const c = lits[e - 1 - j0]; c0 = hval[c]; n0 = hnb[c]; }
-              if (j1 < e - a) { u8 const c = lits[e - 1 - j1]; c1 = hval[c]; n1 = hnb[c]; }
+              // symbol jj = 2f (+1) of the lane is byte 7 - jj of (lo, hi)
+              u32 const b0 = full ? ((f < 2 ? hi : lo) >> (8 * (3 - 2 * (f & 1)))) & 255u : 0u;
+              u32 const b1 = full ? ((f < 2 ? hi : lo) >> (8 * (2 - 2 * (f & 1)))) & 255u : 0u;
+              if (j0 < e - a) { u32 const c = full ? b0 : lits[e - 1 - j0]; c0 = hval[c]; n0 = hnb[c]; }
+              if (j1 < e - a) { u32 const c = full ? b1 : lits[e - 1 - j1]; c1 = hval[c]; n1 = hnb[c]; }
               v[f] = c0 | (c1 << n0);
               nb[f] = n0 + n1;
             }
@@ -1126,12 +1164,12 @@ extern "C" __global__ __launch_bounds__(K2_THREADS) void zh_entropy_kernel(const
     {
       u32 carryCum = 0, carryOff = 0, openIdx = 0, openLL = 0, openMl = 0, openOff = 0;
       bool open = false;
-      u64 nrec = lane < nseq_raw ? seq[lane] : 0;  // next chunk's records, loaded a chunk ahead
+      RecRing ring;  // records loaded RING_DEPTH chunks ahead (this chunk writes only indices <= i)
+      ring.init(seq, nseq_raw, lane);
       for (u32 base = 0; base < nseq_raw; base += 64) {
         u32 const i = base + lane;
         bool const valid = i < nseq_raw;
-        u64 const rec = nrec;
-        nrec = i + 64 < nseq_raw ? seq[i + 64] : 0;  // (this chunk writes only indices <= i)
+        u64 const rec = ring.next(seq, nseq_raw, i);
         u32 const cum = (u32)(rec & 0x1FFFFu), ml = (u32)((rec >> 17) & 255u), off = (u32)((rec >> 25) & 0xFFFFu);
         u32 pc = wave_shr1(cum), po = wave_shr1(off);
         if (lane == 0) { pc = carryCum; po = carryOff; }
@@ -1139,22 +1177,19 @@ extern "C" __global__ __launch_bounds__(K2_THREADS) void zh_entropy_kernel(const
         bool const flag = valid && i > 0 && ll == 0 && off == po;
         bool const head = valid && !flag;
         u64 const hm = __ballot(head);
-        // ml accumulation into the run head (in-batch) or into the open head (carried)
-        if (lane == 0) misc[64 - 1] = 0;
-        for (u32 k = lane; k < 64; k += 64) misc[k] = 0;  // misc[0..63] per-head sums
-        wave_sync();
-        u64 const below = hm & ((lane == 63) ? ~0ull : ((2ull << lane) - 1));
-        int const h = below ? 63 - __builtin_clzll(below) : -1;
-        u32 carryAdd = 0;
-        if (valid) {
-          if (h >= 0) atomicAdd(&misc[h], ml);
-          else carryAdd = ml;
-        }
-        carryAdd = wave_sum(carryAdd);
-        wave_sync();
+        // run sums of ml without LDS: inclusive DPP scan, each head reads the scan at its run's
+        // last lane in this chunk (one ds_bpermute); lanes before the first head extend the
+        // run carried in from the previous chunk
+        u32 const mlv = valid ? ml : 0u;
+        u32 const incl = wave_scan_incl(mlv);
+        u64 const headBitsAfter = hm & ~((lane == 63) ? ~0ull : ((2ull << lane) - 1));
+        u32 const runEnd = headBitsAfter ? (u32)__builtin_ctzll(headBitsAfter) - 1u : 63u;
+        u32 const inclEnd = (u32)__builtin_amdgcn_ds_bpermute((int)(runEnd << 2), (int)incl);
+        u32 const runMl = inclEnd - (incl - mlv);  // (heads: the run's ml within this chunk)
         u32 const hcount = (u32)__popcll(hm);
         u32 const rank = (u32)__popcll(hm & ((1ull << lane) - 1));
-        u64 const headBitsAfter = hm & ~((lane == 63) ? ~0ull : ((2ull << lane) - 1));
+        u32 const firstH = hm ? (u32)__builtin_ctzll(hm) : 64u;
+        u32 const carryAdd = firstH ? lane_value(incl, firstH - 1u) : 0u;
         // finalize the carried open head: closed if this batch has any head, or at the very end
         openMl += carryAdd;
         if (open && hcount) {
@@ -1162,16 +1197,15 @@ extern "C" __global__ __launch_bounds__(K2_THREADS) void zh_entropy_kernel(const
           open = false;
         }
         if (head) {
-          u32 const myMl = misc[lane];
           u32 const idx = nbSeq + rank;
-          if (headBitsAfter) seq[idx] = (u64)ll | ((u64)myMl << 17) | ((u64)off << 34);
+          if (headBitsAfter) seq[idx] = (u64)ll | ((u64)runMl << 17) | ((u64)off << 34);
         }
         if (hcount) {
           int const lastH = 63 - __builtin_clzll(hm);
           openIdx = nbSeq + hcount - 1;
           openLL = lane_value(ll, (u32)lastH);
           openOff = lane_value(off, (u32)lastH);
-          openMl = lane_value(misc[lane], (u32)lastH);
+          openMl = lane_value(runMl, (u32)lastH);
           open = true;
         }
         nbSeq += hcount;
@@ -1209,12 +1243,12 @@ extern "C" __global__ __launch_bounds__(K2_THREADS) void zh_entropy_kernel(const
       ct.load();
       u32 const k3L = ZH_K3_SEGLEN(nbSeq), k3m = zh_k3_magic(k3L);
       u8 *const cb = ws.lits(b) + 128u * k3L;  // codes in encoding order (step nbSeq-1-i), chain layout (zh_common.h)
-      u64 nrec = lane < nbSeq ? seq[lane] : 0;
+      RecRing ring;  // (in place: this chunk writes only indices <= i)
+      ring.init(seq, nbSeq, lane);
       for (u32 base = 0; base < nbSeq; base += 64) {
         u32 const i = base + lane;
         bool const valid = i < nbSeq;
-        u64 const rec = nrec;
-        nrec = i + 64 < nbSeq ? seq[i + 64] : 0;
+        u64 const rec = ring.next(seq, nbSeq, i);
         u32 const ll = (u32)(rec & 0x1FFFFu), ml = (u32)((rec >> 17) & 0x1FFFFu), off = (u32)(rec >> 34);
         u32 r0 = wave_shr1(off);
         if (lane == 0) r0 = cr0;
