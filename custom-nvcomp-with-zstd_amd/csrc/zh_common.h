@@ -43,14 +43,16 @@ enum : u32 {
 #define ZH_SEQ_CAP 13120u
 #define ZH_SEQ_BYTES (ZH_SEQ_CAP * 8u)
 // FSE chain segments (zh_entropy.hip K3): each of the three tables' chains is cut into
-// ZH_K3_SEGS segments of L steps (L a multiple of 16); lane t * ZH_K3_SEGS + g of the chain
-// wave runs segment g of table t.  Step e of table t is element
-//   ((r / 16) * 64 + t * ZH_K3_SEGS + g) * 16 + r % 16,   g = e / L, r = e % L
-// of the state (u16) and code (u8) arrays: every 16-step batch of the 63 lanes is one
-// contiguous run (1 KiB of codes, 2 KiB of states), so the chain kernel's loads and stores
-// are whole cache lines.
+// ZH_K3_SEGS segments of L steps (L a multiple of ZH_K3_RUN); lane t * ZH_K3_SEGS + g of the
+// chain wave runs segment g of table t.  Step e of table t is element
+//   ((r / RUN) * 64 + t * ZH_K3_SEGS + g) * RUN + r % RUN,   g = e / L, r = e % L
+// of the state (u16) and code (u8) arrays, RUN = ZH_K3_RUN: RUN consecutive steps of a
+// segment are contiguous (the packing kernel's 64-step chunks are whole lines) and the 63
+// segments' runs are adjacent.
 #define ZH_K3_SEGS 21u
-#define ZH_K3_SEGLEN(nbseq) ((((nbseq) + ZH_K3_SEGS - 1u) / ZH_K3_SEGS + 15u) & ~15u)
+#define ZH_K3_RUN 16u
+#define ZH_K3_TSTRIDE (ZH_K3_SEGS * ZH_K3_RUN)  // elements between a step's LL, OF and ML entries
+#define ZH_K3_SEGLEN(nbseq) ((((nbseq) + ZH_K3_SEGS - 1u) / ZH_K3_SEGS + ZH_K3_RUN - 1u) & ~(ZH_K3_RUN - 1u))
 #define ZH_K3_BYTES(nbseq) (192u * ZH_K3_SEGLEN(nbseq))
 #define ZH_LIT_BYTES (ZH_K3_BYTES(ZH_SEQ_CAP) > (u32)ZH_BLOCK_MAX ? ZH_K3_BYTES(ZH_SEQ_CAP) : (u32)ZH_BLOCK_MAX)
 static_assert(3u * ZH_K3_SEGS <= 64u, "one lane per (table, segment)");
@@ -88,7 +90,7 @@ struct ZhWorkspace {
 __host__ __device__ __forceinline__ u32 zh_k3_magic(u32 L) { return ((1u << 24) + L - 1u) / L; }
 __device__ __forceinline__ u32 zh_k3_index(u32 e, u32 t, u32 L, u32 m) {
   u32 const g = __umulhi(e << 8, m), r = e - g * L;
-  return (((r >> 4) * 64u + t * ZH_K3_SEGS + g) << 4) + (r & 15u);
+  return ((r / ZH_K3_RUN) * 64u + t * ZH_K3_SEGS + g) * ZH_K3_RUN + (r & (ZH_K3_RUN - 1u));
 }
 
 // Status codes written per item (values of cuda_zstd::Status).

@@ -1283,7 +1283,7 @@ extern "C" __global__ __launch_bounds__(K2_THREADS) void zh_entropy_kernel(const
           seq[i] = (u64)ll | ((u64)mlb << 17) | ((u64)ob << 34) | ((u64)llc << 51) | ((u64)mlc << 57);
           u32 const k = nbSeq - 1 - i;
           u32 const x0 = zh_k3_index(k, 0, k3L, k3m);
-          cb[x0] = (u8)llc; cb[x0 + 16u * ZH_K3_SEGS] = (u8)highbit32(ob); cb[x0 + 32u * ZH_K3_SEGS] = (u8)mlc;
+          cb[x0] = (u8)llc; cb[x0 + ZH_K3_TSTRIDE] = (u8)highbit32(ob); cb[x0 + 2u * ZH_K3_TSTRIDE] = (u8)mlc;
         }
       }
       wave_sync();
@@ -1450,7 +1450,9 @@ extern "C" __global__ __launch_bounds__(64 * K3_WAVES) __attribute__((amdgpu_wav
   u16 *const gst = (u16 *)ws.lits(bb);                 // states
   const u8 *const cbase = ws.lits(bb) + 128u * seglen;  // codes
   u32 const ln = lane;  // (slot 63 exists in the layout and is never read by the packing kernel)
-  auto codes_at = [&](u32 k, u32 slot) { return *(const uint4 *)(cbase + ((64u * k + slot) << 4)); };  // batch k's 16 codes
+  // element of batch k (16 steps) of a slot's segment
+  auto at = [&](u32 k, u32 slot) { return ((k * K3_BATCH / ZH_K3_RUN) * 64u + slot) * ZH_K3_RUN + (k * K3_BATCH) % ZH_K3_RUN; };
+  auto codes_at = [&](u32 k, u32 slot) { return *(const uint4 *)(cbase + at(k, slot)); };  // batch k's 16 codes
   u32 const a = lane < 3 * K3_SEGS ? g * seglen : 3u * K3_SEGS * seglen;  // first step (lane 63: none)
   auto init_state = [&](u32 code) {  // FSE_initCState2
     FseSym const tr = syT[code];
@@ -1498,13 +1500,13 @@ extern "C" __global__ __launch_bounds__(64 * K3_WAVES) __attribute__((amdgpu_wav
   // state when the pass runs to the end.
   auto pass = [&](u32 &s, bool check) {
     uint4 cn = codes_at(0, ln);
-    u32 on = check ? (u32)gst[ln << 4] : 0u;
+    u32 on = check ? (u32)gst[at(0, ln)] : 0u;
     for (u32 k = 0; k < nk; k++) {
       uint4 const c4 = cn;
       u32 const o = on;
       if (k + 1 < nk) {
         cn = codes_at(k + 1, ln);
-        if (check) on = gst[(64u * (k + 1) + ln) << 4];
+        if (check) on = gst[at(k + 1, ln)];
       }
       if (check && s == o) return true;  // met the stored trajectory: the rest is stored
       u32 const w[4] = {c4.x, c4.y, c4.z, c4.w};
@@ -1515,7 +1517,7 @@ extern "C" __global__ __launch_bounds__(64 * K3_WAVES) __attribute__((amdgpu_wav
         u32 const e = a + K3_BATCH * k + q;
         s = step(s, (w[q >> 2] >> (8 * (q & 3))) & 63u, e >= 1 && e < nbSeq);
       }
-      uint4 *dst = (uint4 *)(gst + ((64u * k + ln) << 4));
+      uint4 *dst = (uint4 *)(gst + at(k, ln));
       dst[0] = make_uint4(sv[0] | (sv[1] << 16), sv[2] | (sv[3] << 16), sv[4] | (sv[5] << 16), sv[6] | (sv[7] << 16));
       dst[1] = make_uint4(sv[8] | (sv[9] << 16), sv[10] | (sv[11] << 16), sv[12] | (sv[13] << 16), sv[14] | (sv[15] << 16));
     }
@@ -1581,7 +1583,7 @@ extern "C" __global__ __launch_bounds__(64 * K4_WAVES) void zh_seq_pack_kernel(c
   Out const o{d.dst, d.dst_cap};
   const u64 *seq = ws.seq(b);
   u32 const k3L = ZH_K3_SEGLEN(nbSeq), k3m = zh_k3_magic(k3L);
-  const u16 *gLL = (const u16 *)ws.lits(b), *gOF = gLL + 16u * ZH_K3_SEGS, *gML = gOF + 16u * ZH_K3_SEGS;  // chain layout
+  const u16 *gLL = (const u16 *)ws.lits(b), *gOF = gLL + ZH_K3_TSTRIDE, *gML = gOF + ZH_K3_TSTRIDE;  // chain layout
   CodeTabs ct;
   ct.load();
   wave_sync();
