@@ -74,6 +74,8 @@ if ok.any():
     st_ = np.sort(t0[ok] - base_t)
     print("  K3 wave start times (us) at 10/50/90/100 %:", [round(float(st_[int(q * (len(st_) - 1))]) / 100, 1) for q in (0.1, 0.5, 0.9, 1.0)])
 slow = np.argsort(raw[:, 46])[-5:]
+wb = np.concatenate([raw[:, 28:40], raw[:, 53:55]], 1).astype(np.float64)
+print("  K1 length-phase cycles per worker wave (mean over blocks, waves 0..13; SIMD = wave % 4):", [int(x) for x in wb.mean(0)])
 print("  slowest K3 blocks (cycles, rounds, reruns, nbSeq):", [(int(raw[b, 46]), int(raw[b, 47]), int(raw[b, 48]), int(raw[b, 49])) for b in slow])
 print(f"  of fse_chains: serial chain steps only {raw[:, 18].mean():.0f}  raw seqs mean {raw[:, 19].mean():.0f}")
 # wall clock per block (s_memrealtime, 100 MHz) and placement
