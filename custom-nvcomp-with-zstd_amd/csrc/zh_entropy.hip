@@ -1159,76 +1159,16 @@ extern "C" __global__ __launch_bounds__(K2_THREADS) void zh_entropy_kernel(const
 
     // ======================= sequences section =======================
     if (!early_raw) {
-    // pass A: literal lengths from cumulative counts, merge same-offset continuations (in place)
+    // One pass over K1's records: literal lengths from the cumulative counts, same-offset
+    // continuations merged into their run head (DPP scan), and each closed run handed on as
+    // a sequence (ds_permute compaction, a chunk's runs + the one left open by the chunk
+    // before) to the repcode / code / histogram step, which writes the merged records in
+    // place (record = ll | mlBase << 17 | offBase << 34 | llCode << 51 | mlCode << 57).
     u32 nbSeq = 0;
+    u32 *hLL = hist, *hOF = hist + 64, *hML = hist + 128;
+    for (u32 i = lane; i < 192; i += 64) hist[i] = 0;
+    wave_sync();
     {
-      u32 carryCum = 0, carryOff = 0, openIdx = 0, openLL = 0, openMl = 0, openOff = 0;
-      bool open = false;
-      RecRing ring;  // records loaded RING_DEPTH chunks ahead (this chunk writes only indices <= i)
-      ring.init(seq, nseq_raw, lane);
-      for (u32 base = 0; base < nseq_raw; base += 64) {
-        u32 const i = base + lane;
-        bool const valid = i < nseq_raw;
-        u64 const rec = ring.next(seq, nseq_raw, i);
-        u32 const cum = (u32)(rec & 0x1FFFFu), ml = (u32)((rec >> 17) & 255u), off = (u32)((rec >> 25) & 0xFFFFu);
-        u32 pc = wave_shr1(cum), po = wave_shr1(off);
-        if (lane == 0) { pc = carryCum; po = carryOff; }
-        u32 const ll = cum - pc;
-        bool const flag = valid && i > 0 && ll == 0 && off == po;
-        bool const head = valid && !flag;
-        u64 const hm = __ballot(head);
-        // run sums of ml without LDS: inclusive DPP scan, each head reads the scan at its run's
-        // last lane in this chunk (one ds_bpermute); lanes before the first head extend the
-        // run carried in from the previous chunk
-        u32 const mlv = valid ? ml : 0u;
-        u32 const incl = wave_scan_incl(mlv);
-        u64 const headBitsAfter = hm & ~((lane == 63) ? ~0ull : ((2ull << lane) - 1));
-        u32 const runEnd = headBitsAfter ? (u32)__builtin_ctzll(headBitsAfter) - 1u : 63u;
-        u32 const inclEnd = (u32)__builtin_amdgcn_ds_bpermute((int)(runEnd << 2), (int)incl);
-        u32 const runMl = inclEnd - (incl - mlv);  // (heads: the run's ml within this chunk)
-        u32 const hcount = (u32)__popcll(hm);
-        u32 const rank = (u32)__popcll(hm & ((1ull << lane) - 1));
-        u32 const firstH = hm ? (u32)__builtin_ctzll(hm) : 64u;
-        u32 const carryAdd = firstH ? lane_value(incl, firstH - 1u) : 0u;
-        // finalize the carried open head: closed if this batch has any head, or at the very end
-        openMl += carryAdd;
-        if (open && hcount) {
-          if (lane == 0) seq[openIdx] = (u64)openLL | ((u64)openMl << 17) | ((u64)openOff << 34);
-          open = false;
-        }
-        if (head) {
-          u32 const idx = nbSeq + rank;
-          if (headBitsAfter) seq[idx] = (u64)ll | ((u64)runMl << 17) | ((u64)off << 34);
-        }
-        if (hcount) {
-          int const lastH = 63 - __builtin_clzll(hm);
-          openIdx = nbSeq + hcount - 1;
-          openLL = lane_value(ll, (u32)lastH);
-          openOff = lane_value(off, (u32)lastH);
-          openMl = lane_value(runMl, (u32)lastH);
-          open = true;
-        }
-        nbSeq += hcount;
-        u32 const lastLane = min(63u, nseq_raw - 1 - base);
-        carryCum = lane_value(cum, lastLane);
-        carryOff = lane_value(off, lastLane);
-        wave_sync();
-      }
-      if (open && lane == 0) seq[openIdx] = (u64)openLL | ((u64)openMl << 17) | ((u64)openOff << 34);
-      wave_sync();
-    }
-
-    ZH_STAMP(4);  // merge pass
-    // nbSeq header
-    if (nbSeq < 128) { if (lane == 0) o.put(op, (u8)nbSeq); op += 1; }
-    else if (nbSeq < ZH_LONGNBSEQ) { if (lane == 0) { o.put(op, (u8)((nbSeq >> 8) + 0x80)); o.put(op + 1, (u8)nbSeq); } op += 2; }
-    else { if (lane == 0) { o.put(op, 0xFF); o.put(op + 1, (u8)(nbSeq - ZH_LONGNBSEQ)); o.put(op + 2, (u8)((nbSeq - ZH_LONGNBSEQ) >> 8)); } op += 3; }
-
-    if (nbSeq > 0) {
-      // pass B: repcodes (serial, wave-uniform) + codes + histograms; record = ll | mlBase<<17 | offBase<<34
-      u32 *hLL = hist, *hOF = hist + 64, *hML = hist + 128;
-      for (u32 i = lane; i < 192; i += 64) hist[i] = 0;
-      wave_sync();
       // Repcode resolution, lane-parallel.  With o_i the offset of sequence i:
       //  - r0 before i is o_{i-1} (every zstd repcode update leaves the used offset in rep[0]);
       //  - rep[1] survives sequence j only when j repeats rep[0] with LL > 0, otherwise it
@@ -1241,15 +1181,10 @@ extern "C" __global__ __launch_bounds__(K2_THREADS) void zh_entropy_kernel(const
       u64 const below = (1ull << lane) - 1ull;
       CodeTabs ct;
       ct.load();
-      u32 const k3L = ZH_K3_SEGLEN(nbSeq), k3m = zh_k3_magic(k3L);
-      u8 *const cb = ws.lits(b) + 128u * k3L;  // codes in encoding order (step nbSeq-1-i), chain layout (zh_common.h)
-      RecRing ring;  // (in place: this chunk writes only indices <= i)
-      ring.init(seq, nbSeq, lane);
-      for (u32 base = 0; base < nbSeq; base += 64) {
-        u32 const i = base + lane;
-        bool const valid = i < nbSeq;
-        u64 const rec = ring.next(seq, nbSeq, i);
-        u32 const ll = (u32)(rec & 0x1FFFFu), ml = (u32)((rec >> 17) & 0x1FFFFu), off = (u32)(rec >> 34);
+      // sequences nbSeq + [0, m) in lanes [0, m)
+      auto sequences = [&](u32 m, u32 ll, u32 ml, u32 off) {
+        u32 const i = nbSeq + lane;
+        bool const valid = lane < m;
         u32 r0 = wave_shr1(off);
         if (lane == 0) r0 = cr0;
         bool const keep1 = ll > 0 && off == r0;
@@ -1267,8 +1202,8 @@ extern "C" __global__ __launch_bounds__(K2_THREADS) void zh_entropy_kernel(const
         u32 ob;
         if (ll) ob = off == r0 ? 1u : off == r1 ? 2u : off == r2 ? 3u : off + 3;
         else ob = off == r1 ? 1u : off == r2 ? 2u : (r0 > 1 && off == r0 - 1) ? 3u : off + 3;
-        // reps after the batch's last sequence
-        u32 const lastLane = min(63u, nbSeq - 1 - base);
+        // reps after the last sequence
+        u32 const lastLane = m - 1;
         u32 const n1 = keep1 ? r1 : r0, n2 = keep2 ? r2 : r1;
         cr0 = lane_value(off, lastLane);
         cr1 = lane_value(n1, lastLane);
@@ -1281,12 +1216,91 @@ extern "C" __global__ __launch_bounds__(K2_THREADS) void zh_entropy_kernel(const
           atomicAdd(&hOF[highbit32(ob)], 1u);
           // + the LL / ML codes in the spare top bits (ob < 2^17: offsets stay inside the block)
           seq[i] = (u64)ll | ((u64)mlb << 17) | ((u64)ob << 34) | ((u64)llc << 51) | ((u64)mlc << 57);
-          u32 const k = nbSeq - 1 - i;
-          u32 const x0 = zh_k3_index(k, 0, k3L, k3m);
-          cb[x0] = (u8)llc; cb[x0 + ZH_K3_TSTRIDE] = (u8)highbit32(ob); cb[x0 + 2u * ZH_K3_TSTRIDE] = (u8)mlc;
+        }
+        nbSeq += m;
+      };
+      u32 carryCum = 0, carryOff = 0, openLL = 0, openMl = 0, openOff = 0;
+      bool open = false;
+      RecRing ring;  // records loaded RING_DEPTH chunks ahead (a chunk writes only indices < its end)
+      ring.init(seq, nseq_raw, lane);
+      for (u32 base = 0; base < nseq_raw; base += 64) {
+        u32 const i = base + lane;
+        bool const valid = i < nseq_raw;
+        u64 const rec = ring.next(seq, nseq_raw, i);
+        u32 const cum = (u32)(rec & 0x1FFFFu), ml = (u32)((rec >> 17) & 255u), off = (u32)((rec >> 25) & 0xFFFFu);
+        u32 pc = wave_shr1(cum), po = wave_shr1(off);
+        if (lane == 0) { pc = carryCum; po = carryOff; }
+        u32 const ll = cum - pc;
+        bool const flag = valid && i > 0 && ll == 0 && off == po;
+        bool const head = valid && !flag;
+        u64 const hm = __ballot(head);
+        // run sums of ml: inclusive DPP scan, each head reads the scan at its run's last lane in
+        // this chunk (one ds_bpermute); lanes before the first head extend the open run
+        u32 const mlv = valid ? ml : 0u;
+        u32 const incl = wave_scan_incl(mlv);
+        u64 const headBitsAfter = hm & ~((lane == 63) ? ~0ull : ((2ull << lane) - 1));
+        u32 const runEnd = headBitsAfter ? (u32)__builtin_ctzll(headBitsAfter) - 1u : 63u;
+        u32 const inclEnd = (u32)__builtin_amdgcn_ds_bpermute((int)(runEnd << 2), (int)incl);
+        u32 const runMl = inclEnd - (incl - mlv);  // (heads: the run's ml within this chunk)
+        u32 const hcount = (u32)__popcll(hm);
+        u32 const firstH = hm ? (u32)__builtin_ctzll(hm) : 64u;
+        openMl += firstH ? lane_value(incl, firstH - 1u) : 0u;
+        if (hcount) {
+          // sequences of this step: the run left open before (if any), then this chunk's runs
+          // but its last (which stays open); heads go to lanes hp + rank, the other lanes to
+          // the lanes above (a bijection, as ds_permute needs)
+          u32 const hp = open ? 1u : 0u;
+          u32 const rank = (u32)__popcll(hm & below);
+          u32 const dest = head ? rank + hp : (hcount + hp + (lane - rank)) & 63u;
+          u32 sll = (u32)__builtin_amdgcn_ds_permute((int)(dest << 2), (int)ll);
+          u32 sml = (u32)__builtin_amdgcn_ds_permute((int)(dest << 2), (int)runMl);
+          u32 soff = (u32)__builtin_amdgcn_ds_permute((int)(dest << 2), (int)off);
+          if (hp && lane == 0) { sll = openLL; sml = openMl; soff = openOff; }
+          int const lastH = 63 - __builtin_clzll(hm);
+          openLL = lane_value(ll, (u32)lastH);
+          openOff = lane_value(off, (u32)lastH);
+          openMl = lane_value(runMl, (u32)lastH);
+          open = true;
+          u32 const m = hp + hcount - 1;
+          if (m) sequences(m, sll, sml, soff);
+        }
+        u32 const lastLane = min(63u, nseq_raw - 1 - base);
+        carryCum = lane_value(cum, lastLane);
+        carryOff = lane_value(off, lastLane);
+      }
+      if (open) sequences(1, openLL, openMl, openOff);
+      wave_sync();
+    }
+    ZH_STAMP(4);  // merge + repcodes + codes + histograms
+    // nbSeq header
+    if (nbSeq < 128) { if (lane == 0) o.put(op, (u8)nbSeq); op += 1; }
+    else if (nbSeq < ZH_LONGNBSEQ) { if (lane == 0) { o.put(op, (u8)((nbSeq >> 8) + 0x80)); o.put(op + 1, (u8)nbSeq); } op += 2; }
+    else { if (lane == 0) { o.put(op, 0xFF); o.put(op + 1, (u8)(nbSeq - ZH_LONGNBSEQ)); o.put(op + 2, (u8)((nbSeq - ZH_LONGNBSEQ) >> 8)); } op += 3; }
+
+    if (nbSeq > 0) {
+      // the codes in encoding order (step k = nbSeq-1-i) in the chain layout (zh_common.h):
+      // a lane per 16-step run (contiguous in the layout): its 16 records, three 16-byte stores
+      {
+        u32 const k3L = ZH_K3_SEGLEN(nbSeq), k3m = zh_k3_magic(k3L);
+        u8 *const cb = ws.lits(b) + 128u * k3L;
+        for (u32 k0 = 16u * lane; k0 < nbSeq; k0 += 16u * 64u) {
+          u64 r[16];
+#pragma unroll
+          for (u32 q = 0; q < 16; q++) r[q] = k0 + q < nbSeq ? seq[nbSeq - 1 - (k0 + q)] : 0ull;
+          u32 wl[4] = {0, 0, 0, 0}, wo[4] = {0, 0, 0, 0}, wm[4] = {0, 0, 0, 0};
+#pragma unroll
+          for (u32 q = 0; q < 16; q++) {
+            u32 const ob = (u32)(r[q] >> 34) & 0x1FFFFu;
+            wl[q >> 2] |= ((u32)(r[q] >> 51) & 63u) << (8 * (q & 3));
+            wo[q >> 2] |= (ob ? highbit32(ob) : 0u) << (8 * (q & 3));
+            wm[q >> 2] |= ((u32)(r[q] >> 57)) << (8 * (q & 3));
+          }
+          u32 const x0 = zh_k3_index(k0, 0, k3L, k3m);
+          *(uint4 *)(cb + x0) = make_uint4(wl[0], wl[1], wl[2], wl[3]);
+          *(uint4 *)(cb + x0 + ZH_K3_TSTRIDE) = make_uint4(wo[0], wo[1], wo[2], wo[3]);
+          *(uint4 *)(cb + x0 + 2u * ZH_K3_TSTRIDE) = make_uint4(wm[0], wm[1], wm[2], wm[3]);
         }
       }
-      wave_sync();
       ZH_STAMP(5);  // repcodes + codes + histograms
       // tables: LL, OF, ML (ZSTD_selectEncodingType for strategy dfast + ZSTD_buildCTable)
       u32 const seqHead = op;
