@@ -826,6 +826,122 @@ __device__ u32 huf_write_ctable(u8 *hbuf, u8 *w, const u8 *hnb, u32 maxSV, u32 h
   return ((maxSV + 1) / 2) + 1;
 }
 
+// HUF_writeCTable with the whole wave: weights and their histogram lane-parallel, the weights'
+// FSE table by the wave-parallel normalisation / NCount / table build, and the two-state
+// FSE_compress_usingCTable of the weights as a wave-uniform loop whose table lookups are
+// v_readlane from lane-held copies (weights <= 12, table <= 64 cells).  Same bytes as
+// huf_write_ctable; returns the size (0 = raw literals), uniform.
+__device__ u32 huf_write_ctable_wave(u8 *hbuf, u8 *w, const u8 *hnb, u32 maxSV, u32 huffLog, u16 *st, FseSym *sym, u8 *tsym, s16 *norm,
+                                    SerialScratch *scr) {
+  u32 const lane = lane_id();
+  for (u32 n = lane; n <= maxSV; n += 64) w[n] = (n < maxSV && hnb[n]) ? (u8)(huffLog + 1 - hnb[n]) : 0;
+  wave_sync();
+  u32 h = 0;
+  if (maxSV > 1) {
+    // count[v] on lane v (v <= 12): one ballot per weight value per 64 weights
+    u32 cnt = 0;
+    for (u32 n0 = 0; n0 < maxSV; n0 += 64) {
+      u32 const wv = n0 + lane < maxSV ? w[n0 + lane] : 255u;
+#pragma unroll
+      for (u32 v = 0; v <= 12; v++) {
+        u32 const c = (u32)__popcll(__ballot(wv == v));
+        cnt += lane == v ? c : 0u;
+      }
+    }
+    u64 const nzm = __ballot(lane <= 12 && cnt != 0);
+    u32 const mx = 63u - (u32)__builtin_clzll(nzm);
+    u32 const maxCount = wave_max(lane <= 12 ? cnt : 0u);
+    if (maxCount == maxSV) h = 1;
+    else if (maxCount == 1) h = 0;
+    else {
+      u32 const tableLog = fse_optimal_table_log(6, maxSV, mx, 2);
+      int const nv = fse_normalize_wave(norm, tableLog, lane <= mx ? cnt : 0u, maxSV, mx, false, lane, scr->cumul);
+      u32 const hs = fse_write_ncount_wave(hbuf + 1, nv, mx, tableLog, lane);
+      if (hs) {
+        wave_sync();
+        fse_build_ctable_par(st, sym, tsym, norm, mx, tableLog, scr);
+        wave_sync();
+        u32 cs = 0;
+        if (maxSV > 2) {
+          // lane-held copies: st (<= 64 cells), the symbol transforms, the weights (4 per lane)
+          u32 const stv = lane < (1u << tableLog) ? (u32)st[lane] : 0u;
+          u32 const dnbv = lane <= mx ? sym[lane].dNb : 0u;
+          u32 const dfsv = lane <= mx ? (u32)sym[lane].dFS : 0u;
+          u32 wl[4];
+#pragma unroll
+          for (u32 k = 0; k < 4; k++) wl[k] = 64 * k + lane < maxSV ? w[64 * k + lane] : 0u;
+          auto wat = [&](u32 i) {  // w[i], i uniform
+            u32 const l = i & 63u, r = i >> 6;
+            u32 const a0 = lane_value(wl[0], l), a1 = lane_value(wl[1], l), a2 = lane_value(wl[2], l), a3 = lane_value(wl[3], l);
+            return r == 0 ? a0 : r == 1 ? a1 : r == 2 ? a2 : a3;
+          };
+          auto init = [&](u32 sy) {
+            u32 const dnb = lane_value(dnbv, sy), dfs = lane_value(dfsv, sy);
+            u32 const nbo = (dnb + (1u << 15)) >> 16;
+            return lane_value(stv, (((nbo << 16) - dnb) >> nbo) + dfs);
+          };
+          u8 *const out = hbuf + 1 + hs;
+          u64 acc = 0;
+          u32 nbits = 0, o = 0;
+          auto add = [&](u32 v, u32 nb) {
+            acc |= ((u64)v & ((1ull << nb) - 1ull)) << nbits;
+            nbits += nb;
+            while (nbits >= 8) {
+              if (lane == 0) out[o] = (u8)acc;
+              o++;
+              acc >>= 8;
+              nbits -= 8;
+            }
+          };
+          auto step = [&](u32 &state, u32 sy) {
+            u32 const dnb = lane_value(dnbv, sy), dfs = lane_value(dfsv, sy);
+            u32 const nb = (state + dnb) >> 16;
+            u32 const v = state & ((1u << nb) - 1u);
+            state = lane_value(stv, (state >> nb) + dfs);
+            add(v, nb);
+          };
+          int ip = (int)maxSV;
+          u32 s1, s2;
+          if (maxSV & 1) {
+            s1 = init(wat((u32)--ip));
+            s2 = init(wat((u32)--ip));
+            step(s1, wat((u32)--ip));
+          } else {
+            s2 = init(wat((u32)--ip));
+            s1 = init(wat((u32)--ip));
+          }
+          while (ip > 0) {
+            step(s2, wat((u32)--ip));
+            step(s1, wat((u32)--ip));
+          }
+          add(s2, tableLog);
+          add(s1, tableLog);
+          add(1, 1);
+          if (nbits) {
+            if (lane == 0) out[o] = (u8)acc;
+            o++;
+          }
+          cs = o;
+        }
+        h = cs ? hs + cs : 0;
+      }
+    }
+  }
+  u32 ret;
+  if ((h > 1) & (h < maxSV / 2)) {
+    if (lane == 0) hbuf[0] = (u8)h;
+    ret = h + 1;
+  } else if (maxSV > 128) {
+    ret = 0;
+  } else {
+    if (lane == 0) hbuf[0] = (u8)(128 + (maxSV - 1));
+    for (u32 n = 2 * lane; n < maxSV; n += 128) hbuf[(n / 2) + 1] = (u8)((w[n] << 4) + w[n + 1]);
+    ret = ((maxSV + 1) / 2) + 1;
+  }
+  wave_sync();
+  return ret;
+}
+
 // byte copy global -> Out (wave-parallel)
 // Wave copy of n bytes to o[pos..]: byte head up to a 4-B aligned destination, then
 // dword stores (source realigned with alignbyte, 8 independent loads per lane in
@@ -1048,14 +1164,8 @@ extern "C" __global__ __launch_bounds__(K2_THREADS) void zh_entropy_kernel(const
           u32 hl = fse_optimal_table_log(11, nl, maxSV, 1);
           hl = huf_build_ctable_par(nodes, hval, hnb, hist, maxSV, hl, scr);
           ZH_STAMP(11);  // Huffman tree (parallel part)
-          if (lane == 0) {
-            u32 h = hl ? huf_write_ctable(hbuf, wts, hnb, maxSV, hl, stLL, symLL, tsym, norm, scr) : 0;
-            misc[0] = hl;
-            misc[1] = h;
-          }
-          wave_sync();
-          huffLog = misc[0];
-          hsz = misc[1];
+          huffLog = hl;
+          hsz = hl ? huf_write_ctable_wave(hbuf, wts, hnb, maxSV, hl, stLL, symLL, tsym, norm, scr) : 0;
           ZH_STAMP(1);  // Huffman tree + header (serial)
           if (hsz && hsz + 12 < nl) {
             // stream sizes: sum of code lengths per stream (+ end mark)
