@@ -725,19 +725,28 @@ __device__ u32 huf_build_ctable_par(HufNode *huffNode0, u16 *hval, u8 *hnb, cons
   maxNbBits = __builtin_amdgcn_readfirstlane(maxNbBits);
   if (maxNbBits > 12) return 0;
   // nbPerRank / valPerRank, then codes in symbol order within each rank
-  u16 *nbPerRank = scr->nbPerRank, *valPerRank = scr->valPerRank;
-  if (lane < 16) { nbPerRank[lane] = 0; valPerRank[lane] = 0; }
   for (u32 i = lane; i < 256; i += 64) hnb[i] = 0;
   wave_sync();
   for (u32 nn = lane; nn <= maxSV; nn += 64) hnb[huffNode[nn].byte] = huffNode[nn].nbBits;
   wave_sync();
-  if (lane == 0) {
-    for (int nn = 0; nn <= nonNullRank; nn++) nbPerRank[huffNode[nn].nbBits]++;
-    u16 mn = 0;
-    for (int r = (int)maxNbBits; r > 0; r--) { valPerRank[r] = mn; mn += nbPerRank[r]; mn >>= 1; }
+  // nbPerRank on lane r (ballots over the code lengths), then valPerRank as a uniform loop
+  u32 nbr = 0;
+  for (u32 n0 = 0; n0 <= maxSV; n0 += 64) {
+    u32 const v = n0 + lane <= maxSV ? hnb[n0 + lane] : 0u;
+    for (u32 r = 1; r <= maxNbBits; r++) {
+      u32 const c = (u32)__popcll(__ballot(v == r));
+      nbr += lane == r ? c : 0u;
+    }
   }
-  wave_sync();
-  u32 base = lane < 16 ? valPerRank[lane] : 0u;  // lane r holds the next code of rank r
+  u32 base = 0;  // lane r holds the next code of rank r
+  {
+    u32 mn = 0;
+    for (int r = (int)maxNbBits; r > 0; r--) {
+      if (lane == (u32)r) base = mn;
+      mn += lane_value(nbr, (u32)r);
+      mn = (mn >> 1) & 0xFFFFu;
+    }
+  }
   for (u32 n0 = 0; n0 <= maxSV; n0 += 64) {
     u32 const nn = n0 + lane;
     u32 const v = nn <= maxSV ? hnb[nn] : 255u;
