@@ -633,8 +633,22 @@ __device__ __forceinline__ void wave_set(u32 (&a)[4], u32 i, u32 v) {
   for (u32 k = 0; k < 4; k++) a[k] = (me && r == k) ? v : a[k];
 }
 
+#ifdef ZH_STAMPS
+__device__ u32 g_hst[6];  // diagnostic: Huffman build phase cycles (all blocks)
+#define HSTAMP(k)                                                     \
+  do {                                                                \
+    u64 const t_ = __builtin_amdgcn_s_memtime();                      \
+    if ((k) >= 0 && lane == 0) atomicAdd(&g_hst[(k) < 0 ? 0 : (k)], (u32)(t_ - hst_prev)); \
+    hst_prev = t_;                                                    \
+  } while (0)
+#else
+#define HSTAMP(k) do { } while (0)
+#endif
 __device__ u32 huf_build_ctable_par(HufNode *huffNode0, u16 *hval, u8 *hnb, const u32 *count, u32 maxSV, u32 maxNbBits, SerialScratch *scr) {
   u32 const lane = lane_id();
+#ifdef ZH_STAMPS
+  u64 hst_prev = 0;
+#endif
   HufNode *const huffNode = huffNode0 + 1;
   u32 const STARTNODE = 256;
   for (u32 i = lane; i < 2 * 256 + 2; i += 64) { huffNode0[i].count = 0; huffNode0[i].parent = 0; huffNode0[i].byte = 0; huffNode0[i].nbBits = 0; }
@@ -645,6 +659,7 @@ __device__ u32 huf_build_ctable_par(HufNode *huffNode0, u16 *hval, u8 *hnb, cons
     u32 const sym = 4 * lane + k;
     key[k] = sym <= maxSV ? (count[sym] << 8) | (255u - sym) : 0u;
   }
+  HSTAMP(-1);
   bitonic_sort_desc_256(key);
   wave_sync();
   u32 nz = 0;
@@ -656,37 +671,68 @@ __device__ u32 huf_build_ctable_par(HufNode *huffNode0, u16 *hval, u8 *hnb, cons
   }
   int const nonNullRank = (int)wave_sum(nz) - 1;
   wave_sync();
-  // two-queue merge with the counts in registers (leaf i / internal node m at lane i%64, reg i/64)
+  HSTAMP(0);
+  // Two-queue merge (HUF_buildCTable's order and tie-break: a leaf only when strictly smaller)
+  // with the counts in registers (leaf i / internal node m at lane i%64, reg i/64).  The loop
+  // keeps each queue's head count and fetches only the next entry of the queue it advanced;
+  // it records one bit per pick (1 = internal node), and the parents are written afterwards,
+  // lane-parallel: pick k goes to node 256 + k/2, and its source is leaf
+  // nonNullRank - (leaf picks before k) or internal node 256 + (internal picks before k).
   u32 L[4], I[4] = {0, 0, 0, 0};
 #pragma unroll
   for (u32 r = 0; r < 4; r++) L[r] = huffNode[64 * r + lane].count;
-  int lowS = nonNullRank;
   u32 const nodeRoot = STARTNODE + (u32)nonNullRank - 1;
-  u32 nodeNb = STARTNODE, lowN = STARTNODE;
   {
-    u32 const c = wave_get(L, (u32)lowS) + wave_get(L, (u32)lowS - 1);
-    wave_set(I, 0, c);
-    if (lane == 0) { huffNode[lowS].parent = (u16)nodeNb; huffNode[lowS - 1].parent = (u16)nodeNb; }
-    nodeNb++;
-    lowS -= 2;
-  }
-  while (nodeNb <= nodeRoot) {
-    u32 n1, n2, c1, c2;
-    {
-      u32 const cs = lowS >= 0 ? wave_get(L, (u32)lowS) : (1u << 31);
-      u32 const cn = lowN < nodeNb ? wave_get(I, lowN - STARTNODE) : (1u << 30);
-      if (cs < cn) { n1 = (u32)lowS; c1 = cs; lowS--; } else { n1 = lowN; c1 = cn; lowN++; }
+    int lowS = nonNullRank;
+    u32 lowN = STARTNODE;
+    u32 cs = wave_get(L, (u32)lowS), cn = 1u << 30;  // queue heads (internal queue empty)
+    u64 bits = 0;
+    u32 pwlo = 0, pwhi = 0, npick = 0;  // lane w: pick bits [64 w, 64 w + 64)
+    for (u32 m = STARTNODE; m <= nodeRoot; m++) {
+      u32 c = 0;
+#pragma unroll
+      for (u32 q = 0; q < 2; q++) {
+        bool const internal = !(cs < cn);
+        if (internal) {
+          c += cn;
+          lowN++;
+          cn = lowN < m ? wave_get(I, lowN - STARTNODE) : (1u << 30);
+        } else {
+          c += cs;
+          lowS--;
+          cs = lowS >= 0 ? wave_get(L, (u32)lowS) : (1u << 31);
+        }
+        bits |= (u64)(internal ? 1u : 0u) << (npick & 63u);
+        npick++;
+      }
+      wave_set(I, m - STARTNODE, c);
+      if (lowN == m) cn = c;  // the queue was empty: the new node is its head
+      if ((npick & 63u) == 0) {
+        u32 const w = (npick >> 6) - 1;
+        if (lane == w) { pwlo = (u32)bits; pwhi = (u32)(bits >> 32); }
+        bits = 0;
+      }
     }
-    {
-      u32 const cs = lowS >= 0 ? wave_get(L, (u32)lowS) : (1u << 31);
-      u32 const cn = lowN < nodeNb ? wave_get(I, lowN - STARTNODE) : (1u << 30);
-      if (cs < cn) { n2 = (u32)lowS; c2 = cs; lowS--; } else { n2 = lowN; c2 = cn; lowN++; }
+    if (npick & 63u) {
+      u32 const w = npick >> 6;
+      if (lane == w) { pwlo = (u32)bits; pwhi = (u32)(bits >> 32); }
     }
-    wave_set(I, nodeNb - STARTNODE, c1 + c2);
-    if (lane == 0) { huffNode[n1].parent = (u16)nodeNb; huffNode[n2].parent = (u16)nodeNb; }
-    nodeNb++;
+    u32 const nw = (npick + 63u) >> 6;
+    u32 const pcw = lane < nw ? (u32)__popcll(((u64)pwhi << 32) | pwlo) : 0u;
+    u32 const ibw = wave_scan_incl(pcw) - pcw;  // internal picks before word w
+    u64 const below = (1ull << lane) - 1ull;
+    for (u32 q = 0; q < nw; q++) {
+      u64 const word = ((u64)lane_value(pwhi, q) << 32) | lane_value(pwlo, q);
+      u32 const k = 64u * q + lane;
+      if (k < npick) {
+        u32 const ib = lane_value(ibw, q) + (u32)__popcll(word & below);
+        u32 const node = ((word >> lane) & 1u) ? STARTNODE + ib : (u32)nonNullRank - (k - ib);
+        huffNode[node].parent = (u16)(STARTNODE + (k >> 1));
+      }
+    }
   }
   wave_sync();
+  HSTAMP(1);
   // depths by pointer doubling over leaves 0..nonNull and internal nodes 256..root:
   // jump = parent (root: itself), dist = 1 (root: 0); nbBits of a leaf = its depth
   u32 const nLeaf = (u32)nonNullRank + 1, nInt = (u32)nonNullRank;
@@ -721,9 +767,11 @@ __device__ u32 huf_build_ctable_par(HufNode *huffNode0, u16 *hval, u8 *hnb, cons
     }
     wave_sync();
   }
+  HSTAMP(2);
   if (lane == 0) maxNbBits = huf_set_max_height(huffNode, (u32)nonNullRank, maxNbBits, scr);
   maxNbBits = __builtin_amdgcn_readfirstlane(maxNbBits);
   if (maxNbBits > 12) return 0;
+  HSTAMP(3);
   // nbPerRank / valPerRank, then codes in symbol order within each rank
   for (u32 i = lane; i < 256; i += 64) hnb[i] = 0;
   wave_sync();
@@ -761,6 +809,7 @@ __device__ u32 huf_build_ctable_par(HufNode *huffNode0, u16 *hval, u8 *hnb, cons
     if (nn <= maxSV) hval[nn] = (u16)code;
   }
   wave_sync();
+  HSTAMP(4);
   return maxNbBits;
 }
 
@@ -1764,6 +1813,16 @@ extern "C" __global__ __launch_bounds__(64 * K4_WAVES) void zh_seq_pack_kernel(c
 }
 
 extern "C" u32 zh_entropy_lds_bytes() { return K2_LDS; }
+#ifdef ZH_STAMPS
+extern "C" __global__ void zh_read_hst(u32 *out) { for (int k = 0; k < 6; k++) { out[k] = g_hst[k]; g_hst[k] = 0; } }
+extern "C" void zh_hst_host(u32 *out6) {
+  u32 *d = nullptr;
+  if (hipMalloc(&d, 24) != hipSuccess) return;
+  hipLaunchKernelGGL(zh_read_hst, dim3(1), dim3(1), 0, 0, d);
+  (void)hipMemcpy(out6, d, 24, hipMemcpyDeviceToHost);
+  (void)hipFree(d);
+}
+#endif
 
 namespace zh {
 hipError_t entropy_init() {

@@ -92,3 +92,11 @@ print(f"  per-CU busy fraction of span: mean {np.mean(list(busy.values())) / (t1
 mx = np.array([h[blocks + b * WS + 13120 * 8 + 122880 + 16 + 40 * 4: blocks + b * WS + 13120 * 8 + 122880 + 16 + 42 * 4].view(np.uint32) for b in range(n)])
 if kind:
     print(f"  B-work max over worker waves {mx[:, 0].mean():.0f}   inserter busy max {mx[:, 1].mean():.0f}  (per block)")
+try:
+    import ctypes as _ct
+    _L = _ct.CDLL(os.environ["CUDA_ZSTD_HIP_LIB"])
+    _h = (_ct.c_uint32 * 6)()
+    _L.zh_hst_host(_h)
+    print("  Huffman build phases (cycles summed over blocks; since process start): sort %d merge %d depths %d max_height %d codes %d" % tuple(_h[:5]))
+except Exception as _e:  # noqa: BLE001
+    print("  (no Huffman phase stamps)", _e)
