@@ -128,7 +128,8 @@ extern "C" __global__ __launch_bounds__(64) void zh_checksum_kernel(const ZhItem
   if (item_status[it] != ZH_ST_OK) return;
   ZhItemDesc const id = items[it];
   ZhBlockDesc const d = descs[id.first_block];
-  u64 const h = zh_xxh64(d.src, d.frame_size);
+  __shared__ u64 xb[512];
+  u64 const h = zh_xxh64_wave(d.src, d.frame_size, xb);
   u64 const size = item_size[it];
   __syncthreads();
   if (size + 4 > id.cap) {
