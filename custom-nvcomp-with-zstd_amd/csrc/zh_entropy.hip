@@ -16,18 +16,21 @@
 
 namespace {
 
-constexpr u32 K2_THREADS = 64;
+constexpr u32 K2_THREADS = 128;  // wave 0: literals section; wave 1: frame/sequences section, finish
 constexpr u32 SW_WORDS = 184;  // >= 512 literal codes of <= 11 bits per append (+ pending bits)
 
 // ---------------- LDS layout (bytes) ----------------
+// The literals-only regions come first: wave 1's copy of the layout starts early enough that
+// its (unused) SW / HVAL / HNB overlap the end of wave 0's copy.
 constexpr u32 OFF_SW = 0;                          // bit sink words
-constexpr u32 OFF_MISC = OFF_SW + 4 * SW_WORDS;    // 64 u32 scalars / broadcast
-constexpr u32 OFF_HIST = OFF_MISC + 4 * 64;        // 256 u32 literal histogram; later 121 code counts
-constexpr u32 OFF_HVAL = OFF_HIST + 4 * 256;       // u16[256] Huffman code values
+constexpr u32 OFF_HVAL = OFF_SW + 4 * SW_WORDS;    // u16[256] Huffman code values
 constexpr u32 OFF_HNB = OFF_HVAL + 2 * 256;        // u8[256] Huffman code lengths
-constexpr u32 OFF_HBUF = OFF_HNB + 256;            // u8[768] header scratch (weights / NCount)
+constexpr u32 OFF_MISC = OFF_HNB + 256;            // 64 u32 scalars / broadcast
+constexpr u32 OFF_HIST = OFF_MISC + 4 * 64;        // 256 u32 literal histogram; later 121 code counts
+constexpr u32 OFF_HBUF = OFF_HIST + 4 * 256;       // u8[768] header scratch (weights / NCount)
 constexpr u32 OFF_SCR = OFF_HBUF + 768;            // serial-helper scratch (lane 0)
 constexpr u32 OFF_U = OFF_SCR + 1024;              // union: Huffman nodes | FSE tables
+static_assert(OFF_U % 16 == 0, "alignment");
 // Huffman build view
 constexpr u32 OFF_NODES = OFF_U;                   // 514 nodes x 8 B
 constexpr u32 U_HUF_END = OFF_NODES + 8 * 516;
@@ -40,8 +43,10 @@ constexpr u32 OFF_TSYM = OFF_SYM + 3 * 64 * 8;     // u8[512] spread scratch
 constexpr u32 OFF_NORM = OFF_TSYM + 512;           // s16[64]
 constexpr u32 OFF_WTS = OFF_NORM + 128;            // u8[256] Huffman weights (used during Huffman header)
 constexpr u32 U_FSE_END = OFF_WTS + 256;
-constexpr u32 K2_LDS = (U_HUF_END > U_FSE_END ? U_HUF_END : U_FSE_END);
-static_assert(K2_LDS < 16384, "K2 LDS budget");
+constexpr u32 K2_WAVE_LDS = (U_HUF_END > U_FSE_END ? U_HUF_END : U_FSE_END);  // one wave's layout
+static_assert(K2_WAVE_LDS < 16384, "K2 LDS budget");
+constexpr u32 K2_W1 = (K2_WAVE_LDS - OFF_MISC + 15) & ~15u;  // wave 1's layout base
+constexpr u32 K2_LDS = K2_W1 + K2_WAVE_LDS;
 
 __constant__ u8 c_LL_bits[36] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 1, 1, 1, 1, 2, 2, 3, 3, 4, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16};
 __constant__ u8 c_ML_bits[53] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0,
@@ -1103,7 +1108,14 @@ __device__ __forceinline__ void write_status(const ZhBlockDesc &d, u32 b, u32 to
 extern "C" __global__ __launch_bounds__(K2_THREADS) void zh_entropy_kernel(const ZhBlockDesc *__restrict__ blocks, ZhWorkspace ws, u32 window_log,
                                                                              u32 cfg_block_size, u64 *__restrict__ item_size,
                                                                              u32 *__restrict__ item_status, u32 *__restrict__ blk_size) {
-  extern __shared__ __attribute__((aligned(16))) u8 smem[];
+  extern __shared__ __attribute__((aligned(16))) u8 smem_all[];
+  // Two waves per block, each with its own copy of the LDS layout: wave 0 builds the literals
+  // section, wave 1 (concurrently) the sequences section's merge / repcodes / codes / FSE
+  // tables; after one barrier wave 1 places the sequence headers behind the literals and
+  // finishes the block.  A block's latency is the longer of the two halves, not their sum.
+  u32 const wave = threadIdx.x >> 6;
+  u8 *const smem = smem_all + wave * K2_W1;
+  u32 *const xch = (u32 *)(smem_all + OFF_MISC) + 56;  // wave 0 -> wave 1: literals end, early_raw
   u32 *sw = (u32 *)(smem + OFF_SW);
   u32 *misc = (u32 *)(smem + OFF_MISC);
   u32 *hist = (u32 *)(smem + OFF_HIST);
@@ -1125,7 +1137,7 @@ extern "C" __global__ __launch_bounds__(K2_THREADS) void zh_entropy_kernel(const
   const u32 *meta = ws.meta(b);
   u32 const nseq_raw = meta[0], nlit = meta[1], rle = meta[2];
   Out const o{d.dst, d.dst_cap};
-  if (lane == 0) sw[0] = 0;
+  if (wave == 0 && lane == 0) sw[0] = 0;  // (wave 1's SW overlaps wave 0's layout: never touched)
 #ifdef ZH_STAMPS
   u64 stamp_prev = __builtin_amdgcn_s_memtime();
   u32 st[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
@@ -1151,7 +1163,7 @@ extern "C" __global__ __launch_bounds__(K2_THREADS) void zh_entropy_kernel(const
     u32 const did = (d.flags & ZH_F_DICT) ? d.dict_id : 0u;
     u32 const didf = did == 0 ? 0u : did < 256 ? 1u : did < 65536 ? 2u : 3u;
     u32 const didn = didf == 3 ? 4u : didf;
-    if (lane == 0) {
+    if (wave == 1 && lane == 0) {
       u32 p = 0;
       o.put(p++, 0x28); o.put(p++, 0xB5); o.put(p++, 0x2F); o.put(p++, 0xFD);
       o.put(p++, (u8)((fcs_flag << 6) | (ss ? 0x20 : 0) | ((d.flags & ZH_F_CHECKSUM) ? 0x04 : 0) | didf));
@@ -1167,18 +1179,18 @@ extern "C" __global__ __launch_bounds__(K2_THREADS) void zh_entropy_kernel(const
   u32 const last = (d.flags & ZH_F_LAST) ? 1u : 0u;
   u32 total;
   bool early_raw = false, handoff = false;
-  if (lane == 0) ws.fsef(b)[ZH_FF_NEED] = 0;
+  if (wave == 1 && lane == 0) ws.fsef(b)[ZH_FF_NEED] = 0;
 
   if (rle) {
     u32 const hdr = last + (1u << 1) + (n << 3);
-    if (lane == 0) { o.put(blk, (u8)hdr); o.put(blk + 1, (u8)(hdr >> 8)); o.put(blk + 2, (u8)(hdr >> 16)); o.put(blk + 3, d.src[0]); }
+    if (wave == 1 && lane == 0) { o.put(blk, (u8)hdr); o.put(blk + 1, (u8)(hdr >> 8)); o.put(blk + 2, (u8)(hdr >> 16)); o.put(blk + 3, d.src[0]); }
     total = blk + 4;
   } else {
     const u8 *lits = ws.lits(b);
     u64 *seq = ws.seq(b);
     u32 op = body0;
-    // ======================= literals section (ZSTD_compressLiterals) =======================
-    {
+    // ======================= literals section (ZSTD_compressLiterals), wave 0 =======================
+    if (wave == 0) {
       u32 const nl = nlit;
       u32 const minGain = (nl >> 6) + 2;
       u32 const lhSize = 3 + (nl >= 1024) + (nl >= 16384);
@@ -1323,16 +1335,17 @@ extern "C" __global__ __launch_bounds__(K2_THREADS) void zh_entropy_kernel(const
       }
       (void)huffLog;
       ZH_STAMP(3);  // literal streams
+      if (lane == 0) { xch[0] = op; xch[1] = early_raw ? 1u : 0u; }
     }
 
-    // ======================= sequences section =======================
-    if (!early_raw) {
+    // ======================= sequences section, wave 1 =======================
+    u32 nbSeq = 0, hpos = 0, typesw_ = 0, logLL = 0, logOF = 0, logML = 0;
+    if (wave == 1) {
     // One pass over K1's records: literal lengths from the cumulative counts, same-offset
     // continuations merged into their run head (DPP scan), and each closed run handed on as
     // a sequence (ds_permute compaction, a chunk's runs + the one left open by the chunk
     // before) to the repcode / code / histogram step, which writes the merged records in
     // place (record = ll | mlBase << 17 | offBase << 34 | llCode << 51 | mlCode << 57).
-    u32 nbSeq = 0;
     u32 *hLL = hist, *hOF = hist + 64, *hML = hist + 128;
     for (u32 i = lane; i < 192; i += 64) hist[i] = 0;
     wave_sync();
@@ -1440,39 +1453,9 @@ extern "C" __global__ __launch_bounds__(K2_THREADS) void zh_entropy_kernel(const
       wave_sync();
     }
     ZH_STAMP(4);  // merge + repcodes + codes + histograms
-    // nbSeq header
-    if (nbSeq < 128) { if (lane == 0) o.put(op, (u8)nbSeq); op += 1; }
-    else if (nbSeq < ZH_LONGNBSEQ) { if (lane == 0) { o.put(op, (u8)((nbSeq >> 8) + 0x80)); o.put(op + 1, (u8)nbSeq); } op += 2; }
-    else { if (lane == 0) { o.put(op, 0xFF); o.put(op + 1, (u8)(nbSeq - ZH_LONGNBSEQ)); o.put(op + 2, (u8)((nbSeq - ZH_LONGNBSEQ) >> 8)); } op += 3; }
-
     if (nbSeq > 0) {
-      // the codes in encoding order (step k = nbSeq-1-i) in the chain layout (zh_common.h):
-      // a lane per 16-step run (contiguous in the layout): its 16 records, three 16-byte stores
-      {
-        u32 const k3L = ZH_K3_SEGLEN(nbSeq), k3m = zh_k3_magic(k3L);
-        u8 *const cb = ws.lits(b) + 128u * k3L;
-        for (u32 k0 = 16u * lane; k0 < nbSeq; k0 += 16u * 64u) {
-          u64 r[16];
-#pragma unroll
-          for (u32 q = 0; q < 16; q++) r[q] = k0 + q < nbSeq ? seq[nbSeq - 1 - (k0 + q)] : 0ull;
-          u32 wl[4] = {0, 0, 0, 0}, wo[4] = {0, 0, 0, 0}, wm[4] = {0, 0, 0, 0};
-#pragma unroll
-          for (u32 q = 0; q < 16; q++) {
-            u32 const ob = (u32)(r[q] >> 34) & 0x1FFFFu;
-            wl[q >> 2] |= ((u32)(r[q] >> 51) & 63u) << (8 * (q & 3));
-            wo[q >> 2] |= (ob ? highbit32(ob) : 0u) << (8 * (q & 3));
-            wm[q >> 2] |= ((u32)(r[q] >> 57)) << (8 * (q & 3));
-          }
-          u32 const x0 = zh_k3_index(k0, 0, k3L, k3m);
-          *(uint4 *)(cb + x0) = make_uint4(wl[0], wl[1], wl[2], wl[3]);
-          *(uint4 *)(cb + x0 + ZH_K3_TSTRIDE) = make_uint4(wo[0], wo[1], wo[2], wo[3]);
-          *(uint4 *)(cb + x0 + 2u * ZH_K3_TSTRIDE) = make_uint4(wm[0], wm[1], wm[2], wm[3]);
-        }
-      }
-      ZH_STAMP(5);  // repcodes + codes + histograms
+      ZH_STAMP(5);
       // tables: LL, OF, ML (ZSTD_selectEncodingType for strategy dfast + ZSTD_buildCTable)
-      u32 const seqHead = op;
-      op += 1;
       u64 const rec0 = seq[0], recL = seq[nbSeq - 1];
       u32 hposw = 0, typesw = 0, logsw[3];
       {
@@ -1535,11 +1518,9 @@ extern "C" __global__ __launch_bounds__(K2_THREADS) void zh_entropy_kernel(const
         }
       }
       wave_sync();
-      u32 const hpos = misc[0];
-      if (lane == 0) o.put(seqHead, (u8)misc[1]);
-      for (u32 i = lane; i < hpos; i += 64) o.put(op + i, hbuf[i]);
-      op += hpos;
-      u32 const logLL = misc[2], logOF = misc[3], logML = misc[4];
+      hpos = misc[0];
+      typesw_ = misc[1];
+      logLL = misc[2]; logOF = misc[3]; logML = misc[4];
       ZH_STAMP(6);  // FSE tables (serial)
 
       // hand-off: the FSE state chains run in zh_fse_chain_kernel (lanes = blocks x
@@ -1554,24 +1535,69 @@ extern "C" __global__ __launch_bounds__(K2_THREADS) void zh_entropy_kernel(const
         if (lane < 36) ((FseSym *)(fz + ZH_FT_SYLL))[lane] = symLL[lane];
         if (lane < 32) ((FseSym *)(fz + ZH_FT_SYOF))[lane] = symOF[lane];
         if (lane < 53) ((FseSym *)(fz + ZH_FT_SYML))[lane] = symML[lane];
-        u32 *ff = ws.fsef(b);
-        if (lane == 0) {
-          ff[ZH_FF_NBSEQ] = nbSeq; ff[ZH_FF_OP] = op; ff[ZH_FF_BLK] = blk;
-          ff[ZH_FF_LOGS] = logLL | (logOF << 8) | (logML << 16);
-          ff[ZH_FF_NEED] = 1;
+      }
+    }
+    }  // wave 1
+    __syncthreads();  // the literals section is written; its end and early_raw are in xch
+    if (wave == 1) {
+      op = xch[0];
+      early_raw = xch[1] != 0;
+      if (!early_raw) {
+        // nbSeq header, then (with sequences) the table types and NCount headers
+        if (nbSeq < 128) { if (lane == 0) o.put(op, (u8)nbSeq); op += 1; }
+        else if (nbSeq < ZH_LONGNBSEQ) { if (lane == 0) { o.put(op, (u8)((nbSeq >> 8) + 0x80)); o.put(op + 1, (u8)nbSeq); } op += 2; }
+        else { if (lane == 0) { o.put(op, 0xFF); o.put(op + 1, (u8)(nbSeq - ZH_LONGNBSEQ)); o.put(op + 2, (u8)((nbSeq - ZH_LONGNBSEQ) >> 8)); } op += 3; }
+        if (nbSeq > 0) {
+          if (lane == 0) o.put(op, (u8)typesw_);
+          op += 1;
+          for (u32 i = lane; i < hpos; i += 64) o.put(op + i, hbuf[i]);
+          op += hpos;
+          // the codes in encoding order (step k = nbSeq-1-i) in the chain layout (zh_common.h):
+          // a lane per 16-step run (contiguous in the layout): its 16 records, three 16-byte stores
+          {
+            u32 const k3L = ZH_K3_SEGLEN(nbSeq), k3m = zh_k3_magic(k3L);
+            u8 *const cb = ws.lits(b) + 128u * k3L;
+            for (u32 k0 = 16u * lane; k0 < nbSeq; k0 += 16u * 64u) {
+              u64 r[16];
+    #pragma unroll
+              for (u32 q = 0; q < 16; q++) r[q] = k0 + q < nbSeq ? seq[nbSeq - 1 - (k0 + q)] : 0ull;
+              u32 wl[4] = {0, 0, 0, 0}, wo[4] = {0, 0, 0, 0}, wm[4] = {0, 0, 0, 0};
+    #pragma unroll
+              for (u32 q = 0; q < 16; q++) {
+                u32 const ob = (u32)(r[q] >> 34) & 0x1FFFFu;
+                wl[q >> 2] |= ((u32)(r[q] >> 51) & 63u) << (8 * (q & 3));
+                wo[q >> 2] |= (ob ? highbit32(ob) : 0u) << (8 * (q & 3));
+                wm[q >> 2] |= ((u32)(r[q] >> 57)) << (8 * (q & 3));
+              }
+              u32 const x0 = zh_k3_index(k0, 0, k3L, k3m);
+              *(uint4 *)(cb + x0) = make_uint4(wl[0], wl[1], wl[2], wl[3]);
+              *(uint4 *)(cb + x0 + ZH_K3_TSTRIDE) = make_uint4(wo[0], wo[1], wo[2], wo[3]);
+              *(uint4 *)(cb + x0 + 2u * ZH_K3_TSTRIDE) = make_uint4(wm[0], wm[1], wm[2], wm[3]);
+            }
+          }
+          // hand-off: the FSE state chains run in zh_fse_chain_kernel and the bitstream is
+          // packed by zh_seq_pack_kernel, which also finishes the block
+          u32 *ff = ws.fsef(b);
+          if (lane == 0) {
+            ff[ZH_FF_NBSEQ] = nbSeq; ff[ZH_FF_OP] = op; ff[ZH_FF_BLK] = blk;
+            ff[ZH_FF_LOGS] = logLL | (logOF << 8) | (logML << 16);
+            ff[ZH_FF_NEED] = 1;
+          }
+          handoff = true;
         }
       }
-      handoff = true;
+      if (!handoff) total = finish_block(d, o, blk, op, early_raw);
     }
-
-    }  // !early_raw
-    if (!handoff) total = finish_block(d, o, blk, op, early_raw);
   }
   ZH_STAMP(8);  // tail (raw copy etc.)
 #ifdef ZH_STAMPS
-  if (lane == 0) { u32 *dbg = ws.dbg(b); for (int k = 0; k < 9; k++) dbg[6 + k] = st[k]; dbg[17] = st[9]; dbg[18] = st[10]; dbg[19] = nseq_raw; dbg[42] = st[11]; }
+  if (lane == 0) {  // wave 0: the literal phases, wave 1: the rest
+    u32 *dbg = ws.dbg(b);
+    if (wave == 0) { for (int k = 0; k < 4; k++) dbg[6 + k] = st[k]; dbg[42] = st[11]; }
+    else { for (int k = 4; k < 9; k++) dbg[6 + k] = st[k]; dbg[17] = st[9]; dbg[18] = st[10]; dbg[19] = nseq_raw; }
+  }
 #endif
-  if (!handoff) write_status(d, b, total, item_size, item_status, blk_size);
+  if (wave == 1 && !handoff) write_status(d, b, total, item_size, item_status, blk_size);
 }
 
 // ======================= FSE state chains (K3) =======================
