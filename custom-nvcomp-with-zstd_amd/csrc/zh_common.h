@@ -77,6 +77,11 @@ enum : u32 {
 struct ZhWorkspace {
   u8 *base;          // nblocks * ZH_WS_BLOCK_BYTES
   u32 *ctr;          // K1's block counter (persistent workgroups take the next block from it)
+  // K1 hash tables of the batch dictionary's content, precomputed once per dictionary
+  // (zh::lz_dict_tables; null: none): 2 x 2^14 u16 entries = tail position + 1 over the last
+  // dtab_P content bytes, positions [0, dtab_P - ZH_DTAB_MARGIN) inserted
+  const u16 *dtab;
+  u32 dtab_P;
   __device__ u64 *seq(u32 b) const { return (u64 *)(base + (size_t)b * ZH_WS_BLOCK_BYTES); }
   __device__ u8 *lits(u32 b) const { return base + (size_t)b * ZH_WS_BLOCK_BYTES + ZH_SEQ_BYTES; }
   __device__ u32 *meta(u32 b) const { return (u32 *)(base + (size_t)b * ZH_WS_BLOCK_BYTES + ZH_SEQ_BYTES + ZH_LIT_BYTES); }
@@ -84,6 +89,8 @@ struct ZhWorkspace {
   __device__ u8 *fse(u32 b) const { return base + (size_t)b * ZH_WS_BLOCK_BYTES + ZH_SEQ_BYTES + ZH_LIT_BYTES + ZH_META_BYTES; }
   __device__ u32 *fsef(u32 b) const { return (u32 *)(fse(b) + ZH_FSE_FIELDS); }
 };
+
+#define ZH_DTAB_MARGIN 256u  // tail positions a block inserts itself (>= one inserter batch)
 
 // Element index of step e of table t in the chain layout (see ZH_K3_SEGS); m = zh_k3_magic(L)
 // gives e / L as umulhi(e << 8, m) exactly for e < 2^14, L <= 1024

@@ -321,10 +321,19 @@ struct DevDict {
   size_t cap = 0, n = 0, off = 0;
   u32 id = 0;
   bool owned = true;  // false: a view of caller memory (streaming history)
+  // K1's hash tables of the content tail, built at load (owned dictionaries only): every
+  // record's first block starts from them instead of hashing the dictionary again
+  u16 *tabs = nullptr;
+  u32 *tabs_tmp = nullptr;
+  u32 tabs_P = 0;
   DevDict() = default;
   DevDict(const DevDict &) = delete;
   DevDict &operator=(const DevDict &) = delete;
-  ~DevDict() { if (d && owned) (void)hipFree(d); }
+  ~DevDict() {
+    if (d && owned) (void)hipFree(d);
+    if (tabs) (void)hipFree(tabs);
+    if (tabs_tmp) (void)hipFree(tabs_tmp);
+  }
   // raw-content view of device-resident history (never freed here)
   static void view(DevDict &v, const void *p, size_t bytes) {
     v.owned = false;
@@ -332,6 +341,7 @@ struct DevDict {
     v.cap = v.n = bytes;
     v.off = 0;
     v.id = 0;
+    v.tabs_P = 0;  // (a moving history window: hashed by every block)
   }
   const u8 *content() const { return d + off; }
   size_t content_n() const { return n - off; }
@@ -357,6 +367,13 @@ struct DevDict {
     n = bytes;
     off = co;
     id = did;
+    tabs_P = 0;
+    if (!tabs && hipMalloc(&tabs, 2u * (1u << ZH_HASH_LOG_LONG) + 2u * (1u << ZH_HASH_LOG_SHORT)) != hipSuccess) tabs = nullptr;
+    if (!tabs_tmp && hipMalloc(&tabs_tmp, 4u * ((1u << ZH_HASH_LOG_LONG) + (1u << ZH_HASH_LOG_SHORT))) != hipSuccess) tabs_tmp = nullptr;
+    if (tabs && tabs_tmp) {
+      u32 P = 0;
+      if (zh::lz_dict_tables(content(), content_n(), tabs, tabs_tmp, P, 0) == hipSuccess && hipDeviceSynchronize() == hipSuccess) tabs_P = P;
+    }
     return Status::SUCCESS;
   }
   void fill(ZhDecArgs &a) const {
@@ -473,7 +490,7 @@ class ZstdBatchManager::Impl {
       }
     }
     if (hipMemcpyAsync(base, h, up_bytes, hipMemcpyHostToDevice, stream) != hipSuccess) return Status::ERROR_CUDA_ERROR;
-    ZhWorkspace ws{base + L.blocks, (u32 *)(base + L.counter)};
+    ZhWorkspace ws{base + L.blocks, (u32 *)(base + L.counter), dd && dd->tabs_P ? dd->tabs : nullptr, dd ? dd->tabs_P : 0u};
     hipError_t e = zh::launch_compress((const ZhBlockDesc *)(base + L.descs), (u32)nblocks, ws, config.window_log, config.block_size,
                                        (u64 *)(base + L.item_size), (u32 *)(base + L.item_status), (u32 *)(base + L.blk_size),
                                        (const ZhItemDesc *)(base + L.items), (u32)count, staged,
@@ -850,7 +867,7 @@ Status ZstdBatchManager::compress_batch_device(const void *const *d_in_ptrs, con
                                  (ZhItemDesc *)(base + L.items), item_size, item_status, ck ? ZH_F_CHECKSUM : 0u,
                                  dd ? dd->content() : nullptr, dd ? (u32)dd->content_n() : 0u, dd ? dd->id : 0u, hist, stream);
   if (e != hipSuccess) return Status::ERROR_CUDA_ERROR;
-  ZhWorkspace ws{base + L.blocks, (u32 *)(base + L.counter)};
+  ZhWorkspace ws{base + L.blocks, (u32 *)(base + L.counter), dd && dd->tabs_P ? dd->tabs : nullptr, dd ? dd->tabs_P : 0u};
   e = zh::launch_compress((const ZhBlockDesc *)(base + L.descs), (u32)nblocks, ws, pimpl_->config.window_log, pimpl_->config.block_size, item_size,
                           item_status, (u32 *)(base + L.blk_size), (const ZhItemDesc *)(base + L.items), (u32)count, bpi > 1, ck,
                           pimpl_->config.level >= kLazy2Level, stream);

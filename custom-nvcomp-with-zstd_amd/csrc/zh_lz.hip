@@ -207,7 +207,9 @@ __device__ __forceinline__ void insert_repair(u16 *T, u32 tb0, u32 lane, const u
 // (position + 1, 0 = none) go to creg as u16 pairs.
 template <bool LONG, typename Hook>
 __device__ __forceinline__ void insert_window(const u32 *in32, u16 *T, u32 wsb, u32 we, u32 lim, u32 lane, u32 (&creg)[NCR], u32 &cwe,
-                                              const u32 *arrivals, Hook &&between_tiles) {
+                                              const u32 *arrivals, Hook &&between_tiles, u32 pmin = 0) {
+  // positions below pmin are already in T (a dictionary's precomputed tables): treated like
+  // positions past lim (the junk slot, no candidate)
   constexpr u32 JUNK = LONG ? HL_SIZE : HS_SIZE;
   constexpr u32 BT = 2;  // tiles per LDS round trip
   static_assert(TILES % BT == 0, "batches tile windows");
@@ -241,7 +243,7 @@ __device__ __forceinline__ void insert_window(const u32 *in32, u16 *T, u32 wsb, 
         u32 const lo = __builtin_amdgcn_alignbyte(wv[b][k][1], wv[b][k][0], sh), hi = __builtin_amdgcn_alignbyte(wv[b][k][2], wv[b][k][1], sh);
         u32 const hh = hash_of<LONG>(lo, hi);
         e[b][k] = T[hh];
-        h[b][k] = p < lim_t ? hh : JUNK;
+        h[b][k] = (p < lim_t && p >= pmin) ? hh : JUNK;
       }
 #pragma unroll
       for (u32 k = 0; k < TPL; k++) T[h[b][k]] = (u16)(tb + 64 * k + lane + 1);
@@ -281,6 +283,29 @@ __device__ __forceinline__ void insert_window(const u32 *in32, u16 *T, u32 wsb, 
     u32 lo, hi;
     ld64u(in32, we + lane, lo, hi);
     cwe = T[hash_of<LONG>(lo, hi)];
+  }
+  __asm__ volatile("" ::: "memory");
+}
+
+// Positions [s, e) into T in order (the latest position wins every slot), lookups discarded:
+// the few dictionary positions between a precomputed table's end and the first tile a block
+// processes.  Lanes of one store that hit the same slot leave one value; the lower positions
+// that won rewrite theirs until every slot holds its latest.
+template <bool LONG>
+__device__ __forceinline__ void insert_span(const u32 *in32, u16 *T, u32 s, u32 e, u32 lane) {
+  constexpr u32 JUNK = LONG ? HL_SIZE : HS_SIZE;
+  for (u32 r = s; r < e; r += 64) {
+    u32 const p = r + lane;
+    bool const v = p < e;
+    u32 lo, hi;
+    ld64u(in32, v ? p : s, lo, hi);
+    u32 const h = v ? hash_of<LONG>(lo, hi) : JUNK;
+    T[h] = (u16)(p + 1);
+    for (;;) {
+      bool const lost = v && (u32)T[h] < p + 1;
+      if (!__ballot(lost)) break;
+      if (lost) T[h] = (u16)(p + 1);
+    }
   }
   __asm__ volatile("" ::: "memory");
 }
@@ -365,15 +390,17 @@ __device__ __forceinline__ u32 parse_steps(const u32 *ci, u32 i, u32 wn, u32 la,
 // so the next window's insertion spreads over the whole window step.
 constexpr u32 WIN_BARRIERS = 5;  // R, X, J, E1, E2
 template <bool LONG>
-__device__ __forceinline__ void inserter_loop(const u32 *in32, u16 *T, u8 *ci8, u32 *misc_, u32 n, u32 lim, u32 lane, u32 *dbg) {
+__device__ __forceinline__ void inserter_loop(const u32 *in32, u16 *T, u8 *ci8, u32 *misc_, u32 n, u32 lim, u32 lane, u32 *dbg, u32 wstart,
+                                              u32 pmin, u32 span_s, u32 span_e) {
   u32 creg[NCR];
   u32 cwe = 0;
-  insert_window<LONG>(in32, T, 0, min((u32)ZH_WINDOW, n), lim, lane, creg, cwe, &misc_[MISC_ARR], [](u32) {});
+  if (span_s < span_e) insert_span<LONG>(in32, T, span_s, span_e, lane);
+  insert_window<LONG>(in32, T, wstart, min(wstart + (u32)ZH_WINDOW, n), lim, lane, creg, cwe, &misc_[MISC_ARR], [](u32) {}, pmin);
 #ifdef ZH_STAMPS
   u32 st_ins = 0;
 #endif
   u32 passed = 0;  // window barriers taken so far (all windows)
-  for (u32 wsb = 0; wsb < n; wsb += ZH_WINDOW) {
+  for (u32 wsb = wstart; wsb < n; wsb += ZH_WINDOW) {
     u32 const we = min(wsb + ZH_WINDOW, n);
     dump_window<LONG>(ci8, lane, creg, cwe);
     __syncthreads();  // P: candidates of this window in cinfo
@@ -530,7 +557,32 @@ __device__ __forceinline__ u32 lz_block(const ZhBlockDesc *__restrict__ blocks, 
     for (u32 i = tid; i < n; i += K1_THREADS) { u8 c = src[i]; in[i] = c; same &= c == first; }
   }
   if (tid < 16) in[n + tid] = 0;
-  for (u32 i = tid; i < (HL_SIZE + HS_SIZE + 2 * T_PAD) / 2; i += K1_THREADS) ((u32 *)TL)[i] = 0;  // both tables (adjacent)
+  // A dictionary frame's first block starts from the dictionary's precomputed tables when the
+  // batch has them (ws.dtab): their entries (tail position + 1) move to this block's staged
+  // positions (entries before the staged tail are dropped), the last tail positions up to the
+  // batch of tiles holding `pre` are inserted by the inserter waves (insert_span), and the
+  // window loop starts at the window holding `pre` -- the same tables, candidates and parse as
+  // inserting every history position (the oracle's order), without the history windows.
+  bool const use_dt = ws.dtab && (d.flags & ZH_F_DICT) && (d.flags & ZH_F_FIRST) && pre >= 2 * ZH_DTAB_MARGIN && d.n >= 16 &&
+                      ws.dtab_P >= pre;
+  if (use_dt) {
+    u32 const delta = ws.dtab_P - pre;
+    const u32 *dt32 = (const u32 *)ws.dtab;
+    auto clip = [&](u32 e) { return e > delta ? e - delta : 0u; };
+    for (u32 i = tid; i < (HL_SIZE + HS_SIZE) / 2; i += K1_THREADS) {
+      u32 const w = dt32[i];
+      u32 const v = clip(w & 0xFFFFu) | (clip(w >> 16) << 16);
+      u32 const j = i < HL_SIZE / 2 ? i : i + T_PAD / 2;  // TS follows TL's pad
+      ((u32 *)TL)[j] = v;
+    }
+    if (tid < T_PAD) ((u16 *)TL)[tid < T_PAD / 2 ? HL_SIZE + tid : HL_SIZE + T_PAD + HS_SIZE + (tid - T_PAD / 2)] = 0;
+  } else {
+    for (u32 i = tid; i < (HL_SIZE + HS_SIZE + 2 * T_PAD) / 2; i += K1_THREADS) ((u32 *)TL)[i] = 0;  // both tables (adjacent)
+  }
+  // first window / first tile processed and the tail positions the inserters add themselves
+  u32 const pmin = use_dt ? pre & ~(ZH_TILE - 1) : 0u;  // the tile holding pre
+  u32 const wstart = use_dt ? (pre & ~(ZH_WINDOW - 1)) : 0u;
+  u32 const span_s = use_dt ? pre - ZH_DTAB_MARGIN : 0u, span_e = pmin;
   if (tid < 2) misc[8 + tid] = 0;
   if (tid == 0) misc[MISC_ARR] = 0;
   bool const rle = __syncthreads_and(same) && d.n >= 2;
@@ -554,14 +606,14 @@ __device__ __forceinline__ u32 lz_block(const ZhBlockDesc *__restrict__ blocks, 
     // gate the workers' next window, so they take priority (MI355X_MICROARCH.md, "VALU issue
     // is arbitrated ... by priority, then age").
     __builtin_amdgcn_s_setprio(2);
-    if (tid < INS_TID + 64) inserter_loop<true>(in32, TL, ci8, misc, n, lim, lane, ws.dbg(b));
-    else inserter_loop<false>(in32, TS, ci8, misc, n, lim, lane, ws.dbg(b));
+    if (tid < INS_TID + 64) inserter_loop<true>(in32, TL, ci8, misc, n, lim, lane, ws.dbg(b), wstart, pmin, span_s, span_e);
+    else inserter_loop<false>(in32, TS, ci8, misc, n, lim, lane, ws.dbg(b), wstart, pmin, span_s, span_e);
     __builtin_amdgcn_s_setprio(0);
     return next_b;
   }
 
   u32 const tid_ = tid;
-  for (u32 wsb = 0; wsb < n; wsb += ZH_WINDOW) {
+  for (u32 wsb = wstart; wsb < n; wsb += ZH_WINDOW) {
     u32 const we = min(wsb + ZH_WINDOW, n);
     // opaque per-window thread index: keeps the compiler from hoisting every LDS address
     // derived from it out of the window loop (they would be spilled to scratch)
@@ -876,11 +928,39 @@ extern "C" __global__ __launch_bounds__(K1_THREADS) void zh_lz_lazy2_kernel(cons
 
 extern "C" u32 zh_lz_lds_bytes() { return K1_LDS; }
 
+// A dictionary's K1 tables (ZhWorkspace::dtab), built once per dictionary: t32[slot] = max over
+// tail positions j < B hashing there of j + 1 (the latest, as K1's in-order insertion leaves
+// it), then packed to u16.  tail = the last P content bytes.
+extern "C" __global__ void zh_dict_hash_kernel(const u8 *__restrict__ tail, u32 B, u32 *__restrict__ t32) {
+  for (u32 j = blockIdx.x * blockDim.x + threadIdx.x; j < B; j += gridDim.x * blockDim.x) {
+    u32 const lo = (u32)tail[j] | ((u32)tail[j + 1] << 8) | ((u32)tail[j + 2] << 16) | ((u32)tail[j + 3] << 24);
+    u32 const hi = (u32)tail[j + 4] | ((u32)tail[j + 5] << 8) | ((u32)tail[j + 6] << 16) | ((u32)tail[j + 7] << 24);
+    atomicMax(&t32[hash_of<true>(lo, hi)], j + 1);
+    atomicMax(&t32[HL_SIZE + hash_of<false>(lo, hi)], j + 1);
+  }
+}
+extern "C" __global__ void zh_dict_pack_kernel(const u32 *__restrict__ t32, u16 *__restrict__ out) {
+  u32 const i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < HL_SIZE + HS_SIZE) out[i] = (u16)t32[i];
+}
+
 namespace zh {
 hipError_t lz_init() {
   hipError_t e = hipFuncSetAttribute((const void *)zh_lz_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)K1_LDS);
   if (e != hipSuccess) return e;
   return hipFuncSetAttribute((const void *)zh_lz_lazy2_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)K1_LDS);
+}
+// tables for the last P = min(cn, 65535) content bytes (positions [0, P - ZH_DTAB_MARGIN));
+// out: 2^15 u16 (long table, then short), tmp32: 2^15 u32 scratch.  P = 0: none (too short).
+hipError_t lz_dict_tables(const u8 *content, size_t cn, u16 *out, u32 *tmp32, u32 &P, hipStream_t stream) {
+  P = (u32)std::min(cn, (size_t)65535);
+  if (P < 2 * ZH_DTAB_MARGIN) { P = 0; return hipSuccess; }
+  u32 const B = P - ZH_DTAB_MARGIN;
+  hipError_t e = hipMemsetAsync(tmp32, 0, 4 * (HL_SIZE + HS_SIZE), stream);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(zh_dict_hash_kernel, dim3((B + 255) / 256), dim3(256), 0, stream, content + cn - P, B, tmp32);
+  hipLaunchKernelGGL(zh_dict_pack_kernel, dim3((HL_SIZE + HS_SIZE + 255) / 256), dim3(256), 0, stream, tmp32, out);
+  return hipGetLastError();
 }
 void lz_launch(const ZhBlockDesc *d_descs, u32 nblocks, ZhWorkspace ws, bool lazy2, hipStream_t stream) {
   // one persistent workgroup per CU of the stream's device

@@ -146,3 +146,22 @@ def test_c5_level9_cover_64k(torch_cuda, libzstd):
     ratio0 = total / sum(o.numel() for o in plain)
     print(f"C5 (256 x 16 KiB, level 9): ratio {ratio0:.3f} without -> {ratio:.3f} with the 64 KiB COVER dictionary")
     assert ratio > 1.15 * ratio0
+
+
+def test_dictionary_tables_ragged_sizes(torch_cuda):
+    """A 64 KiB dictionary's precomputed K1 tables (built once at set_dictionary) with record
+    sizes that put the block start `pre` at every alignment (65536 - n for n <= 32 KiB, 32 KiB
+    for the first history block above): frames equal the oracle's, which hashes the whole
+    dictionary tail per frame."""
+    import cuda_zstd
+
+    a = T.gen(T.DG_JSON, 256, 0x5EED0705, 4096)
+    d = cuda_zstd.Dictionary.train([a[i:i + 4096] for i in range(0, len(a), 4096)], 65536).content()
+    src = T.gen(T.DG_JSON, 1, 0x5EED0805, 120000)
+    for level in (3, 9):
+        m = _mgr(level, d)
+        for n in (513, 1000, 3333, 16384, 20001, 32768, 40000, 65535, 99999):
+            data = src[:n]
+            f = m.compress(_dev(torch_cuda, data)).cpu().numpy().tobytes()
+            assert f == T.oracle_frame(data, dictionary=d, level=level), (level, n)
+            assert T.zstd_decompress(f, n, dictionary=d) == data.tobytes(), (level, n)
