@@ -77,4 +77,5 @@ def test_nvcomp_batch_manager_handle(L):
 
 def test_kernel_lds_budget(L):
     assert 150 * 1024 < L.cuda_zstd_hip_kernel_lds_bytes(0) <= 160 * 1024
-    assert L.cuda_zstd_hip_kernel_lds_bytes(1) <= 16 * 1024
+    # K2: two waves per block (literals / sequences), overlapping layouts: 9 blocks per CU
+    assert 160 * 1024 // L.cuda_zstd_hip_kernel_lds_bytes(1) >= 9
