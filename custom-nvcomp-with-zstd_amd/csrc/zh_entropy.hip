@@ -1189,6 +1189,37 @@ extern "C" __global__ __launch_bounds__(K2_THREADS) void zh_entropy_kernel(const
     const u8 *lits = ws.lits(b);
     u64 *seq = ws.seq(b);
     u32 op = body0;
+    // the literal histogram, both waves (wave 1 before its sequence work), into wave 0's hist
+    if (nlit > ZH_COMPRESS_LITERALS_SIZE_MIN) {
+      u32 *const hist0 = (u32 *)(smem_all + OFF_HIST);
+      u32 const nl = nlit;
+      if (wave == 0) for (u32 i = lane; i < 256; i += 64) hist0[i] = 0;
+      __syncthreads();
+      // 16 literals per lane per load (lits is 16-B aligned), two loads in flight
+      for (u32 i0 = 32 * lane + 2048 * wave; i0 < nl; i0 += 4096) {
+        uint4 q[2];
+#pragma unroll
+        for (u32 g = 0; g < 2; g++) {
+          u32 const i = i0 + 16 * g;
+          if (i + 16 <= nl) q[g] = *(const uint4 *)(lits + i);
+          else {
+            u32 t[4] = {0, 0, 0, 0};
+            for (u32 k = 0; i + k < nl && k < 16; k++) t[k >> 2] |= (u32)lits[i + k] << (8 * (k & 3));
+            q[g] = make_uint4(t[0], t[1], t[2], t[3]);
+          }
+        }
+#pragma unroll
+        for (u32 g = 0; g < 2; g++) {
+          u32 const i = i0 + 16 * g;
+          u32 const cnt = i < nl ? min(16u, nl - i) : 0u;
+          u32 const w[4] = {q[g].x, q[g].y, q[g].z, q[g].w};
+#pragma unroll
+          for (u32 k = 0; k < 16; k++)
+            if (k < cnt) atomicAdd(&hist0[(w[k >> 2] >> (8 * (k & 3))) & 255u], 1u);
+        }
+      }
+      __syncthreads();
+    }
     // ======================= literals section (ZSTD_compressLiterals), wave 0 =======================
     if (wave == 0) {
       u32 const nl = nlit;
@@ -1198,32 +1229,6 @@ extern "C" __global__ __launch_bounds__(K2_THREADS) void zh_entropy_kernel(const
       u32 cLit = 0, hsz = 0, huffLog = 0;
       u32 *ssz = misc + 8;  // per-stream byte sizes (LDS, wave-uniform)
       if (nl > ZH_COMPRESS_LITERALS_SIZE_MIN) {
-        for (u32 i = lane; i < 256; i += 64) hist[i] = 0;
-        wave_sync();
-        // 16 literals per lane per load (lits is 16-B aligned), two loads in flight
-        for (u32 i0 = 32 * lane; i0 < nl; i0 += 2048) {
-          uint4 q[2];
-#pragma unroll
-          for (u32 g = 0; g < 2; g++) {
-            u32 const i = i0 + 16 * g;
-            if (i + 16 <= nl) q[g] = *(const uint4 *)(lits + i);
-            else {
-              u32 t[4] = {0, 0, 0, 0};
-              for (u32 k = 0; i + k < nl && k < 16; k++) t[k >> 2] |= (u32)lits[i + k] << (8 * (k & 3));
-              q[g] = make_uint4(t[0], t[1], t[2], t[3]);
-            }
-          }
-#pragma unroll
-          for (u32 g = 0; g < 2; g++) {
-            u32 const i = i0 + 16 * g;
-            u32 const cnt = i < nl ? min(16u, nl - i) : 0u;
-            u32 const w[4] = {q[g].x, q[g].y, q[g].z, q[g].w};
-#pragma unroll
-            for (u32 k = 0; k < 16; k++)
-              if (k < cnt) atomicAdd(&hist[(w[k >> 2] >> (8 * (k & 3))) & 255u], 1u);
-          }
-        }
-        wave_sync();
         u32 mx = 0, lg = 0;
         for (u32 i = lane; i < 256; i += 64) { u32 c = hist[i]; if (c) mx = max(mx, i); lg = max(lg, c); }
         u32 const maxSV = wave_max(mx), largest = wave_max(lg);
@@ -1539,6 +1544,11 @@ extern "C" __global__ __launch_bounds__(K2_THREADS) void zh_entropy_kernel(const
     }
     }  // wave 1
     __syncthreads();  // the literals section is written; its end and early_raw are in xch
+    if (xch[1] != 0) {  // raw block (the literals alone pass its minGain): both waves copy half
+      u32 const h = (n / 2) & ~63u;
+      if (wave == 0) copy_bytes(o, body0, d.src, h);
+      else copy_bytes(o, body0 + h, d.src + h, n - h);
+    }
     if (wave == 1) {
       op = xch[0];
       early_raw = xch[1] != 0;
@@ -1586,7 +1596,13 @@ extern "C" __global__ __launch_bounds__(K2_THREADS) void zh_entropy_kernel(const
           handoff = true;
         }
       }
-      if (!handoff) total = finish_block(d, o, blk, op, early_raw);
+      if (early_raw) {
+        u32 const hdr = last + (n << 3);
+        if (lane == 0) { o.put(blk, (u8)hdr); o.put(blk + 1, (u8)(hdr >> 8)); o.put(blk + 2, (u8)(hdr >> 16)); }
+        total = body0 + n;
+      } else if (!handoff) {
+        total = finish_block(d, o, blk, op, false);
+      }
     }
   }
   ZH_STAMP(8);  // tail (raw copy etc.)
