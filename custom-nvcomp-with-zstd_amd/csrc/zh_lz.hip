@@ -579,10 +579,15 @@ __device__ __forceinline__ u32 lz_block(const ZhBlockDesc *__restrict__ blocks, 
   } else {
     for (u32 i = tid; i < (HL_SIZE + HS_SIZE + 2 * T_PAD) / 2; i += K1_THREADS) ((u32 *)TL)[i] = 0;  // both tables (adjacent)
   }
+  // History without precomputed tables (a frame's later blocks, stream history, dictionary
+  // views): only the final table over positions [0, pmin) -- the latest position per slot --
+  // matters, so every wave inserts them at once (below) instead of the inserter waves walking
+  // the history windows.
+  bool const par_hist = !use_dt && pre >= 2 * ZH_TILE && d.n >= 16;
   // first window / first tile processed and the tail positions the inserters add themselves
-  u32 const pmin = use_dt ? pre & ~(ZH_TILE - 1) : 0u;  // the tile holding pre
-  u32 const wstart = use_dt ? (pre & ~(ZH_WINDOW - 1)) : 0u;
-  u32 const span_s = use_dt ? pre - ZH_DTAB_MARGIN : 0u, span_e = pmin;
+  u32 const pmin = (use_dt || par_hist) ? pre & ~(ZH_TILE - 1) : 0u;  // the tile holding pre
+  u32 const wstart = (use_dt || par_hist) ? (pre & ~(ZH_WINDOW - 1)) : 0u;
+  u32 const span_s = use_dt ? pre - ZH_DTAB_MARGIN : 0u, span_e = use_dt ? pmin : 0u;
   if (tid < 2) misc[8 + tid] = 0;
   if (tid == 0) misc[MISC_ARR] = 0;
   bool const rle = __syncthreads_and(same) && d.n >= 2;
@@ -591,6 +596,28 @@ __device__ __forceinline__ u32 lz_block(const ZhBlockDesc *__restrict__ blocks, 
   if (rle) {
     if (tid == 0) { meta[0] = 0; meta[1] = 0; meta[2] = 1; }
     return next_b;
+  }
+  if (par_hist) {
+    // store every position, then rounds of read-back: a slot holding an older position than
+    // one hashing there is raised (values only grow) until no thread changes anything
+    for (u32 round = 0;; round++) {
+      bool ch = false;
+      for (u32 p = tid; p < pmin; p += K1_THREADS) {
+        u32 lo, hi;
+        ld64u(in32, p, lo, hi);
+        u32 const hl = hash_of<true>(lo, hi), hs = hash_of<false>(lo, hi);
+        u16 const v = (u16)(p + 1);
+        if (round == 0) {
+          TL[hl] = v;
+          TS[hs] = v;
+        } else {
+          if (TL[hl] < v) { TL[hl] = v; ch = true; }
+          if (TS[hs] < v) { TS[hs] = v; ch = true; }
+        }
+      }
+      if (round == 0) __syncthreads();
+      else if (!__syncthreads_or(ch)) break;
+    }
   }
 
   ZH_STAMP(st_stage);
