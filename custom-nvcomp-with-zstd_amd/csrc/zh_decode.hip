@@ -1246,14 +1246,26 @@ extern "C" __global__ __launch_bounds__(DEC_THREADS) void zh_decode_kernel(ZhDec
   }
 }
 
-// Sequence bitstreams of deferred buffers, lanes = buffers (64 per wave): the serial
-// FSE state chains of 64 blocks advance together, one instruction stream for all of
-// them.  Each lane reads its block's tables from the hand-off record (5 KB per block, L2 /
-// Infinity-Cache resident) and, per sequence, one 128-bit window of its bitstream below
-// its bit position (a worst-case sequence is 89 bits), so the six field reads of a
-// sequence are register shifts and the only memory latency per step is one round of
-// independent loads (window + three table entries).
-constexpr u32 D2_LANES = 64;
+// Sequence bitstreams of deferred buffers: one wave per D2_BUF buffers, lane j < D2_BUF
+// decoding buffer j.  The wave first stages the D2_BUF blocks' FSE decode tables (5 KB each,
+// from the hand-off records) into LDS, so the three table reads of a step are LDS reads, and
+// the buffers of a group spread over all CUs (a group of 4096 buffers is 4096 / D2_BUF
+// waves) instead of crowding 64 scattered streams into one wave's memory pipeline.  Per
+// sequence a lane reads one 128-bit window of its bitstream below its bit position (a
+// worst-case sequence is 89 bits), so the six field reads are register shifts and a step's
+// memory latency is one window load (L1 resident: the window moves down ~4 bytes a step)
+// beside three LDS reads.
+#ifndef ZH_D2_BUF
+#define ZH_D2_BUF 64
+#endif
+#ifndef ZH_D2_LDS_TABS
+#define ZH_D2_LDS_TABS 0
+#endif
+constexpr u32 D2_BUF = ZH_D2_BUF;
+// Decoded sequences go to an LDS ring and leave in 256-byte bursts every D2_RUN steps:
+// CDNA's vmcnt counts stores too and retires in order, so a per-step global store would
+// make every window load wait for the previous step's write acknowledgement.
+constexpr u32 D2_RUN = 32;
 
 // 16 bytes [wb, wb + 16) of stream p (n bytes, n >= 1), bytes outside [0, n) as zeros
 // (aligned dword loads of in-stream words only) -> (hi, lo)
@@ -1329,72 +1341,153 @@ __device__ __forceinline__ u32 resolve_off_bf(u32 ofv, u32 ll, u32 &r0, u32 &r1,
   return off;
 }
 
+// a 320-bit bitstream window: the five little-endian words from an 8-aligned address
+struct Win5 {
+  u64 w0, w1, w2, w3, w4;
+};
+
+// 64 bits of the window ending at bit t (t < 320), bit t - 1 as the MSB; bits below the
+// window read as zeros (t < 64: the stream's first bits).  Two halving selects, not a word
+// index: an indexed form is lowered to a scratch array.
+__device__ __forceinline__ u64 win64(const Win5 &w, u32 t) {
+  u32 const b = t - 64u, r = b & 63u;
+  bool const h2 = b >= 128u, h1 = (b & 64u) != 0u;
+  u64 const y0 = h2 ? w.w2 : w.w0, y1 = h2 ? w.w3 : w.w1, y2 = h2 ? w.w4 : w.w2;
+  u64 const lo = h1 ? y1 : y0, hi = h1 ? y2 : y1;
+  u64 const v = r ? (lo >> r) | (hi << (64u - r)) : lo;
+  return (s32)b < 0 ? w.w0 << ((64u - t) & 63u) : v;
+}
+
+typedef const __attribute__((address_space(1))) u64 *gptr64;
+
+// the five words from the 8-aligned address A (global, not flat, loads: LDS waits do not
+// wait for them; one address, four immediate offsets)
+__device__ __forceinline__ Win5 win_fetch(uintptr_t A) {
+  gptr64 const q = (gptr64)A;
+  return Win5{q[0], q[1], q[2], q[3], q[4]};
+}
+
 extern "C" __global__ __launch_bounds__(64) void zh_dec_seq_kernel(ZhDecArgs a, u32 nitems) {
   __shared__ u32 info[2][64];
+#if ZH_D2_LDS_TABS
+  __shared__ uint4 tabs[D2_BUF][320];  // DecHandoff::tabs of the wave's buffers
+#endif
+  __shared__ u64 ring[D2_BUF][D2_RUN];
   u32 const lane = lane_id();
   if (lane < 36) info[0][lane] = c_LL_info[lane];
   if (lane < 53) info[1][lane] = c_ML_info[lane];
+  u32 const it0 = a.item0 + blockIdx.x * D2_BUF, end = a.item0 + nitems;
+#if ZH_D2_LDS_TABS
+  for (u32 j = 0; j < D2_BUF && it0 + j < end; j++) {
+    const DecHandoff *const hj = handoff(a, it0 + j);
+    if (hj->flag != 1) continue;  // uniform: every lane reads the same flag
+    const uint4 *const src = (const uint4 *)hj->tabs;
+#pragma unroll
+    for (u32 w = 0; w < 5; w++) tabs[j][lane + 64 * w] = src[lane + 64 * w];
+  }
+#endif
   __syncthreads();
-  u32 const it = a.item0 + blockIdx.x * D2_LANES + lane;
-  if (it >= a.item0 + nitems) return;
+  u32 const it = it0 + lane;
+  if (lane >= D2_BUF || it >= end) return;
   DecHandoff *const ho = handoff(a, it);
   if (ho->flag != 1) return;
+#if ZH_D2_LDS_TABS
+  const u32 *const TLL = (const u32 *)tabs[lane];
+#else
+  const u32 *const TLL = ho->tabs;
+#endif
+  const u32 *const TOF = TLL + 512, *const TML = TLL + 768;
   const u8 *const sp = (const u8 *)ho->sp;
   u32 const nseq = ho->nseq, lg = ho->lg;
   s32 const n = (s32)ho->rem;
-  const u32 *const TLL = ho->tabs, *const TOF = ho->tabs + 512, *const TML = ho->tabs + 768;
   u64 *const seq = (u64 *)(a.ws + (size_t)it * a.slot_bytes + a.lit_bytes);
   u32 const last = n > 0 ? sp[n - 1] : 0u;
-  bool bad = last == 0;
+  bool const bad = last == 0;
   s32 pos = bad ? 0 : 8 * (n - 1) + (s32)hb32(last);
-  u32 rep0 = ho->rep[0], rep1 = ho->rep[1], rep2 = ho->rep[2], sLL = 0, sOF = 0, sML = 0;
+  u32 rep0 = ho->rep[0], rep1 = ho->rep[1], rep2 = ho->rep[2];
   bool big = false;
   u64 sumLL = 0, sumML = 0;
   if (!bad) {
-    for (u32 i = 0; i <= nseq; i++) {  // step 0: initial states; step i: sequence i - 1
-      s32 const hb = (pos + 7) >> 3;
-      s32 const wb = hb - 16;
-      u64 whi, wlo;
-      win_load(sp, n, wb, whi, wlo);
-      u32 t = (u32)(pos - 8 * wb);  // bit position inside the window (121..128)
+    // Bitstream window: w holds the 40 bytes from A, fetched one step ahead -- the window
+    // a step reads was fetched at the start of the previous step for that step's position,
+    // which covers the 128 bits below the current one (a step consumes <= 89 bits), so the
+    // fetch latency hides behind a step of arithmetic.
+    // The window start is clamped to the stream's aligned words [wlo, whi]: near the stream
+    // start bits below the window read as zeros, near its end the window still covers the
+    // top.  A stream of at most 33 bytes fits one window: it is fetched once, word by word.
+    uintptr_t const base = (uintptr_t)sp, wlo = base & ~(uintptr_t)7, whi = (base + (u32)n - 1) & ~(uintptr_t)7;
+    bool const small = whi < wlo + 32;
+    uintptr_t const ahi = small ? wlo : whi - 32;
+    auto wbase = [&](s32 p) {
+      uintptr_t const A = (base + (uintptr_t)(intptr_t)(((p + 7) >> 3) - 32)) & ~(uintptr_t)7;
+      return small ? wlo : (intptr_t)A < (intptr_t)wlo ? wlo : A > ahi ? ahi : A;
+    };
+    uintptr_t A = wbase(pos);
+    Win5 w;
+    if (small) {
+      auto ld = [&](uintptr_t q) { return *(gptr64)(q > whi ? whi : q); };
+      w = Win5{ld(wlo), ld(wlo + 8), ld(wlo + 16), ld(wlo + 24), ld(wlo + 32)};
+    } else {
+      w = win_fetch(A);
+    }
+    auto tpos = [&](s32 p) { return (u32)((s32)(8 * (intptr_t)(base - A)) + p); };
+    u32 sLL, sOF, sML;
+    {  // initial states
+      u64 T = win64(w, tpos(pos));
+      u32 const kL = lg & 0xFFu, kO = (lg >> 8) & 0xFFu, kM = lg >> 16;
+      sLL = take(T, kL);
+      sOF = take(T, kO);
+      sML = take(T, kM);
+      pos -= (s32)(kL + kO + kM);
+    }
+    for (u32 i = 1; i <= nseq; i++) {  // step i: sequence i - 1
+      u32 const eLL = TLL[sLL], eOF = TOF[sOF], eML = TML[sML];
+      // issued after the table reads: vmcnt retires in order, so waiting for the tables
+      // leaves this fetch in flight (it is consumed by the next step)
+      uintptr_t const An = wbase(pos);
+      // (a small stream keeps its window; its lane fetches from its own hand-off record
+      // instead, so the fetch is unconditional and the table wait can leave it in flight)
+      Win5 wn = win_fetch(small ? (uintptr_t)ho : An);  // for step i + 1
+      if (small) wn = w;
+      u32 const ofc = eOF & 0xFFu;
+      u32 const mi = info[1][eML & 0xFFu], li = info[0][eLL & 0xFFu];
+      u32 const mb = mi >> 24, lb = li >> 24;
+      u32 t = tpos(pos);
       u32 const t0 = t;
-      if (i == 0) {
-        u64 T = win_top(whi, wlo, t);
-        u32 const kL = lg & 0xFFu, kO = (lg >> 8) & 0xFFu, kM = lg >> 16;
-        sLL = take(T, kL);
-        sOF = take(T, kO);
-        sML = take(T, kM);
-        t -= kL + kO + kM;
-      } else {
-        u32 const eLL = TLL[sLL], eOF = TOF[sOF], eML = TML[sML];
-        u32 const ofc = eOF & 0xFFu;
-        u32 const mi = info[1][eML & 0xFFu], li = info[0][eLL & 0xFFu];
-        u32 const mb = mi >> 24, lb = li >> 24;
-        u64 T = win_top(whi, wlo, t);
-        u32 const ofv = (1u << ofc) + take(T, ofc);
-        u32 const ml = (mi & 0xFFFFFFu) + take(T, mb);
-        u32 const ll = (li & 0xFFFFFFu) + take(T, lb);
-        t -= ofc + mb + lb;
-        u32 const off = resolve_off_bf(ofv, ll, rep0, rep1, rep2);
-        big |= off >= OFF_LIMIT;
-        sumLL += ll;
-        sumML += ml;
-        seq[i - 1] = (u64)ll | (u64)(ml - 3) << 17 | (u64)off << 34;
-        if (i < nseq) {
-          u32 const kL = (eLL >> 8) & 0xFFu, kM = (eML >> 8) & 0xFFu, kO = (eOF >> 8) & 0xFFu;
-          u64 U = win_top(whi, wlo, t);
-          sLL = (eLL >> 16) + take(U, kL);
-          sML = (eML >> 16) + take(U, kM);
-          sOF = (eOF >> 16) + take(U, kO);
-          t -= kL + kM + kO;
-        }
+      u64 T = win64(w, t);
+      u32 const ofv = (1u << ofc) + take(T, ofc);
+      u32 const ml = (mi & 0xFFFFFFu) + take(T, mb);
+      u32 const ll = (li & 0xFFFFFFu) + take(T, lb);
+      t -= ofc + mb + lb;
+      u32 const off = resolve_off_bf(ofv, ll, rep0, rep1, rep2);
+      big |= off >= OFF_LIMIT;
+      sumLL += ll;
+      sumML += ml;
+      u32 const r = (i - 1) & (D2_RUN - 1);
+      ring[lane][r] = (u64)ll | (u64)(ml - 3) << 17 | (u64)off << 34;
+      if (r == D2_RUN - 1) {  // a full run: 32 sequences, 256-byte aligned
+        uint4 *const dst = (uint4 *)(seq + (i - D2_RUN));
+        const uint4 *const srcr = (const uint4 *)ring[lane];
+#pragma unroll
+        for (u32 k = 0; k < D2_RUN / 2; k++) dst[k] = srcr[k];
+      }
+      if (i < nseq) {
+        u32 const kL = (eLL >> 8) & 0xFFu, kM = (eML >> 8) & 0xFFu, kO = (eOF >> 8) & 0xFFu;
+        u64 U = win64(w, t);
+        sLL = (eLL >> 16) + take(U, kL);
+        sML = (eML >> 16) + take(U, kM);
+        sOF = (eOF >> 16) + take(U, kO);
+        t -= kL + kM + kO;
       }
       pos -= (s32)(t0 - t);
+      A = An;
+      w = wn;
     }
+    for (u32 k = nseq & ~(D2_RUN - 1); k < nseq; k++) seq[k] = ring[lane][k & (D2_RUN - 1)];  // the partial last run
   }
   ho->sumLL = sumLL;
   ho->sumML = sumML;
-  ho->sbad = (bad || pos > 0 || big) ? 1u : 0u;
+  ho->sbad = (bad || pos != 0 || big) ? 1u : 0u;
 }
 
 namespace {
@@ -1421,7 +1514,7 @@ hipError_t launch_decompress(const ZhDecArgs &a0, u32 nitems, hipStream_t stream
     hipLaunchKernelGGL(zh_decode_kernel, dim3(cnt), dim3(DEC_THREADS), 0, s, a);
     check("phase 1");
     if (after_p1) (void)hipEventRecord(after_p1, s);
-    hipLaunchKernelGGL(zh_dec_seq_kernel, dim3((cnt + D2_LANES - 1) / D2_LANES), dim3(64), 0, s, a, cnt);
+    hipLaunchKernelGGL(zh_dec_seq_kernel, dim3((cnt + D2_BUF - 1) / D2_BUF), dim3(64), 0, s, a, cnt);
     check("sequences");
     a.phase = 3;
     hipLaunchKernelGGL(zh_decode_kernel, dim3(cnt), dim3(DEC_THREADS), 0, s, a);
@@ -1429,7 +1522,7 @@ hipError_t launch_decompress(const ZhDecArgs &a0, u32 nitems, hipStream_t stream
   };
   // Large batches run as G groups on staggered streams (zh_pipe.h): group k's phase 1 starts
   // once group k-1's phase 1 is done, so the latency-bound sequence kernel of a group (one
-  // wave per 64 buffers) overlaps the throughput-bound phase 1 of the next groups and
+  // wave per D2_BUF buffers) overlaps the throughput-bound phase 1 of the next groups and
   // phase 3 of the earlier ones.
   constexpr u32 G = 4, MIN_GROUP = 1024;
   StreamPipe<G> *p = (!dbg && nitems >= G * MIN_GROUP) ? stream_pipe<DecPipeTag, G>(stream) : nullptr;
