@@ -884,9 +884,9 @@ __device__ bool execute_block(LDS &L, const Slot &sl, u8 *ob, s64 fpos, const Li
 // ---- split pipeline.  A buffer holding one frame of one compressed block (every chunk
 // of a batch) is decoded by three kernels: phase 1 (this kernel) does the headers, the
 // literals and the sequence tables and leaves a hand-off record; zh_dec_seq_kernel runs
-// the sequence bitstreams of eight such buffers at once, one lane each (the serial FSE
-// chains of eight blocks interleave in one wave instead of one chain per wave); phase 3
-// executes the block and finishes the frame.  Anything else is decoded in phase 1.
+// the sequence bitstreams of 64 such buffers at once, one lane each (the serial FSE chains
+// of 64 blocks interleave in one wave instead of one chain per wave); zh_dec_exec_kernel
+// (phase 3) executes the block and finishes the frame.  Anything else is decoded in phase 1.
 struct DecHandoff {
   u32 tabs[1280];  // DecLds::fse of the block
   u64 sp;          // sequence bitstream
@@ -1273,77 +1273,19 @@ extern "C" __global__ __launch_bounds__(DEC_THREADS) void zh_dec_exec_kernel(ZhD
   return;
 }
 
-// Sequence bitstreams of deferred buffers: one wave per D2_BUF buffers, lane j < D2_BUF
-// decoding buffer j.  The wave first stages the D2_BUF blocks' FSE decode tables (5 KB each,
-// from the hand-off records) into LDS, so the three table reads of a step are LDS reads, and
-// the buffers of a group spread over all CUs (a group of 4096 buffers is 4096 / D2_BUF
-// waves) instead of crowding 64 scattered streams into one wave's memory pipeline.  Per
-// sequence a lane reads one 128-bit window of its bitstream below its bit position (a
-// worst-case sequence is 89 bits), so the six field reads are register shifts and a step's
-// memory latency is one window load (L1 resident: the window moves down ~4 bytes a step)
-// beside three LDS reads.
-#ifndef ZH_D2_BUF
-#define ZH_D2_BUF 64
-#endif
-#ifndef ZH_D2_LDS_TABS
-#define ZH_D2_LDS_TABS 0
-#endif
-constexpr u32 D2_BUF = ZH_D2_BUF;
+// Sequence bitstreams of deferred buffers: lanes = buffers, 64 per wave, so the serial FSE
+// state chains of 64 blocks advance under one instruction stream.  A step's only exposed
+// memory latency is the three table reads (each lane's tables sit in its hand-off record);
+// the bitstream window it needs was fetched one step earlier (win_fetch below), and decoded
+// sequences leave through an LDS ring.  The chain is issue-latency bound: one wave per SIMD,
+// ~180 dependent instructions a step.  Measured alternatives (profiles/r02m_dec_seq.json):
+// 4-32 buffers per wave with the tables staged in LDS (32- or 16-bit entries) were slower,
+// both isolated and pipelined -- LDS-limited occupancy, no shorter chain.
+constexpr u32 D2_BUF = 64;
 // Decoded sequences go to an LDS ring and leave in 256-byte bursts every D2_RUN steps:
 // CDNA's vmcnt counts stores too and retires in order, so a per-step global store would
 // make every window load wait for the previous step's write acknowledgement.
 constexpr u32 D2_RUN = 32;
-
-// 16 bytes [wb, wb + 16) of stream p (n bytes, n >= 1), bytes outside [0, n) as zeros
-// (aligned dword loads of in-stream words only) -> (hi, lo)
-__device__ __forceinline__ void win_load(const u8 *p, s32 n, s32 wb, u64 &hi, u64 &lo) {
-  uintptr_t const a0 = (uintptr_t)p;
-  s32 const sh = (s32)(a0 & 3u);
-  const u32 *const w = (const u32 *)(a0 - (uintptr_t)sh);
-  // stream byte b lives in word (b + sh) >> 2; load the 5 words covering [wb, wb + 16)
-  s32 const q0 = (wb + sh) >> 2;
-  s32 const qlo = 0, qhi = (n - 1 + sh) >> 2;  // words holding stream bytes
-  u32 x[5];
-  if (q0 >= qlo && q0 + 4 <= qhi) {  // all five words in the stream: every step but the first / last few
-#pragma unroll
-    for (s32 k = 0; k < 5; k++) x[k] = w[q0 + k];
-  } else {
-#pragma unroll
-    for (s32 k = 0; k < 5; k++) {
-      s32 const q = q0 + k;
-      x[k] = (q >= qlo && q <= qhi) ? w[q] : 0u;
-    }
-  }
-  u32 const o = (u32)((wb + sh) & 3);
-  u32 const b0 = __builtin_amdgcn_alignbyte(x[1], x[0], o), b1 = __builtin_amdgcn_alignbyte(x[2], x[1], o),
-            b2 = __builtin_amdgcn_alignbyte(x[3], x[2], o), b3 = __builtin_amdgcn_alignbyte(x[4], x[3], o);
-  lo = (u64)b1 << 32 | b0;
-  hi = (u64)b3 << 32 | b2;
-  // bytes of the first / last word outside the stream: zero them
-  s32 const below = -wb;  // window bytes before the stream start
-  if (below > 0) {
-    u32 const z = (u32)min(below, 16) * 8u;
-    if (z >= 64) { lo = 0; hi = z >= 128 ? 0 : hi & (~0ull << (z - 64)); }
-    else lo &= ~0ull << z;
-  }
-  s32 const above = wb + 16 - n;  // window bytes past the stream end
-  if (above > 0) {
-    u32 const z = (u32)min(above, 16) * 8u;
-    if (z >= 64) { hi = 0; lo = z >= 128 ? 0 : lo & (~0ull >> (z - 64)); }
-    else hi &= ~0ull >> z;
-  }
-}
-
-// 64 bits of the window (hi:lo) ending at bit t (32 <= t <= 128), bit t - 1 as the MSB;
-// bits below the window read as zeros.  A step reads its fields from two of these: the
-// three extra-bit fields (<= 31 + 16 + 16 bits), then the three state updates (<= 26 bits).
-__device__ __forceinline__ u64 win_top(u64 hi, u64 lo, u32 t) {
-  s32 const b = (s32)t - 64;  // lowest bit taken
-  u32 const r = (u32)b & 63u;
-  u64 const mid = (lo >> r) | ((hi << 1) << (63u - r));
-  u64 const v = b >= 64 ? hi : b > 0 ? mid : lo;
-  return b >= 0 ? v : lo << (u32)(-b);
-}
 
 // the top k (<= 31) bits of T; T <<= k
 __device__ __forceinline__ u32 take(u64 &T, u32 k) {
@@ -1396,34 +1338,17 @@ __device__ __forceinline__ Win5 win_fetch(uintptr_t A) {
 
 extern "C" __global__ __launch_bounds__(64) void zh_dec_seq_kernel(ZhDecArgs a, u32 nitems) {
   __shared__ u32 info[2][64];
-#if ZH_D2_LDS_TABS
-  __shared__ uint4 tabs[D2_BUF][320];  // DecHandoff::tabs of the wave's buffers
-#endif
   __shared__ u64 ring[D2_BUF][D2_RUN];
   u32 const lane = lane_id();
   if (lane < 36) info[0][lane] = c_LL_info[lane];
   if (lane < 53) info[1][lane] = c_ML_info[lane];
   u32 const it0 = a.item0 + blockIdx.x * D2_BUF, end = a.item0 + nitems;
-#if ZH_D2_LDS_TABS
-  for (u32 j = 0; j < D2_BUF && it0 + j < end; j++) {
-    const DecHandoff *const hj = handoff(a, it0 + j);
-    if (hj->flag != 1) continue;  // uniform: every lane reads the same flag
-    const uint4 *const src = (const uint4 *)hj->tabs;
-#pragma unroll
-    for (u32 w = 0; w < 5; w++) tabs[j][lane + 64 * w] = src[lane + 64 * w];
-  }
-#endif
   __syncthreads();
   u32 const it = it0 + lane;
   if (lane >= D2_BUF || it >= end) return;
   DecHandoff *const ho = handoff(a, it);
   if (ho->flag != 1) return;
-#if ZH_D2_LDS_TABS
-  const u32 *const TLL = (const u32 *)tabs[lane];
-#else
-  const u32 *const TLL = ho->tabs;
-#endif
-  const u32 *const TOF = TLL + 512, *const TML = TLL + 768;
+  const u32 *const TLL = ho->tabs, *const TOF = TLL + 512, *const TML = TLL + 768;
   const u8 *const sp = (const u8 *)ho->sp;
   u32 const nseq = ho->nseq, lg = ho->lg;
   s32 const n = (s32)ho->rem;
