@@ -1337,6 +1337,9 @@ __device__ __forceinline__ Win5 win_fetch(uintptr_t A) {
 }
 
 extern "C" __global__ __launch_bounds__(64) void zh_dec_seq_kernel(ZhDecArgs a, u32 nitems) {
+  // highest issue priority: the chains are issue-latency bound and share SIMDs with the
+  // phase-1 / phase-3 waves of the other groups of the pipeline
+  __builtin_amdgcn_s_setprio(3);
   __shared__ u32 info[2][64];
   __shared__ u64 ring[D2_BUF][D2_RUN];
   u32 const lane = lane_id();
@@ -1472,19 +1475,23 @@ hipError_t launch_decompress(const ZhDecArgs &a0, u32 nitems, hipStream_t stream
     check("phase 3");
   };
   // Large batches run as G groups on staggered streams (zh_pipe.h): group k's phase 1 starts
-  // once group k-1's phase 1 is done, so the latency-bound sequence kernel of a group (one
-  // wave per D2_BUF buffers) overlaps the throughput-bound phase 1 of the next groups and
-  // phase 3 of the earlier ones.
-  constexpr u32 G = 4, MIN_GROUP = 1024;
+  // once group k-1's phase 1 is done, so the sequence kernel of a group (one wave per 64
+  // buffers, a ~7 ms issue-latency-bound chain whatever the group size) overlaps the phase 1
+  // of the later group and the execution of the earlier one.  The end is about phase 1 of
+  // every group + one chain + the last group's execution, so the first group is the larger
+  // (2 : 1).  Measured (profiles/r02m_dec_seq.json): G = 1 / 2 / 3 / 4 / 8 -> 56.8 / 59.1 /
+  // 56.0 / 56.2 / 36.6 GB/s, 2 : 1 and 3 : 1 splits 59.3 / 59.7.
+  constexpr u32 G = 2, W0 = 2, MIN_GROUP = 1024;
   StreamPipe<G> *p = (!dbg && nitems >= G * MIN_GROUP) ? stream_pipe<DecPipeTag, G>(stream) : nullptr;
   if (!p) {
     group(0, nitems, stream, nullptr);
     return hipGetLastError();
   }
-  u32 const per = (nitems + G - 1) / G;
+  u32 const shares = W0 + G - 1, unit = nitems / shares;  // group 0: W0 shares, others one
   p->run(stream, [&](u32 k, hipStream_t s, hipEvent_t after_first) {
-    u32 const first = k * per;
-    group(first, std::min(per, nitems - first), s, after_first);
+    u32 const first = k == 0 ? 0u : (W0 + k - 1) * unit;
+    u32 const last = k + 1 == G ? nitems : (W0 + k) * unit;
+    group(first, last - first, s, after_first);
   });
   return hipGetLastError();
 }
