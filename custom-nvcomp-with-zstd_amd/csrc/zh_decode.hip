@@ -422,12 +422,13 @@ __device__ u32 huf_read_weights(DecLds &L, const u8 *p, u32 avail) {
       if (r.pos < 0) { L.hufw[nw++] = (u8)(L.wt[s1] & 0xFF); break; }
     }
   }
-  u32 rs[16] = {};
-  u32 sum = 0;
+  // only the count of weight-1 symbols is checked: no rank array (a dynamically indexed
+  // private array lives in scratch)
+  u32 sum = 0, rs1 = 0;
   for (u32 i = 0; i < nw; i++) {
     u32 const w = L.hufw[i];
     if (w >= 12) return 0;
-    rs[w]++;
+    rs1 += w == 1;
     sum += (1u << w) >> 1;
   }
   if (sum == 0) return 0;
@@ -437,8 +438,8 @@ __device__ u32 huf_read_weights(DecLds &L, const u8 *p, u32 avail) {
   if (rest & (rest - 1)) return 0;
   u32 const lastw = hb32(rest) + 1;
   L.hufw[nw] = (u8)lastw;
-  rs[lastw]++;
-  if (rs[1] < 2 || (rs[1] & 1)) return 0;
+  rs1 += lastw == 1;
+  if (rs1 < 2 || (rs1 & 1)) return 0;
   L.hlog = tlog;
   L.hnsym = nw + 1;
   return used;
@@ -480,11 +481,17 @@ __device__ void huf_build_dtable(DecLds &L) {
   }
   __syncthreads();
   for (u32 e = lane; e < (1u << tlog); e += 64) {
-    u32 w = 1;
+    // class of entry e by selects (rk/cs indexed only by unrolled constants: registers)
+    u32 w = 1, rkw = rk[1], csw = cs[1];
 #pragma unroll
-    for (u32 v = 2; v <= 11; v++) w = (cnt[v] && e >= rk[v]) ? v : w;
-    u32 const idx = (e - rk[w]) >> (w - 1);
-    u32 const s = L.symlist[cs[w] + idx];
+    for (u32 v = 2; v <= 11; v++) {
+      bool const in = cnt[v] && e >= rk[v];
+      w = in ? v : w;
+      rkw = in ? rk[v] : rkw;
+      csw = in ? cs[v] : csw;
+    }
+    u32 const idx = (e - rkw) >> (w - 1);
+    u32 const s = L.symlist[csw + idx];
     L.u.h.dt[e] = (u16)(s | (tlog + 1 - w) << 8);
   }
   __syncthreads();
