@@ -49,7 +49,10 @@ namespace {
 constexpr u32 K1_THREADS = 1024;
 constexpr u32 NPSEG = ZH_WINDOW / 64;       // parse segments per window (64 positions = one wave)
 constexpr u32 INS_TID = 896;                // first inserter thread (waves 14, 15)
-constexpr u32 SB = 5;                       // positions per thread in the length phase
+#ifndef ZH_K1_SB
+#define ZH_K1_SB 5
+#endif
+constexpr u32 SB = ZH_K1_SB;                // positions per thread in the length phase
 constexpr u32 NB = (ZH_WINDOW + SB - 1) / SB;  // length-phase threads (thread NB takes position `we`)
 constexpr u32 TILES = ZH_WINDOW / ZH_TILE;  // 16 tiles per window
 constexpr u32 TPL = ZH_TILE / 64;           // positions per inserter lane per tile
@@ -113,7 +116,7 @@ __device__ __forceinline__ u32 prefix8(const u32 *in32, u32 b, u32 olo, u32 ohi)
 // min(E - i, cap) without touching the input again.  Bytes 8.. are compared as
 // dwords with every load issued up front; bytes past the block end read LDS
 // padding/tables and are cut off by n - p.
-constexpr u32 EXT_SPAN = ZH_MAX_MATCH + SB - 1;
+constexpr u32 EXT_SPAN = 8 + (ZH_MAX_MATCH + SB - 1 - 8 + 3) / 4 * 4;  // (>= cap + SB - 1, whole dwords)
 static_assert((EXT_SPAN - 8) % 4 == 0, "dword span");
 __device__ __forceinline__ u32 ext_head(const u32 *in32, u32 p, u32 q, u32 n) {
   constexpr u32 NW = (EXT_SPAN - 8) / 4;  // dwords compared
@@ -475,6 +478,20 @@ __device__ __forceinline__ void prefetch_block(const ZhBlockDesc *__restrict__ b
   }
 }
 
+// Workgroup role of a thread: virtual wave = K1_WAVE_MAP nibble of its hardware wave.  The
+// wave-to-SIMD assignment is wave id mod 4 (a CU's 16 waves, 4 per SIMD); roles are placed so
+// the SIMDs carry equal length-phase work: ZH_K1_PERM 1 puts both inserters (virtual 14, 15)
+// on SIMD 3 with one length wave, the 12 other length waves 4 per SIMD 0-2.
+#ifndef ZH_K1_PERM
+#define ZH_K1_PERM 1
+#endif
+// nibble p = virtual wave of hardware wave p
+constexpr u64 K1_WAVE_MAP = ZH_K1_PERM ? 0xDBA9C876F543E210ull : 0xFEDCBA9876543210ull;
+__device__ __forceinline__ u32 k1_tid() {
+  u32 const t = threadIdx.x;
+  return (u32)((K1_WAVE_MAP >> (4 * (t >> 6))) & 15u) << 6 | (t & 63u);
+}
+
 template <bool LAZY2>
 __device__ __forceinline__ u32 lz_block(const ZhBlockDesc *__restrict__ blocks, ZhWorkspace ws, u32 b, u32 nblocks, u32 *s_take, Prefetch &pf) {
   extern __shared__ __attribute__((aligned(16))) u8 smem[];
@@ -492,7 +509,7 @@ __device__ __forceinline__ u32 lz_block(const ZhBlockDesc *__restrict__ blocks, 
   // opaque per-block thread index: stops the compiler from hoisting LDS addresses derived
   // from it out of the persistent block loop (they would stay live, and spill, across it)
   u32 tid;
-  __asm__ volatile("v_mov_b32 %0, %1" : "=v"(tid) : "v"((u32)threadIdx.x));
+  __asm__ volatile("v_mov_b32 %0, %1" : "=v"(tid) : "v"(k1_tid()));
   u32 const lane = tid & 63;
   ZhBlockDesc const d = blocks[b];
   // the next block for this workgroup (dynamic: a slow block does not hold up a fixed share)
@@ -672,14 +689,16 @@ __device__ __forceinline__ u32 lz_block(const ZhBlockDesc *__restrict__ blocks, 
       u32 cv[SB], plp = 0, psp = 0;  // prefixes packed 4 bits per position
       // the thread's own bytes [s, s + SB + 7) from four aligned dwords, shared by its SB
       // positions (positions past lim have cv = 0: their bytes are never compared)
-      static_assert(SB <= 5, "own[] holds 12 bytes");
-      u32 own[3];
+      static_assert(SB <= 8 && ZH_WINDOW + 2 + SB <= CI_WORDS, "heads: bit j (L) and 8 + j (S); junk slots");
+      constexpr u32 NOWN = (SB + 7 + 3) / 4;  // dwords of own bytes
+      u32 own[NOWN];
       {
         u32 const w = s >> 2, sh = s & 3u;
-        u32 const w0 = in32[w], w1 = in32[w + 1], w2 = in32[w + 2], w3 = in32[w + 3];
-        own[0] = __builtin_amdgcn_alignbyte(w1, w0, sh);
-        own[1] = __builtin_amdgcn_alignbyte(w2, w1, sh);
-        own[2] = __builtin_amdgcn_alignbyte(w3, w2, sh);
+        u32 aw[NOWN + 1];
+#pragma unroll
+        for (u32 k = 0; k <= NOWN; k++) aw[k] = in32[w + k];
+#pragma unroll
+        for (u32 k = 0; k < NOWN; k++) own[k] = __builtin_amdgcn_alignbyte(aw[k + 1], aw[k], sh);
       }
 #pragma unroll
       for (u32 j = 0; j < SB; j++) {
@@ -713,8 +732,10 @@ __device__ __forceinline__ u32 lz_block(const ZhBlockDesc *__restrict__ blocks, 
       //     e = 8 matching bytes (nibble bit 3 of the packed prefix; 0 without a
       //     candidate), continuation = candidate == previous position's candidate + 1.
       auto nib8 = [](u32 pk) {  // bit j = nibble j == 8
-        u32 const x = (pk >> 3) & 0x11111u;
-        return (x & 1u) | ((x >> 3) & 2u) | ((x >> 6) & 4u) | ((x >> 9) & 8u) | ((x >> 12) & 16u);
+        u32 r = 0;
+#pragma unroll
+        for (u32 j = 0; j < SB; j++) r |= ((pk >> (4 * j + 3)) & 1u) << j;
+        return r;
       };
       u32 const eL = nib8(plp), eS = nib8(psp);
       u32 dL = 0, dS = 0, fromSL = 0, fromSS = 0, heads = 0;  // heads: bit j = L, bit 8 + j = S
@@ -939,7 +960,7 @@ __device__ __forceinline__ void lz_blocks(const ZhBlockDesc *__restrict__ blocks
   __syncthreads();
   u32 b = s_take;
   Prefetch pf;
-  prefetch_block(blocks, b, nblocks, threadIdx.x, pf);
+  prefetch_block(blocks, b, nblocks, k1_tid(), pf);
   while (b < nblocks) {
     b = lz_block<LAZY2>(blocks, ws, b, nblocks, &s_take, pf);  // returns the next block taken
     __syncthreads();  // every wave is done with this block's LDS before the next is staged
