@@ -478,12 +478,13 @@ __device__ __forceinline__ void prefetch_block(const ZhBlockDesc *__restrict__ b
   }
 }
 
-// Workgroup role of a thread: virtual wave = K1_WAVE_MAP nibble of its hardware wave.  The
-// wave-to-SIMD assignment is wave id mod 4 (a CU's 16 waves, 4 per SIMD); roles are placed so
-// the SIMDs carry equal length-phase work: ZH_K1_PERM 1 puts both inserters (virtual 14, 15)
-// on SIMD 3 with one length wave, the 12 other length waves 4 per SIMD 0-2.
+// Workgroup role of a thread: virtual wave = K1_WAVE_MAP nibble of its hardware wave (the
+// wave-to-SIMD assignment is wave id mod 4).  ZH_K1_PERM 1 puts both inserters (virtual 14,
+// 15) on SIMD 3 with one length wave and four length waves on each other SIMD: mix 13.74 ->
+// 13.68 ms, but random data (few matches, the inserters are the critical path) 10.15 -> 10.72
+// ms, so the default keeps the identity (inserters on SIMDs 2 and 3).
 #ifndef ZH_K1_PERM
-#define ZH_K1_PERM 1
+#define ZH_K1_PERM 0
 #endif
 // nibble p = virtual wave of hardware wave p
 constexpr u64 K1_WAVE_MAP = ZH_K1_PERM ? 0xDBA9C876F543E210ull : 0xFEDCBA9876543210ull;
