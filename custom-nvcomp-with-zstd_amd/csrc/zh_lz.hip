@@ -796,20 +796,20 @@ __device__ __forceinline__ u32 lz_block(const ZhBlockDesc *__restrict__ blocks, 
         u32 const cL = cv[j] & 0xFFFFu, cS = cv[j] >> 16;
         u32 const capj = min((u32)ZH_MAX_MATCH, n - min(p, n));
         u32 const hx = ci[cidx(cbase + j)];  // head extensions from (3)
-        u32 nL = PL(j);
-        if (dL & (1u << j)) nL = ((fromSL >> j) & 1u ? ES : EL) - 1;
-        else if ((heads >> j) & 1u) nL = hx & 255u;
-        u32 nS = PS(j);
-        if (dS & (1u << j)) nS = ((fromSS >> j) & 1u ? ES : EL) - 1;
-        else if ((heads >> (8 + j)) & 1u) nS = (hx >> 16) & 255u;
-        if (cS && cS == cL) nS = nL;
+        // selects only (no divergent branches: exec-mask work on the scalar unit)
+        u32 const eFL = ((fromSL >> j) & 1u) ? ES : EL, eFS = ((fromSS >> j) & 1u) ? ES : EL;
+        u32 nL = ((heads >> j) & 1u) ? (hx & 255u) : PL(j);
+        nL = ((dL >> j) & 1u) ? eFL - 1u : nL;
+        u32 nS = ((heads >> (8 + j)) & 1u) ? ((hx >> 16) & 255u) : PS(j);
+        nS = ((dS >> j) & 1u) ? eFS - 1u : nS;
+        nS = (cS && cS == cL) ? nL : nS;
         EL = nL; ES = nS;
         u32 const rL = min(nL, capj), rS = min(nS, capj);
         u32 const lL = (cL && rL >= ZH_MIN_MATCH_LONG) ? rL : 0u;
         u32 const lS = (cS && rS >= ZH_MIN_MATCH_SHORT) ? rS : 0u;
-        u32 v = 0;
-        if (lL && lL >= lS) v = ((p - (cL - 1)) << 8) | lL;
-        else if (lS) v = ((p - (cS - 1)) << 8) | lS;
+        bool const useL = lL && lL >= lS;
+        u32 const ml = useL ? lL : lS, cm = useL ? cL : cS;
+        u32 const v = ml ? ((p - (cm - 1u)) << 8) | ml : 0u;
         ci[p < se ? cidx(cbase + j) : ZH_WINDOW + 2 + j] = v;  // (past the run: junk slots)
       }
       if (tid == NB && we >= n) ci[cidx(ZH_WINDOW)] = 0;          // no position after the block
