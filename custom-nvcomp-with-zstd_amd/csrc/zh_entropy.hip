@@ -1542,12 +1542,36 @@ extern "C" __global__ __launch_bounds__(K2_THREADS) void zh_entropy_kernel(const
         if (lane < 53) ((FseSym *)(fz + ZH_FT_SYML))[lane] = symML[lane];
       }
     }
+    if (wave == 1 && lane == 0) xch[2] = nbSeq;
     }  // wave 1
     __syncthreads();  // the literals section is written; its end and early_raw are in xch
     if (xch[1] != 0) {  // raw block (the literals alone pass its minGain): both waves copy half
       u32 const h = (n / 2) & ~63u;
       if (wave == 0) copy_bytes(o, body0, d.src, h);
       else copy_bytes(o, body0 + h, d.src + h, n - h);
+    } else if (u32 const ns = xch[2]; ns > 0) {
+      // the codes in encoding order (step k = ns-1-i) in the chain layout (zh_common.h), both
+      // waves (wave 0 is otherwise idle here): a lane per 16-step run (contiguous in the
+      // layout), its 16 records, three 16-byte stores
+      u32 const k3L = ZH_K3_SEGLEN(ns), k3m = zh_k3_magic(k3L);
+      u8 *const cb = ws.lits(b) + 128u * k3L;
+      for (u32 k0 = 16u * (lane + 64u * wave); k0 < ns; k0 += 16u * K2_THREADS) {
+        u64 r[16];
+#pragma unroll
+        for (u32 q = 0; q < 16; q++) r[q] = k0 + q < ns ? seq[ns - 1 - (k0 + q)] : 0ull;
+        u32 wl[4] = {0, 0, 0, 0}, wo[4] = {0, 0, 0, 0}, wm[4] = {0, 0, 0, 0};
+#pragma unroll
+        for (u32 q = 0; q < 16; q++) {
+          u32 const ob = (u32)(r[q] >> 34) & 0x1FFFFu;
+          wl[q >> 2] |= ((u32)(r[q] >> 51) & 63u) << (8 * (q & 3));
+          wo[q >> 2] |= (ob ? highbit32(ob) : 0u) << (8 * (q & 3));
+          wm[q >> 2] |= ((u32)(r[q] >> 57)) << (8 * (q & 3));
+        }
+        u32 const x0 = zh_k3_index(k0, 0, k3L, k3m);
+        *(uint4 *)(cb + x0) = make_uint4(wl[0], wl[1], wl[2], wl[3]);
+        *(uint4 *)(cb + x0 + ZH_K3_TSTRIDE) = make_uint4(wo[0], wo[1], wo[2], wo[3]);
+        *(uint4 *)(cb + x0 + 2u * ZH_K3_TSTRIDE) = make_uint4(wm[0], wm[1], wm[2], wm[3]);
+      }
     }
     if (wave == 1) {
       op = xch[0];
@@ -1562,29 +1586,7 @@ extern "C" __global__ __launch_bounds__(K2_THREADS) void zh_entropy_kernel(const
           op += 1;
           for (u32 i = lane; i < hpos; i += 64) o.put(op + i, hbuf[i]);
           op += hpos;
-          // the codes in encoding order (step k = nbSeq-1-i) in the chain layout (zh_common.h):
-          // a lane per 16-step run (contiguous in the layout): its 16 records, three 16-byte stores
-          {
-            u32 const k3L = ZH_K3_SEGLEN(nbSeq), k3m = zh_k3_magic(k3L);
-            u8 *const cb = ws.lits(b) + 128u * k3L;
-            for (u32 k0 = 16u * lane; k0 < nbSeq; k0 += 16u * 64u) {
-              u64 r[16];
-    #pragma unroll
-              for (u32 q = 0; q < 16; q++) r[q] = k0 + q < nbSeq ? seq[nbSeq - 1 - (k0 + q)] : 0ull;
-              u32 wl[4] = {0, 0, 0, 0}, wo[4] = {0, 0, 0, 0}, wm[4] = {0, 0, 0, 0};
-    #pragma unroll
-              for (u32 q = 0; q < 16; q++) {
-                u32 const ob = (u32)(r[q] >> 34) & 0x1FFFFu;
-                wl[q >> 2] |= ((u32)(r[q] >> 51) & 63u) << (8 * (q & 3));
-                wo[q >> 2] |= (ob ? highbit32(ob) : 0u) << (8 * (q & 3));
-                wm[q >> 2] |= ((u32)(r[q] >> 57)) << (8 * (q & 3));
-              }
-              u32 const x0 = zh_k3_index(k0, 0, k3L, k3m);
-              *(uint4 *)(cb + x0) = make_uint4(wl[0], wl[1], wl[2], wl[3]);
-              *(uint4 *)(cb + x0 + ZH_K3_TSTRIDE) = make_uint4(wo[0], wo[1], wo[2], wo[3]);
-              *(uint4 *)(cb + x0 + 2u * ZH_K3_TSTRIDE) = make_uint4(wm[0], wm[1], wm[2], wm[3]);
-            }
-          }
+          // (the codes in encoding order: both waves, above)
           // hand-off: the FSE state chains run in zh_fse_chain_kernel and the bitstream is
           // packed by zh_seq_pack_kernel, which also finishes the block
           u32 *ff = ws.fsef(b);
