@@ -34,7 +34,7 @@ enum : u32 {
 };
 
 // Per-block workspace carved from the caller's temp buffer.
-//   seq   : ZH_SEQ_CAP u64 records (K1: cumLit | ml<<17 | off<<25; K2 rewrites in place)
+//   seq   : ZH_SEQ_CAP u64 records (K1: cumLit | ml<<17 | off<<32; K2 rewrites in place)
 //   lits  : ZH_BLOCK_MAX literal bytes; once the literals section is written, the
 //           sequences' FSE states and codes in encoding order in the segment-interleaved
 //           layout of the chain kernel (below): states u16 [0, 128 L), codes u8 [128 L, 192 L),
@@ -128,5 +128,7 @@ __device__ __forceinline__ u32 wave_scan_max_incl(u32 v) {
 }
 // value of lane - 1 (lane 0 reads 0): DPP wave_shr:1
 __device__ __forceinline__ u32 wave_shr1(u32 v) { return ZH_DPP(v, 0x138, 0xf); }
+// value of lane + 1 (lane 63 reads 0): DPP wave_shl:1
+__device__ __forceinline__ u32 wave_shl1(u32 v) { return ZH_DPP(v, 0x130, 0xf); }
 // v of a wave-uniform lane (v_readlane into an SGPR)
 __device__ __forceinline__ u32 lane_value(u32 v, u32 uniform_lane) { return (u32)__builtin_amdgcn_readlane((int)v, (int)uniform_lane); }

@@ -1413,7 +1413,7 @@ extern "C" __global__ __launch_bounds__(K2_THREADS) void zh_entropy_kernel(const
         u32 const i = base + lane;
         bool const valid = i < nseq_raw;
         u64 const rec = ring.next(seq, nseq_raw, i);
-        u32 const cum = (u32)(rec & 0x1FFFFu), ml = (u32)((rec >> 17) & 255u), off = (u32)((rec >> 25) & 0xFFFFu);
+        u32 const cum = (u32)(rec & 0x1FFFFu), ml = (u32)((rec >> 17) & 0x7FFFu), off = (u32)((rec >> 32) & 0x1FFFFu);
         u32 pc = wave_shr1(cum), po = wave_shr1(off);
         if (lane == 0) { pc = carryCum; po = carryOff; }
         u32 const ll = cum - pc;

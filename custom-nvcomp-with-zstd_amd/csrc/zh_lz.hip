@@ -11,8 +11,9 @@
 //   in[]   the block, staged once with 16-B loads (64 KiB)
 //   TL/TS  2 x 2^14 u16 hash tables, entry = position + 1 (0 = empty)
 //   cinfo  one 4096-position window: candidates -> match info (off<<8|len) in place
-//   exb    per-position exits of the 64-position parse segments
-// Wave roles (wave specialisation, all synchronised with workgroup barriers):
+//   hm/lm  per 64-position segment: has-match and literal bit masks
+//   mlist  the window's matches in position order, with their catch-up lengths
+// Wave roles (wave specialisation, synchronised with workgroup barriers):
 //   waves 14, 15  inserters: one wave per hash table walks the next window's
 //                 tiles of ZH_TILE positions.  A single wave needs no barrier
 //                 between a tile's lookups and its inserts because LDS executes
@@ -20,17 +21,23 @@
 //                 same slot are resolved to the latest position by a read-back.
 //                 Candidates are held in registers and dumped into cinfo at the
 //                 window switch, so the next window's insertion overlaps this
-//                 window's lengths.
-//   waves 0..13   match lengths of the window, 5 positions per thread, with
-//                 same-offset chains resolved in registers.
-//   waves 0..13   the serial greedy/lazy-1 parse, lanes = positions: pointer
-//                 doubling gives every position's exit from its 64-position
-//                 segment, wave 0 finds the segment entries as a Jacobi fixed
-//                 point, binary lifting marks the visited positions, and scans of
-//                 the marks place literals and sequence records.
+//                 window's parse.
+//   waves 0..13   match lengths, lanes = positions: each candidate's common prefix
+//                 from its first 8 bytes, and along same-offset chains (the candidate
+//                 of p+1 is the candidate of p plus one) lcp(p) = 1 + lcp(p+1): a ballot
+//                 of the chain ends and one ds_bpermute give every position its length,
+//                 only chain ends past 8 bytes are extended.
+//   wave 0        the parse, lanes = 64-position segments: each lane walks its segment
+//                 (literal runs skipped through the has-match mask) from a guessed entry;
+//                 Jacobi rounds re-walk the segments whose entry changed until the walk
+//                 meets the previous one -- exactly the serial parse -- and lists the
+//                 window's matches.
+//   waves 0..13   lanes = matches: each match grows backwards over the literals before it
+//                 (catch-up), then the sequence records; lanes = positions: the literals.
 #include "zh_common.h"
 
 #include <algorithm>
+#include <vector>
 
 #ifdef ZH_STAMPS
 __device__ u32 g_fixups;  // diagnostic: inserter read-back fix-up rounds (all blocks)
@@ -47,17 +54,13 @@ extern "C" u32 zh_fixups_host() {
 namespace {
 
 constexpr u32 K1_THREADS = 1024;
-constexpr u32 NPSEG = ZH_WINDOW / 64;       // parse segments per window (64 positions = one wave)
+constexpr u32 NSEG = ZH_WINDOW / 64;        // 64-position segments (= length rounds) per window
 constexpr u32 INS_TID = 896;                // first inserter thread (waves 14, 15)
-#ifndef ZH_K1_SB
-#define ZH_K1_SB 5
-#endif
-constexpr u32 SB = ZH_K1_SB;                // positions per thread in the length phase
-constexpr u32 NB = (ZH_WINDOW + SB - 1) / SB;  // length-phase threads (thread NB takes position `we`)
-constexpr u32 TILES = ZH_WINDOW / ZH_TILE;  // 16 tiles per window
+constexpr u32 NWW = INS_TID / 64;           // worker waves
+constexpr u32 TILES = ZH_WINDOW / ZH_TILE;  // 32 tiles per window
 constexpr u32 TPL = ZH_TILE / 64;           // positions per inserter lane per tile
 constexpr u32 NCR = TILES * TPL / 2;        // candidate registers per inserter lane (u16 pairs)
-static_assert(NPSEG == 64 && NB + 1 <= INS_TID, "thread roles");
+static_assert(NSEG == 64, "one walk lane per segment");
 static_assert(ZH_WINDOW % ZH_TILE == 0 && ZH_TILE % 64 == 0 && TILES * TPL % 2 == 0, "tiles tile windows");
 
 constexpr u32 HL_SIZE = 1u << ZH_HASH_LOG_LONG;
@@ -67,22 +70,19 @@ constexpr u32 OFF_IN = 0;
 constexpr u32 OFF_TL = OFF_IN + ZH_BLOCK_MAX + 16;
 constexpr u32 OFF_TS = OFF_TL + 2 * (HL_SIZE + T_PAD);
 constexpr u32 OFF_CI = OFF_TS + 2 * (HS_SIZE + T_PAD);
-constexpr u32 CI_WORDS = ZH_WINDOW + 8;  // + the lookahead slot of position `we`
+constexpr u32 CI_WORDS = ZH_WINDOW + 8;  // + the lookahead slots of positions `we`, `we + 1`
 __device__ __forceinline__ u32 cidx(u32 i) { return i; }
-constexpr u32 OFF_EXB = OFF_CI + 4 * CI_WORDS;      // u8 per position: its parse segment exit (relative)
-constexpr u32 OFF_SEG = OFF_EXB + ZH_WINDOW + 16;   // parse segment entries + the window exit (exb: + a junk byte)
-constexpr u32 NWW = INS_TID / 64;                   // worker waves
-constexpr u32 PR = (ZH_WINDOW + INS_TID - 1) / INS_TID;  // lane-per-position rounds over a window
-constexpr u32 WP_OFF = 80, WP_TOT = 160;
-static_assert(PR * NWW <= WP_OFF, "emission scan slots");
-constexpr u32 OFF_WP = OFF_SEG + 4 * (NPSEG + 4);     // emission scan: wave counts, offsets, total
-constexpr u32 HB_STRIDE = 65;                        // per worker wave: 64 head slots + a junk slot
-constexpr u32 OFF_HB = OFF_WP + 4 * 164;
-constexpr u32 OFF_MISC = OFF_HB + 4 * HB_STRIDE * (INS_TID / 64);  // [0..3] scan partials, [4..6] barrier-or words
+constexpr u32 OFF_HM = OFF_CI + 4 * CI_WORDS;        // u64 per segment: positions with a match
+constexpr u32 OFF_LM = OFF_HM + 8 * NSEG;            // u64 per segment: literal positions
+constexpr u32 ML_CAP = (ZH_WINDOW + ZH_MIN_MATCH_SHORT - 1) / ZH_MIN_MATCH_SHORT + 12;  // matches per window
+constexpr u32 OFF_ML = OFF_LM + 8 * NSEG;            // the window's match starts (window index), in order
+constexpr u32 OFF_ME = OFF_ML + 4 * ML_CAP;          // their starts after catch-up
+constexpr u32 OFF_MR = OFF_ME + 4 * ML_CAP;          // their (length after catch-up) | offset << 13
+constexpr u32 OFF_MISC = OFF_MR + 4 * ML_CAP;        // [1] matches of the window, [2] its exit
 constexpr u32 K1_LDS = OFF_MISC + 4 * 16;
 constexpr u32 MISC_ARR = 12;  // misc[12]: worker-wave barrier arrivals (cumulative)
 static_assert(K1_LDS <= 163840 - 256, "K1 LDS budget");
-static_assert(OFF_TL % 16 == 0 && OFF_CI % 16 == 0 && OFF_SEG % 16 == 0, "alignment");
+static_assert(OFF_TL % 16 == 0 && OFF_CI % 16 == 0 && OFF_HM % 16 == 0, "alignment");
 
 __device__ __forceinline__ u32 hash_long(u64 v) {
   return (u32)((v * ZH_PRIME_LONG) >> (64 - ZH_HASH_LOG_LONG));
@@ -110,37 +110,30 @@ __device__ __forceinline__ u32 prefix8(const u32 *in32, u32 b, u32 olo, u32 ohi)
   return (x ? cx : 32u + cy) >> 3;
 }
 
-// Extension of a chain head (p, q) whose first 8 bytes match: E = min(common prefix,
-// EXT_SPAN, n - p).  EXT_SPAN = cap 64 + SB - 1, so every later position of the
-// thread's run continuing the same offset gets its exact capped length as
-// min(E - i, cap) without touching the input again.  Bytes 8.. are compared as
-// dwords with every load issued up front; bytes past the block end read LDS
-// padding/tables and are cut off by n - p.
-constexpr u32 EXT_SPAN = 8 + (ZH_MAX_MATCH + SB - 1 - 8 + 3) / 4 * 4;  // (>= cap + SB - 1, whole dwords)
-static_assert((EXT_SPAN - 8) % 4 == 0, "dword span");
-__device__ __forceinline__ u32 ext_head(const u32 *in32, u32 p, u32 q, u32 n) {
-  constexpr u32 NW = (EXT_SPAN - 8) / 4;  // dwords compared
-  constexpr u32 H = (NW + 1) / 2;         // in two halves (bounded register use)
-  u32 const pa = p + 8, qa = q + 8;
-  u32 const wp = pa >> 2, sp = pa & 3, wq = qa >> 2, sq = qa & 3;
-  u32 l = EXT_SPAN;
+// Common prefix of in[p..] and in[c..], capped at ZH_MAX_MATCH, for lanes `act` whose first 8
+// bytes match (other lanes: any value).  Bytes 8.. are compared as dwords, 16 bytes per step
+// with the step's loads issued together, until no active lane still matches; bytes past the
+// block end read LDS padding / tables and are cut off by n - p later.
+__device__ __forceinline__ u32 ext8(const u32 *in32, u32 p, u32 c, bool act) {
+  constexpr u32 NW = ZH_MAX_MATCH / 4;  // dwords of a capped match
+  u32 const wp = p >> 2, sp = p & 3, wq = c >> 2, sq = c & 3;
+  u32 l = ZH_MAX_MATCH;
 #pragma unroll
-  for (u32 h0 = 0; h0 < NW; h0 += H) {
-    // the second half only when some lane's match reaches past the first one
-    if (h0 && !__ballot(l == EXT_SPAN)) break;
-    u32 A[H + 1], B[H + 1];
+  for (u32 k0 = 2; k0 < NW; k0 += 4) {
+    if (!__ballot(act && l == ZH_MAX_MATCH)) break;
+    u32 A[5], B[5];
 #pragma unroll
-    for (u32 k = 0; k <= H; k++) { A[k] = in32[wp + h0 + k]; B[k] = in32[wq + h0 + k]; }
-    u32 lh = EXT_SPAN;
+    for (u32 k = 0; k < 5; k++) { A[k] = in32[wp + k0 + k]; B[k] = in32[wq + k0 + k]; }
+    u32 lh = ZH_MAX_MATCH;
 #pragma unroll
-    for (int k = (int)H - 1; k >= 0; k--) {
-      if (h0 + (u32)k >= NW) continue;
+    for (int k = 3; k >= 0; k--) {
+      if (k0 + (u32)k >= NW) continue;
       u32 const x = __builtin_amdgcn_alignbyte(A[k + 1], A[k], sp) ^ __builtin_amdgcn_alignbyte(B[k + 1], B[k], sq);
-      if (x) lh = 8 + 4 * (h0 + (u32)k) + (__builtin_ctz(x) >> 3);
+      if (x) lh = 4 * (k0 + (u32)k) + (__builtin_ctz(x) >> 3);
     }
-    l = l == EXT_SPAN ? lh : l;
+    l = l == ZH_MAX_MATCH ? lh : l;
   }
-  return min(l, n - p);
+  return l;
 }
 
 template <bool LONG>
@@ -331,67 +324,208 @@ __device__ __forceinline__ void dump_window(u8 *ci8, u32 lane_, const u32 (&creg
   if (lane < 2) *(u16 *)(ci8 + 4 * cidx(ZH_WINDOW + lane) + (LONG ? 0 : 2)) = (u16)cwe;
 }
 
-// Lane-per-position parse steps for window index i (a wave's 64 lanes = one parse
-// segment of 64 positions): X[k] = position reached after 2^k parse steps from i, for
-// k < 6, and X[6] = the segment exit, relative to the segment start (values >= the
-// segment length mean "left the segment").  Returns the match info of i if the parse
-// takes a match there, else 0.
 // v from lane `src` (< 64) of the wave: ds_bpermute on a byte address, no lane-base math
 __device__ __forceinline__ u32 bperm(u32 v, u32 src) { return (u32)__builtin_amdgcn_ds_bpermute((int)(src << 2), (int)v); }
+__device__ __forceinline__ u32 ctz64(u64 v) { return (u32)__builtin_ctzll(v); }
+// bits [a, b) of a u64, 0 <= a <= b <= 64
+__device__ __forceinline__ u64 bit_range(u32 a, u32 b) {
+  u64 const hi = b >= 64 ? ~0ull : (1ull << b) - 1ull;
+  return hi & ~((1ull << a) - 1ull);
+}
 
-// (wave_scan_incl, wave_shr1: DPP helpers in zh_common.h)
+// ---- match lengths, lanes = positions -------------------------------------------------------
+// Chain state carried from a round to the one below it (rounds run from high positions to low):
+// the candidates and capped common prefixes of the position just above the round.
+struct LenCarry {
+  u32 cL, cS, lL, lS;
+};
 
+// Length of position p's candidate from the chain structure: T = ballot of the chain ends
+// (lanes whose lcp is their own: fewer than 8 bytes, or the next position does not continue
+// the candidate), e = their lcp.  A lane inside a chain is 1 + its successor's: the distance
+// to its chain end plus that end's lcp; a chain running past the round takes the carry.
+__device__ __forceinline__ u32 chain_lcp(u64 T, u32 e, u32 carry, u32 lane) {
+  u64 const rest = T >> lane;
+  u32 const q = rest ? ctz64(rest) : 64u - lane;
+  u32 const v = bperm(e, min(lane + q, 63u));
+  return min((u32)ZH_MAX_MATCH, q + (rest ? v : carry));
+}
+
+// One round of 64 consecutive positions (window indices 64 r + lane): candidates in cinfo ->
+// match info (off << 8 | len, 0 = none) in place + the round's has-match mask.  Semantics of
+// oracle/zstd_oracle.c orc_lz_match_info: lcp capped at ZH_MAX_MATCH and at the block end,
+// long candidates from 8 bytes, short from 5, the longer (long on ties).
+__device__ __forceinline__ void len_round(const u32 *in32, u32 *ci, u64 *hm, u32 r, u32 wsb, u32 we, u32 n, u32 lim, u32 lane, LenCarry &cy) {
+  u32 const i = 64 * r + lane, p = wsb + i;
+  bool const hv = p < we && p < lim;
+  u32 const cw = ci[cidx(i)];
+  u32 const cL = hv ? (cw & 0xFFFFu) : 0u, cS = hv ? (cw >> 16) : 0u;
+  u32 lo, hi;
+  ld64u(in32, p, lo, hi);
+  // both prefixes unconditionally (clamped addresses), then selects
+  u32 const tL = prefix8(in32, cL ? cL - 1u : 0u, lo, hi);
+  u32 const tS = prefix8(in32, cS ? cS - 1u : 0u, lo, hi);
+  u32 const pL = cL ? tL : 0u, pS = cS ? tS : 0u;
+  // does p+1's candidate continue p's?  (lane 63: the carried position above the round)
+  u32 cLn = wave_shl1(cL), cSn = wave_shl1(cS);
+  cLn = lane == 63 ? cy.cL : cLn;
+  cSn = lane == 63 ? cy.cS : cSn;
+  bool const fL = pL == 8 && cLn == cL + 1u, fS = pS == 8 && cSn == cS + 1u;
+  // chain ends with 8 matching bytes: extended (a short candidate equal to the long one
+  // takes the long one's extension)
+  bool const xL = pL == 8 && !fL;
+  bool const xS = pS == 8 && !fS && !(cS == cL && xL);
+  u32 eL = pL, eS = pS;
+  if (__ballot(xL)) {
+    u32 const e = ext8(in32, xL ? p : 0u, xL ? cL - 1u : 0u, xL);
+    eL = xL ? e : eL;
+  }
+  eS = (cS == cL && xL && pS == 8 && !fS) ? eL : eS;
+  if (__ballot(xS)) {
+    u32 const e = ext8(in32, xS ? p : 0u, xS ? cS - 1u : 0u, xS);
+    eS = xS ? e : eS;
+  }
+  u32 const lL = chain_lcp(__ballot(!fL), eL, cy.lL, lane);
+  u32 const lS = chain_lcp(__ballot(!fS), eS, cy.lS, lane);
+  cy.cL = lane_value(cL, 0); cy.cS = lane_value(cS, 0);
+  cy.lL = lane_value(lL, 0); cy.lS = lane_value(lS, 0);
+  u32 const capj = min((u32)ZH_MAX_MATCH, n - min(p, n));
+  u32 const rL = min(lL, capj), rS = min(lS, capj);
+  u32 const mL = (cL && rL >= ZH_MIN_MATCH_LONG) ? rL : 0u;
+  u32 const mS = (cS && rS >= ZH_MIN_MATCH_SHORT) ? rS : 0u;
+  bool const useL = mL && mL >= mS;
+  u32 const ml = useL ? mL : mS, cm = useL ? cL : cS;
+  u32 const v = ml ? ((p - (cm - 1u)) << 8) | ml : 0u;
+  ci[cidx(i)] = v;
+  u64 const hb = __ballot(v != 0);
+  if (lane == 0) hm[r] = hb;
+}
+
+// Match info of one position from scratch (the lookahead positions `we`, `we + 1` of the
+// next window, which the next window's rounds compute again): c = candidate word.
+__device__ __forceinline__ u32 info_one(const u32 *in32, u32 p, u32 cw, u32 n, u32 lim, bool act) {
+  bool const hv = act && p < lim;
+  u32 const cL = hv ? (cw & 0xFFFFu) : 0u, cS = hv ? (cw >> 16) : 0u;
+  u32 lo, hi;
+  ld64u(in32, hv ? p : 0u, lo, hi);
+  u32 const tL = prefix8(in32, cL ? cL - 1u : 0u, lo, hi), tS = prefix8(in32, cS ? cS - 1u : 0u, lo, hi);
+  u32 const pL = cL ? tL : 0u, pS = cS ? tS : 0u;
+  u32 const e1 = ext8(in32, pL == 8 ? p : 0u, pL == 8 ? cL - 1u : 0u, pL == 8);
+  u32 const e2 = ext8(in32, pS == 8 ? p : 0u, pS == 8 ? cS - 1u : 0u, pS == 8);
+  u32 const lL = pL == 8 ? e1 : pL, lS = pS == 8 ? e2 : pS;
+  u32 const capj = min((u32)ZH_MAX_MATCH, n - min(p, n));
+  u32 const rL = min(lL, capj), rS = min(lS, capj);
+  u32 const mL = (cL && rL >= ZH_MIN_MATCH_LONG) ? rL : 0u;
+  u32 const mS = (cS && rS >= ZH_MIN_MATCH_SHORT) ? rS : 0u;
+  bool const useL = mL && mL >= mS;
+  u32 const ml = useL ? mL : mS, cm = useL ? cL : cS;
+  return ml ? ((p - (cm - 1u)) << 8) | ml : 0u;
+}
+
+// ---- catch-up ----------------------------------------------------------------------------------
+// The 4 bytes in[a-4, a) (a >= 1; bytes before the buffer start read as 0s shifted out)
+__device__ __forceinline__ u32 ld4_before(const u32 *in32, u32 a) {
+  u32 const t = a >= 4 ? a - 4 : 0u, w = t >> 2, sh = t & 3;
+  u32 const v = __builtin_amdgcn_alignbyte(in32[w + 1], in32[w], sh);
+  return a >= 4 ? v : v << (8 * (4 - a));
+}
+// Bytes a match at staged position P with offset off grows backwards (oracle orc_lz_parse_pre's
+// catch-up): while P - e > lo and P - e > off and in[P-e-1] == in[P-e-1-off].  Compared four
+// bytes at a time from the top byte down; at most a few steps.
+__device__ __forceinline__ u32 catch_up(const u32 *in32, u32 P, u32 off, u32 lo, bool act) {
+  u32 maxe = (act && P > lo && P > off) ? min(P - lo, P - off) : 0u;
+  u32 e = 0;
+  while (__ballot(e < maxe)) {
+    if (e < maxe) {
+      u32 const a = P - e, x = ld4_before(in32, a) ^ ld4_before(in32, a - off);
+      u32 const m = x ? (u32)__builtin_clz(x) >> 3 : 4u;
+      e += min(m, maxe - e);
+      maxe = m < 4 ? e : maxe;
+    }
+  }
+  return e;
+}
+
+// ---- the parse, lanes = segments --------------------------------------------------------------
 // Parse cost of a match: libzstd's lazy "gain" (4 per byte, minus the offset's bit length)
 __device__ __forceinline__ int match_gain(u32 inf) {
   return inf ? 4 * (int)(inf & 255u) - (31 - (int)__builtin_clz((inf >> 8) + 1u)) : -1000;
 }
 
-// LAZY2 (levels >= 9): a match at i is deferred when the match at i+1 gains
-// more than 4 over it or the one at i+2 more than 7 (libzstd ZSTD_compressBlock_lazy_generic,
-// depth 2); otherwise (levels < 9) when the match at i+1 is longer.  la / la2: the match info
-// of the next window's first two positions.
+// The serial parse's step at window index i with match info inf = ci[i] != 0: take the match
+// unless the one at i+1 is longer (levels < 9) -- or, LAZY2 (levels >= 9), unless
+// the match at i+1 gains more than 4 over it or the one at i+2 more than 7 (libzstd
+// ZSTD_compressBlock_lazy_generic, depth 2).  ci[wn..] holds the next window's first two
+// positions (or 0 past the block).
 template <bool LAZY2>
-__device__ __forceinline__ u32 parse_steps(const u32 *ci, u32 i, u32 wn, u32 la, u32 la2, u32 lane, u32 (&X)[7]) {
-  u32 const sb = i & ~63u;
-  u32 const slen = wn > sb ? min(64u, wn - sb) : 0u;
-  // unconditional (clamped) loads, then selects: no exec-mask branches
-  u32 const r0 = ci[min(i, (u32)ZH_WINDOW)], r1 = ci[min(i + 1, (u32)ZH_WINDOW)];
-  u32 const inf = i < wn ? r0 : 0u;
-  u32 const inf1 = i + 1 < wn ? r1 : la;
-  u32 const l = inf & 255u;
-  bool tk;
+__device__ __forceinline__ bool take_at(const u32 *ci, u32 i, u32 inf) {
+  u32 const inf1 = ci[cidx(i + 1)];
   if (LAZY2) {
-    u32 const r2 = ci[min(i + 2, (u32)ZH_WINDOW + 1)];
-    u32 const inf2 = i + 2 < wn ? r2 : (i + 2 == wn ? la : la2);
+    u32 const inf2 = ci[cidx(i + 2)];
     int const g0 = match_gain(inf);
-    tk = l != 0 && match_gain(inf1) <= g0 + 4 && match_gain(inf2) <= g0 + 7;
-  } else {
-    tk = l != 0 && (inf1 & 255u) <= l;
+    return match_gain(inf1) <= g0 + 4 && match_gain(inf2) <= g0 + 7;
   }
-  u32 x = lane + (tk ? l : 1u);
-  if (__ballot(tk)) {
-#pragma unroll
-    for (u32 k = 0; k < 6; k++) {
-      X[k] = x;
-      u32 const y = bperm(x, min(x, 63u));
-      x = x < slen ? y : x;
-    }
-  } else {  // all literals in this segment: 2^k steps are 2^k positions
-#pragma unroll
-    for (u32 k = 0; k < 6; k++) {
-      X[k] = x;
-      x = x < slen ? min(x + (1u << k), slen) : x;
+  return (inf1 & 255u) <= (inf & 255u);
+}
+
+// Walk of segment [S, SE) from position p by the lanes `act`: literal runs are skipped through
+// the has-match mask hmk, every position with a match candidate is one step.  LM / MM: the
+// segment's literal and match-start bits, ex: the exit (first position >= SE).  With old
+// visited bits (a Jacobi re-walk from a new entry), the walk stops where it meets a position
+// the old walk visited -- from there on both are the same -- and keeps the old bits above it.
+template <bool LAZY2>
+__device__ __forceinline__ void seg_walk(const u32 *ci, u64 hmk, u32 S, u32 SE, u32 p, bool act0, u64 &LM, u64 &MM, u32 &ex) {
+  u64 const old = act0 ? (LM | MM) : 0ull;
+  u64 nl = 0, nm = 0;
+  bool act = act0 && p < SE, merged = false;
+  u32 mpos = 0;
+  while (__ballot(act)) {
+    if (act) {
+      u32 const o = p - S;
+      u64 const m = hmk >> o, ov = old >> o;
+      u32 const q = m ? p + ctz64(m) : SE;
+      u32 const x = ov ? p + ctz64(ov) : ~0u;
+      if (x <= q) {
+        nl |= bit_range(o, x - S);
+        merged = true;
+        mpos = x - S;
+        act = false;
+      } else {
+        nl |= bit_range(o, q - S);
+        p = q;
+        if (p < SE) {
+          u32 const inf = ci[cidx(p)];
+          u64 const b = 1ull << (p - S);
+          if (take_at<LAZY2>(ci, p, inf)) {
+            nm |= b;
+            p += inf & 255u;
+          } else {
+            nl |= b;
+            p += 1;
+          }
+        }
+        act = p < SE;
+      }
     }
   }
-  X[6] = x;
-  return tk ? inf : 0u;
+  if (act0) {
+    if (merged) {
+      u64 const keep = ~((1ull << mpos) - 1ull);
+      LM = nl | (LM & keep);
+      MM = nm | (MM & keep);
+    } else {
+      LM = nl;
+      MM = nm;
+      ex = p;
+    }
+  }
 }
 
 // Inserter wave main loop.  It mirrors the workers' barrier sequence window by window
-// (P, R, X, J, E1, E2) but fills the slack: between two tiles it takes the next
-// barrier only once all 14 worker waves have arrived there (an LDS arrival counter),
-// so the next window's insertion spreads over the whole window step.
-constexpr u32 WIN_BARRIERS = 5;  // R, X, J, E1, E2
+// (P, R, W1, W2) but fills the slack: between two tiles it takes the next barrier only once
+// all 14 worker waves have arrived there (an LDS arrival counter), so the next window's
+// insertion spreads over the whole window step.
+constexpr u32 WIN_BARRIERS = 3;  // R (lengths done), W1 (parse done), W2 (catch-up done)
 template <bool LONG>
 __device__ __forceinline__ void inserter_loop(const u32 *in32, u16 *T, u8 *ci8, u32 *misc_, u32 n, u32 lim, u32 lane, u32 *dbg, u32 wstart,
                                               u32 pmin, u32 span_s, u32 span_e) {
@@ -501,10 +635,8 @@ __device__ __forceinline__ u32 lz_block(const ZhBlockDesc *__restrict__ blocks, 
   u16 *TL = (u16 *)(smem + OFF_TL), *TS = (u16 *)(smem + OFF_TS);
   u32 *ci = (u32 *)(smem + OFF_CI);
   u8 *ci8 = smem + OFF_CI;
-  u8 *exb = smem + OFF_EXB;
-  u32 *wpart = (u32 *)(smem + OFF_WP);
-  u32 *hbuf = (u32 *)(smem + OFF_HB);
-  u32 *segx = (u32 *)(smem + OFF_SEG);
+  u64 *hm = (u64 *)(smem + OFF_HM);
+  u64 *lmk = (u64 *)(smem + OFF_LM);
   u32 *misc = (u32 *)(smem + OFF_MISC);
 
   // opaque per-block thread index: stops the compiler from hoisting LDS addresses derived
@@ -531,7 +663,7 @@ __device__ __forceinline__ u32 lz_block(const ZhBlockDesc *__restrict__ blocks, 
   u64 const rt0 = __builtin_amdgcn_s_memrealtime();
   u64 stamp_prev = __builtin_amdgcn_s_memtime();
   u64 const mt0 = stamp_prev;
-  u32 st_stage = 0, st_A = 0, st_X = 0, st_E1 = 0, st_Bmax = 0, st_Imax = 0, st_Bw = 0, st_B = 0, st_J = 0, st_E = 0, st_rounds = 0;
+  u32 st_stage = 0, st_A = 0, st_X = 0, st_E1 = 0, st_Bmax = 0, st_Imax = 0, st_Bw = 0, st_B = 0, st_J = 0, st_E = 0, st_E2 = 0, st_rounds = 0;
 #endif
 
   // ---- stage the block into LDS (16 B per lane when the source allows it) and probe RLE
@@ -658,6 +790,13 @@ __device__ __forceinline__ u32 lz_block(const ZhBlockDesc *__restrict__ blocks, 
   }
 
   u32 const tid_ = tid;
+  u32 const wave = tid >> 6;
+  // rounds (64-position segments) of this worker wave in the length phase and the literals:
+  // waves 0..5 four, waves 6..13 five (wave 0 also walks the window)
+  constexpr u32 NR_LO = NSEG / NWW, NR_HI_WAVES = NSEG - NR_LO * NWW;
+  static_assert(NR_HI_WAVES < NWW, "round split");
+  u32 const r_lo = wave < NWW - NR_HI_WAVES ? NR_LO * wave : NR_LO * wave + (wave - (NWW - NR_HI_WAVES));
+  u32 const r_hi = r_lo + (wave < NWW - NR_HI_WAVES ? NR_LO : NR_LO + 1);
   for (u32 wsb = wstart; wsb < n; wsb += ZH_WINDOW) {
     u32 const we = min(wsb + ZH_WINDOW, n);
     // opaque per-window thread index: keeps the compiler from hoisting every LDS address
@@ -674,266 +813,122 @@ __device__ __forceinline__ u32 lz_block(const ZhBlockDesc *__restrict__ blocks, 
       }
       continue;
     }
-#ifdef ZH_STAMPS
-    u64 const tP = __builtin_amdgcn_s_memtime();
-#endif
 
-    // ---- match lengths (threads 0..NB), while the inserter waves build the next window
-    // (a worker wave without positions skips the phase: wave-uniform)
-    if ((tid & ~63u) <= NB) {
-      // thread tid < NB: positions [s, se) of the window; thread NB: position `we`;
-      // threads above NB take part in the wave-level steps with no positions
-      u32 const s = tid < NB ? wsb + SB * tid : we;
-      u32 const se = tid < NB ? min(s + SB, we) : (tid == NB ? min(we + 2, n) : s);  // (we, we+1: lookahead)
-      u32 const cbase = tid < NB ? SB * tid : ZH_WINDOW;  // window index of position s
-      // (1) candidates, own bytes and first-8-byte prefixes; loads unconditional
-      u32 cv[SB], plp = 0, psp = 0;  // prefixes packed 4 bits per position
-      // the thread's own bytes [s, s + SB + 7) from four aligned dwords, shared by its SB
-      // positions (positions past lim have cv = 0: their bytes are never compared)
-      static_assert(SB <= 8 && ZH_WINDOW + 2 + SB <= CI_WORDS, "heads: bit j (L) and 8 + j (S); junk slots");
-      constexpr u32 NOWN = (SB + 7 + 3) / 4;  // dwords of own bytes
-      u32 own[NOWN];
-      {
-        u32 const w = s >> 2, sh = s & 3u;
-        u32 aw[NOWN + 1];
-#pragma unroll
-        for (u32 k = 0; k <= NOWN; k++) aw[k] = in32[w + k];
-#pragma unroll
-        for (u32 k = 0; k < NOWN; k++) own[k] = __builtin_amdgcn_alignbyte(aw[k + 1], aw[k], sh);
+    // ---- match lengths of the window's positions (and of the two lookahead positions),
+    // while the inserter waves build the next window's candidates
+    {
+      LenCarry cy = {0u, 0u, 0u, 0u};
+      for (u32 r = r_hi; r-- > r_lo;) len_round(in32, ci, hm, r, wsb, we, n, lim, lane, cy);
+      if (wave == 0 && lane < 2) {
+        u32 const p = we + lane;
+        u32 const cw = ci[cidx(ZH_WINDOW + lane)];
+        ci[cidx(ZH_WINDOW + lane)] = info_one(in32, p, cw, n, lim, p < n);
       }
-#pragma unroll
-      for (u32 j = 0; j < SB; j++) {
-        u32 const p = s + j;
-        bool const v = p < se && p < lim;
-        u32 const cw = ci[cidx(cbase + j)];
-        cv[j] = v ? cw : 0u;
-        u32 const q = j >> 2, r = j & 3u;
-        u32 const olo = r ? __builtin_amdgcn_alignbyte(own[q + 1], own[q], r) : own[q];
-        u32 const ohi = r ? __builtin_amdgcn_alignbyte(own[q + 2], own[q + 1], r) : own[q + 1];
-        u32 const cL = cv[j] & 0xFFFFu, cS = cv[j] >> 16;
-        // wave-uniform skips (no lane has a candidate: rare matches), branch-free inside
-        u32 xL = 0, xS = 0;
-        if (__ballot(cL != 0)) {
-          u32 const t = prefix8(in32, cL ? cL - 1 : 0u, olo, ohi);
-          xL = cL ? t : 0u;
-        }
-        bool const hasS = cS && cS != cL;
-        if (__ballot(hasS)) {
-          u32 const t = prefix8(in32, hasS ? cS - 1 : 0u, olo, ohi);
-          xS = hasS ? t : 0u;
-        }
-        plp |= xL << (4 * j);
-        psp |= xS << (4 * j);
-      }
-#define PL(j) ((plp >> (4 * (j))) & 15u)
-#define PS(j) ((psp >> (4 * (j))) & 15u)
-      // (2) chains: a candidate with 8 matching bytes that continues a previous-position
-      //     candidate with the same offset (also 8 matching) is a follower; else a head
-      //     Bit-parallel over the thread's SB positions (bit j = position j), no branches:
-      //     e = 8 matching bytes (nibble bit 3 of the packed prefix; 0 without a
-      //     candidate), continuation = candidate == previous position's candidate + 1.
-      auto nib8 = [](u32 pk) {  // bit j = nibble j == 8
-        u32 r = 0;
-#pragma unroll
-        for (u32 j = 0; j < SB; j++) r |= ((pk >> (4 * j + 3)) & 1u) << j;
-        return r;
-      };
-      u32 const eL = nib8(plp), eS = nib8(psp);
-      u32 dL = 0, dS = 0, fromSL = 0, fromSS = 0, heads = 0;  // heads: bit j = L, bit 8 + j = S
-      if (__ballot((eL | eS) != 0)) {  // (wave-uniform skip: no 8-byte match in the wave)
-        u32 mLL = 0, mLS = 0, mSL = 0, mSS = 0;  // bit j: cX_j == cY_{j-1} + 1
-#pragma unroll
-        for (u32 j = 1; j < SB; j++) {
-          u32 const cL = cv[j] & 0xFFFFu, cS = cv[j] >> 16, pL1 = (cv[j - 1] & 0xFFFFu) + 1, pS1 = (cv[j - 1] >> 16) + 1;
-          mLL |= cL == pL1 ? 1u << j : 0u;
-          mLS |= cL == pS1 ? 1u << j : 0u;
-          mSL |= cS == pL1 ? 1u << j : 0u;
-          mSS |= cS == pS1 ? 1u << j : 0u;
-        }
-        u32 const peL = eL << 1, peS = eS << 1;
-        u32 const fLL = eL & peL & mLL, fLS = eL & ~fLL & peS & mLS;
-        u32 const fSL = eS & peL & mSL, fSS = eS & ~fSL & peS & mSS;
-        dL = fLL | fLS; dS = fSL | fSS; fromSL = fLS; fromSS = fSS;
-        heads = (eL & ~dL) | ((eS & ~dS) << 8);
-      }
-      // (3) extend the heads, compacted across the wave: heads are ranked in (lane, bit)
-      //     order and handed out 64 at a time, one per lane (wave-private LDS slots;
-      //     a wave's LDS operations execute in order, so no barrier is needed).  The
-      //     extension goes back into the head position's own cinfo word (byte 0 for L,
-      //     byte 2 for S: the half that was just consumed), read back in (4).
-      {
-        u32 const nh = __builtin_popcount(heads);
-        u32 const inc = wave_scan_incl(nh);
-        u32 const hbase = inc - nh, htot = __builtin_amdgcn_readlane(inc, 63);
-        u32 *hb = hbuf + (tid >> 6) * HB_STRIDE;
-        for (u32 c0 = 0; c0 < htot; c0 += 64) {
-          // branch-free scatter: slots not in this pass (or not heads) write the junk slot
-          u32 r = hbase - c0;
-#pragma unroll
-          for (u32 k = 0; k < 2 * SB; k++) {
-            u32 const bit = k < SB ? k : 8 + (k - SB);
-            u32 const h = (heads >> bit) & 1u;
-            hb[h && r < 64u ? r : 64u] = (cbase + (k < SB ? k : k - SB)) | (k < SB ? 0u : 0x8000u);
-            r += h;
-          }
-          __asm__ volatile("" ::: "memory");
-          if (c0 + lane < htot) {
-            u32 const e = hb[lane];  // window index (13 bits) | S flag (bit 15)
-            u32 const w = e & 0x1FFFu, sf = e >> 15;
-            u32 const cw = ci[cidx(w)];
-            u32 const c = sf ? cw >> 16 : cw & 0xFFFFu;
-            ci8[4 * cidx(w) + 2 * sf] = (u8)ext_head(in32, wsb + w, c - 1, n);
-          }
-          __asm__ volatile("" ::: "memory");
-        }
-      }
-      // (4) lengths in position order; E = exact prefix below 8, the head's extension,
-      //     or the predecessor's E - 1; capped length = min(E, 64, n - p)
-      u32 EL = 0, ES = 0;
-#pragma unroll
-      for (u32 j = 0; j < SB; j++) {
-        u32 const p = s + j;
-        u32 const cL = cv[j] & 0xFFFFu, cS = cv[j] >> 16;
-        u32 const capj = min((u32)ZH_MAX_MATCH, n - min(p, n));
-        u32 const hx = ci[cidx(cbase + j)];  // head extensions from (3)
-        // selects only (no divergent branches: exec-mask work on the scalar unit)
-        u32 const eFL = ((fromSL >> j) & 1u) ? ES : EL, eFS = ((fromSS >> j) & 1u) ? ES : EL;
-        u32 nL = ((heads >> j) & 1u) ? (hx & 255u) : PL(j);
-        nL = ((dL >> j) & 1u) ? eFL - 1u : nL;
-        u32 nS = ((heads >> (8 + j)) & 1u) ? ((hx >> 16) & 255u) : PS(j);
-        nS = ((dS >> j) & 1u) ? eFS - 1u : nS;
-        nS = (cS && cS == cL) ? nL : nS;
-        EL = nL; ES = nS;
-        u32 const rL = min(nL, capj), rS = min(nS, capj);
-        u32 const lL = (cL && rL >= ZH_MIN_MATCH_LONG) ? rL : 0u;
-        u32 const lS = (cS && rS >= ZH_MIN_MATCH_SHORT) ? rS : 0u;
-        bool const useL = lL && lL >= lS;
-        u32 const ml = useL ? lL : lS, cm = useL ? cL : cS;
-        u32 const v = ml ? ((p - (cm - 1u)) << 8) | ml : 0u;
-        ci[p < se ? cidx(cbase + j) : ZH_WINDOW + 2 + j] = v;  // (past the run: junk slots)
-      }
-      if (tid == NB && we >= n) ci[cidx(ZH_WINDOW)] = 0;          // no position after the block
-      if (tid == NB && we + 1 >= n) ci[cidx(ZH_WINDOW + 1)] = 0;
-#undef PL
-#undef PS
     }
-    ZH_STAMP(st_Bw);
-#ifdef ZH_STAMPS
-    if (lane == 0) atomicMax(&misc[8], (u32)(__builtin_amdgcn_s_memtime() - tP));
-#endif
-    if (lane == 0) atomicAdd(&misc[MISC_ARR], 1u);
-    __syncthreads();  // R
     ZH_STAMP(st_B);
-#ifdef ZH_STAMPS
-    if (tid == 0) { st_Bmax += misc[8]; st_Imax += misc[9]; misc[8] = 0; misc[9] = 0; }
-#endif
-    u32 const info_ahead = __builtin_amdgcn_readfirstlane(ci[cidx(ZH_WINDOW)]);
-    u32 const info_ahead2 = LAZY2 ? __builtin_amdgcn_readfirstlane(ci[cidx(ZH_WINDOW + 1)]) : 0u;
-
-    // ---- parse.  Lanes = positions (PR rounds of the 896 worker lanes); each wave's 64
-    // lanes are one parse segment of 64 positions.  step(p) = next position the greedy /
-    // lazy-1 parse visits after p; pointer doubling inside the segment (ds_bpermute)
-    // gives X_k = 2^k steps for k < 6 and the segment exit of every position.
-    u32 const wn = we - wsb;
-    u32 const la = info_ahead;  // match info of position `we` (lazy rule at the window end)
-    u32 xk[PR][6];              // [round][k]: X_{2^k}, relative to the segment start
-    u32 infr[PR];               // match info of positions where the parse takes a match
-#pragma unroll
-    for (u32 rr = 0; rr < PR; rr++) {
-      u32 const i = INS_TID * rr + tid;
-      u32 X[7];
-      infr[rr] = parse_steps<LAZY2>(ci, i, wn, la, info_ahead2, lane, X);
-#pragma unroll
-      for (u32 k = 0; k < 6; k++) xk[rr][k] = X[k];
-      exb[i < wn ? i : (u32)ZH_WINDOW] = (u8)X[6];  // (past the window: junk byte)
-    }
     if (lane == 0) atomicAdd(&misc[MISC_ARR], 1u);
-    __syncthreads();  // X: exits of all positions
+    __syncthreads();  // R: match info of the window
     ZH_STAMP(st_X);
-    // Jacobi fixed point of the 64 segment entries (wave 0, lane = segment, no barrier
-    // needed): entry(t) = max(start(t), exit of segment t-1 from its entry) == the
-    // serial parse once no entry changes
-    if (tid < 64) {
-      u32 const S = wsb + 64 * lane;
-      u32 const SE = min(S + 64, we);
-      u32 entry = lane == 0 ? max(wsb, e_in) : S;
-      u32 ex = entry;
+
+    // ---- the parse (wave 0, lanes = segments) and the window's match list
+    u32 *mlist = (u32 *)(smem + OFF_ML), *mext = (u32 *)(smem + OFF_ME), *mrec = (u32 *)(smem + OFF_MR);
+    u32 const e0 = e_in - wsb;  // first parsed position (< 64 except in the window holding `pre`)
+    if (wave == 0) {
+      u32 const wn = we - wsb;
+      u32 const S = 64 * lane, SE = min(S + 64, wn);
+      u64 const hmk = hm[lane];
+      u32 entry = lane == 0 ? e0 : max(S, e0), ex = entry;
+      u64 LM = 0, MM = 0;
+      seg_walk<LAZY2>(ci, hmk, S, SE, entry, true, LM, MM, ex);
+      // Jacobi rounds: a segment's entry is its predecessor's exit
       for (;;) {
-        ex = entry < SE ? S + exb[64 * lane + (entry - S)] : entry;
         u32 const pe = wave_shr1(ex);
-        u32 const ne = lane == 0 ? max(wsb, e_in) : max(S, pe);
+        u32 const ne = lane == 0 ? e0 : max(pe, e0);
         bool const ch = ne != entry;
-        entry = ne;
 #ifdef ZH_STAMPS
         st_rounds++;
 #endif
         if (!__ballot(ch)) break;
+        seg_walk<LAZY2>(ci, hmk, S, SE, ne, ch, LM, MM, ex);
+        entry = ne;
       }
-      segx[lane] = entry;
-      if (lane == ((wn - 1) >> 6)) segx[64] = ex;  // the window's exit = next window's entry
-    }
-    if (lane == 0) atomicAdd(&misc[MISC_ARR], 1u);
-    __syncthreads();  // J: converged segment entries
-    ZH_STAMP(st_J);
-    u32 const e_out = __builtin_amdgcn_readfirstlane(segx[64]);
-
-    // ---- emission, lanes = positions: a position is on the parse path iff binary
-    // lifting from its segment's entry (X_32 .. X_1) lands on it; scans of the
-    // take/literal flags give each record's and literal's slot
-    u32 fl[PR];    // bit 0 literal, bit 1 match start
-#pragma unroll
-    for (u32 rr = 0; rr < PR; rr++) {
-      u32 const i = INS_TID * rr + tid;
-      u32 const sb = i & ~63u;
-      u32 cur = segx[min(i >> 6, 63u)] - (wsb + sb);  // >= 64 when the segment is skipped
-      if (__ballot(infr[rr] != 0)) {
-#pragma unroll
-        for (int k = 5; k >= 0; k--) {
-          u32 const y = bperm(xk[rr][k], min(cur, 63u));
-          if (cur <= lane && y <= lane) cur = y;
+      ZH_STAMP(st_J);
+      u32 const ns = (u32)__popcll(MM);
+      u32 const is = wave_scan_incl(ns);
+      lmk[lane] = LM;
+      u64 mm = MM;
+      u32 k = is - ns;
+      while (__ballot(mm != 0)) {
+        if (mm) {
+          mlist[k++] = S + ctz64(mm);
+          mm &= mm - 1ull;
         }
-      } else {  // all literals: every position from the entry on is visited
-        cur = cur <= lane ? lane : cur;
       }
-      bool const vis = i < wn && cur == lane;
-      fl[rr] = vis ? (infr[rr] ? 2u : 1u) : 0u;
-    }
-    u32 lcnt[PR], scnt[PR];
-#pragma unroll
-    for (u32 rr = 0; rr < PR; rr++) {
-      u64 const ml = __ballot(fl[rr] & 1u), ms = __ballot(fl[rr] & 2u);
-      lcnt[rr] = __builtin_amdgcn_mbcnt_hi((u32)(ml >> 32), __builtin_amdgcn_mbcnt_lo((u32)ml, 0u));
-      scnt[rr] = __builtin_amdgcn_mbcnt_hi((u32)(ms >> 32), __builtin_amdgcn_mbcnt_lo((u32)ms, 0u));
-      if (lane == 0) wpart[rr * NWW + (tid >> 6)] = (u32)__popcll(ml) | ((u32)__popcll(ms) << 16);
+      if (lane == 63) {
+        misc[1] = is;
+        misc[2] = wsb + ex;
+      }
     }
     if (lane == 0) atomicAdd(&misc[MISC_ARR], 1u);
-    __syncthreads();  // E1: per-wave counts (cinfo is free for the inserters from here on)
+    __syncthreads();  // W1: literal masks and the match list (cinfo stays: match info)
     ZH_STAMP(st_E1);
-    if (tid < 64) {   // exclusive scan of the PR*NWW (round, wave) counts, in position order
-      u32 carry = 0;
-#pragma unroll
-      for (u32 c0 = 0; c0 < PR * NWW; c0 += 64) {
-        u32 const v = c0 + lane < PR * NWW ? wpart[c0 + lane] : 0u;
-        u32 const inc = wave_scan_incl(v);
-        if (c0 + lane < PR * NWW) wpart[WP_OFF + c0 + lane] = carry + inc - v;
-        carry += __builtin_amdgcn_readlane(inc, 63);
+    u32 const nm = __builtin_amdgcn_readfirstlane(misc[1]);
+    // ---- catch-up, lanes = matches: a match's lower bound is the end of the match before it
+    // (the window's first parsed position for the first); the bytes it takes back are no
+    // longer literals
+    for (u32 j0 = 64 * wave; j0 < nm; j0 += 64 * NWW) {
+      u32 const j = j0 + lane;
+      bool const v = j < nm;
+      u32 const ms = v ? mlist[j] : 0u, inf = ci[cidx(ms)];
+      u32 const pm = (v && j) ? mlist[j - 1] : 0u;
+      u32 const lo = (v && j) ? pm + (ci[cidx(pm)] & 255u) : e0;
+      u32 const e = catch_up(in32, wsb + ms, inf >> 8, wsb + lo, v);
+      if (v) {
+        mext[j] = ms - e;
+        mrec[j] = ((inf & 255u) + e) | ((inf >> 8) << 13);
       }
-      if (tid == 0) wpart[WP_TOT] = carry;
+      if (e) {
+        for (u32 g = (ms - e) >> 6; g <= (ms - 1) >> 6; g++) {
+          u32 const a = max(ms - e, 64 * g) - 64 * g, bnd = min(ms - 64 * g, 64u);
+          atomicAnd((unsigned long long *)&lmk[g], ~bit_range(a, bnd));
+        }
+      }
     }
     if (lane == 0) atomicAdd(&misc[MISC_ARR], 1u);
-    __syncthreads();  // E2: offsets
-#pragma unroll
-    for (u32 rr = 0; rr < PR; rr++) {
-      u32 const i = INS_TID * rr + tid;
-      u32 const off = wpart[WP_OFF + rr * NWW + (tid >> 6)];
-      u32 const li = (off & 0xFFFFu) + lcnt[rr], si = (off >> 16) + scnt[rr];
-      if (fl[rr] & 1u) lit_out[nlit_tot + li] = in[wsb + i];
-      if (fl[rr] & 2u) seq_out[nseq_tot + si] = (u64)(nlit_tot + li) | ((u64)(infr[rr] & 255u) << 17) | ((u64)(infr[rr] >> 8) << 25);
+    __syncthreads();  // W2: final literal masks and match records (cinfo is free for the inserters)
+    ZH_STAMP(st_E2);
+    // literal offsets of the 64 segments (every wave the same scan: lane = segment)
+    u64 const lmg = lmk[lane];
+    u32 const lc = (u32)__popcll(lmg), lincl = wave_scan_incl(lc), lb = lincl - lc;
+    u32 const nlw = lane_value(lincl, 63);
+    // ---- sequence records, lanes = matches: cumLit | ml << 17 | off << 32
+    for (u32 j0 = 64 * wave; j0 < nm; j0 += 64 * NWW) {
+      u32 const j = j0 + lane;
+      bool const v = j < nm;
+      u32 const st = v ? mext[j] : 0u, mr = v ? mrec[j] : 0u, g = st >> 6;
+      u32 const lbg = bperm(lb, g);  // (all lanes: ds_bpermute sources)
+      u64 const lg = lmk[g];
+      u32 const cum = nlit_tot + lbg + (u32)__popcll(lg & ((1ull << (st & 63)) - 1ull));
+      if (v) seq_out[nseq_tot + j] = (u64)cum | ((u64)(mr & 0x1FFFu) << 17) | ((u64)(mr >> 13) << 32);
     }
-    u32 const total = __builtin_amdgcn_readfirstlane(wpart[WP_TOT]);
-    nseq_tot += total >> 16;
-    nlit_tot += total & 0xFFFFu;
-    e_in = e_out;
+    // ---- literals, lanes = positions
+    for (u32 r = r_lo; r < r_hi; r++) {
+      u64 const lm = ((u64)(u32)__builtin_amdgcn_readfirstlane((u32)(lmk[r] >> 32)) << 32) | (u32)__builtin_amdgcn_readfirstlane((u32)lmk[r]);
+      u32 const lbr = lane_value(lb, r);
+#ifdef ZH_K1_DEBUG
+      if (lane == 0) {  // diagnostic build: the masks the literal phase sees, per window and segment
+        u32 *dbgw = (u32 *)(lit_out + ZH_BLOCK_MAX) + 4 * (64 * ((wsb - wstart) / ZH_WINDOW) + r);
+        dbgw[0] = (u32)lm; dbgw[1] = (u32)(lm >> 32); dbgw[2] = lbr; dbgw[3] = nlit_tot;
+      }
+#endif
+      if ((lm >> lane) & 1ull) {
+        u32 const rank = __builtin_amdgcn_mbcnt_hi((u32)(lm >> 32), __builtin_amdgcn_mbcnt_lo((u32)lm, 0u));
+        lit_out[nlit_tot + lbr + rank] = in[wsb + 64 * r + lane];
+      }
+    }
+    nlit_tot += nlw;
+    nseq_tot += nm;
+    e_in = __builtin_amdgcn_readfirstlane(misc[2]);
     ZH_STAMP(st_E);
   }
   if (tid == 0) { meta[0] = nseq_tot; meta[1] = nlit_tot; meta[2] = 0; }
@@ -1022,3 +1017,45 @@ void lz_launch(const ZhBlockDesc *d_descs, u32 nblocks, ZhWorkspace ws, bool laz
   else hipLaunchKernelGGL(zh_lz_kernel, dim3(grid), dim3(K1_THREADS), K1_LDS, stream, d_descs, nblocks, ws);
 }
 }  // namespace zh
+
+// Test hook (tests/test_gpu_k1.py, not a product entry point): K1 alone over single-block items
+// in[i * stride, + sizes[i]) (each <= ZH_BLOCK_MAX, no dictionary), its raw output copied back:
+// per item ZH_SEQ_CAP records, ZH_LIT_BYTES of the literal area and meta {nseq, nlit, rle}.
+extern "C" int zh_test_lz(const u8 *d_in, u32 nitems, u32 stride, const u32 *h_sizes, int lazy2, u64 *h_recs, u8 *h_lits, u32 *h_meta) {
+  if (!nitems) return 0;
+  std::vector<ZhBlockDesc> descs(nitems);
+  for (u32 i = 0; i < nitems; i++) {
+    if (h_sizes[i] > ZH_BLOCK_MAX) return 2;
+    ZhBlockDesc d{};
+    d.src = d_in + (size_t)i * stride;
+    d.n = h_sizes[i];
+    d.frame_size = h_sizes[i];
+    d.item = i;
+    d.flags = ZH_F_FIRST | ZH_F_LAST | ZH_F_DIRECT;
+    descs[i] = d;
+  }
+  ZhBlockDesc *dd = nullptr;
+  u8 *base = nullptr;
+  u32 *ctr = nullptr;
+  int rc = 0;
+  if (zh::lz_init() != hipSuccess || hipMalloc(&dd, sizeof(ZhBlockDesc) * nitems) != hipSuccess ||
+      hipMalloc(&base, (size_t)ZH_WS_BLOCK_BYTES * nitems) != hipSuccess || hipMalloc(&ctr, 4) != hipSuccess) {
+    rc = 1;
+  } else {
+    (void)hipMemcpy(dd, descs.data(), sizeof(ZhBlockDesc) * nitems, hipMemcpyHostToDevice);
+    (void)hipMemset(ctr, 0, 4);
+    ZhWorkspace ws{base, ctr, nullptr, 0u};
+    zh::lz_launch(dd, nitems, ws, lazy2 != 0, nullptr);
+    if (hipDeviceSynchronize() != hipSuccess) rc = 1;
+    for (u32 i = 0; i < nitems && !rc; i++) {
+      u8 *const b = base + (size_t)i * ZH_WS_BLOCK_BYTES;
+      (void)hipMemcpy(h_recs + (size_t)i * ZH_SEQ_CAP, b, ZH_SEQ_BYTES, hipMemcpyDeviceToHost);
+      (void)hipMemcpy(h_lits + (size_t)i * ZH_LIT_BYTES, b + ZH_SEQ_BYTES, ZH_LIT_BYTES, hipMemcpyDeviceToHost);
+      (void)hipMemcpy(h_meta + 4 * i, b + ZH_SEQ_BYTES + ZH_LIT_BYTES, 16, hipMemcpyDeviceToHost);
+    }
+  }
+  (void)hipFree(dd);
+  (void)hipFree(base);
+  (void)hipFree(ctr);
+  return rc;
+}

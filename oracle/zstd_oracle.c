@@ -856,9 +856,18 @@ size_t orc_lz_parse_pre(const u8 *src, u32 pre, u32 n, orc_seq_t *seq, u32 *last
       defer = match_gain(len, off, p + 1) > g0 + 4 || match_gain(len, off, p + 2) > g0 + 7;
     } else defer = len[p + 1] > len[p];
     if (defer) { p++; continue; }
-    u32 ll = p - anchor;
-    if (ns && ll == 0 && seq[ns - 1].off == off[p]) seq[ns - 1].ml += len[p]; /* continuation merge */
-    else { seq[ns].ll = ll; seq[ns].ml = len[p]; seq[ns].off = off[p]; ns++; }
+    /* catch-up (libzstd 1.4.9 ZSTD_compressBlock_doubleFast_generic / lazy_generic "catch
+     * up"): the match grows backwards over the literals since the last sequence while the
+     * bytes before it equal the bytes before its source, bounded by the start of the
+     * ZH_WINDOW-position parse window holding p (the device parses window by window; windows
+     * start at multiples of ZH_WINDOW of the staged buffer).  The parse itself continues at
+     * p + len[p] either way. */
+    u32 ms = p, ml = len[p];
+    u32 const of = off[p], wlo = p & ~(u32)(ZH_WINDOW - 1), lo = anchor > wlo ? anchor : wlo;
+    while (ms > lo && ms > of && src[ms - 1] == src[ms - 1 - of]) { ms--; ml++; }
+    u32 ll = ms - anchor;
+    if (ns && ll == 0 && seq[ns - 1].off == of) seq[ns - 1].ml += ml; /* continuation merge */
+    else { seq[ns].ll = ll; seq[ns].ml = ml; seq[ns].off = of; ns++; }
     p += len[p];
     anchor = p;
   }

@@ -1,0 +1,123 @@
+"""GPU parity of the LZ stage alone: K1's raw output (sequence records + literal bytes, read
+back through the library's zh_test_lz hook) equals the oracle's parse
+(oracle/zstd_oracle.c orc_lz_parse: tile-lagged dual hash, lazy-1 parse, catch-up) on the
+same inputs.  Finer-grained than the frame tests: a mismatch names the first differing
+sequence.  K1's records carry a cumulative literal count; consecutive same-offset records
+with no literals between them are merged (K2 merges them the same way)."""
+import ctypes
+
+import numpy as np
+import pytest
+
+import zh_testlib as T
+
+pytestmark = pytest.mark.gpu
+
+SEQ_CAP = 13120
+BLOCK = 65536
+LIT_AREA = 122880  # ZH_LIT_BYTES
+
+
+def k1_raw(datas):
+    import torch
+
+    import cuda_zstd
+
+    L = cuda_zstd.lib()
+    n = len(datas)
+    stride = BLOCK
+    buf = np.zeros(n * stride, dtype=np.uint8)
+    for i, d in enumerate(datas):
+        buf[i * stride:i * stride + len(d)] = d
+    dev = torch.from_numpy(buf).cuda()
+    sizes = np.array([len(d) for d in datas], dtype=np.uint32)
+    recs = np.zeros(n * SEQ_CAP, dtype=np.uint64)
+    lits = np.zeros(n * LIT_AREA, dtype=np.uint8)
+    meta = np.zeros(n * 4, dtype=np.uint32)
+    f = L.zh_test_lz
+    f.restype = ctypes.c_int
+    f.argtypes = [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
+                  ctypes.c_void_p]
+    torch.cuda.synchronize()
+    rc = f(dev.data_ptr(), n, stride, sizes.ctypes.data, 0, recs.ctypes.data, lits.ctypes.data, meta.ctypes.data)
+    assert rc == 0
+    out = []
+    for i in range(n):
+        ns, nl, rle = (int(x) for x in meta[4 * i:4 * i + 3])
+        r = recs[i * SEQ_CAP:i * SEQ_CAP + ns]
+        out.append((r, lits[i * LIT_AREA:i * LIT_AREA + nl].tobytes(), rle))
+    k1_raw.area = lits
+    return out
+
+
+def merged(recs):
+    """K1 records -> (ll, ml, off) with same-offset continuations merged, + literal count"""
+    seqs, prev = [], 0
+    for v in recs:
+        v = int(v)
+        cum, ml, off = v & 0x1FFFF, (v >> 17) & 0x7FFF, (v >> 32) & 0x1FFFF
+        ll = cum - prev
+        prev = cum
+        if seqs and ll == 0 and seqs[-1][2] == off:
+            seqs[-1][1] += ml
+        else:
+            seqs.append([ll, ml, off])
+    return [tuple(s) for s in seqs], prev
+
+
+def oracle_parse(d):
+    O = T.oracle()
+    d = np.ascontiguousarray(d, dtype=np.uint8)
+    seq = (ctypes.c_uint32 * (3 * (len(d) // 5 + 2)))()
+    last = ctypes.c_uint32(0)
+    ns = O.orc_lz_parse(d.ctypes.data_as(ctypes.c_void_p), ctypes.c_uint32(len(d)), seq, ctypes.byref(last))
+    return [(seq[3 * i], seq[3 * i + 1], seq[3 * i + 2]) for i in range(ns)], last.value
+
+
+def expected_literals(d, seqs, last):
+    out, pos = bytearray(), 0
+    for ll, ml, _ in seqs:
+        out += bytes(d[pos:pos + ll])
+        pos += ll + ml
+    out += bytes(d[pos:pos + last])
+    return bytes(out)
+
+
+def _compare(datas, names):
+    got = k1_raw(datas)
+    for (recs, lits, rle), d, nm in zip(got, datas, names):
+        if rle:
+            assert len(d) >= 2 and (d == d[0]).all(), f"{nm}: RLE flag on a non-RLE block"
+            continue
+        want, last = oracle_parse(d)
+        have, cum_end = merged(recs)
+        if have != want:
+            k = next((i for i, (a, b) in enumerate(zip(have, want)) if a != b), min(len(have), len(want)))
+            pos = sum(a + b for a, b, _ in want[:k])
+            raise AssertionError(f"{nm}: sequence {k} (position {pos}) GPU {have[k:k + 3]} oracle {want[k:k + 3]}; "
+                                 f"counts {len(have)} vs {len(want)}")
+        exp = expected_literals(d, want, last)
+        if lits != exp:
+            k = next((i for i, (a, b) in enumerate(zip(lits, exp)) if a != b), min(len(lits), len(exp)))
+            raise AssertionError(f"{nm}: literal bytes differ at literal {k} of {len(lits)} (oracle {len(exp)}): "
+                                 f"GPU {lits[k:k + 12].hex()} oracle {exp[k:k + 12].hex()}")
+
+
+def test_k1_corpora_vs_oracle():
+    names, datas = [], []
+    for kname in ("mix", "text", "source", "csv", "exe", "sensor", "json", "random", "sym16"):
+        for i in range(3):
+            names.append(f"{kname}[{i}]")
+            datas.append(T.gen(T.KINDS[kname], 1, 0x5EED0003, BLOCK, first=i))
+    _compare(datas, names)
+
+
+def test_k1_special_and_ragged_vs_oracle():
+    items = T.special_inputs()
+    names = sorted(k for k in items if 0 < len(items[k]) <= BLOCK)
+    datas = [items[k] for k in names]
+    rng = np.random.default_rng(5)
+    for n in (1, 7, 63, 64, 65, 4095, 4096, 4097, 8191, 12345, 40000, 65535):
+        names.append(f"text{n}")
+        datas.append(T.gen(T.DG_TEXT, 1, int(rng.integers(1 << 30)), 65536)[:n].copy())
+    _compare(datas, names)
