@@ -61,6 +61,7 @@ constexpr u32 TILES = ZH_WINDOW / ZH_TILE;  // 32 tiles per window
 constexpr u32 TPL = ZH_TILE / 64;           // positions per inserter lane per tile
 constexpr u32 NCR = TILES * TPL / 2;        // candidate registers per inserter lane (u16 pairs)
 static_assert(NSEG == 64, "one walk lane per segment");
+static_assert(INS_TID == 896 && ZH_WINDOW == 4096, "round split: 8 waves x 5 + 6 waves x 4 rounds");
 static_assert(ZH_WINDOW % ZH_TILE == 0 && ZH_TILE % 64 == 0 && TILES * TPL % 2 == 0, "tiles tile windows");
 
 constexpr u32 HL_SIZE = 1u << ZH_HASH_LOG_LONG;
@@ -84,11 +85,19 @@ constexpr u32 MISC_ARR = 12;  // misc[12]: worker-wave barrier arrivals (cumulat
 static_assert(K1_LDS <= 163840 - 256, "K1 LDS budget");
 static_assert(OFF_TL % 16 == 0 && OFF_CI % 16 == 0 && OFF_HM % 16 == 0, "alignment");
 
-__device__ __forceinline__ u32 hash_long(u64 v) {
-  return (u32)((v * ZH_PRIME_LONG) >> (64 - ZH_HASH_LOG_LONG));
+// Hashes of include/zstd_hip_params.h: full-rate v_mad_u32_u24 sums (the 24-bit multiplies
+// take the low 24 bits of each operand, so byte groups need no masking but the short hash's
+// bytes 3-4)
+__device__ __forceinline__ u32 hash_long(u32 lo, u32 hi) {
+  u32 t = __umul24(lo, ZH_HK_L0);
+  t += __umul24(__builtin_amdgcn_alignbyte(hi, lo, 3), ZH_HK_L1);
+  t += __umul24(hi >> 16, ZH_HK_L2);
+  return t >> (32 - ZH_HASH_LOG_LONG);
 }
-__device__ __forceinline__ u32 hash_short(u64 v) {
-  return (u32)(((v << 24) * ZH_PRIME_SHORT) >> (64 - ZH_HASH_LOG_SHORT));
+__device__ __forceinline__ u32 hash_short(u32 lo, u32 hi) {
+  u32 t = __umul24(lo, ZH_HK_S0);
+  t += __umul24(__builtin_amdgcn_alignbyte(hi, lo, 3) & 0xFFFFu, ZH_HK_S1);
+  return t >> (32 - ZH_HASH_LOG_SHORT);
 }
 
 // 8 bytes at p from LDS as (lo, hi): three aligned dwords + v_alignbyte
@@ -138,8 +147,7 @@ __device__ __forceinline__ u32 ext8(const u32 *in32, u32 p, u32 c, bool act) {
 
 template <bool LONG>
 __device__ __forceinline__ u32 hash_of(u32 lo, u32 hi) {
-  u64 const v = ((u64)hi << 32) | lo;
-  return LONG ? hash_long(v) : hash_short(v);
+  return LONG ? hash_long(lo, hi) : hash_short(lo, hi);
 }
 
 // Inserter wave: the tiles of window [wsb, we) against one table (u16 entries = position
@@ -334,11 +342,15 @@ __device__ __forceinline__ u64 bit_range(u32 a, u32 b) {
 }
 
 // ---- match lengths, lanes = positions -------------------------------------------------------
-// Chain state carried from a round to the one below it (rounds run from high positions to low):
-// the candidates and capped common prefixes of the position just above the round.
-struct LenCarry {
-  u32 cL, cS, lL, lS;
-};
+// A worker wave takes a span of consecutive 64-position rounds in three passes:
+//  A  (rounds high to low) per position and candidate the common prefix of the first 8 bytes
+//     and whether p+1's candidate continues p's (then lcp(p) = 1 + lcp(p+1)); chain ends
+//     with 8 matching bytes go to the wave's extension queue (flushed 64 at a time);
+//  B  the queued chain ends extended, lanes = queue entries, results into their cinfo byte;
+//  C  (rounds high to low) lengths from the chain structure -> match info in place.
+constexpr u32 MAX_RW = 5;   // rounds per worker wave
+constexpr u32 XQ_CAP = 192; // extension queue entries per worker wave (u16: window index | S << 15)
+static_assert(NWW * XQ_CAP * 2 <= 3 * 4 * ML_CAP, "the extension queues alias the match lists");
 
 // Length of position p's candidate from the chain structure: T = ballot of the chain ends
 // (lanes whose lcp is their own: fewer than 8 bytes, or the next position does not continue
@@ -351,54 +363,96 @@ __device__ __forceinline__ u32 chain_lcp(u64 T, u32 e, u32 carry, u32 lane) {
   return min((u32)ZH_MAX_MATCH, q + (rest ? v : carry));
 }
 
-// One round of 64 consecutive positions (window indices 64 r + lane): candidates in cinfo ->
-// match info (off << 8 | len, 0 = none) in place + the round's has-match mask.  Semantics of
+// Pass B: extend queue entries [0, k) (k <= 64) of xq, one per lane; the extension (<= 64)
+// goes to byte 0 (long candidate) or byte 2 (short) of the position's cinfo word.
+__device__ __forceinline__ void xq_flush(const u32 *in32, u32 *ci, const u16 *xq, u32 k, u32 wsb, u32 lane) {
+  bool const act = lane < k;
+  u32 const e = act ? xq[lane] : 0u;
+  u32 const i = e & 0x1FFFu, sh = (e >> 15) * 16u;
+  u32 const c = (ci[cidx(i)] >> sh) & 0xFFFFu;
+  u32 const x = ext8(in32, act ? wsb + i : 0u, act && c ? c - 1u : 0u, act);
+  if (act) ((u8 *)ci)[4 * cidx(i) + (sh >> 3)] = (u8)x;
+}
+
+// Flags of a position after pass A
+enum : u32 { LF_FL = 1u << 8, LF_FS = 1u << 9, LF_XL = 1u << 10, LF_XS = 1u << 11, LF_SL = 1u << 12 };
+
+// The match lengths of rounds [r_lo, r_hi) (r_hi - r_lo <= MAX_RW): candidates in cinfo ->
+// match info (off << 8 | len, 0 = none) in place + the rounds' has-match masks.  Semantics of
 // oracle/zstd_oracle.c orc_lz_match_info: lcp capped at ZH_MAX_MATCH and at the block end,
 // long candidates from 8 bytes, short from 5, the longer (long on ties).
-__device__ __forceinline__ void len_round(const u32 *in32, u32 *ci, u64 *hm, u32 r, u32 wsb, u32 we, u32 n, u32 lim, u32 lane, LenCarry &cy) {
-  u32 const i = 64 * r + lane, p = wsb + i;
-  bool const hv = p < we && p < lim;
-  u32 const cw = ci[cidx(i)];
-  u32 const cL = hv ? (cw & 0xFFFFu) : 0u, cS = hv ? (cw >> 16) : 0u;
-  u32 lo, hi;
-  ld64u(in32, p, lo, hi);
-  // both prefixes unconditionally (clamped addresses), then selects
-  u32 const tL = prefix8(in32, cL ? cL - 1u : 0u, lo, hi);
-  u32 const tS = prefix8(in32, cS ? cS - 1u : 0u, lo, hi);
-  u32 const pL = cL ? tL : 0u, pS = cS ? tS : 0u;
-  // does p+1's candidate continue p's?  (lane 63: the carried position above the round)
-  u32 cLn = wave_shl1(cL), cSn = wave_shl1(cS);
-  cLn = lane == 63 ? cy.cL : cLn;
-  cSn = lane == 63 ? cy.cS : cSn;
-  bool const fL = pL == 8 && cLn == cL + 1u, fS = pS == 8 && cSn == cS + 1u;
-  // chain ends with 8 matching bytes: extended (a short candidate equal to the long one
-  // takes the long one's extension)
-  bool const xL = pL == 8 && !fL;
-  bool const xS = pS == 8 && !fS && !(cS == cL && xL);
-  u32 eL = pL, eS = pS;
-  if (__ballot(xL)) {
-    u32 const e = ext8(in32, xL ? p : 0u, xL ? cL - 1u : 0u, xL);
-    eL = xL ? e : eL;
+__device__ __forceinline__ void span_lengths(const u32 *in32, u32 *ci, u64 *hm, u16 *xq, u32 r_lo, u32 r_hi, u32 wsb, u32 we, u32 n, u32 lim,
+                                             u32 lane) {
+  u32 cwr[MAX_RW], flg[MAX_RW];
+  u32 ccL = 0, ccS = 0;  // candidates of the position above the round being processed
+  u32 nq = 0;            // queued entries (wave-uniform)
+#pragma unroll
+  for (u32 k = 0; k < MAX_RW; k++) {
+    cwr[k] = 0;
+    flg[k] = 0;
+    if (r_lo + k >= r_hi) continue;
+    u32 const r = r_hi - 1 - k, i = 64 * r + lane, p = wsb + i;
+    bool const hv = p < we && p < lim;
+    u32 const cw0 = ci[cidx(i)];
+    u32 const cw = hv ? cw0 : 0u;
+    u32 const cL = cw & 0xFFFFu, cS = cw >> 16;
+    u32 lo, hi;
+    ld64u(in32, p, lo, hi);
+    u32 const tL = prefix8(in32, cL ? cL - 1u : 0u, lo, hi);
+    u32 const tS = prefix8(in32, cS ? cS - 1u : 0u, lo, hi);
+    u32 const pL = cL ? tL : 0u, pS = cS ? tS : 0u;
+    u32 cLn = wave_shl1(cL), cSn = wave_shl1(cS);
+    cLn = lane == 63 ? ccL : cLn;
+    cSn = lane == 63 ? ccS : cSn;
+    bool const fL = pL == 8 && cLn == cL + 1u, fS = pS == 8 && cSn == cS + 1u;
+    bool const xL = pL == 8 && !fL;
+    bool const sL = cS == cL && xL && pS == 8 && !fS;  // S takes L's extension
+    bool const xS = pS == 8 && !fS && !sL;
+    cwr[k] = cw;
+    flg[k] = pL | (pS << 4) | (fL ? LF_FL : 0u) | (fS ? LF_FS : 0u) | (xL ? LF_XL : 0u) | (xS ? LF_XS : 0u) | (sL ? LF_SL : 0u);
+    ccL = lane_value(cL, 0);
+    ccS = lane_value(cS, 0);
+    // queue the chain ends to extend (L then S), flushing 64 at a time from the top
+    u64 const bL = __ballot(xL), bS = __ballot(xS);
+    u32 const rL = __builtin_amdgcn_mbcnt_hi((u32)(bL >> 32), __builtin_amdgcn_mbcnt_lo((u32)bL, 0u));
+    u32 const rS = __builtin_amdgcn_mbcnt_hi((u32)(bS >> 32), __builtin_amdgcn_mbcnt_lo((u32)bS, 0u));
+    u32 const nL = (u32)__popcll(bL);
+    if (xL) xq[nq + rL] = (u16)i;
+    if (xS) xq[nq + nL + rS] = (u16)(i | 0x8000u);
+    nq += nL + (u32)__popcll(bS);
+    while (nq >= 64) {
+      nq -= 64;
+      xq_flush(in32, ci, xq + nq, 64, wsb, lane);
+    }
   }
-  eS = (cS == cL && xL && pS == 8 && !fS) ? eL : eS;
-  if (__ballot(xS)) {
-    u32 const e = ext8(in32, xS ? p : 0u, xS ? cS - 1u : 0u, xS);
-    eS = xS ? e : eS;
+  if (nq) xq_flush(in32, ci, xq, nq, wsb, lane);
+  // pass C
+  u32 clL = 0, clS = 0;  // lcps of the position above the round
+#pragma unroll
+  for (u32 k = 0; k < MAX_RW; k++) {
+    if (r_lo + k >= r_hi) continue;
+    u32 const r = r_hi - 1 - k, i = 64 * r + lane, p = wsb + i;
+    u32 const f = flg[k], cw = cwr[k];
+    u32 const cL = cw & 0xFFFFu, cS = cw >> 16;
+    u32 const ce = ci[cidx(i)];
+    u32 const pL = f & 15u, pS = (f >> 4) & 15u;
+    u32 const eL = (f & LF_XL) ? (ce & 255u) : pL;
+    u32 const eS = (f & LF_XS) ? ((ce >> 16) & 255u) : ((f & LF_SL) ? eL : pS);
+    u32 const lL = chain_lcp(__ballot(!(f & LF_FL)), eL, clL, lane);
+    u32 const lS = chain_lcp(__ballot(!(f & LF_FS)), eS, clS, lane);
+    clL = lane_value(lL, 0);
+    clS = lane_value(lS, 0);
+    u32 const capj = min((u32)ZH_MAX_MATCH, n - min(p, n));
+    u32 const rL = min(lL, capj), rS = min(lS, capj);
+    u32 const mL = (cL && rL >= ZH_MIN_MATCH_LONG) ? rL : 0u;
+    u32 const mS = (cS && rS >= ZH_MIN_MATCH_SHORT) ? rS : 0u;
+    bool const useL = mL && mL >= mS;
+    u32 const ml = useL ? mL : mS, cm = useL ? cL : cS;
+    u32 const v = ml ? ((p - (cm - 1u)) << 8) | ml : 0u;
+    ci[cidx(i)] = v;
+    u64 const hb = __ballot(v != 0);
+    if (lane == 0) hm[r] = hb;
   }
-  u32 const lL = chain_lcp(__ballot(!fL), eL, cy.lL, lane);
-  u32 const lS = chain_lcp(__ballot(!fS), eS, cy.lS, lane);
-  cy.cL = lane_value(cL, 0); cy.cS = lane_value(cS, 0);
-  cy.lL = lane_value(lL, 0); cy.lS = lane_value(lS, 0);
-  u32 const capj = min((u32)ZH_MAX_MATCH, n - min(p, n));
-  u32 const rL = min(lL, capj), rS = min(lS, capj);
-  u32 const mL = (cL && rL >= ZH_MIN_MATCH_LONG) ? rL : 0u;
-  u32 const mS = (cS && rS >= ZH_MIN_MATCH_SHORT) ? rS : 0u;
-  bool const useL = mL && mL >= mS;
-  u32 const ml = useL ? mL : mS, cm = useL ? cL : cS;
-  u32 const v = ml ? ((p - (cm - 1u)) << 8) | ml : 0u;
-  ci[cidx(i)] = v;
-  u64 const hb = __ballot(v != 0);
-  if (lane == 0) hm[r] = hb;
 }
 
 // Match info of one position from scratch (the lookahead positions `we`, `we + 1` of the
@@ -479,34 +533,27 @@ __device__ __forceinline__ void seg_walk(const u32 *ci, u64 hmk, u32 S, u32 SE, 
   u64 nl = 0, nm = 0;
   bool act = act0 && p < SE, merged = false;
   u32 mpos = 0;
+  // branch-free steps (selects, no exec-mask branches): each is one literal run and the
+  // position after it, or the point where the walk meets the old one
   while (__ballot(act)) {
-    if (act) {
-      u32 const o = p - S;
-      u64 const m = hmk >> o, ov = old >> o;
-      u32 const q = m ? p + ctz64(m) : SE;
-      u32 const x = ov ? p + ctz64(ov) : ~0u;
-      if (x <= q) {
-        nl |= bit_range(o, x - S);
-        merged = true;
-        mpos = x - S;
-        act = false;
-      } else {
-        nl |= bit_range(o, q - S);
-        p = q;
-        if (p < SE) {
-          u32 const inf = ci[cidx(p)];
-          u64 const b = 1ull << (p - S);
-          if (take_at<LAZY2>(ci, p, inf)) {
-            nm |= b;
-            p += inf & 255u;
-          } else {
-            nl |= b;
-            p += 1;
-          }
-        }
-        act = p < SE;
-      }
-    }
+    u32 const o = min(p - S, 63u);
+    u64 const m = hmk >> o, ov = old >> o;
+    u32 const q = m ? p + ctz64(m) : SE;
+    u32 const x = ov ? p + ctz64(ov) : ~0u;
+    bool const mg = act && x <= q;
+    bool const st = act && !mg && q < SE;
+    u32 const re = mg ? x : q;
+    nl |= act ? bit_range(o, re - S) : 0ull;
+    u32 const qq = st ? q : 0u;
+    u32 const inf = ci[cidx(qq)];
+    bool const tk = st && take_at<LAZY2>(ci, qq, inf);
+    u64 const b = st ? 1ull << (q - S) : 0ull;
+    nm |= tk ? b : 0ull;
+    nl |= tk ? 0ull : b;
+    mpos = mg ? x - S : mpos;
+    merged = merged || mg;
+    p = mg ? p : (st ? q + (tk ? (inf & 255u) : 1u) : (act ? q : p));
+    act = act && !mg && p < SE;
   }
   if (act0) {
     if (merged) {
@@ -744,7 +791,11 @@ __device__ __forceinline__ u32 lz_block(const ZhBlockDesc *__restrict__ blocks, 
   u32 const next_b = *s_take;  // (written before the barrier above)
   prefetch_block(blocks, next_b, nblocks, tid, pf);  // the next block's input, in flight from here
   if (rle) {
-    if (tid == 0) { meta[0] = 0; meta[1] = 0; meta[2] = 1; }
+    if (tid == 0) {
+      u32 one;  // (opaque: a constant {0, 0, 1} vector would be hoisted out of the block loop and spilled)
+      __asm__ volatile("v_mov_b32 %0, 1" : "=v"(one));
+      meta[0] = one - 1u; meta[1] = one - 1u; meta[2] = one;
+    }
     return next_b;
   }
   if (par_hist) {
@@ -792,11 +843,12 @@ __device__ __forceinline__ u32 lz_block(const ZhBlockDesc *__restrict__ blocks, 
   u32 const tid_ = tid;
   u32 const wave = tid >> 6;
   // rounds (64-position segments) of this worker wave in the length phase and the literals:
-  // waves 0..5 four, waves 6..13 five (wave 0 also walks the window)
-  constexpr u32 NR_LO = NSEG / NWW, NR_HI_WAVES = NSEG - NR_LO * NWW;
-  static_assert(NR_HI_WAVES < NWW, "round split");
-  u32 const r_lo = wave < NWW - NR_HI_WAVES ? NR_LO * wave : NR_LO * wave + (wave - (NWW - NR_HI_WAVES));
-  u32 const r_hi = r_lo + (wave < NWW - NR_HI_WAVES ? NR_LO : NR_LO + 1);
+  // five for the waves on SIMDs 0 and 1, four for those sharing SIMDs 2 and 3 with the
+  // inserters (a CU's waves go to SIMDs by wave id mod 4): 8 x 5 + 6 x 4 = 64
+  auto rounds_of = [](u32 w) { return (w & 2u) ? MAX_RW - 1 : MAX_RW; };
+  u32 r_lo = 0;
+  for (u32 w = 0; w < wave; w++) r_lo += rounds_of(w);
+  u32 const r_hi = r_lo + rounds_of(wave);
   for (u32 wsb = wstart; wsb < n; wsb += ZH_WINDOW) {
     u32 const we = min(wsb + ZH_WINDOW, n);
     // opaque per-window thread index: keeps the compiler from hoisting every LDS address
@@ -817,8 +869,7 @@ __device__ __forceinline__ u32 lz_block(const ZhBlockDesc *__restrict__ blocks, 
     // ---- match lengths of the window's positions (and of the two lookahead positions),
     // while the inserter waves build the next window's candidates
     {
-      LenCarry cy = {0u, 0u, 0u, 0u};
-      for (u32 r = r_hi; r-- > r_lo;) len_round(in32, ci, hm, r, wsb, we, n, lim, lane, cy);
+      span_lengths(in32, ci, hm, (u16 *)(smem + OFF_ML) + XQ_CAP * wave, r_lo, r_hi, wsb, we, n, lim, lane);
       if (wave == 0 && lane < 2) {
         u32 const p = we + lane;
         u32 const cw = ci[cidx(ZH_WINDOW + lane)];
@@ -940,7 +991,11 @@ __device__ __forceinline__ u32 lz_block(const ZhBlockDesc *__restrict__ blocks, 
     dbg[26] = __builtin_amdgcn_s_getreg((31 << 11) | 20);  // XCC_ID
     dbg[27] = (u32)(__builtin_amdgcn_s_memtime() - mt0);
     dbg[40] = st_Bmax; dbg[41] = st_Imax;
-    dbg[0] = st_stage; dbg[1] = st_A; dbg[2] = st_B; dbg[3] = st_J; dbg[4] = st_E; dbg[5] = st_rounds; dbg[20] = st_Bw; dbg[21] = st_X; dbg[22] = st_E1;
+    dbg[0] = st_stage; dbg[1] = st_A; dbg[2] = st_B; dbg[3] = st_J; dbg[4] = st_E; dbg[5] = st_rounds; dbg[20] = st_E2; dbg[21] = st_X; dbg[22] = st_E1;
+  }
+  if ((tid & 63) == 0 && tid < INS_TID) {  // each worker wave's length-phase cycles
+    u32 const w = tid >> 6;
+    ws.dbg(b)[w < 12 ? 28 + w : 53 + (w - 12)] = st_B;
   }
 #endif
   return next_b;

@@ -29,8 +29,16 @@
 #define ZH_MIN_MATCH_LONG 8
 #define ZH_MIN_MATCH_SHORT 5
 #define ZH_MAX_MATCH 64             /* per-position length cap; continuations are merged */
-#define ZH_PRIME_LONG 0xCF1BBCDCB7A56463ull
-#define ZH_PRIME_SHORT 0x9E3779B185EBCA87ull
+/* Hashes: sums of 24 x 24-bit products (low 32 bits; gfx950 v_mad_u32_u24 runs at the full VALU
+ * rate, a 64-bit multiply takes three quarter-rate v_mul_lo/hi_u32), top ZH_HASH_LOG bits.
+ * Long (bytes 0..7): bytes 0-2, 3-5, 6-7 times ZH_HK_L0..2; short (bytes 0..4): bytes 0-2, 3-4
+ * times ZH_HK_S0..1.  Same ratio as libzstd's 64-bit multiplicative hashes on the C3 mix
+ * (tools/lz3_model.c: 2.7584 vs 2.7585). */
+#define ZH_HK_L0 0x9E3779u
+#define ZH_HK_L1 0x85EBCAu
+#define ZH_HK_L2 0xC2B2AEu
+#define ZH_HK_S0 0x27D4EBu
+#define ZH_HK_S1 0x165667u
 #define ZH_COMPRESS_LITERALS_SIZE_MIN 63
 #define ZH_LONGNBSEQ 0x7F00
 #define ZH_MAGIC 0xFD2FB528u

@@ -794,8 +794,16 @@ size_t orc_encode_block_body(u8 *dst, size_t cap, const u8 *src, size_t n, const
 /* LZ stage (deterministic tile-lagged dual hash, lazy-1 greedy parse)       */
 /* ------------------------------------------------------------------------ */
 static inline u64 rd64(const u8 *p) { u64 v; memcpy(&v, p, 8); return v; }
-static inline u32 zh_hash_long(u64 v) { return (u32)((v * ZH_PRIME_LONG) >> (64 - ZH_HASH_LOG_LONG)); }
-static inline u32 zh_hash_short(u64 v) { return (u32)(((v << 24) * ZH_PRIME_SHORT) >> (64 - ZH_HASH_LOG_SHORT)); }
+/* hashes of include/zstd_hip_params.h (24 x 24-bit products, low 32 bits, top bits) */
+static inline u32 mul24(u32 a, u32 b) { return (a & 0xFFFFFFu) * (b & 0xFFFFFFu); }
+static inline u32 zh_hash_long(u64 v) {
+  u32 const t = mul24((u32)v, ZH_HK_L0) + mul24((u32)(v >> 24), ZH_HK_L1) + mul24((u32)(v >> 48), ZH_HK_L2);
+  return t >> (32 - ZH_HASH_LOG_LONG);
+}
+static inline u32 zh_hash_short(u64 v) {
+  u32 const t = mul24((u32)v, ZH_HK_S0) + mul24((u32)(v >> 24) & 0xFFFFu, ZH_HK_S1);
+  return t >> (32 - ZH_HASH_LOG_SHORT);
+}
 
 static u32 common_prefix(const u8 *src, u32 a, u32 b, u32 n, u32 cap) {
   u32 l = 0;

@@ -14,8 +14,24 @@ void dg_fill(uint8_t *dst, size_t n_chunks, size_t chunk_size, uint64_t seed, in
 
 static inline uint64_t rd64(const uint8_t *p) { uint64_t v; memcpy(&v, p, 8); return v; }
 static inline uint32_t rd32(const uint8_t *p) { uint32_t v; memcpy(&v, p, 4); return v; }
-static inline uint32_t hashL(uint64_t v, int hl) { return (uint32_t)((v * 0xCF1BBCDCB7A56463ull) >> (64 - hl)); }
-static inline uint32_t hashS(uint64_t v, int hl) { return (uint32_t)(((v << 24) * 0x9E3779B185EBCA87ull) >> (64 - hl)); }
+static int g_hash = 0;  /* 0: 64-bit multiply (r02), 1: 24-bit multiply-adds (full-rate v_mad_u32_u24) */
+static inline uint32_t mu24(uint32_t a, uint32_t b) { return (a & 0xFFFFFFu) * (b & 0xFFFFFFu); }
+static inline uint32_t hashL(uint64_t v, int hl) {
+  if (g_hash) {
+    uint32_t lo = (uint32_t)v, hi = (uint32_t)(v >> 32), b = (uint32_t)(v >> 24);
+    uint32_t t = mu24(lo, 0x9E3779u) + mu24(b, 0x85EBCAu) + mu24(hi >> 16, 0xC2B2AEu);
+    return t >> (32 - hl);
+  }
+  return (uint32_t)((v * 0xCF1BBCDCB7A56463ull) >> (64 - hl));
+}
+static inline uint32_t hashS(uint64_t v, int hl) {
+  if (g_hash) {
+    uint32_t lo = (uint32_t)v, b = (uint32_t)(v >> 24) & 0xFFFFu;
+    uint32_t t = mu24(lo, 0x27D4EBu) + mu24(b, 0x165667u);
+    return t >> (32 - hl);
+  }
+  return (uint32_t)(((v << 24) * 0x9E3779B185EBCA87ull) >> (64 - hl));
+}
 static int cnt(const uint8_t *a, const uint8_t *b, const uint8_t *end) { int n = 0; while (a + n < end && a[n] == b[n]) n++; return n; }
 
 typedef struct {
@@ -185,6 +201,7 @@ static size_t parse_dfast(const uint8_t *src, int n, const cfg_t *c, ZSTD_Sequen
 }
 
 int main(int argc, char **argv) {
+  if (argc > 2) g_hash = atoi(argv[2]);
   int nch = argc > 1 ? atoi(argv[1]) : 128, cs = 65536;
   uint8_t *buf = malloc((size_t)nch * cs), *out = malloc(200000);
   ZSTD_Sequence *seqs = malloc(sizeof(ZSTD_Sequence) * (cs + 8));

@@ -43,12 +43,12 @@ print('block 0 meta (nseq, nlit, rle):', m0[:3].tolist(), 'temp', temp.numel(), 
 raw = np.array([h[blocks + b * WS + 13120 * 8 + 122880 + 16: blocks + b * WS + 13120 * 8 + 122880 + 16 + 56 * 4].view(np.uint32) for b in range(n)])
 st = raw[:, :6]
 k2 = raw[:, 6:15].astype(np.float64)
-names = ["stage", "A(insert)", "B(lengths+exit)", "J(jacobi)", "E(emit)", "rounds"]
+names = ["stage", "A(P wait)", "B(lengths)", "J(walk+list)", "E(records+lits)", "rounds"]
 tot = st[:, :5].sum(1).mean()
 print(kind, "mean cycles/block (s_memtime units)", int(tot))
 for k, nm in enumerate(names):
     print(f"  {nm:16s} mean {st[:, k].mean():12.0f}  share {st[:, k].mean() / tot * 100 if k < 5 else 0:5.1f}%")
-print(f"  inserter busy (A of next window) {raw[:, 16].mean():12.0f}   worker B work (wave 0) {raw[:, 20].mean():12.0f}  exits {raw[:, 21].mean():12.0f}  emission-to-E1 {raw[:, 22].mean():12.0f}")
+print(f"  inserter busy (next window) {raw[:, 16].mean():12.0f}   R wait {raw[:, 21].mean():12.0f}  list + W1 {raw[:, 22].mean():12.0f}  catch-up + W2 {raw[:, 20].mean():12.0f}")
 
 k2 = np.concatenate([k2, raw[:, 17:18].astype(np.float64)], 1)
 k2n = ["lit_hist", "huf_build(serial)", "stream_sizes", "lit_streams", "merge", "repcode+codes", "fse_tables(serial)", "fse_pack", "tail", "fse_chains"]
