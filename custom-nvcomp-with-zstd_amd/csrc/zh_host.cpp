@@ -326,6 +326,7 @@ struct DevDict {
   u16 *tabs = nullptr;
   u32 *tabs_tmp = nullptr;
   u32 tabs_P = 0;
+  std::vector<u8> host;  // the loaded bytes (a reload of the same dictionary keeps everything)
   DevDict() = default;
   DevDict(const DevDict &) = delete;
   DevDict &operator=(const DevDict &) = delete;
@@ -351,6 +352,7 @@ struct DevDict {
     std::vector<u8> h(bytes);
     Status s = copy_any(h.data(), p, bytes, stream);
     if (s != Status::SUCCESS) return s;
+    if (owned && d && n == bytes && host == h) return Status::SUCCESS;  // the same dictionary: tables kept
     u32 did = 0;
     size_t co = 0;
     if (!zh::dict_layout(h.data(), bytes, did, co)) return Status::ERROR_DICTIONARY_FAILED;
@@ -372,8 +374,10 @@ struct DevDict {
     if (!tabs_tmp && hipMalloc(&tabs_tmp, 4u * ((1u << ZH_HASH_LOG_LONG) + (1u << ZH_HASH_LOG_SHORT))) != hipSuccess) tabs_tmp = nullptr;
     if (tabs && tabs_tmp) {
       u32 P = 0;
-      if (zh::lz_dict_tables(content(), content_n(), tabs, tabs_tmp, P, 0) == hipSuccess && hipDeviceSynchronize() == hipSuccess) tabs_P = P;
+      if (zh::lz_dict_tables(content(), content_n(), tabs, tabs_tmp, P, stream) == hipSuccess && hipStreamSynchronize(stream) == hipSuccess)
+        tabs_P = P;
     }
+    host.swap(h);
     return Status::SUCCESS;
   }
   void fill(ZhDecArgs &a) const {
@@ -730,8 +734,8 @@ void ZstdBatchManager::reset_stats() { pimpl_->stats = CompressionStats{}; }
 size_t ZstdBatchManager::get_batch_compress_temp_size(const std::vector<size_t> &sizes) const {
   size_t nb = 0;
   bool staged = false;
-  bool const dict = pimpl_->active() != nullptr;  // the manager's dictionary, if set before this query
-  for (size_t s : sizes) { size_t k = blocks_of(s, dict); nb += k; staged |= k > 1; }
+  // (the block layout does not depend on a dictionary: ZH_FRAME_BLOCK)
+  for (size_t s : sizes) { size_t k = blocks_of(s); nb += k; staged |= k > 1; }
   return WsLayout::make(nb, sizes.size(), staged).total;
 }
 size_t ZstdBatchManager::get_batch_decompress_temp_size(const std::vector<size_t> &sizes) const {
@@ -935,7 +939,9 @@ struct HistWindow {
     if (hipMemcpyAsync(dst + keep, (const u8 *)src + len - take, take, hipMemcpyDefault, stream) != hipSuccess) return Status::ERROR_CUDA_ERROR;
     cur ^= 1;
     n = keep + take;
-    return Status::SUCCESS;
+    // the chunk calls return with the caller's buffer free for reuse: the copy must have read
+    // it (a refill on another stream would otherwise race with it)
+    return hipStreamSynchronize(stream) == hipSuccess ? Status::SUCCESS : Status::ERROR_CUDA_ERROR;
   }
   void clear() { n = 0; }
 };
@@ -949,6 +955,10 @@ class ZstdStreamingManager::Impl {
   size_t ws_size = 0;
   bool comp = false, decomp = false;
   HistWindow chist, dhist;  // compressor's and decompressor's stream windows
+  // the session compresses chunks against the stream history (init_compression_with_history /
+  // compress_chunk_with_history): decompress_chunk then decodes against the decoded window;
+  // otherwise chunks are frames of their own and decode with the manager's dictionary, if any
+  bool hist_mode = false;
   explicit Impl(const CompressionConfig &c) : config(c), mgr(c) {}
   ~Impl() { if (ws) (void)hipFree(ws); }
   Status ensure_ws(size_t need) {
@@ -973,6 +983,7 @@ Status ZstdStreamingManager::init_compression(hipStream_t, size_t max_chunk) {
 Status ZstdStreamingManager::init_compression_with_history(hipStream_t st, size_t m) {
   Status s = init_compression(st, m);
   if (s == Status::SUCCESS) s = pimpl_->chist.ensure();
+  if (s == Status::SUCCESS) pimpl_->hist_mode = true;
   return s;
 }
 Status ZstdStreamingManager::init_decompression(hipStream_t) {
@@ -1012,12 +1023,20 @@ Status ZstdStreamingManager::decompress_chunk(const void *in, size_t n, void *ou
   if (is_last) *is_last = true;  // every chunk is a complete frame
   Status s = pimpl_->ensure_ws(pimpl_->mgr.get_decompress_temp_size(n));
   if (s != Status::SUCCESS) return s;
-  s = pimpl_->mgr.decompress_with_history(in, n, out, out_size, pimpl_->ws, pimpl_->ws_size, pimpl_->dhist.data(), pimpl_->dhist.n, stream);
+  // the decoded window is the chunk's history only in a history session, or when no
+  // dictionary is set (an independent frame never reaches before its start, so the window is
+  // harmless there); with a dictionary, a frame of its own decodes with the dictionary
+  dictionary::Dictionary dct;
+  (void)pimpl_->mgr.get_dictionary(dct);
+  bool const use_hist = pimpl_->dhist.n && (pimpl_->hist_mode || dct.raw_content.empty());
+  s = pimpl_->mgr.decompress_with_history(in, n, out, out_size, pimpl_->ws, pimpl_->ws_size, use_hist ? pimpl_->dhist.data() : nullptr,
+                                          use_hist ? pimpl_->dhist.n : 0, stream);
   if (s == Status::SUCCESS) s = pimpl_->dhist.append(out, *out_size, stream);
   return s;
 }
 Status ZstdStreamingManager::reset() {
   pimpl_->comp = pimpl_->decomp = false;
+  pimpl_->hist_mode = false;
   pimpl_->chist.clear();
   pimpl_->dhist.clear();
   return Status::SUCCESS;

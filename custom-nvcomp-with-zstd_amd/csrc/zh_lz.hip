@@ -54,14 +54,16 @@ extern "C" u32 zh_fixups_host() {
 namespace {
 
 constexpr u32 K1_THREADS = 1024;
-constexpr u32 NSEG = ZH_WINDOW / 64;        // 64-position segments (= length rounds) per window
+constexpr u32 NROUND = ZH_WINDOW / 64;      // 64-position length rounds per window
+constexpr u32 SEGP = 32;                    // positions per walk segment (one lane of wave 0)
+constexpr u32 NSEG = ZH_WINDOW / SEGP;      // walk segments per window
 constexpr u32 INS_TID = 896;                // first inserter thread (waves 14, 15)
 constexpr u32 NWW = INS_TID / 64;           // worker waves
-constexpr u32 TILES = ZH_WINDOW / ZH_TILE;  // 32 tiles per window
+constexpr u32 TILES = ZH_WINDOW / ZH_TILE;  // 16 tiles per window
 constexpr u32 TPL = ZH_TILE / 64;           // positions per inserter lane per tile
 constexpr u32 NCR = TILES * TPL / 2;        // candidate registers per inserter lane (u16 pairs)
 static_assert(NSEG == 64, "one walk lane per segment");
-static_assert(INS_TID == 896 && ZH_WINDOW == 4096, "round split: 8 waves x 5 + 6 waves x 4 rounds");
+static_assert(INS_TID == 896 && NROUND == 32, "round split: waves 1..13 take 6 x 3 + 7 x 2 rounds");
 static_assert(ZH_WINDOW % ZH_TILE == 0 && ZH_TILE % 64 == 0 && TILES * TPL % 2 == 0, "tiles tile windows");
 
 constexpr u32 HL_SIZE = 1u << ZH_HASH_LOG_LONG;
@@ -73,17 +75,21 @@ constexpr u32 OFF_TS = OFF_TL + 2 * (HL_SIZE + T_PAD);
 constexpr u32 OFF_CI = OFF_TS + 2 * (HS_SIZE + T_PAD);
 constexpr u32 CI_WORDS = ZH_WINDOW + 8;  // + the lookahead slots of positions `we`, `we + 1`
 __device__ __forceinline__ u32 cidx(u32 i) { return i; }
-constexpr u32 OFF_HM = OFF_CI + 4 * CI_WORDS;        // u64 per segment: positions with a match
-constexpr u32 OFF_LM = OFF_HM + 8 * NSEG;            // u64 per segment: literal positions
-constexpr u32 ML_CAP = (ZH_WINDOW + ZH_MIN_MATCH_SHORT - 1) / ZH_MIN_MATCH_SHORT + 12;  // matches per window
-constexpr u32 OFF_ML = OFF_LM + 8 * NSEG;            // the window's match starts (window index), in order
+// two cinfo buffers: window k's candidates / match info in buffer k & 1 (the parse of window k
+// overlaps the lengths of window k + 1)
+constexpr u32 OFF_HM = OFF_CI + 2 * 4 * CI_WORDS;    // per buffer u64 per round: positions with a match
+constexpr u32 OFF_LM = OFF_HM + 2 * 8 * NROUND;      // u32 per walk segment: literal positions
+constexpr u32 ML_CAP = ((ZH_WINDOW + ZH_MIN_MATCH_SHORT - 1) / ZH_MIN_MATCH_SHORT + 12 + 3) & ~3u;  // matches per window
+constexpr u32 OFF_ML = OFF_LM + 4 * NSEG;            // the window's match starts (window index), in order
 constexpr u32 OFF_ME = OFF_ML + 4 * ML_CAP;          // their starts after catch-up
 constexpr u32 OFF_MR = OFF_ME + 4 * ML_CAP;          // their (length after catch-up) | offset << 13
-constexpr u32 OFF_MISC = OFF_MR + 4 * ML_CAP;        // [1] matches of the window, [2] its exit
+constexpr u32 XQ_CAP = 192;                          // chain-end queue entries per worker wave
+constexpr u32 OFF_XQ = OFF_MR + 4 * ML_CAP;          // u16 per entry: window index | S << 15
+constexpr u32 OFF_MISC = OFF_XQ + 2 * XQ_CAP * NWW;  // [1] matches of the window being recorded
 constexpr u32 K1_LDS = OFF_MISC + 4 * 16;
 constexpr u32 MISC_ARR = 12;  // misc[12]: worker-wave barrier arrivals (cumulative)
 static_assert(K1_LDS <= 163840 - 256, "K1 LDS budget");
-static_assert(OFF_TL % 16 == 0 && OFF_CI % 16 == 0 && OFF_HM % 16 == 0, "alignment");
+static_assert(OFF_TL % 16 == 0 && OFF_CI % 16 == 0 && OFF_HM % 16 == 0 && OFF_MISC % 4 == 0, "alignment");
 
 // Hashes of include/zstd_hip_params.h: full-rate v_mad_u32_u24 sums (the 24-bit multiplies
 // take the low 24 bits of each operand, so byte groups need no masking but the short hash's
@@ -335,10 +341,10 @@ __device__ __forceinline__ void dump_window(u8 *ci8, u32 lane_, const u32 (&creg
 // v from lane `src` (< 64) of the wave: ds_bpermute on a byte address, no lane-base math
 __device__ __forceinline__ u32 bperm(u32 v, u32 src) { return (u32)__builtin_amdgcn_ds_bpermute((int)(src << 2), (int)v); }
 __device__ __forceinline__ u32 ctz64(u64 v) { return (u32)__builtin_ctzll(v); }
-// bits [a, b) of a u64, 0 <= a <= b <= 64
-__device__ __forceinline__ u64 bit_range(u32 a, u32 b) {
-  u64 const hi = b >= 64 ? ~0ull : (1ull << b) - 1ull;
-  return hi & ~((1ull << a) - 1ull);
+// bits [a, b) of a u32, 0 <= a <= b <= 32
+__device__ __forceinline__ u32 bit_range32(u32 a, u32 b) {
+  u32 const hi = b >= 32 ? ~0u : (1u << b) - 1u;
+  return hi & ~((1u << a) - 1u);
 }
 
 // ---- match lengths, lanes = positions -------------------------------------------------------
@@ -348,9 +354,7 @@ __device__ __forceinline__ u64 bit_range(u32 a, u32 b) {
 //     with 8 matching bytes go to the wave's extension queue (flushed 64 at a time);
 //  B  the queued chain ends extended, lanes = queue entries, results into their cinfo byte;
 //  C  (rounds high to low) lengths from the chain structure -> match info in place.
-constexpr u32 MAX_RW = 5;   // rounds per worker wave
-constexpr u32 XQ_CAP = 192; // extension queue entries per worker wave (u16: window index | S << 15)
-static_assert(NWW * XQ_CAP * 2 <= 3 * 4 * ML_CAP, "the extension queues alias the match lists");
+constexpr u32 MAX_RW = 3;   // rounds per worker wave
 
 // Length of position p's candidate from the chain structure: T = ballot of the chain ends
 // (lanes whose lcp is their own: fewer than 8 bytes, or the next position does not continue
@@ -528,28 +532,28 @@ __device__ __forceinline__ bool take_at(const u32 *ci, u32 i, u32 inf) {
 // visited bits (a Jacobi re-walk from a new entry), the walk stops where it meets a position
 // the old walk visited -- from there on both are the same -- and keeps the old bits above it.
 template <bool LAZY2>
-__device__ __forceinline__ void seg_walk(const u32 *ci, u64 hmk, u32 S, u32 SE, u32 p, bool act0, u64 &LM, u64 &MM, u32 &ex) {
-  u64 const old = act0 ? (LM | MM) : 0ull;
-  u64 nl = 0, nm = 0;
+__device__ __forceinline__ void seg_walk(const u32 *ci, u32 hmk, u32 S, u32 SE, u32 p, bool act0, u32 &LM, u32 &MM, u32 &ex) {
+  u32 const old = act0 ? (LM | MM) : 0u;
+  u32 nl = 0, nm = 0;
   bool act = act0 && p < SE, merged = false;
   u32 mpos = 0;
   // branch-free steps (selects, no exec-mask branches): each is one literal run and the
   // position after it, or the point where the walk meets the old one
   while (__ballot(act)) {
-    u32 const o = min(p - S, 63u);
-    u64 const m = hmk >> o, ov = old >> o;
-    u32 const q = m ? p + ctz64(m) : SE;
-    u32 const x = ov ? p + ctz64(ov) : ~0u;
+    u32 const o = min(p - S, SEGP - 1);
+    u32 const m = hmk >> o, ov = old >> o;
+    u32 const q = m ? p + (u32)__builtin_ctz(m) : SE;
+    u32 const x = ov ? p + (u32)__builtin_ctz(ov) : ~0u;
     bool const mg = act && x <= q;
     bool const st = act && !mg && q < SE;
     u32 const re = mg ? x : q;
-    nl |= act ? bit_range(o, re - S) : 0ull;
+    nl |= act ? bit_range32(o, re - S) : 0u;
     u32 const qq = st ? q : 0u;
     u32 const inf = ci[cidx(qq)];
     bool const tk = st && take_at<LAZY2>(ci, qq, inf);
-    u64 const b = st ? 1ull << (q - S) : 0ull;
-    nm |= tk ? b : 0ull;
-    nl |= tk ? 0ull : b;
+    u32 const b = st ? 1u << (q - S) : 0u;
+    nm |= tk ? b : 0u;
+    nl |= tk ? 0u : b;
     mpos = mg ? x - S : mpos;
     merged = merged || mg;
     p = mg ? p : (st ? q + (tk ? (inf & 255u) : 1u) : (act ? q : p));
@@ -557,7 +561,7 @@ __device__ __forceinline__ void seg_walk(const u32 *ci, u64 hmk, u32 S, u32 SE, 
   }
   if (act0) {
     if (merged) {
-      u64 const keep = ~((1ull << mpos) - 1ull);
+      u32 const keep = ~((1u << mpos) - 1u);
       LM = nl | (LM & keep);
       MM = nm | (MM & keep);
     } else {
@@ -568,11 +572,12 @@ __device__ __forceinline__ void seg_walk(const u32 *ci, u64 hmk, u32 S, u32 SE, 
   }
 }
 
-// Inserter wave main loop.  It mirrors the workers' barrier sequence window by window
-// (P, R, W1, W2) but fills the slack: between two tiles it takes the next barrier only once
-// all 14 worker waves have arrived there (an LDS arrival counter), so the next window's
-// insertion spreads over the whole window step.
-constexpr u32 WIN_BARRIERS = 3;  // R (lengths done), W1 (parse done), W2 (catch-up done)
+// Inserter wave main loop.  Step k (the workers' window step: lengths of window k, parse of
+// window k - 1) opens with barrier P once window k's candidates are dumped into cinfo buffer
+// k & 1, and the inserters then build window k + 1's candidates in registers.  They take the
+// step's barrier X only once all 14 worker waves have arrived there (an LDS arrival counter),
+// between two tiles, so the insertion spreads over the whole step.
+constexpr u32 WIN_BARRIERS = 1;  // X (window k's lengths and window k - 1's parse done)
 template <bool LONG>
 __device__ __forceinline__ void inserter_loop(const u32 *in32, u16 *T, u8 *ci8, u32 *misc_, u32 n, u32 lim, u32 lane, u32 *dbg, u32 wstart,
                                               u32 pmin, u32 span_s, u32 span_e) {
@@ -583,16 +588,16 @@ __device__ __forceinline__ void inserter_loop(const u32 *in32, u16 *T, u8 *ci8, 
 #ifdef ZH_STAMPS
   u32 st_ins = 0;
 #endif
-  u32 passed = 0;  // window barriers taken so far (all windows)
-  for (u32 wsb = wstart; wsb < n; wsb += ZH_WINDOW) {
-    u32 const we = min(wsb + ZH_WINDOW, n);
-    dump_window<LONG>(ci8, lane, creg, cwe);
-    __syncthreads();  // P: candidates of this window in cinfo
+  u32 passed = 0;  // X barriers taken so far
+  for (u32 wsb = wstart, kb = 0;; wsb += ZH_WINDOW, kb ^= 1u) {
+    bool const have = wsb < n;
+    if (have) dump_window<LONG>(ci8 + kb * 4 * CI_WORDS, lane, creg, cwe);
+    __syncthreads();  // P: candidates of window k in buffer k & 1
     u32 const done = passed + WIN_BARRIERS;
     // arr: the arrival counter as read with the last tile's read-back; a barrier taken
     // here means the counter is re-read for the next one
     auto take_ready = [&](u32 arr) {
-      while (passed < done && arr >= (INS_TID / 64) * (passed + 1)) {
+      while (passed < done && arr >= NWW * (passed + 1)) {
         __syncthreads();
         passed++;
         arr = __atomic_load_n(&misc_[MISC_ARR], __ATOMIC_RELAXED);
@@ -601,13 +606,13 @@ __device__ __forceinline__ void inserter_loop(const u32 *in32, u16 *T, u8 *ci8, 
 #ifdef ZH_STAMPS
     u64 const ti0 = __builtin_amdgcn_s_memtime();
 #endif
-    if (we < n) insert_window<LONG>(in32, T, we, min(we + ZH_WINDOW, n), lim, lane, creg, cwe, &misc_[MISC_ARR], take_ready);
+    u32 const nx = wsb + ZH_WINDOW;
+    if (nx < n) insert_window<LONG>(in32, T, nx, min(nx + ZH_WINDOW, n), lim, lane, creg, cwe, &misc_[MISC_ARR], take_ready);
 #ifdef ZH_STAMPS
-    u32 const dti = (u32)(__builtin_amdgcn_s_memtime() - ti0);
-    st_ins += dti;
-    if (lane == 0) atomicMax(&misc_[9], dti);
+    st_ins += (u32)(__builtin_amdgcn_s_memtime() - ti0);
 #endif
     while (passed < done) { __syncthreads(); passed++; }
+    if (!have) break;
   }
 #ifdef ZH_STAMPS
   if (LONG && lane == 0) dbg[16] = st_ins;
@@ -683,7 +688,6 @@ __device__ __forceinline__ u32 lz_block(const ZhBlockDesc *__restrict__ blocks, 
   u32 *ci = (u32 *)(smem + OFF_CI);
   u8 *ci8 = smem + OFF_CI;
   u64 *hm = (u64 *)(smem + OFF_HM);
-  u64 *lmk = (u64 *)(smem + OFF_LM);
   u32 *misc = (u32 *)(smem + OFF_MISC);
 
   // opaque per-block thread index: stops the compiler from hoisting LDS addresses derived
@@ -842,55 +846,51 @@ __device__ __forceinline__ u32 lz_block(const ZhBlockDesc *__restrict__ blocks, 
 
   u32 const tid_ = tid;
   u32 const wave = tid >> 6;
-  // rounds (64-position segments) of this worker wave in the length phase and the literals:
-  // five for the waves on SIMDs 0 and 1, four for those sharing SIMDs 2 and 3 with the
-  // inserters (a CU's waves go to SIMDs by wave id mod 4): 8 x 5 + 6 x 4 = 64
-  auto rounds_of = [](u32 w) { return (w & 2u) ? MAX_RW - 1 : MAX_RW; };
+  // rounds (64-position segments) of this worker wave in the length phase: waves 1..13 (wave 0
+  // parses), three for the waves on SIMDs 0 and 1, two for those sharing SIMDs 2 and 3 with the
+  // inserters (a CU's waves go to SIMDs by wave id mod 4) and wave 13 (the lookahead positions)
+  auto rounds_of = [](u32 w) { return w == 0 ? 0u : ((w & 2u) || w == 13) ? MAX_RW - 1 : MAX_RW; };
   u32 r_lo = 0;
   for (u32 w = 0; w < wave; w++) r_lo += rounds_of(w);
   u32 const r_hi = r_lo + rounds_of(wave);
-  for (u32 wsb = wstart; wsb < n; wsb += ZH_WINDOW) {
+  u32 *const ci0 = ci;
+  u32 *mlist = (u32 *)(smem + OFF_ML), *mext = (u32 *)(smem + OFF_ME), *mrec = (u32 *)(smem + OFF_MR);
+  u32 *lm32 = (u32 *)(smem + OFF_LM);
+  u16 *const xq = (u16 *)(smem + OFF_XQ) + XQ_CAP * wave;
+  // Step k: the lengths of window k (waves 1..13) beside the parse + catch-up of window k - 1
+  // (wave 0); barrier X; window k - 1's records and literals (all worker waves).
+  for (u32 wsb = wstart, kb = 0;; wsb += ZH_WINDOW, kb ^= 1u) {
+    bool const have = wsb < n;
     u32 const we = min(wsb + ZH_WINDOW, n);
-    // opaque per-window thread index: keeps the compiler from hoisting every LDS address
-    // derived from it out of the window loop (they would be spilled to scratch)
+    u32 const wsp = wsb - ZH_WINDOW, wep = min(wsb, n);  // window k - 1 (when wsb > wstart)
+    bool const prev = wsb > wstart && wep > pre;  // window k - 1 has positions to parse
+    // opaque per-step thread index: keeps the compiler from hoisting every LDS address
+    // derived from it out of the loop (they would be spilled to scratch)
     u32 tid;
     __asm__ volatile("v_mov_b32 %0, %1" : "=v"(tid) : "v"(tid_));
     u32 const lane = tid & 63;
-    __syncthreads();  // P
+    u32 *const ciK = ci0 + kb * CI_WORDS, *const ciP = ci0 + (kb ^ 1u) * CI_WORDS;
+    u64 *const hmK = hm + kb * NROUND, *const hmP = hm + (kb ^ 1u) * NROUND;
+    __syncthreads();  // P: candidates of window k in buffer k & 1
     ZH_STAMP(st_A);
-    if (we <= pre) {  // dictionary history only: nothing to parse, keep the barrier sequence
-      for (u32 k = 0; k < WIN_BARRIERS; k++) {
-        if (lane == 0) atomicAdd(&misc[MISC_ARR], 1u);
-        __syncthreads();
-      }
-      continue;
-    }
-
-    // ---- match lengths of the window's positions (and of the two lookahead positions),
-    // while the inserter waves build the next window's candidates
-    {
-      span_lengths(in32, ci, hm, (u16 *)(smem + OFF_ML) + XQ_CAP * wave, r_lo, r_hi, wsb, we, n, lim, lane);
-      if (wave == 0 && lane < 2) {
+    if (have && we > pre && wave != 0) {
+      span_lengths(in32, ciK, hmK, xq, r_lo, r_hi, wsb, we, n, lim, lane);
+      if (wave == NWW - 1 && lane < 2) {  // the lookahead positions `we`, `we + 1`
         u32 const p = we + lane;
-        u32 const cw = ci[cidx(ZH_WINDOW + lane)];
-        ci[cidx(ZH_WINDOW + lane)] = info_one(in32, p, cw, n, lim, p < n);
+        u32 const cw = ciK[cidx(ZH_WINDOW + lane)];
+        ciK[cidx(ZH_WINDOW + lane)] = info_one(in32, p, cw, n, lim, p < n);
       }
+      ZH_STAMP(st_B);
     }
-    ZH_STAMP(st_B);
-    if (lane == 0) atomicAdd(&misc[MISC_ARR], 1u);
-    __syncthreads();  // R: match info of the window
-    ZH_STAMP(st_X);
-
-    // ---- the parse (wave 0, lanes = segments) and the window's match list
-    u32 *mlist = (u32 *)(smem + OFF_ML), *mext = (u32 *)(smem + OFF_ME), *mrec = (u32 *)(smem + OFF_MR);
-    u32 const e0 = e_in - wsb;  // first parsed position (< 64 except in the window holding `pre`)
-    if (wave == 0) {
-      u32 const wn = we - wsb;
-      u32 const S = 64 * lane, SE = min(S + 64, wn);
-      u64 const hmk = hm[lane];
+    if (wave == 0 && prev) {
+      // ---- the parse of window k - 1, lanes = 32-position segments
+      u32 const wn = wep - wsp;
+      u32 const S = SEGP * lane, SE = min(S + SEGP, wn);
+      u32 const hmk = (u32)(hmP[lane >> 1] >> (32 * (lane & 1)));
+      u32 const e0 = e_in - wsp;  // first parsed position (< 64 except in the window holding `pre`)
       u32 entry = lane == 0 ? e0 : max(S, e0), ex = entry;
-      u64 LM = 0, MM = 0;
-      seg_walk<LAZY2>(ci, hmk, S, SE, entry, true, LM, MM, ex);
+      u32 LM = 0, MM = 0;
+      seg_walk<LAZY2>(ciP, hmk, S, SE, entry, true, LM, MM, ex);
       // Jacobi rounds: a segment's entry is its predecessor's exit
       for (;;) {
         u32 const pe = wave_shr1(ex);
@@ -900,87 +900,77 @@ __device__ __forceinline__ u32 lz_block(const ZhBlockDesc *__restrict__ blocks, 
         st_rounds++;
 #endif
         if (!__ballot(ch)) break;
-        seg_walk<LAZY2>(ci, hmk, S, SE, ne, ch, LM, MM, ex);
+        seg_walk<LAZY2>(ciP, hmk, S, SE, ne, ch, LM, MM, ex);
         entry = ne;
       }
-      ZH_STAMP(st_J);
-      u32 const ns = (u32)__popcll(MM);
+      e_in = wsp + lane_value(ex, 63);
+      // the window's matches in position order
+      u32 const ns = (u32)__popc(MM);
       u32 const is = wave_scan_incl(ns);
-      lmk[lane] = LM;
-      u64 mm = MM;
-      u32 k = is - ns;
+      u32 const nm = lane_value(is, 63);
+      lm32[lane] = LM;
+      u32 mm = MM, k = is - ns;
       while (__ballot(mm != 0)) {
         if (mm) {
-          mlist[k++] = S + ctz64(mm);
-          mm &= mm - 1ull;
+          mlist[k++] = S + (u32)__builtin_ctz(mm);
+          mm &= mm - 1u;
         }
       }
-      if (lane == 63) {
-        misc[1] = is;
-        misc[2] = wsb + ex;
-      }
-    }
-    if (lane == 0) atomicAdd(&misc[MISC_ARR], 1u);
-    __syncthreads();  // W1: literal masks and the match list (cinfo stays: match info)
-    ZH_STAMP(st_E1);
-    u32 const nm = __builtin_amdgcn_readfirstlane(misc[1]);
-    // ---- catch-up, lanes = matches: a match's lower bound is the end of the match before it
-    // (the window's first parsed position for the first); the bytes it takes back are no
-    // longer literals
-    for (u32 j0 = 64 * wave; j0 < nm; j0 += 64 * NWW) {
-      u32 const j = j0 + lane;
-      bool const v = j < nm;
-      u32 const ms = v ? mlist[j] : 0u, inf = ci[cidx(ms)];
-      u32 const pm = (v && j) ? mlist[j - 1] : 0u;
-      u32 const lo = (v && j) ? pm + (ci[cidx(pm)] & 255u) : e0;
-      u32 const e = catch_up(in32, wsb + ms, inf >> 8, wsb + lo, v);
-      if (v) {
-        mext[j] = ms - e;
-        mrec[j] = ((inf & 255u) + e) | ((inf >> 8) << 13);
-      }
-      if (e) {
-        for (u32 g = (ms - e) >> 6; g <= (ms - 1) >> 6; g++) {
-          u32 const a = max(ms - e, 64 * g) - 64 * g, bnd = min(ms - 64 * g, 64u);
-          atomicAnd((unsigned long long *)&lmk[g], ~bit_range(a, bnd));
+      // catch-up, lanes = matches: a match's lower bound is the end of the match before it
+      // (the window's first parsed position for the first); the bytes it takes back are no
+      // longer literals
+      for (u32 j0 = 0; j0 < nm; j0 += 64) {
+        u32 const j = j0 + lane;
+        bool const v = j < nm;
+        u32 const ms = v ? mlist[j] : 0u, inf = ciP[cidx(ms)];
+        u32 const pm = (v && j) ? mlist[j - 1] : 0u;
+        u32 const lo = (v && j) ? pm + (ciP[cidx(pm)] & 255u) : e0;
+        u32 const e = catch_up(in32, wsp + ms, inf >> 8, wsp + lo, v);
+        if (v) {
+          mext[j] = ms - e;
+          mrec[j] = ((inf & 255u) + e) | ((inf >> 8) << 13);
+        }
+        if (e) {
+          for (u32 g = (ms - e) / SEGP; g <= (ms - 1) / SEGP; g++) {
+            u32 const a = max(ms - e, SEGP * g) - SEGP * g, bnd = min(ms - SEGP * g, SEGP);
+            atomicAnd(&lm32[g], ~bit_range32(a, bnd));
+          }
         }
       }
+      if (lane == 0) misc[1] = nm;
+      ZH_STAMP(st_J);
     }
     if (lane == 0) atomicAdd(&misc[MISC_ARR], 1u);
-    __syncthreads();  // W2: final literal masks and match records (cinfo is free for the inserters)
-    ZH_STAMP(st_E2);
-    // literal offsets of the 64 segments (every wave the same scan: lane = segment)
-    u64 const lmg = lmk[lane];
-    u32 const lc = (u32)__popcll(lmg), lincl = wave_scan_incl(lc), lb = lincl - lc;
-    u32 const nlw = lane_value(lincl, 63);
-    // ---- sequence records, lanes = matches: cumLit | ml << 17 | off << 32
-    for (u32 j0 = 64 * wave; j0 < nm; j0 += 64 * NWW) {
-      u32 const j = j0 + lane;
-      bool const v = j < nm;
-      u32 const st = v ? mext[j] : 0u, mr = v ? mrec[j] : 0u, g = st >> 6;
-      u32 const lbg = bperm(lb, g);  // (all lanes: ds_bpermute sources)
-      u64 const lg = lmk[g];
-      u32 const cum = nlit_tot + lbg + (u32)__popcll(lg & ((1ull << (st & 63)) - 1ull));
-      if (v) seq_out[nseq_tot + j] = (u64)cum | ((u64)(mr & 0x1FFFu) << 17) | ((u64)(mr >> 13) << 32);
-    }
-    // ---- literals, lanes = positions
-    for (u32 r = r_lo; r < r_hi; r++) {
-      u64 const lm = ((u64)(u32)__builtin_amdgcn_readfirstlane((u32)(lmk[r] >> 32)) << 32) | (u32)__builtin_amdgcn_readfirstlane((u32)lmk[r]);
-      u32 const lbr = lane_value(lb, r);
-#ifdef ZH_K1_DEBUG
-      if (lane == 0) {  // diagnostic build: the masks the literal phase sees, per window and segment
-        u32 *dbgw = (u32 *)(lit_out + ZH_BLOCK_MAX) + 4 * (64 * ((wsb - wstart) / ZH_WINDOW) + r);
-        dbgw[0] = (u32)lm; dbgw[1] = (u32)(lm >> 32); dbgw[2] = lbr; dbgw[3] = nlit_tot;
+    __syncthreads();  // X: window k's match info; window k - 1's literal masks and match records
+    ZH_STAMP(st_X);
+    if (prev) {
+      u32 const nm = __builtin_amdgcn_readfirstlane(misc[1]);
+      // literal offsets of the 64 segments (every wave the same scan: lane = segment)
+      u32 const lc = (u32)__popc(lm32[lane]), lincl = wave_scan_incl(lc), lb = lincl - lc;
+      u32 const nlw = lane_value(lincl, 63);
+      // ---- sequence records, lanes = matches: cumLit | ml << 17 | off << 32
+      for (u32 j0 = 64 * wave; j0 < nm; j0 += 64 * NWW) {
+        u32 const j = j0 + lane;
+        bool const v = j < nm;
+        u32 const st = v ? mext[j] : 0u, mr = v ? mrec[j] : 0u, g = st / SEGP;
+        u32 const lbg = bperm(lb, g);  // (all lanes: ds_bpermute sources)
+        u32 const cum = nlit_tot + lbg + (u32)__popc(lm32[g] & ((1u << (st % SEGP)) - 1u));
+        if (v) seq_out[nseq_tot + j] = (u64)cum | ((u64)(mr & 0x1FFFu) << 17) | ((u64)(mr >> 13) << 32);
       }
-#endif
-      if ((lm >> lane) & 1ull) {
-        u32 const rank = __builtin_amdgcn_mbcnt_hi((u32)(lm >> 32), __builtin_amdgcn_mbcnt_lo((u32)lm, 0u));
-        lit_out[nlit_tot + lbr + rank] = in[wsb + 64 * r + lane];
+      // ---- literals, lanes = positions (round r = segments 2r, 2r + 1)
+      for (u32 r = wave; r < NROUND; r += NWW) {
+        u64 const lm = ((u64)(u32)__builtin_amdgcn_readfirstlane(lm32[2 * r + 1]) << 32) | (u32)__builtin_amdgcn_readfirstlane(lm32[2 * r]);
+        u32 const lbr = lane_value(lb, 2 * r);
+        if ((lm >> lane) & 1ull) {
+          u32 const rank = __builtin_amdgcn_mbcnt_hi((u32)(lm >> 32), __builtin_amdgcn_mbcnt_lo((u32)lm, 0u));
+          lit_out[nlit_tot + lbr + rank] = in[wsp + 64 * r + lane];
+        }
       }
+      nlit_tot += nlw;
+      nseq_tot += nm;
+      ZH_STAMP(st_E);
     }
-    nlit_tot += nlw;
-    nseq_tot += nm;
-    e_in = __builtin_amdgcn_readfirstlane(misc[2]);
-    ZH_STAMP(st_E);
+    if (!have) break;
   }
   if (tid == 0) { meta[0] = nseq_tot; meta[1] = nlit_tot; meta[2] = 0; }
 #ifdef ZH_STAMPS

@@ -268,18 +268,26 @@ class Manager:
         content size.  Host bytes in -> bytes out (reference PyManager.decompress)."""
         if _is_host(frame):
             return _host_bytes(self.decompress(_to_device(frame), capacity, stream))
-        if capacity is None:
+        auto = capacity is None
+        if auto:
             capacity = _frame_size(frame)
         torch = _torch()
         frame = frame.contiguous().view(torch.uint8)
-        out = torch.empty(max(capacity, 1), dtype=torch.uint8, device=frame.device)
-        ws = self._workspace(lib().cuda_zstd_get_decompress_workspace_size(self._h, frame.numel()))
-        size = ctypes.c_size_t(capacity)
-        rc = lib().cuda_zstd_decompress(self._h, frame.data_ptr(), frame.numel(), out.data_ptr(), ctypes.byref(size), ws.data_ptr(), ws.numel(),
-                                        _stream_ptr(stream))
-        if rc:
-            raise ZstdError(rc, "cuda_zstd_decompress")
-        return out[: size.value]
+        # a derived capacity (the first frame's content size, or 16x the input without one)
+        # grows on BUFFER_TOO_SMALL: concatenated frames, frames without a content size
+        for _ in range(4 if auto else 1):
+            out = torch.empty(max(capacity, 1), dtype=torch.uint8, device=frame.device)
+            ws = self._workspace(lib().cuda_zstd_get_decompress_workspace_size(self._h, frame.numel()))
+            size = ctypes.c_size_t(capacity)
+            rc = lib().cuda_zstd_decompress(self._h, frame.data_ptr(), frame.numel(), out.data_ptr(), ctypes.byref(size), ws.data_ptr(),
+                                            ws.numel(), _stream_ptr(stream))
+            if rc == TOO_SMALL and auto:
+                capacity *= 4
+                continue
+            if rc:
+                raise ZstdError(rc, "cuda_zstd_decompress")
+            return out[: size.value]
+        raise ZstdError(TOO_SMALL, "cuda_zstd_decompress")
 
     def decompress_batch(self, frames: Sequence, capacities: Sequence[int] = None, stream=None, raise_on_error=True):
         """ZstdBatchManager::decompress_batch over device tensors: one GPU launch for all.
@@ -488,16 +496,22 @@ class StreamingManager:
     def decompress_chunk(self, frame, capacity: int = None, stream=None):
         torch = _torch()
         frame = frame.contiguous().view(torch.uint8)
-        if capacity is None:
+        auto = capacity is None
+        if auto:
             capacity = _frame_size(frame)
-        out = torch.empty(max(capacity, 1), dtype=torch.uint8, device=frame.device)
-        size = ctypes.c_size_t(capacity)
-        last = ctypes.c_int()
-        rc = lib().cuda_zstd_stream_decompress_chunk(self._h, frame.data_ptr(), frame.numel(), out.data_ptr(), ctypes.byref(size),
-                                                     ctypes.byref(last), _stream_ptr(stream))
-        if rc:
-            raise ZstdError(rc, "cuda_zstd_stream_decompress_chunk")
-        return out[: size.value]
+        for _ in range(4 if auto else 1):  # (a derived capacity grows on BUFFER_TOO_SMALL)
+            out = torch.empty(max(capacity, 1), dtype=torch.uint8, device=frame.device)
+            size = ctypes.c_size_t(capacity)
+            last = ctypes.c_int()
+            rc = lib().cuda_zstd_stream_decompress_chunk(self._h, frame.data_ptr(), frame.numel(), out.data_ptr(), ctypes.byref(size),
+                                                         ctypes.byref(last), _stream_ptr(stream))
+            if rc == TOO_SMALL and auto:
+                capacity *= 4
+                continue
+            if rc:
+                raise ZstdError(rc, "cuda_zstd_stream_decompress_chunk")
+            return out[: size.value]
+        raise ZstdError(TOO_SMALL, "cuda_zstd_stream_decompress_chunk")
 
     def reset(self):
         rc = lib().cuda_zstd_stream_reset(self._h)

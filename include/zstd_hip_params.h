@@ -16,13 +16,15 @@
 #define ZH_HIST_BLOCK 32768         /* device block of a history frame (below) */
 #define ZH_HIST_WINDOW_LOG 16       /* history needs a window of >= 64 KiB */
 /* Device block size of a frame of n bytes: frames up to 64 KiB are one
- * block; larger frames, and dictionary frames over 32 KiB, are cut into 32 KiB blocks that are
- * each staged behind the 32 KiB before them (the previous block, or the dictionary's tail for
- * the first), so matches reach across block boundaries within the 64 KiB of LDS. */
-#define ZH_FRAME_BLOCK(n, dict) ((((n) <= ZH_BLOCK_MAX) && !((dict) && (n) > ZH_HIST_BLOCK)) ? ZH_BLOCK_MAX : ZH_HIST_BLOCK)
+ * block (a dictionary frame's block staged behind the last 64 KiB - n bytes of the dictionary
+ * content); larger frames are cut into 32 KiB blocks that are each staged behind the 32 KiB
+ * before them (the previous block, or the dictionary's tail for the first), so matches reach
+ * across block boundaries within the 64 KiB of LDS.  The layout -- and so the workspace size --
+ * does not depend on whether a dictionary is set (the reference's temp size does not,
+ * src/cuda_zstd_manager.cu:5661). */
+#define ZH_FRAME_BLOCK(n, dict) ((void)(dict), ((n) <= ZH_BLOCK_MAX ? ZH_BLOCK_MAX : ZH_HIST_BLOCK))
 #define ZH_TILE 128                 /* hash insertion granularity (positions) */
-#define ZH_WINDOW 4096              /* parse window (positions) */
-#define ZH_SEG 16                   /* positions per thread in the parse */
+#define ZH_WINDOW 2048              /* parse window (positions); catch-up stays inside one */
 #define ZH_HASH_LOG_LONG 14         /* 8-byte hash table: 2^14 u16 entries */
 #define ZH_HASH_LOG_SHORT 14        /* 5-byte hash table: 2^14 u16 entries */
 #define ZH_HASH_READ 8              /* bytes read per hashed position */

@@ -14,6 +14,10 @@
 //                                  reference tests/test_inference_api.cu:398-410: a workspace
 //                                  from allocate_inference_workspace(frame, chunk) and
 //                                  decompress_to_preallocated into an exactly-sized output
+//   boundary stream_dict <dir> <h>  ZstdStreamingManager with set_dictionary(<dir>/dict.bin)
+//                                  (raw content or a formatted dictionary): every chunk through
+//                                  compress_chunk (h = 0) or compress_chunk_with_history (h = 1),
+//                                  then every frame through decompress_chunk in order
 //
 // <dir>/in.bin = the chunks back to back, <dir>/sizes.bin = u64 sizes.  Writes
 // <dir>/frames.bin (frames back to back), <dir>/fsizes.bin (u64), and for `nvcomp`
@@ -165,6 +169,33 @@ int main(int argc, char **argv) {
       CK(hipMemcpy(back.data() + offs[i], d_o, sizes[i], hipMemcpyDeviceToHost));
       (void)m.free_inference_workspace(ws);
       CK(hipFree(d_o));
+    }
+    dump(dir + "/back.bin", back.data(), back.size());
+  } else if (mode == "stream_dict") {
+    if (argc < 4) return 1;
+    bool const hist = std::stoul(argv[3]) != 0;
+    std::vector<char> db = slurp(dir + "/dict.bin");
+    dictionary::Dictionary dct;
+    dct.raw_content.assign(db.begin(), db.end());
+    ZstdStreamingManager sm(CompressionConfig::from_level(3));
+    Status st = sm.set_dictionary(dct);
+    if (st == Status::SUCCESS) st = hist ? sm.init_compression_with_history(0, 0) : sm.init_compression(0, 0);
+    if (st != Status::SUCCESS) { fprintf(stderr, "init: %s\n", status_to_string(st)); return 3; }
+    for (size_t i = 0; i < n; i++) {
+      fsz[i] = cap;
+      st = hist ? sm.compress_chunk_with_history(d_in[i], sizes[i], d_out[i], &fsz[i], i + 1 == n, 0)
+                : sm.compress_chunk(d_in[i], sizes[i], d_out[i], &fsz[i], i + 1 == n, 0);
+      if (st != Status::SUCCESS) { fprintf(stderr, "compress_chunk %zu: %s\n", i, status_to_string(st)); return 3; }
+    }
+    std::vector<char> back(in.size());
+    void *d_o;
+    CK(hipMalloc(&d_o, std::max<size_t>(*std::max_element(sizes.begin(), sizes.end()), 1)));
+    for (size_t i = 0; i < n; i++) {
+      size_t got = sizes[i];
+      bool last = false;
+      st = sm.decompress_chunk(d_out[i], fsz[i], d_o, &got, &last, 0);
+      if (st != Status::SUCCESS || got != sizes[i]) { fprintf(stderr, "decompress_chunk %zu: %s, %zu B\n", i, status_to_string(st), got); return 4; }
+      CK(hipMemcpy(back.data() + offs[i], d_o, sizes[i], hipMemcpyDeviceToHost));
     }
     dump(dir + "/back.bin", back.data(), back.size());
   } else {

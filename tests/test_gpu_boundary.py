@@ -120,3 +120,23 @@ def test_nvcomp_single_buffer_c_api(libzstd):
             assert us.value == n and torch.equal(back, din)
     finally:
         L.nvcomp_zstd_destroy_manager_v5(h)
+
+
+@pytest.mark.parametrize("formatted", [False, True])
+@pytest.mark.parametrize("history", [0, 1])
+def test_streaming_with_dictionary(tmp_path, libzstd, formatted, history):
+    """ZstdStreamingManager::set_dictionary, then compress_chunk (history 0) or
+    compress_chunk_with_history (1) over 5 chunks and decompress_chunk in order: the stream
+    comes back (chunks of their own decode with the dictionary, not with the decoded window;
+    advisor round 2).  Chunks of their own equal the oracle's frame with the dictionary and
+    decode with libzstd ZSTD_decompress_usingDict."""
+    recs = [T.gen(T.DG_JSON, 1, 0x5EED0005, 16384, first=i) for i in range(64)]
+    dct = T.zdict_train(recs, 32768) if formatted else b"".join(r.tobytes() for r in recs[:2])
+    datas = [T.gen(T.DG_JSON, 1, 0x5EED0005, n, first=100 + i) for i, n in enumerate([16384, 40000, 65536, 777, 30000])]
+    (tmp_path / "dict.bin").write_bytes(dct)
+    frames = _run("stream_dict", datas, tmp_path, str(history))
+    assert (tmp_path / "back.bin").read_bytes() == b"".join(d.tobytes() for d in datas)
+    if not history:
+        for k, (f, d) in enumerate(zip(frames, datas)):
+            assert f == T.oracle_frame(d, dictionary=dct), f"chunk {k}"
+            assert T.zstd_decompress(f, len(d), dictionary=dct) == d.tobytes()
