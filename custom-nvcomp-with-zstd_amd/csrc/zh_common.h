@@ -34,7 +34,8 @@ enum : u32 {
 };
 
 // Per-block workspace carved from the caller's temp buffer.
-//   seq   : ZH_SEQ_CAP u64 records (K1: cumLit | ml<<17 | off<<32; K2 rewrites in place)
+//   seq   : ZH_SEQ_CAP u64 records (K1: walk literals before the match | len << 17 | catch-up << 24 |
+//           off << 36, the literal run being walk literals - catch-up; K2 rewrites them in place)
 //   lits  : ZH_BLOCK_MAX literal bytes; once the literals section is written, the
 //           sequences' FSE states and codes in encoding order in the segment-interleaved
 //           layout of the chain kernel (below): states u16 [0, 128 L), codes u8 [128 L, 192 L),

@@ -1413,10 +1413,13 @@ extern "C" __global__ __launch_bounds__(K2_THREADS) void zh_entropy_kernel(const
         u32 const i = base + lane;
         bool const valid = i < nseq_raw;
         u64 const rec = ring.next(seq, nseq_raw, i);
-        u32 const cum = (u32)(rec & 0x1FFFFu), ml = (u32)((rec >> 17) & 0x7FFFu), off = (u32)((rec >> 32) & 0x1FFFFu);
+        // K1 record: the walk's literals before the match | length | catch-up | offset; the
+        // catch-up e moves e bytes of the literal run into the match (zh_lz.hip)
+        u32 const cum = (u32)(rec & 0x1FFFFu), ce = (u32)((rec >> 24) & 0xFFFu);
+        u32 const ml = (u32)((rec >> 17) & 0x7Fu) + ce, off = (u32)((rec >> 36) & 0x1FFFFu);
         u32 pc = wave_shr1(cum), po = wave_shr1(off);
         if (lane == 0) { pc = carryCum; po = carryOff; }
-        u32 const ll = cum - pc;
+        u32 const ll = cum - pc - ce;
         bool const flag = valid && i > 0 && ll == 0 && off == po;
         bool const head = valid && !flag;
         u64 const hm = __ballot(head);

@@ -11,7 +11,8 @@
 //   in[]   the block, staged once with 16-B loads (64 KiB)
 //   TL/TS  2 x 2^14 u16 hash tables, entry = position + 1 (0 = empty)
 //   cinfo  one 4096-position window: candidates -> match info (off<<8|len) in place
-//   hm/lm  per 64-position segment: has-match and literal bit masks
+//   tm     take masks (per 64-position round); per walk segment: the walk's literal and match
+//          bits, the literal bits after catch-up, the end of its last match
 //   mlist  the window's matches in position order, with their catch-up lengths
 // Wave roles (wave specialisation, synchronised with workgroup barriers):
 //   waves 14, 15  inserters: one wave per hash table walks the next window's
@@ -77,15 +78,16 @@ constexpr u32 CI_WORDS = ZH_WINDOW + 8;  // + the lookahead slots of positions `
 __device__ __forceinline__ u32 cidx(u32 i) { return i; }
 // two cinfo buffers: window k's candidates / match info in buffer k & 1 (the parse of window k
 // overlaps the lengths of window k + 1)
-constexpr u32 OFF_HM = OFF_CI + 2 * 4 * CI_WORDS;    // per buffer u64 per round: positions with a match
-constexpr u32 OFF_LM = OFF_HM + 2 * 8 * NROUND;      // u32 per walk segment: literal positions
+constexpr u32 OFF_HM = OFF_CI + 2 * 4 * CI_WORDS;    // per buffer u64 per round: take masks (see span_lengths)
+constexpr u32 OFF_SEGM = OFF_HM + 2 * 8 * NROUND;    // per window parity, per walk segment (u32 each):
+constexpr u32 SEGM_WALK_LIT = 0, SEGM_MATCH = 1, SEGM_LIT = 2, SEGM_END = 3;  // the walk's literal bits, its
+// match starts, the literal bits left after catch-up, the end of the segment's last match
+__device__ __forceinline__ u32 segm(u32 par, u32 kind) { return (4 * par + kind) * NSEG; }
 constexpr u32 ML_CAP = ((ZH_WINDOW + ZH_MIN_MATCH_SHORT - 1) / ZH_MIN_MATCH_SHORT + 12 + 3) & ~3u;  // matches per window
-constexpr u32 OFF_ML = OFF_LM + 4 * NSEG;            // the window's match starts (window index), in order
-constexpr u32 OFF_ME = OFF_ML + 4 * ML_CAP;          // their starts after catch-up
-constexpr u32 OFF_MR = OFF_ME + 4 * ML_CAP;          // their (length after catch-up) | offset << 13
+constexpr u32 OFF_ML = OFF_SEGM + 4 * 8 * NSEG;      // the parsed window's match starts, in order
 constexpr u32 XQ_CAP = 192;                          // chain-end queue entries per worker wave
-constexpr u32 OFF_XQ = OFF_MR + 4 * ML_CAP;          // u16 per entry: window index | S << 15
-constexpr u32 OFF_MISC = OFF_XQ + 2 * XQ_CAP * NWW;  // [1] matches of the window being recorded
+constexpr u32 OFF_XQ = OFF_ML + 4 * ML_CAP;          // u16 per entry: window index | S << 15
+constexpr u32 OFF_MISC = OFF_XQ + 2 * XQ_CAP * NWW;  // [2 par + 0] matches, [2 par + 1] first parsed position
 constexpr u32 K1_LDS = OFF_MISC + 4 * 16;
 constexpr u32 MISC_ARR = 12;  // misc[12]: worker-wave barrier arrivals (cumulative)
 static_assert(K1_LDS <= 163840 - 256, "K1 LDS budget");
@@ -131,17 +133,19 @@ __device__ __forceinline__ u32 prefix8(const u32 *in32, u32 b, u32 olo, u32 ohi)
 // block end read LDS padding / tables and are cut off by n - p later.
 __device__ __forceinline__ u32 ext8(const u32 *in32, u32 p, u32 c, bool act) {
   constexpr u32 NW = ZH_MAX_MATCH / 4;  // dwords of a capped match
+  constexpr u32 H = 4;                  // dwords per step: 16 bytes, early exit (a whole-match batch
+                                        // of loads costs more LDS time than it saves in latency)
   u32 const wp = p >> 2, sp = p & 3, wq = c >> 2, sq = c & 3;
   u32 l = ZH_MAX_MATCH;
 #pragma unroll
-  for (u32 k0 = 2; k0 < NW; k0 += 4) {
+  for (u32 k0 = 2; k0 < NW; k0 += H) {
     if (!__ballot(act && l == ZH_MAX_MATCH)) break;
-    u32 A[5], B[5];
+    u32 A[H + 1], B[H + 1];
 #pragma unroll
-    for (u32 k = 0; k < 5; k++) { A[k] = in32[wp + k0 + k]; B[k] = in32[wq + k0 + k]; }
+    for (u32 k = 0; k <= H; k++) { A[k] = in32[wp + k0 + k]; B[k] = in32[wq + k0 + k]; }
     u32 lh = ZH_MAX_MATCH;
 #pragma unroll
-    for (int k = 3; k >= 0; k--) {
+    for (int k = (int)H - 1; k >= 0; k--) {
       if (k0 + (u32)k >= NW) continue;
       u32 const x = __builtin_amdgcn_alignbyte(A[k + 1], A[k], sp) ^ __builtin_amdgcn_alignbyte(B[k + 1], B[k], sq);
       if (x) lh = 4 * (k0 + (u32)k) + (__builtin_ctz(x) >> 3);
@@ -347,6 +351,31 @@ __device__ __forceinline__ u32 bit_range32(u32 a, u32 b) {
   return hi & ~((1u << a) - 1u);
 }
 
+// ---- the parse step rule ---------------------------------------------------------------------
+// Match info words: off << 8 | len (off < 2^16).
+// Parse cost of a match: libzstd's lazy "gain" (4 per byte, minus the offset's bit length)
+__device__ __forceinline__ int match_gain(u32 inf) {
+  return (inf & 255u) ? 4 * (int)(inf & 255u) - (31 - (int)__builtin_clz(((inf >> 8) & 0xFFFFu) + 1u)) : -1000;
+}
+// The serial parse at a position with a match (inf) takes it unless the match at the next
+// position is longer (levels < 9) -- or, LAZY2 (levels >= 9), unless the match at
+// the next position gains more than 4 over it or the one after more than 7 (libzstd
+// ZSTD_compressBlock_lazy_generic, depth 2).
+template <bool LAZY2>
+__device__ __forceinline__ bool take_rule(u32 inf, u32 inf1, u32 inf2) {
+  if (LAZY2) {
+    int const g0 = match_gain(inf);
+    return match_gain(inf1) <= g0 + 4 && match_gain(inf2) <= g0 + 7;
+  }
+  return (inf1 & 255u) <= (inf & 255u);
+}
+
+// The 4 bytes in[a-4, a) (a >= 1; bytes before the buffer start read as 0s shifted out)
+__device__ __forceinline__ u32 ld4_before(const u32 *in32, u32 a) {
+  u32 const t = a >= 4 ? a - 4 : 0u, w = t >> 2, sh = t & 3;
+  u32 const v = __builtin_amdgcn_alignbyte(in32[w + 1], in32[w], sh);
+  return a >= 4 ? v : v << (8 * (4 - a));
+}
 // ---- match lengths, lanes = positions -------------------------------------------------------
 // A worker wave takes a span of consecutive 64-position rounds in three passes:
 //  A  (rounds high to low) per position and candidate the common prefix of the first 8 bytes
@@ -355,6 +384,13 @@ __device__ __forceinline__ u32 bit_range32(u32 a, u32 b) {
 //  B  the queued chain ends extended, lanes = queue entries, results into their cinfo byte;
 //  C  (rounds high to low) lengths from the chain structure -> match info in place.
 constexpr u32 MAX_RW = 3;   // rounds per worker wave
+// Rounds (64-position segments) of worker wave w in a window's length phase: waves 1..13
+// (wave 0 parses), by SIMD (a CU's waves go to SIMDs by wave id mod 4): three for the waves on
+// SIMDs 0 and 1 but wave 13 (it takes the window's top span and the lookahead positions), two
+// for the waves sharing SIMDs 2 and 3 with the inserters.  3 x 6 + 2 x 7 = 32.
+__device__ __forceinline__ u32 rounds_of(u32 w) {
+  return w == 0 ? 0u : (((w & 3u) == 1u && w != 13u) || (w & 3u) == 0u) ? 3u : 2u;
+}
 
 // Length of position p's candidate from the chain structure: T = ballot of the chain ends
 // (lanes whose lcp is their own: fewer than 8 bytes, or the next position does not continue
@@ -382,29 +418,50 @@ __device__ __forceinline__ void xq_flush(const u32 *in32, u32 *ci, const u16 *xq
 enum : u32 { LF_FL = 1u << 8, LF_FS = 1u << 9, LF_XL = 1u << 10, LF_XS = 1u << 11, LF_SL = 1u << 12 };
 
 // The match lengths of rounds [r_lo, r_hi) (r_hi - r_lo <= MAX_RW): candidates in cinfo ->
-// match info (off << 8 | len, 0 = none) in place + the rounds' has-match masks.  Semantics of
-// oracle/zstd_oracle.c orc_lz_match_info: lcp capped at ZH_MAX_MATCH and at the block end,
-// long candidates from 8 bytes, short from 5, the longer (long on ties).
-__device__ __forceinline__ void span_lengths(const u32 *in32, u32 *ci, u64 *hm, u16 *xq, u32 r_lo, u32 r_hi, u32 wsb, u32 we, u32 n, u32 lim,
-                                             u32 lane) {
+// match info (off << 8 | len, 0 = none) in place.  Semantics of oracle/zstd_oracle.c
+// orc_lz_match_info: lcp capped at ZH_MAX_MATCH and at the block end, long candidates from 8
+// bytes, short from 5, the longer (long on ties).  Then per position whether the parse takes its
+// match if it gets there (take_rule on the next positions' info: DPP within the round, the
+// round above by carry; la1 / la2 = the two positions above the span when it is the window's
+// top one) -> the rounds' take masks tm.  At the top of a span that is not the window's top the next positions
+// belong to another wave: those take bits stay clear and wave 0 decides them (span_tops).
+template <bool LAZY2>
+__device__ __forceinline__ void span_lengths(const u32 *in32, u32 *ci, u64 *tm, u16 *xq, u32 r_lo, u32 r_hi, u32 wsb, u32 we, u32 n, u32 lim,
+                                             u32 lane, bool top, u32 la1, u32 la2) {
   u32 cwr[MAX_RW], flg[MAX_RW];
+  // pass A, rounds high to low: a round's candidates, own bytes and candidate bytes are loaded
+  // at the top of the round (hoisting every round's loads to the top of the pass was slower:
+  // the longer LDS bursts delay the inserter waves, which are on the step's critical path)
+  u32 olo[MAX_RW], ohi[MAX_RW], Lw[MAX_RW][3], Sw[MAX_RW][3];
+  auto loadA = [&](u32 k) {
+    u32 const r = r_hi - 1 - min(k, r_hi - 1 - r_lo), i = 64 * r + lane, p = wsb + i;  // (rounds past the span: repeat the last)
+    bool const hv = p < we && p < lim;
+    u32 const cw0 = ci[cidx(i)];
+    u32 const cw = hv ? cw0 : 0u;
+    cwr[k] = cw;
+    ld64u(in32, p, olo[k], ohi[k]);
+    u32 const cL = cw & 0xFFFFu, cS = cw >> 16;
+    u32 const aL = (cL ? cL - 1u : 0u) >> 2, aS = (cS ? cS - 1u : 0u) >> 2;
+#pragma unroll
+    for (u32 t = 0; t < 3; t++) { Lw[k][t] = in32[aL + t]; Sw[k][t] = in32[aS + t]; }
+  };
   u32 ccL = 0, ccS = 0;  // candidates of the position above the round being processed
   u32 nq = 0;            // queued entries (wave-uniform)
 #pragma unroll
   for (u32 k = 0; k < MAX_RW; k++) {
-    cwr[k] = 0;
     flg[k] = 0;
-    if (r_lo + k >= r_hi) continue;
-    u32 const r = r_hi - 1 - k, i = 64 * r + lane, p = wsb + i;
-    bool const hv = p < we && p < lim;
-    u32 const cw0 = ci[cidx(i)];
-    u32 const cw = hv ? cw0 : 0u;
+    if (r_lo + k >= r_hi) { cwr[k] = 0; continue; }
+    loadA(k);
+    u32 const r = r_hi - 1 - k, i = 64 * r + lane;
+    u32 const cw = cwr[k];
     u32 const cL = cw & 0xFFFFu, cS = cw >> 16;
-    u32 lo, hi;
-    ld64u(in32, p, lo, hi);
-    u32 const tL = prefix8(in32, cL ? cL - 1u : 0u, lo, hi);
-    u32 const tS = prefix8(in32, cS ? cS - 1u : 0u, lo, hi);
-    u32 const pL = cL ? tL : 0u, pS = cS ? tS : 0u;
+    auto pref = [&](u32 c, const u32 (&w)[3]) {
+      u32 const sh = (c ? c - 1u : 0u) & 3u;
+      u32 const x = olo[k] ^ __builtin_amdgcn_alignbyte(w[1], w[0], sh), y = ohi[k] ^ __builtin_amdgcn_alignbyte(w[2], w[1], sh);
+      u32 const cx = __builtin_ctzg(x, 32), cy = __builtin_ctzg(y, 32);
+      return c ? (x ? cx : 32u + cy) >> 3 : 0u;
+    };
+    u32 const pL = pref(cL, Lw[k]), pS = pref(cS, Sw[k]);
     u32 cLn = wave_shl1(cL), cSn = wave_shl1(cS);
     cLn = lane == 63 ? ccL : cLn;
     cSn = lane == 63 ? ccS : cSn;
@@ -412,7 +469,6 @@ __device__ __forceinline__ void span_lengths(const u32 *in32, u32 *ci, u64 *hm, 
     bool const xL = pL == 8 && !fL;
     bool const sL = cS == cL && xL && pS == 8 && !fS;  // S takes L's extension
     bool const xS = pS == 8 && !fS && !sL;
-    cwr[k] = cw;
     flg[k] = pL | (pS << 4) | (fL ? LF_FL : 0u) | (fS ? LF_FS : 0u) | (xL ? LF_XL : 0u) | (xS ? LF_XS : 0u) | (sL ? LF_SL : 0u);
     ccL = lane_value(cL, 0);
     ccS = lane_value(cS, 0);
@@ -430,20 +486,36 @@ __device__ __forceinline__ void span_lengths(const u32 *in32, u32 *ci, u64 *hm, 
     }
   }
   if (nq) xq_flush(in32, ci, xq, nq, wsb, lane);
-  // pass C
-  u32 clL = 0, clS = 0;  // lcps of the position above the round
-#pragma unroll
-  for (u32 k = 0; k < MAX_RW; k++) {
-    if (r_lo + k >= r_hi) continue;
-    u32 const r = r_hi - 1 - k, i = 64 * r + lane, p = wsb + i;
-    u32 const f = flg[k], cw = cwr[k];
-    u32 const cL = cw & 0xFFFFu, cS = cw >> 16;
+  // pass C.  C1: every round's chain lengths without the carry (the ds_bpermutes of all rounds
+  // in flight together); C2, rounds high to low: lanes whose chain runs past the round take the
+  // carry, then the match info and the take decision.
+  u32 lLr[MAX_RW], lSr[MAX_RW], runs[MAX_RW];
+  auto c1 = [&](u32 k) {
+    u32 const r = r_hi - 1 - min(k, r_hi - 1 - r_lo), i = 64 * r + lane;
+    u32 const f = flg[k];
     u32 const ce = ci[cidx(i)];
     u32 const pL = f & 15u, pS = (f >> 4) & 15u;
     u32 const eL = (f & LF_XL) ? (ce & 255u) : pL;
     u32 const eS = (f & LF_XS) ? ((ce >> 16) & 255u) : ((f & LF_SL) ? eL : pS);
-    u32 const lL = chain_lcp(__ballot(!(f & LF_FL)), eL, clL, lane);
-    u32 const lS = chain_lcp(__ballot(!(f & LF_FS)), eS, clS, lane);
+    u64 const RL = __ballot(!(f & LF_FL)) >> lane, RS = __ballot(!(f & LF_FS)) >> lane;
+    u32 const qL = RL ? ctz64(RL) : 64u - lane, qS = RS ? ctz64(RS) : 64u - lane;
+    u32 const vL = bperm(eL, min(lane + qL, 63u)), vS = bperm(eS, min(lane + qS, 63u));
+    lLr[k] = RL ? min((u32)ZH_MAX_MATCH, qL + vL) : qL;  // (a chain running past: + carry in C2)
+    lSr[k] = RS ? min((u32)ZH_MAX_MATCH, qS + vS) : qS;
+    runs[k] = (RL ? 0u : 1u) | (RS ? 0u : 2u);
+  };
+#pragma unroll
+  for (u32 k = 0; k < MAX_RW; k++) c1(k);
+  u32 clL = 0, clS = 0;  // lcps of the position above the round
+  u32 cv1 = la1, cv2 = la2;  // infos of the two positions above the round
+#pragma unroll
+  for (u32 k = 0; k < MAX_RW; k++) {
+    if (r_lo + k >= r_hi) continue;
+    u32 const r = r_hi - 1 - k, i = 64 * r + lane, p = wsb + i;
+    u32 const cw = cwr[k];
+    u32 const cL = cw & 0xFFFFu, cS = cw >> 16;
+    u32 const lL = (runs[k] & 1u) ? min((u32)ZH_MAX_MATCH, lLr[k] + clL) : lLr[k];
+    u32 const lS = (runs[k] & 2u) ? min((u32)ZH_MAX_MATCH, lSr[k] + clS) : lSr[k];
     clL = lane_value(lL, 0);
     clS = lane_value(lS, 0);
     u32 const capj = min((u32)ZH_MAX_MATCH, n - min(p, n));
@@ -453,9 +525,17 @@ __device__ __forceinline__ void span_lengths(const u32 *in32, u32 *ci, u64 *hm, 
     bool const useL = mL && mL >= mS;
     u32 const ml = useL ? mL : mS, cm = useL ? cL : cS;
     u32 const v = ml ? ((p - (cm - 1u)) << 8) | ml : 0u;
+    u32 v1 = wave_shl1(v);
+    v1 = lane == 63 ? cv1 : v1;
+    u32 v2 = wave_shl1(v1);
+    v2 = lane == 63 ? cv2 : v2;
+    cv1 = lane_value(v, 0);
+    cv2 = lane_value(v, 1);
+    bool const unk = k == 0 && !top && (lane == 63 || (LAZY2 && lane == 62));
+    bool const tk = v != 0 && !unk && take_rule<LAZY2>(v, v1, v2);
     ci[cidx(i)] = v;
-    u64 const hb = __ballot(v != 0);
-    if (lane == 0) hm[r] = hb;
+    u64 const tb = __ballot(tk);
+    if (lane == 0) tm[r] = tb;
   }
 }
 
@@ -481,12 +561,6 @@ __device__ __forceinline__ u32 info_one(const u32 *in32, u32 p, u32 cw, u32 n, u
 }
 
 // ---- catch-up ----------------------------------------------------------------------------------
-// The 4 bytes in[a-4, a) (a >= 1; bytes before the buffer start read as 0s shifted out)
-__device__ __forceinline__ u32 ld4_before(const u32 *in32, u32 a) {
-  u32 const t = a >= 4 ? a - 4 : 0u, w = t >> 2, sh = t & 3;
-  u32 const v = __builtin_amdgcn_alignbyte(in32[w + 1], in32[w], sh);
-  return a >= 4 ? v : v << (8 * (4 - a));
-}
 // Bytes a match at staged position P with offset off grows backwards (oracle orc_lz_parse_pre's
 // catch-up): while P - e > lo and P - e > off and in[P-e-1] == in[P-e-1-off].  Compared four
 // bytes at a time from the top byte down; at most a few steps.
@@ -505,34 +579,13 @@ __device__ __forceinline__ u32 catch_up(const u32 *in32, u32 P, u32 off, u32 lo,
 }
 
 // ---- the parse, lanes = segments --------------------------------------------------------------
-// Parse cost of a match: libzstd's lazy "gain" (4 per byte, minus the offset's bit length)
-__device__ __forceinline__ int match_gain(u32 inf) {
-  return inf ? 4 * (int)(inf & 255u) - (31 - (int)__builtin_clz((inf >> 8) + 1u)) : -1000;
-}
-
-// The serial parse's step at window index i with match info inf = ci[i] != 0: take the match
-// unless the one at i+1 is longer (levels < 9) -- or, LAZY2 (levels >= 9), unless
-// the match at i+1 gains more than 4 over it or the one at i+2 more than 7 (libzstd
-// ZSTD_compressBlock_lazy_generic, depth 2).  ci[wn..] holds the next window's first two
-// positions (or 0 past the block).
-template <bool LAZY2>
-__device__ __forceinline__ bool take_at(const u32 *ci, u32 i, u32 inf) {
-  u32 const inf1 = ci[cidx(i + 1)];
-  if (LAZY2) {
-    u32 const inf2 = ci[cidx(i + 2)];
-    int const g0 = match_gain(inf);
-    return match_gain(inf1) <= g0 + 4 && match_gain(inf2) <= g0 + 7;
-  }
-  return (inf1 & 255u) <= (inf & 255u);
-}
-
-// Walk of segment [S, SE) from position p by the lanes `act`: literal runs are skipped through
-// the has-match mask hmk, every position with a match candidate is one step.  LM / MM: the
+// Walk of segment [S, SE) from position p by the lanes `act`: the take mask tmk names the
+// positions where the parse takes a match once it gets there, so every step is one run of
+// literals (the positions before the next take bit) and the match after it.  LM / MM: the
 // segment's literal and match-start bits, ex: the exit (first position >= SE).  With old
 // visited bits (a Jacobi re-walk from a new entry), the walk stops where it meets a position
 // the old walk visited -- from there on both are the same -- and keeps the old bits above it.
-template <bool LAZY2>
-__device__ __forceinline__ void seg_walk(const u32 *ci, u32 hmk, u32 S, u32 SE, u32 p, bool act0, u32 &LM, u32 &MM, u32 &ex) {
+__device__ __forceinline__ void seg_walk(const u32 *ci, u32 tmk, u32 S, u32 SE, u32 p, bool act0, u32 &LM, u32 &MM, u32 &ex) {
   u32 const old = act0 ? (LM | MM) : 0u;
   u32 nl = 0, nm = 0;
   bool act = act0 && p < SE, merged = false;
@@ -541,22 +594,18 @@ __device__ __forceinline__ void seg_walk(const u32 *ci, u32 hmk, u32 S, u32 SE, 
   // position after it, or the point where the walk meets the old one
   while (__ballot(act)) {
     u32 const o = min(p - S, SEGP - 1);
-    u32 const m = hmk >> o, ov = old >> o;
+    u32 const m = tmk >> o, ov = old >> o;
     u32 const q = m ? p + (u32)__builtin_ctz(m) : SE;
     u32 const x = ov ? p + (u32)__builtin_ctz(ov) : ~0u;
     bool const mg = act && x <= q;
     bool const st = act && !mg && q < SE;
     u32 const re = mg ? x : q;
     nl |= act ? bit_range32(o, re - S) : 0u;
-    u32 const qq = st ? q : 0u;
-    u32 const inf = ci[cidx(qq)];
-    bool const tk = st && take_at<LAZY2>(ci, qq, inf);
-    u32 const b = st ? 1u << (q - S) : 0u;
-    nm |= tk ? b : 0u;
-    nl |= tk ? 0u : b;
+    u32 const len = ci[cidx(st ? q : 0u)] & 255u;
+    nm |= st ? 1u << (q - S) : 0u;
     mpos = mg ? x - S : mpos;
     merged = merged || mg;
-    p = mg ? p : (st ? q + (tk ? (inf & 255u) : 1u) : (act ? q : p));
+    p = mg ? p : (st ? q + len : (act ? q : p));
     act = act && !mg && p < SE;
   }
   if (act0) {
@@ -572,12 +621,13 @@ __device__ __forceinline__ void seg_walk(const u32 *ci, u32 hmk, u32 S, u32 SE, 
   }
 }
 
-// Inserter wave main loop.  Step k (the workers' window step: lengths of window k, parse of
-// window k - 1) opens with barrier P once window k's candidates are dumped into cinfo buffer
-// k & 1, and the inserters then build window k + 1's candidates in registers.  They take the
-// step's barrier X only once all 14 worker waves have arrived there (an LDS arrival counter),
-// between two tiles, so the insertion spreads over the whole step.
-constexpr u32 WIN_BARRIERS = 1;  // X (window k's lengths and window k - 1's parse done)
+// Inserter wave main loop.  Step k of the workers (the lengths of window k, the parse and
+// records of window k - 1, then its literals) opens with barrier P once window k's candidates
+// are dumped into cinfo buffer k & 1, and the inserters then build window k + 1's candidates in
+// registers.  They take the step's barrier X only once
+// all 14 worker waves have arrived there (an LDS arrival counter), between two tiles, so the
+// insertion spreads over the whole step.
+constexpr u32 WIN_BARRIERS = 1;  // X
 template <bool LONG>
 __device__ __forceinline__ void inserter_loop(const u32 *in32, u16 *T, u8 *ci8, u32 *misc_, u32 n, u32 lim, u32 lane, u32 *dbg, u32 wstart,
                                               u32 pmin, u32 span_s, u32 span_e) {
@@ -588,10 +638,11 @@ __device__ __forceinline__ void inserter_loop(const u32 *in32, u16 *T, u8 *ci8, 
 #ifdef ZH_STAMPS
   u32 st_ins = 0;
 #endif
+  u32 const nwin = (n - wstart + ZH_WINDOW - 1) / ZH_WINDOW;
   u32 passed = 0;  // X barriers taken so far
-  for (u32 wsb = wstart, kb = 0;; wsb += ZH_WINDOW, kb ^= 1u) {
-    bool const have = wsb < n;
-    if (have) dump_window<LONG>(ci8 + kb * 4 * CI_WORDS, lane, creg, cwe);
+  for (u32 k = 0; k < nwin + 1; k++) {
+    u32 const wsb = wstart + k * ZH_WINDOW;
+    if (k < nwin) dump_window<LONG>(ci8 + (k & 1u) * 4 * CI_WORDS, lane, creg, cwe);
     __syncthreads();  // P: candidates of window k in buffer k & 1
     u32 const done = passed + WIN_BARRIERS;
     // arr: the arrival counter as read with the last tile's read-back; a barrier taken
@@ -607,12 +658,11 @@ __device__ __forceinline__ void inserter_loop(const u32 *in32, u16 *T, u8 *ci8, 
     u64 const ti0 = __builtin_amdgcn_s_memtime();
 #endif
     u32 const nx = wsb + ZH_WINDOW;
-    if (nx < n) insert_window<LONG>(in32, T, nx, min(nx + ZH_WINDOW, n), lim, lane, creg, cwe, &misc_[MISC_ARR], take_ready);
+    if (k + 1 < nwin) insert_window<LONG>(in32, T, nx, min(nx + ZH_WINDOW, n), lim, lane, creg, cwe, &misc_[MISC_ARR], take_ready);
 #ifdef ZH_STAMPS
     st_ins += (u32)(__builtin_amdgcn_s_memtime() - ti0);
 #endif
     while (passed < done) { __syncthreads(); passed++; }
-    if (!have) break;
   }
 #ifdef ZH_STAMPS
   if (LONG && lane == 0) dbg[16] = st_ins;
@@ -714,7 +764,7 @@ __device__ __forceinline__ u32 lz_block(const ZhBlockDesc *__restrict__ blocks, 
   u64 const rt0 = __builtin_amdgcn_s_memrealtime();
   u64 stamp_prev = __builtin_amdgcn_s_memtime();
   u64 const mt0 = stamp_prev;
-  u32 st_stage = 0, st_A = 0, st_X = 0, st_E1 = 0, st_Bmax = 0, st_Imax = 0, st_Bw = 0, st_B = 0, st_J = 0, st_E = 0, st_E2 = 0, st_rounds = 0;
+  u32 st_stage = 0, st_A = 0, st_X = 0, st_E1 = 0, st_Bmax = 0, st_Imax = 0, st_Bw = 0, st_B = 0, st_J = 0, st_E = 0, st_E2 = 0, st_rounds = 0, st_J1 = 0, st_J2 = 0, st_J3 = 0;
 #endif
 
   // ---- stage the block into LDS (16 B per lane when the source allows it) and probe RLE
@@ -846,51 +896,62 @@ __device__ __forceinline__ u32 lz_block(const ZhBlockDesc *__restrict__ blocks, 
 
   u32 const tid_ = tid;
   u32 const wave = tid >> 6;
-  // rounds (64-position segments) of this worker wave in the length phase: waves 1..13 (wave 0
-  // parses), three for the waves on SIMDs 0 and 1, two for those sharing SIMDs 2 and 3 with the
-  // inserters (a CU's waves go to SIMDs by wave id mod 4) and wave 13 (the lookahead positions)
-  auto rounds_of = [](u32 w) { return w == 0 ? 0u : ((w & 2u) || w == 13) ? MAX_RW - 1 : MAX_RW; };
   u32 r_lo = 0;
   for (u32 w = 0; w < wave; w++) r_lo += rounds_of(w);
   u32 const r_hi = r_lo + rounds_of(wave);
   u32 *const ci0 = ci;
-  u32 *mlist = (u32 *)(smem + OFF_ML), *mext = (u32 *)(smem + OFF_ME), *mrec = (u32 *)(smem + OFF_MR);
-  u32 *lm32 = (u32 *)(smem + OFF_LM);
+  u32 *const sgm = (u32 *)(smem + OFF_SEGM);
   u16 *const xq = (u16 *)(smem + OFF_XQ) + XQ_CAP * wave;
-  // Step k: the lengths of window k (waves 1..13) beside the parse + catch-up of window k - 1
-  // (wave 0); barrier X; window k - 1's records and literals (all worker waves).
-  for (u32 wsb = wstart, kb = 0;; wsb += ZH_WINDOW, kb ^= 1u) {
-    bool const have = wsb < n;
+  u32 const nwin = (n - wstart + ZH_WINDOW - 1) / ZH_WINDOW;
+  u32 *const mlist = (u32 *)(smem + OFF_ML);
+  u32 nwalk_tot = 0;  // the walk's literal count before the parsed window (records carry it)
+  // Step k (window j at wstart + j * ZH_WINDOW, parity j & 1):
+  //   phase A  lengths of window k (waves 1..13) | parse, catch-up and sequence records of
+  //            window k - 1 (wave 0)
+  //   X
+  //   phase B  take decisions at window k's span tops (wave 1), the literals of window k - 1
+  //            (lanes = positions, all worker waves)
+  for (u32 k = 0; k < nwin + 1; k++) {
+    u32 const wsb = wstart + k * ZH_WINDOW;
     u32 const we = min(wsb + ZH_WINDOW, n);
-    u32 const wsp = wsb - ZH_WINDOW, wep = min(wsb, n);  // window k - 1 (when wsb > wstart)
-    bool const prev = wsb > wstart && wep > pre;  // window k - 1 has positions to parse
+    u32 const kb = k & 1u;
+    bool const have = k < nwin && we > pre;                    // window k: lengths
+    u32 const wsp = wsb - ZH_WINDOW, wep = min(wsp + ZH_WINDOW, n);
+    bool const prev = k >= 1 && wep > pre;                     // window k - 1: parse, records, literals
     // opaque per-step thread index: keeps the compiler from hoisting every LDS address
     // derived from it out of the loop (they would be spilled to scratch)
     u32 tid;
     __asm__ volatile("v_mov_b32 %0, %1" : "=v"(tid) : "v"(tid_));
     u32 const lane = tid & 63;
     u32 *const ciK = ci0 + kb * CI_WORDS, *const ciP = ci0 + (kb ^ 1u) * CI_WORDS;
-    u64 *const hmK = hm + kb * NROUND, *const hmP = hm + (kb ^ 1u) * NROUND;
+    u64 *const tmK = hm + kb * NROUND, *const tmP = hm + (kb ^ 1u) * NROUND;
+    u32 *const lmf = sgm + segm(0, SEGM_LIT);  // window k - 1's literal bits after catch-up
     __syncthreads();  // P: candidates of window k in buffer k & 1
     ZH_STAMP(st_A);
-    if (have && we > pre && wave != 0) {
-      span_lengths(in32, ciK, hmK, xq, r_lo, r_hi, wsb, we, n, lim, lane);
-      if (wave == NWW - 1 && lane < 2) {  // the lookahead positions `we`, `we + 1`
+    if (have && wave != 0) {
+      // the window's top span (wave 13) first takes the lookahead positions `we`, `we + 1`:
+      // the take decisions at the window's end need their info
+      u32 la1 = 0, la2 = 0;
+      if (wave == NWW - 1) {
         u32 const p = we + lane;
-        u32 const cw = ciK[cidx(ZH_WINDOW + lane)];
-        ciK[cidx(ZH_WINDOW + lane)] = info_one(in32, p, cw, n, lim, p < n);
+        u32 const cw = ciK[cidx(ZH_WINDOW + (lane & 1))];
+        u32 const li = info_one(in32, p, cw, n, lim, lane < 2 && p < n);
+        if (lane < 2) ciK[cidx(ZH_WINDOW + lane)] = li;
+        la1 = lane_value(li, 0);
+        la2 = lane_value(li, 1);
       }
+      span_lengths<LAZY2>(in32, ciK, tmK, xq, r_lo, r_hi, wsb, we, n, lim, lane, wave == NWW - 1, la1, la2);
       ZH_STAMP(st_B);
     }
     if (wave == 0 && prev) {
       // ---- the parse of window k - 1, lanes = 32-position segments
       u32 const wn = wep - wsp;
       u32 const S = SEGP * lane, SE = min(S + SEGP, wn);
-      u32 const hmk = (u32)(hmP[lane >> 1] >> (32 * (lane & 1)));
+      u32 const tmk = (u32)(tmP[lane >> 1] >> (32 * (lane & 1)));
       u32 const e0 = e_in - wsp;  // first parsed position (< 64 except in the window holding `pre`)
       u32 entry = lane == 0 ? e0 : max(S, e0), ex = entry;
       u32 LM = 0, MM = 0;
-      seg_walk<LAZY2>(ciP, hmk, S, SE, entry, true, LM, MM, ex);
+      seg_walk(ciP, tmk, S, SE, entry, true, LM, MM, ex);
       // Jacobi rounds: a segment's entry is its predecessor's exit
       for (;;) {
         u32 const pe = wave_shr1(ex);
@@ -900,77 +961,84 @@ __device__ __forceinline__ u32 lz_block(const ZhBlockDesc *__restrict__ blocks, 
         st_rounds++;
 #endif
         if (!__ballot(ch)) break;
-        seg_walk<LAZY2>(ciP, hmk, S, SE, ne, ch, LM, MM, ex);
+        seg_walk(ciP, tmk, S, SE, ne, ch, LM, MM, ex);
         entry = ne;
       }
       e_in = wsp + lane_value(ex, 63);
+      ZH_STAMP(st_J1);
       // the window's matches in position order
       u32 const ns = (u32)__popc(MM);
       u32 const is = wave_scan_incl(ns);
       u32 const nm = lane_value(is, 63);
-      lm32[lane] = LM;
-      u32 mm = MM, k = is - ns;
+      lmf[lane] = LM;
+      u32 const nwl = lane_value(wave_scan_incl((u32)__popc(LM)), 63);
+      u32 mm = MM, q = is - ns;
       while (__ballot(mm != 0)) {
         if (mm) {
-          mlist[k++] = S + (u32)__builtin_ctz(mm);
+          mlist[q++] = S + (u32)__builtin_ctz(mm);
           mm &= mm - 1u;
         }
       }
-      // catch-up, lanes = matches: a match's lower bound is the end of the match before it
-      // (the window's first parsed position for the first); the bytes it takes back are no
-      // longer literals
+      ZH_STAMP(st_J2);
+      // ---- catch-up and sequence records, lanes = matches.  A match's lower bound is the end
+      // of the match before it (the window's first parsed position for the first); it takes
+      // back e bytes of the literal run.  Record: the walk's literals before the match (its
+      // start - e0 - the lengths of the matches before it) | length | e | offset; K2 takes e off
+      // the literal run (zh_entropy.hip).
+      u32 covered = 0;  // walk lengths of the matches before this pass
       for (u32 j0 = 0; j0 < nm; j0 += 64) {
         u32 const j = j0 + lane;
         bool const v = j < nm;
         u32 const ms = v ? mlist[j] : 0u, inf = ciP[cidx(ms)];
         u32 const pm = (v && j) ? mlist[j - 1] : 0u;
         u32 const lo = (v && j) ? pm + (ciP[cidx(pm)] & 255u) : e0;
-        u32 const e = catch_up(in32, wsp + ms, inf >> 8, wsp + lo, v);
-        if (v) {
-          mext[j] = ms - e;
-          mrec[j] = ((inf & 255u) + e) | ((inf >> 8) << 13);
-        }
+        u32 const len = v ? inf & 255u : 0u, off = (inf >> 8) & 0xFFFFu;
+        u32 const e = catch_up(in32, wsp + ms, off, wsp + lo, v);
+        u32 const incl = wave_scan_incl(len);
+        u32 const cum = nwalk_tot + (ms - e0) - (covered + incl - len);
+        covered += lane_value(incl, 63);
+        if (v) seq_out[nseq_tot + j] = (u64)cum | ((u64)len << 17) | ((u64)e << 24) | ((u64)off << 36);
         if (e) {
           for (u32 g = (ms - e) / SEGP; g <= (ms - 1) / SEGP; g++) {
             u32 const a = max(ms - e, SEGP * g) - SEGP * g, bnd = min(ms - SEGP * g, SEGP);
-            atomicAnd(&lm32[g], ~bit_range32(a, bnd));
+            atomicAnd(&lmf[g], ~bit_range32(a, bnd));
           }
         }
       }
+      nwalk_tot += nwl;  // the window's walk literals (its last match may run past its end)
       if (lane == 0) misc[1] = nm;
       ZH_STAMP(st_J);
     }
     if (lane == 0) atomicAdd(&misc[MISC_ARR], 1u);
-    __syncthreads();  // X: window k's match info; window k - 1's literal masks and match records
+    __syncthreads();  // X: window k's match info and take masks; window k - 1's records and literal bits
     ZH_STAMP(st_X);
+    if (wave == 1 && have) {
+      // ---- take decisions at window k's span tops (the next positions were another wave's)
+      constexpr u32 PER = LAZY2 ? 2u : 1u;
+      u32 const w = 1u + lane / PER;
+      u32 rh = 0;
+      for (u32 v = 0; v <= min(w, NWW - 1); v++) rh += rounds_of(v);
+      bool const act = lane < PER * (NWW - 2);  // spans of waves 1..12
+      u32 const i = act ? 64 * rh - 1 - lane % PER : 0u;
+      u32 const inf = ciK[cidx(i)], inf1 = ciK[cidx(i + 1)], inf2 = ciK[cidx(i + 2)];
+      if (act && i < we - wsb && (inf & 255u) && take_rule<LAZY2>(inf, inf1, inf2)) atomicOr((unsigned long long *)&tmK[i >> 6], 1ull << (i & 63));
+    }
     if (prev) {
+      // ---- literals of window k - 1, lanes = positions (round r = segments 2r, 2r + 1)
       u32 const nm = __builtin_amdgcn_readfirstlane(misc[1]);
-      // literal offsets of the 64 segments (every wave the same scan: lane = segment)
-      u32 const lc = (u32)__popc(lm32[lane]), lincl = wave_scan_incl(lc), lb = lincl - lc;
-      u32 const nlw = lane_value(lincl, 63);
-      // ---- sequence records, lanes = matches: cumLit | ml << 17 | off << 32
-      for (u32 j0 = 64 * wave; j0 < nm; j0 += 64 * NWW) {
-        u32 const j = j0 + lane;
-        bool const v = j < nm;
-        u32 const st = v ? mext[j] : 0u, mr = v ? mrec[j] : 0u, g = st / SEGP;
-        u32 const lbg = bperm(lb, g);  // (all lanes: ds_bpermute sources)
-        u32 const cum = nlit_tot + lbg + (u32)__popc(lm32[g] & ((1u << (st % SEGP)) - 1u));
-        if (v) seq_out[nseq_tot + j] = (u64)cum | ((u64)(mr & 0x1FFFu) << 17) | ((u64)(mr >> 13) << 32);
-      }
-      // ---- literals, lanes = positions (round r = segments 2r, 2r + 1)
+      u32 const lc = (u32)__popc(lmf[lane]), lincl = wave_scan_incl(lc), lb = lincl - lc;
       for (u32 r = wave; r < NROUND; r += NWW) {
-        u64 const lm = ((u64)(u32)__builtin_amdgcn_readfirstlane(lm32[2 * r + 1]) << 32) | (u32)__builtin_amdgcn_readfirstlane(lm32[2 * r]);
+        u64 const lm = ((u64)(u32)__builtin_amdgcn_readfirstlane(lmf[2 * r + 1]) << 32) | (u32)__builtin_amdgcn_readfirstlane(lmf[2 * r]);
         u32 const lbr = lane_value(lb, 2 * r);
         if ((lm >> lane) & 1ull) {
           u32 const rank = __builtin_amdgcn_mbcnt_hi((u32)(lm >> 32), __builtin_amdgcn_mbcnt_lo((u32)lm, 0u));
           lit_out[nlit_tot + lbr + rank] = in[wsp + 64 * r + lane];
         }
       }
-      nlit_tot += nlw;
+      nlit_tot += lane_value(lincl, 63);
       nseq_tot += nm;
-      ZH_STAMP(st_E);
     }
-    if (!have) break;
+    ZH_STAMP(st_E);
   }
   if (tid == 0) { meta[0] = nseq_tot; meta[1] = nlit_tot; meta[2] = 0; }
 #ifdef ZH_STAMPS
@@ -980,7 +1048,7 @@ __device__ __forceinline__ u32 lz_block(const ZhBlockDesc *__restrict__ blocks, 
     dbg[25] = __builtin_amdgcn_s_getreg((31 << 11) | 4);   // HW_ID
     dbg[26] = __builtin_amdgcn_s_getreg((31 << 11) | 20);  // XCC_ID
     dbg[27] = (u32)(__builtin_amdgcn_s_memtime() - mt0);
-    dbg[40] = st_Bmax; dbg[41] = st_Imax;
+    dbg[40] = st_Bmax; dbg[41] = st_Imax; dbg[55] = st_J1; dbg[56] = st_J2; dbg[57] = st_J3;
     dbg[0] = st_stage; dbg[1] = st_A; dbg[2] = st_B; dbg[3] = st_J; dbg[4] = st_E; dbg[5] = st_rounds; dbg[20] = st_E2; dbg[21] = st_X; dbg[22] = st_E1;
   }
   if ((tid & 63) == 0 && tid < INS_TID) {  // each worker wave's length-phase cycles

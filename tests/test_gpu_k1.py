@@ -2,8 +2,8 @@
 back through the library's zh_test_lz hook) equals the oracle's parse
 (oracle/zstd_oracle.c orc_lz_parse: tile-lagged dual hash, lazy-1 parse, catch-up) on the
 same inputs.  Finer-grained than the frame tests: a mismatch names the first differing
-sequence.  K1's records carry a cumulative literal count; consecutive same-offset records
-with no literals between them are merged (K2 merges them the same way)."""
+sequence.  K1's records carry the walk's cumulative literal count and the catch-up length; consecutive
+same-offset records with no literals between them are merged (K2 merges them the same way)."""
 import ctypes
 
 import numpy as np
@@ -51,12 +51,14 @@ def k1_raw(datas):
 
 
 def merged(recs):
-    """K1 records -> (ll, ml, off) with same-offset continuations merged, + literal count"""
+    """K1 records -> (ll, ml, off) with same-offset continuations merged.  A record holds the
+    walk's literal count before the match, its length, its catch-up e (bytes of the literal run
+    before it that join the match) and its offset."""
     seqs, prev = [], 0
     for v in recs:
         v = int(v)
-        cum, ml, off = v & 0x1FFFF, (v >> 17) & 0x7FFF, (v >> 32) & 0x1FFFF
-        ll = cum - prev
+        cum, ln, e, off = v & 0x1FFFF, (v >> 17) & 0x7F, (v >> 24) & 0xFFF, (v >> 36) & 0x1FFFF
+        ll, ml = cum - prev - e, ln + e
         prev = cum
         if seqs and ll == 0 and seqs[-1][2] == off:
             seqs[-1][1] += ml

@@ -4,7 +4,7 @@ import os
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-os.environ["CUDA_ZSTD_HIP_LIB"] = os.path.join(ROOT, "tools", "libcuda_zstd_hip_stamps.so")
+os.environ["CUDA_ZSTD_HIP_LIB"] = os.environ.get("STAMPS_LIB") or os.path.join(ROOT, "tools", "libcuda_zstd_hip_stamps.so")
 sys.path.insert(0, os.path.join(ROOT, "custom-nvcomp-with-zstd_amd"))
 sys.path.insert(0, os.path.join(ROOT, "tests"))
 import numpy as np
@@ -40,7 +40,7 @@ WS = 13120 * 8 + 122880 + 256 + 4096
 h = temp.cpu().numpy()
 m0 = h[blocks + 13120 * 8 + 122880: blocks + 13120 * 8 + 122880 + 16].view(np.uint32)
 print('block 0 meta (nseq, nlit, rle):', m0[:3].tolist(), 'temp', temp.numel(), 'blocks off', blocks, 'n*WS', n * WS)
-raw = np.array([h[blocks + b * WS + 13120 * 8 + 122880 + 16: blocks + b * WS + 13120 * 8 + 122880 + 16 + 56 * 4].view(np.uint32) for b in range(n)])
+raw = np.array([h[blocks + b * WS + 13120 * 8 + 122880 + 16: blocks + b * WS + 13120 * 8 + 122880 + 16 + 60 * 4].view(np.uint32) for b in range(n)])
 st = raw[:, :6]
 k2 = raw[:, 6:15].astype(np.float64)
 names = ["stage", "A(P wait)", "B(lengths)", "J(walk+list)", "E(records+lits)", "rounds"]
@@ -50,6 +50,7 @@ for k, nm in enumerate(names):
     print(f"  {nm:16s} mean {st[:, k].mean():12.0f}  share {st[:, k].mean() / tot * 100 if k < 5 else 0:5.1f}%")
 print(f"  inserter busy (next window) {raw[:, 16].mean():12.0f}   R wait {raw[:, 21].mean():12.0f}  list + W1 {raw[:, 22].mean():12.0f}  catch-up + W2 {raw[:, 20].mean():12.0f}")
 
+print(f"  wave 0 parse: span tops {raw[:, 55].mean():10.0f}  walk+Jacobi {raw[:, 56].mean():10.0f}  list {raw[:, 57].mean():10.0f}  catch-up+records {raw[:, 3].mean():10.0f}")
 k2 = np.concatenate([k2, raw[:, 17:18].astype(np.float64)], 1)
 k2n = ["lit_hist", "huf_build(serial)", "stream_sizes", "lit_streams", "merge", "repcode+codes", "fse_tables(serial)", "fse_pack", "tail", "fse_chains"]
 t2 = k2.sum(1).mean()
