@@ -17,10 +17,12 @@ RCCL all-gather of the padded frame slots) is timed separately (--payload-gather
 Prints one JSON line (driver contract).  roofline = the dominant kernel's algorithmic
 bytes (input + compressed output) per launch / its average HIP-event
 duration on the launch stream, plus the measured issue-rate fraction of that kernel from
-the committed rocprofv3 SQ summary (profiles/*_sq_summary.json): K1 is bound by VALU
-issue, not by HBM.  cpu_baseline = libzstd level 3 (the reference's own CPU route,
+the committed rocprofv3 SQ summary (profiles/*_sq_summary.json); `limiter` compares the
+two fractions.  cpu_baseline = libzstd level 3 (the reference's own CPU route,
 src/cuda_zstd_manager.cu:1604-1668) through tools/libcpubench.so: one ZSTD_CCtx per
-POSIX thread, ZSTD_compressCCtx over the same chunks, 1 thread and the box's host share.
+POSIX thread, ZSTD_compressCCtx over the same chunks, a 1, 2, 4, ... thread curve up to
+the box's host share (--cpu-threads all: every thread of the affinity).  vs_baseline
+stays null: BASELINE.md publishes no number for this metric on any hardware.
 Extra legs at N=1 (not `value`): C3 on uniform random bytes, C2 (one 64 MiB frame through
 ZstdManager::compress), and GPU decompression of the C3 frames.
 """
@@ -105,28 +107,44 @@ def cpu_run(mode, data, nchunks, threads, passes=5, sizes=None, slot=0):
 
 
 def cpu_baseline(host, threads, gpu_gbs):
-    """libzstd level 3 over the same chunks: 1 thread on a 1024-chunk (64 MiB) sample and
-    `threads` threads on the whole rank-0 batch; median of 5 sweeps after a warm-up."""
+    """libzstd level 3 over the same chunks, median of 5 sweeps after a warm-up each:
+    1 thread on a 1024-chunk (64 MiB) sample, then 2, 4, 8, ... threads on 1024 chunks per
+    thread, up to `threads` threads on the whole rank-0 batch (the reported value).  The
+    all-core figure extrapolates the 1-thread rate to every physical core at the parallel
+    efficiency measured at `threads`; with --cpu-threads all it is measured instead."""
     n = len(host) // CHUNK
-    n1 = min(n, 1024)
-    one = cpu_run(0, host, n1, 1)
-    many = cpu_run(0, host, n, threads)
-    if one is None or many is None:
-        return None
+    curve, t = [], 1
+    while True:
+        nt = n if t >= threads else min(n, 1024 * t)
+        r = cpu_run(0, host, nt, t)
+        if r is None:
+            return None
+        curve.append({"threads": t, "chunks": nt, "GBps": round(nt * CHUNK / r["seconds"] / 1e9, 4), "_r": r})
+        if t >= threads:
+            break
+        t = min(2 * t, threads)
+    one, many = curve[0], curve[-1]
+    g1, gm = one["GBps"], many["GBps"]
     info = host_info()
-    g1 = n1 * CHUNK / one["seconds"] / 1e9
-    gm = n * CHUNK / many["seconds"] / 1e9
     cores = info["physical_cores"] or threads
-    model_all = g1 * cores  # linear model: every physical core at the 1-thread rate (upper bound for the CPU)
+    eff = gm / (threads * g1)
+    all_core = g1 * cores * min(1.0, eff)
+    r = many.pop("_r")
+    for c in curve:
+        c.pop("_r", None)
+    measured_all = threads >= (info["affinity_threads"] or threads)
     return {"value": round(gm, 3), "unit": "GB/s", "cores": threads, "kind": "reference",
-            "sample": f"libzstd {one['version']} ZSTD_compressCCtx level 3 (one CCtx per POSIX thread, tools/cpubench.c) over the same 64 KiB "
-                      f"chunks: {threads} threads x {n} chunks ({n * CHUNK >> 20} MiB), median of 5 sweeps; ratio {n * CHUNK / many['out_bytes']:.4f}",
-            "single_thread": {"value": round(g1, 4), "unit": "GB/s", "sample": f"{n1} chunks, median of 5 sweeps"},
+            "sample": f"libzstd {r['version']} ZSTD_compressCCtx level 3 (one CCtx per POSIX thread, tools/cpubench.c) over the same 64 KiB "
+                      f"chunks: {threads} threads x {n} chunks ({n * CHUNK >> 20} MiB), median of 5 sweeps; ratio {n * CHUNK / r['out_bytes']:.4f}",
+            "single_thread": {"value": g1, "unit": "GB/s", "sample": f"{curve[0]['chunks']} chunks, median of 5 sweeps"},
+            "thread_curve": curve,
             "host": info,
-            "all_core_model": {"value": round(model_all, 2), "unit": "GB/s",
-                               "how": f"1-thread rate x {cores} physical cores (linear, no SMT gain); the box grants {threads} threads per GPU"},
+            "all_core": {"value": round(gm if measured_all else all_core, 2), "unit": "GB/s", "measured": measured_all,
+                         "how": ("measured: every thread of the process affinity" if measured_all else
+                                 f"1-thread rate x {cores} physical cores x the parallel efficiency {eff:.3f} measured at {threads} threads "
+                                 f"(the pool grants {threads} host threads per GPU; bench.py --cpu-threads all measures it on a whole machine)")},
             "gpu_speedup": {"vs_measured_threads": round(gpu_gbs / gm, 2), "vs_single_thread": round(gpu_gbs / g1, 1),
-                            "vs_all_core_model": round(gpu_gbs / model_all, 2)}}
+                            "vs_all_core": round(gpu_gbs / (gm if measured_all else all_core), 2)}}
 
 
 def libzstd_roundtrip(frames, sizes, slot, host):
@@ -333,6 +351,9 @@ def main():
     ap.add_argument("--no-verify", action="store_true", help="skip the libzstd decode of every rank-0 frame after timing")
     ap.add_argument("--no-decompress", action="store_true", help="skip the GPU decompression leg")
     ap.add_argument("--no-legs", action="store_true", help="skip the C3-random and C2 legs (N=1)")
+    ap.add_argument("--cpu-threads", default=None,
+                    help="libzstd baseline threads: a number, or 'all' (the process affinity); default: the host share "
+                         "OMP_NUM_THREADS (16 on the GPU pool), capped by the affinity")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -436,6 +457,16 @@ def main():
         full = args.dataset == "mix" and b.n == CHUNKS
         traffic, traffic_src = pmc_traffic(dom) if full else (None, None)
         issue = issue_fraction(dom) if full else None
+        # limiter: the larger of the kernel's HBM fraction (PMC traffic, else algorithmic bytes,
+        # over its measured duration) and its VALU issue fraction (committed SQ summary)
+        hbm_frac = ((traffic or per_launch_bytes) / (dom_ms / 1e3) / 1e9) / HBM_PEAK_GBS if dom_ms > 0 else 0.0
+        iss = (issue or {}).get("valu_issue_frac")
+        if iss is None:
+            limiter = "unknown (no SQ summary for this workload)"
+        elif hbm_frac >= iss:
+            limiter = f"hbm ({hbm_frac:.3f} of peak >= VALU issue {iss:.3f})"
+        else:
+            limiter = f"instruction issue / LDS latency (VALU issue {iss:.3f} of peak, HBM {hbm_frac:.4f} of peak)"
         line = {
             "metric": METRIC, "value": round(gbs, 3), "unit": "GB/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": round(el / args.steps * 1e3, 3), "higher_is_better": True, "scaling": "weak" if args.weak else "strong",
@@ -447,15 +478,22 @@ def main():
                        "kernel_ms": {"zh_lz_kernel": round(k1, 3), "entropy_stage": round(k2, 3)},
                        "parallelism": f"dp{world} (contiguous chunk shards, RCCL all-gather of sizes inside the step)",
                        "libzstd_verified": verified, "gathered_frame_bytes": gathered_total},
+            # (byte work, no MFMA: HBM is the only roofline; the limiter says what bounds it)
             "roofline": {"kernel": dom, "bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
                          "algorithmic_bytes_per_launch": int(per_launch_bytes), "traffic_source": traffic_src,
-                         "limiter": "VALU/SALU instruction issue (not HBM): see issue" if dom == "zh_lz_kernel" else "latency (serial FSE chains)",
+                         "limiter": limiter,
                          "issue": issue},
         }
         if gather:
             line["payload_gather"] = gather
-        threads = min(len(os.sched_getaffinity(0)), int(os.environ.get("OMP_NUM_THREADS", "0")) or 16)
+        aff = len(os.sched_getaffinity(0))
+        if args.cpu_threads == "all":
+            threads = aff
+        elif args.cpu_threads:
+            threads = max(1, min(aff, int(args.cpu_threads)))
+        else:
+            threads = min(aff, int(os.environ.get("OMP_NUM_THREADS", "0")) or 16)
         if dec is not None:
             if not args.no_cpu_baseline and world == 1:
                 dec["cpu_baseline"] = cpu_decompress_baseline(b, threads)

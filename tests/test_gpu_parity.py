@@ -177,7 +177,9 @@ def test_c3_full_batch_roundtrip(torch_cuda):
     for i in range(0, n, 257):
         assert host[i * slot:i * slot + sizes[i]].tobytes() == T.oracle_frame(data[i * cs:(i + 1) * cs]), f"chunk {i}"
     ratio = n * cs / sizes.sum()
-    assert ratio > 2.3
+    # libzstd level 3 on the same 1 GiB: 2.759; the GPU parse (catch-up
+    # included) measures 2.7621
+    assert ratio >= 2.75
 
 
 def test_checksum_frames(torch_cuda):
