@@ -750,15 +750,32 @@ Status ZstdBatchManager::compress_batch(const std::vector<BatchItem> &items, voi
   std::vector<size_t> sizes(items.size());
   for (size_t i = 0; i < items.size(); i++) sizes[i] = items[i].input_size;
   if (temp_size < get_batch_compress_temp_size(sizes)) return Status::ERROR_BUFFER_TOO_SMALL;
-  // items with invalid arguments never reach the device
+  // items with invalid arguments never reach the device; the reference's batch loop calls
+  // compress() per item (src/cuda_zstd_manager.cu:5744-5768), so an item below cpu_threshold
+  // takes compress()'s libzstd route (without a dictionary, as compress() decides) and the rest
+  // share one device launch
+  const DevDict *dd = pimpl_->active();
   std::vector<const void *> ip;
   std::vector<void *> op;
   std::vector<size_t> isz, osz, idx;
   bool any_bad = false;
+  auto t0 = std::chrono::steady_clock::now();
   for (size_t i = 0; i < items.size(); i++) {
     if (!items[i].input_ptr || !items[i].output_ptr || items[i].input_size == 0) {
       mut[i].status = Status::ERROR_INVALID_PARAMETER;
       any_bad = true;
+      continue;
+    }
+    if (!dd && select_execution_path(items[i].input_size, (int)pimpl_->config.cpu_threshold) == ExecutionPath::CPU) {
+      size_t o = items[i].output_size;
+      mut[i].status = cpu_compress(items[i].input_ptr, items[i].input_size, items[i].output_ptr, &o, pimpl_->config.level, stream);
+      if (mut[i].status == Status::SUCCESS) {
+        mut[i].output_size = o;
+        pimpl_->stats.input_bytes += items[i].input_size;
+        pimpl_->stats.output_bytes += o;
+      } else {
+        any_bad = true;
+      }
       continue;
     }
     ip.push_back(items[i].input_ptr);
@@ -767,10 +784,8 @@ Status ZstdBatchManager::compress_batch(const std::vector<BatchItem> &items, voi
     osz.push_back(items[i].output_size);
     idx.push_back(i);
   }
-  auto t0 = std::chrono::steady_clock::now();
   std::vector<Status> st(idx.size());
-  Status r = idx.empty() ? Status::SUCCESS : pimpl_->run(ip.data(), isz.data(), idx.size(), op.data(), osz.data(), st.data(), temp, temp_size, stream,
-                                                                 pimpl_->active());
+  Status r = idx.empty() ? Status::SUCCESS : pimpl_->run(ip.data(), isz.data(), idx.size(), op.data(), osz.data(), st.data(), temp, temp_size, stream, dd);
   pimpl_->stats.compression_time_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
   if (r != Status::SUCCESS && r != Status::ERROR_GENERIC) return r;
   for (size_t j = 0; j < idx.size(); j++) {

@@ -10,6 +10,10 @@
 //                                  ZstdManager::compress of every chunk (device buffers); chunks
 //                                  below T take the libzstd route (reference
 //                                  src/cuda_zstd_manager.cu:1604-1668), the rest the GPU
+//   boundary batch_threshold <dir> <T>  ZstdBatchManager::compress_batch of every chunk as one
+//                                  BatchItem vector with cpu_threshold = T: items below T take
+//                                  libzstd (the reference's per-item compress() loop,
+//                                  src/cuda_zstd_manager.cu:5744-5768), the rest one GPU launch
 //   boundary inference <dir>       GPU compress of every chunk, then the inference flow of
 //                                  reference tests/test_inference_api.cu:398-410: a workspace
 //                                  from allocate_inference_workspace(frame, chunk) and
@@ -144,6 +148,27 @@ int main(int argc, char **argv) {
         return 3;
       }
     }
+  } else if (mode == "batch_threshold") {
+    if (argc < 4) return 1;
+    CompressionConfig c = CompressionConfig::from_level(3);
+    c.cpu_threshold = (u32)std::stoul(argv[3]);
+    ZstdBatchManager m(c);
+    std::vector<BatchItem> items(n);
+    for (size_t i = 0; i < n; i++) {
+      items[i].input_ptr = d_in[i];
+      items[i].input_size = sizes[i];
+      items[i].output_ptr = d_out[i];
+      items[i].output_size = cap;
+    }
+    size_t const ts = m.get_batch_compress_temp_size(sizes);
+    void *d_temp;
+    CK(hipMalloc(&d_temp, ts));
+    Status st = m.compress_batch(items, d_temp, ts, 0);
+    if (st != Status::SUCCESS) {
+      fprintf(stderr, "compress_batch: %s\n", status_to_string(st));
+      return 3;
+    }
+    for (size_t i = 0; i < n; i++) fsz[i] = items[i].output_size;
   } else if (mode == "inference") {
     ZstdBatchManager m(CompressionConfig::from_level(3));
     size_t const ts = m.get_compress_temp_size(*std::max_element(sizes.begin(), sizes.end()));

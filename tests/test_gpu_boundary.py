@@ -6,6 +6,7 @@ inference API), on the GPU:
   with device arrays -- through the C++ API (tests/cpp/boundary.cpp);
 * CompressionConfig::cpu_threshold routing (reference src/cuda_zstd_manager.cu:1604-1668):
   a 64 KiB device item below a 1 MiB threshold takes the libzstd route, a 2 MiB one the GPU;
+  per item in compress_batch (the reference's per-item compress() loop, :5744-5768);
 * the single-buffer C entry nvcomp_zstd_compress_async_v5 / nvcomp_zstd_decompress_async_v5;
 * the inference flow (allocate_inference_workspace + decompress_to_preallocated, reference
   tests/test_inference_api.cu:398-410) with outputs below 128 KiB.
@@ -73,6 +74,42 @@ def test_cpu_threshold_routing(tmp_path, libzstd):
     # threshold 0 (the default): the 64 KiB item goes to the GPU
     frames0 = _run("threshold", [small], tmp_path, "0")
     assert frames0[0] == T.oracle_frame(small)
+
+
+def _libzstd_l3(d):
+    """ZSTD_compress(level 3) frames of d from every libzstd on the box (the CPU route's output)."""
+    cands = set()
+    for p in ("/opt/conda/lib/libzstd.so.1", "libzstd.so.1", "/usr/lib/x86_64-linux-gnu/libzstd.so.1"):
+        try:
+            L = ctypes.CDLL(p)
+        except OSError:
+            continue
+        L.ZSTD_compress.restype = ctypes.c_size_t
+        L.ZSTD_compress.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int]
+        cap = len(d) + (len(d) >> 7) + 1024
+        out = np.zeros(cap, np.uint8)
+        r = L.ZSTD_compress(out.ctypes.data, cap, d.ctypes.data, len(d), 3)
+        cands.add(out[:r].tobytes())
+    return cands
+
+
+def test_compress_batch_per_item_threshold(tmp_path, libzstd):
+    """ZstdBatchManager::compress_batch with cpu_threshold = 48 KiB over mixed sizes: items
+    below it equal libzstd ZSTD_compress(3) (the reference's per-item compress() route), the
+    rest equal the oracle's GPU frame; all decode."""
+    datas = _chunks() + [T.gen(T.DG_MIX, 1, 950, 300000)]
+    thr = 48 * 1024
+    frames = _run("batch_threshold", datas, tmp_path, str(thr))
+    for k, (f, d) in enumerate(zip(frames, datas)):
+        if len(d) < thr:
+            assert f in _libzstd_l3(d), f"item {k} ({len(d)} B): not the libzstd route"
+        else:
+            assert f == T.oracle_frame(d), f"item {k} ({len(d)} B)"
+        assert T.zstd_decompress(f, len(d)) == d.tobytes()
+    # threshold 0: every item on the GPU
+    frames0 = _run("batch_threshold", datas, tmp_path, "0")
+    for k, (f, d) in enumerate(zip(frames0, datas)):
+        assert f == T.oracle_frame(d), f"item {k}"
 
 
 def test_inference_workspace(tmp_path, libzstd):
