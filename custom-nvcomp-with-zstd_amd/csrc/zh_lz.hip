@@ -90,6 +90,8 @@ constexpr u32 OFF_XQ = OFF_ML + 4 * ML_CAP;          // u16 per entry: window in
 constexpr u32 OFF_MISC = OFF_XQ + 2 * XQ_CAP * NWW;  // [2 par + 0] matches, [2 par + 1] first parsed position
 constexpr u32 K1_LDS = OFF_MISC + 4 * 16;
 constexpr u32 MISC_ARR = 12;  // misc[12]: worker-wave barrier arrivals (cumulative)
+constexpr u32 MISC_NM = 4;    // misc[4 + (j & 3)]: matches the parse took in window j (miss skip)
+constexpr u32 MISC_ANY = 13;  // misc[13]: block_any's flag (0 between calls)
 static_assert(K1_LDS <= 163840 - 256, "K1 LDS budget");
 static_assert(OFF_TL % 16 == 0 && OFF_CI % 16 == 0 && OFF_HM % 16 == 0 && OFF_MISC % 4 == 0, "alignment");
 
@@ -219,14 +221,15 @@ __device__ __forceinline__ void insert_repair(u16 *T, u32 tb0, u32 lane, const u
 // slot verifies (insert_repair otherwise).  BT tiles are issued per LDS round trip together
 // with the next batch's input dwords and the workers' arrival counter.  Candidates
 // (position + 1, 0 = none) go to creg as u16 pairs.
-template <bool LONG, typename Hook>
+template <bool LONG, u32 NT, typename Hook>
 __device__ __forceinline__ void insert_window(const u32 *in32, u16 *T, u32 wsb, u32 we, u32 lim, u32 lane, u32 (&creg)[NCR], u32 &cwe,
                                               const u32 *arrivals, Hook &&between_tiles, u32 pmin = 0) {
   // positions below pmin are already in T (a dictionary's precomputed tables): treated like
-  // positions past lim (the junk slot, no candidate)
+  // positions past lim (the junk slot, no candidate); tiles from NT on (a miss-skip window,
+  // orc_lz_parse_pre) are neither looked up nor inserted and their candidates never dumped
   constexpr u32 JUNK = LONG ? HL_SIZE : HS_SIZE;
   constexpr u32 BT = 2;  // tiles per LDS round trip
-  static_assert(TILES % BT == 0, "batches tile windows");
+  static_assert(TILES % BT == 0 && ZH_SKIP_TILES % BT == 0, "batches tile windows");
   u32 wv[BT][TPL][3];
   auto load_in = [&](u32 tb0, u32 lim_t) {
 #pragma unroll
@@ -241,7 +244,7 @@ __device__ __forceinline__ void insert_window(const u32 *in32, u16 *T, u32 wsb, 
   };
   load_in(wsb, lim);
 #pragma unroll
-  for (u32 t0 = 0; t0 < TILES; t0 += BT) {
+  for (u32 t0 = 0; t0 < NT; t0 += BT) {
     // opaque per-batch copy of lim: keeps the compiler from hoisting every tile's
     // bounds checks (64 masks) to the top of the unrolled loop
     u32 lim_t;
@@ -264,7 +267,7 @@ __device__ __forceinline__ void insert_window(const u32 *in32, u16 *T, u32 wsb, 
 #pragma unroll
       for (u32 k = 0; k < TPL; k++) r[b][k] = T[h[b][k]];
     }
-    if (t0 + BT < TILES) load_in(tb0 + BT * ZH_TILE, lim_t);
+    if (t0 + BT < NT) load_in(tb0 + BT * ZH_TILE, lim_t);
     u32 const arr = __atomic_load_n(arrivals, __ATOMIC_RELAXED);
     bool lost = false;
 #pragma unroll
@@ -324,14 +327,21 @@ __device__ __forceinline__ void insert_span(const u32 *in32, u16 *T, u32 s, u32 
   __asm__ volatile("" ::: "memory");
 }
 
+// Miss skip (oracle orc_lz_parse_pre): window k of the block's loop searches only its first
+// ZH_SKIP_TILES tiles when the parse took no match in window k - 3; windows before kskip0 (up to
+// three past the one holding `pre`) never skip.  Wave-uniform.
+__device__ __forceinline__ bool skip_window(const u32 *misc, u32 k, u32 kskip0) {
+  return k >= kskip0 && (u32)__builtin_amdgcn_readfirstlane(__atomic_load_n(&misc[MISC_NM + ((k - 3) & 3)], __ATOMIC_RELAXED)) == 0;
+}
+
 // Dump an inserter's candidates into its half of the cinfo words (LONG: low half).
-template <bool LONG>
+template <bool LONG, u32 NT>
 __device__ __forceinline__ void dump_window(u8 *ci8, u32 lane_, const u32 (&creg)[NCR], u32 cwe) {
   // opaque lane copy: stops the 64 addresses from being hoisted out of the window loop
   u32 lane;
   __asm__ volatile("v_mov_b32 %0, %1" : "=v"(lane) : "v"(lane_));
 #pragma unroll
-  for (u32 t = 0; t < TILES; t++) {
+  for (u32 t = 0; t < NT; t++) {
 #pragma unroll
     for (u32 k = 0; k < TPL; k++) {
       u32 const i = t * ZH_TILE + 64 * k + lane, j = t * TPL + k;
@@ -630,11 +640,12 @@ __device__ __forceinline__ void seg_walk(const u32 *ci, u32 tmk, u32 S, u32 SE, 
 constexpr u32 WIN_BARRIERS = 1;  // X
 template <bool LONG>
 __device__ __forceinline__ void inserter_loop(const u32 *in32, u16 *T, u8 *ci8, u32 *misc_, u32 n, u32 lim, u32 lane, u32 *dbg, u32 wstart,
-                                              u32 pmin, u32 span_s, u32 span_e) {
+                                              u32 pmin, u32 span_s, u32 span_e, u32 kskip0) {
   u32 creg[NCR];
   u32 cwe = 0;
   if (span_s < span_e) insert_span<LONG>(in32, T, span_s, span_e, lane);
-  insert_window<LONG>(in32, T, wstart, min(wstart + (u32)ZH_WINDOW, n), lim, lane, creg, cwe, &misc_[MISC_ARR], [](u32) {}, pmin);
+  insert_window<LONG, TILES>(in32, T, wstart, min(wstart + (u32)ZH_WINDOW, n), lim, lane, creg, cwe, &misc_[MISC_ARR], [](u32) {}, pmin);
+  bool skipc = false;  // the window whose candidates creg holds is a miss-skip window
 #ifdef ZH_STAMPS
   u32 st_ins = 0;
 #endif
@@ -642,7 +653,10 @@ __device__ __forceinline__ void inserter_loop(const u32 *in32, u16 *T, u8 *ci8, 
   u32 passed = 0;  // X barriers taken so far
   for (u32 k = 0; k < nwin + 1; k++) {
     u32 const wsb = wstart + k * ZH_WINDOW;
-    if (k < nwin) dump_window<LONG>(ci8 + (k & 1u) * 4 * CI_WORDS, lane, creg, cwe);
+    if (k < nwin) {
+      if (skipc) dump_window<LONG, ZH_SKIP_TILES>(ci8 + (k & 1u) * 4 * CI_WORDS, lane, creg, cwe);
+      else dump_window<LONG, TILES>(ci8 + (k & 1u) * 4 * CI_WORDS, lane, creg, cwe);
+    }
     __syncthreads();  // P: candidates of window k in buffer k & 1
     u32 const done = passed + WIN_BARRIERS;
     // arr: the arrival counter as read with the last tile's read-back; a barrier taken
@@ -658,7 +672,14 @@ __device__ __forceinline__ void inserter_loop(const u32 *in32, u16 *T, u8 *ci8, 
     u64 const ti0 = __builtin_amdgcn_s_memtime();
 #endif
     u32 const nx = wsb + ZH_WINDOW;
-    if (k + 1 < nwin) insert_window<LONG>(in32, T, nx, min(nx + ZH_WINDOW, n), lim, lane, creg, cwe, &misc_[MISC_ARR], take_ready);
+    // window k + 1: the parse of window k - 2 ended in step k - 1 (before this step's P)
+    skipc = skip_window(misc_, k + 1, kskip0);
+    // (a second, short instantiation for miss-skip windows: a runtime tile bound in the full one
+    // costs its unrolled batches more than the extra code does)
+    if (k + 1 < nwin) {
+      if (skipc) insert_window<LONG, ZH_SKIP_TILES>(in32, T, nx, min(nx + ZH_WINDOW, n), lim, lane, creg, cwe, &misc_[MISC_ARR], take_ready);
+      else insert_window<LONG, TILES>(in32, T, nx, min(nx + ZH_WINDOW, n), lim, lane, creg, cwe, &misc_[MISC_ARR], take_ready);
+    }
 #ifdef ZH_STAMPS
     st_ins += (u32)(__builtin_amdgcn_s_memtime() - ti0);
 #endif
@@ -724,13 +745,31 @@ __device__ __forceinline__ void prefetch_block(const ZhBlockDesc *__restrict__ b
 #endif
 // nibble p = virtual wave of hardware wave p
 constexpr u64 K1_WAVE_MAP = ZH_K1_PERM ? 0xDBA9C876F543E210ull : 0xFEDCBA9876543210ull;
-__device__ __forceinline__ u32 k1_tid() {
-  u32 const t = threadIdx.x;
-  return (u32)((K1_WAVE_MAP >> (4 * (t >> 6))) & 15u) << 6 | (t & 63u);
+// __syncthreads_or for the K1 workgroup: a flag word (0 between calls) raised by one lane per
+// wave, read after a barrier and cleared between two more.  (The runtime's version computes the
+// flat work-item id, whose entry VGPRs would then stay live -- spilled -- across the
+// persistent block loop.)
+__device__ __forceinline__ bool block_any(bool v, u32 *flag, u32 tid) {
+  if (__ballot(v) && (tid & 63) == 0) atomicOr(flag, 1u);
+  __syncthreads();
+  bool const r = *flag != 0;
+  __syncthreads();
+  if (tid == 0) *flag = 0;
+  __syncthreads();
+  return r;
+}
+
+// The K1 thread index from the wave id w (an SGPR, read once) and the lane, recomputed at each
+// use (opaque mbcnt): nothing from the kernel's entry VGPRs stays live, or spilled, across the
+// persistent block loop.
+__device__ __forceinline__ u32 k1_tid(u32 w) {
+  u32 lane;
+  __asm__ volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(lane));
+  return (u32)((K1_WAVE_MAP >> (4 * w)) & 15u) << 6 | lane;
 }
 
 template <bool LAZY2>
-__device__ __forceinline__ u32 lz_block(const ZhBlockDesc *__restrict__ blocks, ZhWorkspace ws, u32 b, u32 nblocks, u32 *s_take, Prefetch &pf) {
+__device__ __forceinline__ u32 lz_block(const ZhBlockDesc *__restrict__ blocks, ZhWorkspace ws, u32 b, u32 nblocks, u32 *s_take, Prefetch &pf, u32 wv) {
   extern __shared__ __attribute__((aligned(16))) u8 smem[];
   u8 *in = smem + OFF_IN;
   u32 *in32 = (u32 *)in;
@@ -743,7 +782,7 @@ __device__ __forceinline__ u32 lz_block(const ZhBlockDesc *__restrict__ blocks, 
   // opaque per-block thread index: stops the compiler from hoisting LDS addresses derived
   // from it out of the persistent block loop (they would stay live, and spill, across it)
   u32 tid;
-  __asm__ volatile("v_mov_b32 %0, %1" : "=v"(tid) : "v"(k1_tid()));
+  __asm__ volatile("v_mov_b32 %0, %1" : "=v"(tid) : "v"(k1_tid(wv)));
   u32 const lane = tid & 63;
   ZhBlockDesc const d = blocks[b];
   // the next block for this workgroup (dynamic: a slow block does not hold up a fixed share)
@@ -839,9 +878,13 @@ __device__ __forceinline__ u32 lz_block(const ZhBlockDesc *__restrict__ blocks, 
   u32 const pmin = (use_dt || par_hist) ? pre & ~(ZH_TILE - 1) : 0u;  // the tile holding pre
   u32 const wstart = (use_dt || par_hist) ? (pre & ~(ZH_WINDOW - 1)) : 0u;
   u32 const span_s = use_dt ? pre - ZH_DTAB_MARGIN : 0u, span_e = use_dt ? pmin : 0u;
-  if (tid < 2) misc[8 + tid] = 0;
+#ifdef ZH_NO_SKIP
+  u32 const kskip0 = 1u << 20;
+#else
+  u32 const kskip0 = pre / ZH_WINDOW + 3 - wstart / ZH_WINDOW;  // first loop window that may skip
+#endif
   if (tid == 0) misc[MISC_ARR] = 0;
-  bool const rle = __syncthreads_and(same) && d.n >= 2;
+  bool const rle = !block_any(!same, &misc[MISC_ANY], tid) && d.n >= 2;
   u32 const next_b = *s_take;  // (written before the barrier above)
   prefetch_block(blocks, next_b, nblocks, tid, pf);  // the next block's input, in flight from here
   if (rle) {
@@ -871,7 +914,7 @@ __device__ __forceinline__ u32 lz_block(const ZhBlockDesc *__restrict__ blocks, 
         }
       }
       if (round == 0) __syncthreads();
-      else if (!__syncthreads_or(ch)) break;
+      else if (!block_any(ch, &misc[MISC_ANY], tid)) break;
     }
   }
 
@@ -888,8 +931,8 @@ __device__ __forceinline__ u32 lz_block(const ZhBlockDesc *__restrict__ blocks, 
     // gate the workers' next window, so they take priority (MI355X_MICROARCH.md, "VALU issue
     // is arbitrated ... by priority, then age").
     __builtin_amdgcn_s_setprio(2);
-    if (tid < INS_TID + 64) inserter_loop<true>(in32, TL, ci8, misc, n, lim, lane, ws.dbg(b), wstart, pmin, span_s, span_e);
-    else inserter_loop<false>(in32, TS, ci8, misc, n, lim, lane, ws.dbg(b), wstart, pmin, span_s, span_e);
+    if (tid < INS_TID + 64) inserter_loop<true>(in32, TL, ci8, misc, n, lim, lane, ws.dbg(b), wstart, pmin, span_s, span_e, kskip0);
+    else inserter_loop<false>(in32, TS, ci8, misc, n, lim, lane, ws.dbg(b), wstart, pmin, span_s, span_e, kskip0);
     __builtin_amdgcn_s_setprio(0);
     return next_b;
   }
@@ -928,7 +971,20 @@ __device__ __forceinline__ u32 lz_block(const ZhBlockDesc *__restrict__ blocks, 
     u32 *const lmf = sgm + segm(0, SEGM_LIT);  // window k - 1's literal bits after catch-up
     __syncthreads();  // P: candidates of window k in buffer k & 1
     ZH_STAMP(st_A);
-    if (have && wave != 0) {
+    // a miss-skip window has candidates in its first RS rounds only: waves 1..RS take one each
+    // (the top one, wave RS, knows its next positions have none), the others clear the info and
+    // take masks of the rounds above
+    constexpr u32 RS = 2 * ZH_SKIP_TILES;
+    static_assert(RS < NWW && (RS & 1) == 0, "miss-skip rounds");
+    bool const skipk = have && skip_window(misc, k, kskip0);
+    if (skipk && wave != 0) {
+      if (wave <= RS) span_lengths<LAZY2>(in32, ciK, tmK, xq, wave - 1, wave, wsb, we, n, lim, lane, wave == RS, 0u, 0u);
+      for (u32 r = RS + wave - 1; r < NROUND; r += NWW - 1) {
+        ciK[cidx(64 * r + lane)] = 0;
+        if (lane == 0) tmK[r] = 0;
+      }
+      ZH_STAMP(st_B);
+    } else if (have && wave != 0) {
       // the window's top span (wave 13) first takes the lookahead positions `we`, `we + 1`:
       // the take decisions at the window's end need their info
       u32 la1 = 0, la2 = 0;
@@ -1006,7 +1062,7 @@ __device__ __forceinline__ u32 lz_block(const ZhBlockDesc *__restrict__ blocks, 
         }
       }
       nwalk_tot += nwl;  // the window's walk literals (its last match may run past its end)
-      if (lane == 0) misc[1] = nm;
+      if (lane == 0) { misc[1] = nm; misc[MISC_NM + ((k - 1) & 3)] = nm; }
       ZH_STAMP(st_J);
     }
     if (lane == 0) atomicAdd(&misc[MISC_ARR], 1u);
@@ -1018,7 +1074,8 @@ __device__ __forceinline__ u32 lz_block(const ZhBlockDesc *__restrict__ blocks, 
       u32 const w = 1u + lane / PER;
       u32 rh = 0;
       for (u32 v = 0; v <= min(w, NWW - 1); v++) rh += rounds_of(v);
-      bool const act = lane < PER * (NWW - 2);  // spans of waves 1..12
+      if (skipk) rh = w;  // (a miss-skip window: one round per wave)
+      bool const act = lane < PER * (skipk ? RS - 1 : NWW - 2);  // spans of waves 1..12 (1..RS-1)
       u32 const i = act ? 64 * rh - 1 - lane % PER : 0u;
       u32 const inf = ciK[cidx(i)], inf1 = ciK[cidx(i + 1)], inf2 = ciK[cidx(i + 2)];
       if (act && i < we - wsb && (inf & 255u) && take_rule<LAZY2>(inf, inf1, inf2)) atomicOr((unsigned long long *)&tmK[i >> 6], 1ull << (i & 63));
@@ -1064,14 +1121,19 @@ __device__ __forceinline__ u32 lz_block(const ZhBlockDesc *__restrict__ blocks, 
 // one was processed, so the HBM latency of staging and the per-block launch gap overlap work.
 template <bool LAZY2>
 __device__ __forceinline__ void lz_blocks(const ZhBlockDesc *__restrict__ blocks, u32 nblocks, ZhWorkspace ws) {
+  extern __shared__ __attribute__((aligned(16))) u8 smem[];
   __shared__ u32 s_take;  // block index taken from the counter, broadcast to the workgroup
-  if (threadIdx.x == 0) s_take = atomicAdd(ws.ctr, 1u);
+  if (threadIdx.x == 0) {
+    s_take = atomicAdd(ws.ctr, 1u);
+    ((u32 *)(smem + OFF_MISC))[MISC_ANY] = 0;
+  }
   __syncthreads();
   u32 b = s_take;
   Prefetch pf;
-  prefetch_block(blocks, b, nblocks, k1_tid(), pf);
+  u32 const wv = (u32)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  prefetch_block(blocks, b, nblocks, k1_tid(wv), pf);
   while (b < nblocks) {
-    b = lz_block<LAZY2>(blocks, ws, b, nblocks, &s_take, pf);  // returns the next block taken
+    b = lz_block<LAZY2>(blocks, ws, b, nblocks, &s_take, pf, wv);  // returns the next block taken
     __syncthreads();  // every wave is done with this block's LDS before the next is staged
   }
 }

@@ -25,6 +25,7 @@
 #define ZH_FRAME_BLOCK(n, dict) ((void)(dict), ((n) <= ZH_BLOCK_MAX ? ZH_BLOCK_MAX : ZH_HIST_BLOCK))
 #define ZH_TILE 128                 /* hash insertion granularity (positions) */
 #define ZH_WINDOW 2048              /* parse window (positions); catch-up stays inside one */
+#define ZH_SKIP_TILES 2             /* tiles a window searches after a window without matches (miss skip) */
 #define ZH_HASH_LOG_LONG 14         /* 8-byte hash table: 2^14 u16 entries */
 #define ZH_HASH_LOG_SHORT 14        /* 5-byte hash table: 2^14 u16 entries */
 #define ZH_HASH_READ 8              /* bytes read per hashed position */

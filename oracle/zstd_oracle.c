@@ -811,21 +811,19 @@ static u32 common_prefix(const u8 *src, u32 a, u32 b, u32 n, u32 cap) {
   return l;
 }
 
-/* Per-position best match: len[p] (0 or >= ZH_MIN_MATCH_*), off[p]. Arrays sized n+1. */
-void orc_lz_match_info(const u8 *src, u32 n, u8 *len, u16 *off) {
-  static u32 TL[1 << ZH_HASH_LOG_LONG], TS[1 << ZH_HASH_LOG_SHORT];
+/* Per-position best match over the tiles [t0, t1) of src[0, n) (tile-aligned, t1 <= lim):
+ * len[p] (0 or >= ZH_MIN_MATCH_*), off[p].  Each tile's lookups see the tables after every
+ * earlier tile's insertions (K1's inserter waves: zh_lz.hip insert_window).  `skip_from`:
+ * tiles at or above it are neither looked up nor inserted (len 0), see orc_lz_parse_pre. */
+static u32 g_TL[1 << ZH_HASH_LOG_LONG], g_TS[1 << ZH_HASH_LOG_SHORT];
+static void match_info_tiles(const u8 *src, u32 n, u32 t0, u32 t1, u32 skip_from, u8 *len, u16 *off) {
   const u32 EMPTY = 0xFFFFFFFFu;
-  for (u32 i = 0; i < (1u << ZH_HASH_LOG_LONG); i++) TL[i] = EMPTY;
-  for (u32 i = 0; i < (1u << ZH_HASH_LOG_SHORT); i++) TS[i] = EMPTY;
-  memset(len, 0, n + 1);
-  memset(off, 0, sizeof(u16) * (n + 1));
-  if (n <= ZH_HASH_READ) return;
   u32 const lim = n - ZH_HASH_READ;
-  for (u32 t = 0; t < lim; t += ZH_TILE) {
+  for (u32 t = t0; t < t1 && t < skip_from; t += ZH_TILE) {
     u32 e = t + ZH_TILE < lim ? t + ZH_TILE : lim;
     for (u32 p = t; p < e; p++) {
       u64 v = rd64(src + p);
-      u32 qL = TL[zh_hash_long(v)], qS = TS[zh_hash_short(v)];
+      u32 qL = g_TL[zh_hash_long(v)], qS = g_TS[zh_hash_short(v)];
       u32 lL = qL != EMPTY ? common_prefix(src, p, qL, n, ZH_MAX_MATCH) : 0;
       u32 lS = qS != EMPTY ? common_prefix(src, p, qS, n, ZH_MAX_MATCH) : 0;
       if (lL < ZH_MIN_MATCH_LONG) lL = 0;
@@ -833,8 +831,22 @@ void orc_lz_match_info(const u8 *src, u32 n, u8 *len, u16 *off) {
       if (lL && lL >= lS) { len[p] = (u8)lL; off[p] = (u16)(p - qL); }
       else if (lS) { len[p] = (u8)lS; off[p] = (u16)(p - qS); }
     }
-    for (u32 p = t; p < e; p++) { u64 v = rd64(src + p); TL[zh_hash_long(v)] = p; TS[zh_hash_short(v)] = p; }
+    for (u32 p = t; p < e; p++) { u64 v = rd64(src + p); g_TL[zh_hash_long(v)] = p; g_TS[zh_hash_short(v)] = p; }
   }
+}
+static void match_info_reset(u32 n, u8 *len, u16 *off) {
+  for (u32 i = 0; i < (1u << ZH_HASH_LOG_LONG); i++) g_TL[i] = 0xFFFFFFFFu;
+  for (u32 i = 0; i < (1u << ZH_HASH_LOG_SHORT); i++) g_TS[i] = 0xFFFFFFFFu;
+  memset(len, 0, n + 1);
+  memset(off, 0, sizeof(u16) * (n + 1));
+}
+
+/* Per-position best match of every tile (no skipping). Arrays sized n+1. */
+void orc_lz_match_info(const u8 *src, u32 n, u8 *len, u16 *off) {
+  match_info_reset(n, len, off);
+  if (n <= ZH_HASH_READ) return;
+  u32 const lim = n - ZH_HASH_READ;
+  match_info_tiles(src, n, 0, (lim + ZH_TILE - 1) / ZH_TILE * ZH_TILE, 0xFFFFFFFFu, len, off);
 }
 
 /* Parse + merge over src[0, n).  Positions [0, pre) are dictionary history:
@@ -849,38 +861,56 @@ static int orc_parse_lazy2 = 0;
 static int match_gain(const u8 *len, const u16 *off, u32 p) {
   return len[p] ? 4 * (int)len[p] - (31 - __builtin_clz((u32)off[p] + 1u)) : -1000;
 }
+/* Miss skip (libzstd dfast's kSearchStrength idea at window granularity): the matcher and the
+ * parse run window by window (ZH_WINDOW positions, aligned in the staged buffer, as K1's
+ * pipeline does), and a window whose window three before it -- the newest one K1's parse has
+ * finished when its insertion starts -- took no match (counted at the match position before
+ * catch-up) searches and inserts only its first ZH_SKIP_TILES tiles; the rest of it has no
+ * candidates.  Windows up to three past the one holding `pre` never skip. */
 size_t orc_lz_parse_pre(const u8 *src, u32 pre, u32 n, orc_seq_t *seq, u32 *last_lits) {
   u8 *len = malloc(n + 2);
   u16 *off = malloc(sizeof(u16) * (n + 2));
-  orc_lz_match_info(src, n, len, off);
+  match_info_reset(n, len, off);
   len[n + 1] = 0; off[n + 1] = 0;
   size_t ns = 0;
   u32 p = pre, anchor = pre, lim = n > ZH_HASH_READ ? n - ZH_HASH_READ : 0;
-  while (p < lim) {
-    int defer;
-    if (len[p] == 0) defer = 1;
-    else if (orc_parse_lazy2) {
-      int const g0 = match_gain(len, off, p);
-      defer = match_gain(len, off, p + 1) > g0 + 4 || match_gain(len, off, p + 2) > g0 + 7;
-    } else defer = len[p + 1] > len[p];
-    if (defer) { p++; continue; }
-    /* catch-up (libzstd 1.4.9 ZSTD_compressBlock_doubleFast_generic / lazy_generic "catch
-     * up"): the match grows backwards over the literals since the last sequence while the
-     * bytes before it equal the bytes before its source, bounded by the start of the
-     * ZH_WINDOW-position parse window holding p (the device parses window by window; windows
-     * start at multiples of ZH_WINDOW of the staged buffer).  The parse itself continues at
-     * p + len[p] either way. */
-    u32 ms = p, ml = len[p];
-    u32 const of = off[p], wlo = p & ~(u32)(ZH_WINDOW - 1), lo = anchor > wlo ? anchor : wlo;
-    while (ms > lo && ms > of && src[ms - 1] == src[ms - 1 - of]) { ms--; ml++; }
-    u32 ll = ms - anchor;
-    if (ns && ll == 0 && seq[ns - 1].off == of) seq[ns - 1].ml += ml; /* continuation merge */
-    else { seq[ns].ll = ll; seq[ns].ml = ml; seq[ns].off = of; ns++; }
-    p += len[p];
-    anchor = p;
+  u32 const nwin = (lim + ZH_WINDOW - 1) / ZH_WINDOW, a0 = pre / ZH_WINDOW;
+  u32 *mcount = calloc(nwin + 1, sizeof(u32));
+  for (u32 a = 0; a <= nwin; a++) {
+    if (a < nwin) {
+      u32 const t0 = a * ZH_WINDOW, t1 = (a + 1) * ZH_WINDOW;
+      int const skip = a >= a0 + 3 && mcount[a - 3] == 0;
+      match_info_tiles(src, n, t0, t1, skip ? t0 + ZH_SKIP_TILES * ZH_TILE : 0xFFFFFFFFu, len, off);
+    }
+    /* the parse of every window before a (its lookahead p + 1, p + 2 is in window a's first tile) */
+    u32 const pe = a < nwin ? a * ZH_WINDOW : lim;
+    while (p < lim && p < pe) {
+      int defer;
+      if (len[p] == 0) defer = 1;
+      else if (orc_parse_lazy2) {
+        int const g0 = match_gain(len, off, p);
+        defer = match_gain(len, off, p + 1) > g0 + 4 || match_gain(len, off, p + 2) > g0 + 7;
+      } else defer = len[p + 1] > len[p];
+      if (defer) { p++; continue; }
+      /* catch-up (libzstd 1.4.9 ZSTD_compressBlock_doubleFast_generic / lazy_generic "catch
+       * up"): the match grows backwards over the literals since the last sequence while the
+       * bytes before it equal the bytes before its source, bounded by the start of the
+       * ZH_WINDOW-position parse window holding p (the device parses window by window; windows
+       * start at multiples of ZH_WINDOW of the staged buffer).  The parse itself continues at
+       * p + len[p] either way. */
+      mcount[p / ZH_WINDOW]++;
+      u32 ms = p, ml = len[p];
+      u32 const of = off[p], wlo = p & ~(u32)(ZH_WINDOW - 1), lo = anchor > wlo ? anchor : wlo;
+      while (ms > lo && ms > of && src[ms - 1] == src[ms - 1 - of]) { ms--; ml++; }
+      u32 ll = ms - anchor;
+      if (ns && ll == 0 && seq[ns - 1].off == of) seq[ns - 1].ml += ml; /* continuation merge */
+      else { seq[ns].ll = ll; seq[ns].ml = ml; seq[ns].off = of; ns++; }
+      p += len[p];
+      anchor = p;
+    }
   }
   *last_lits = n - anchor;
-  free(len); free(off);
+  free(len); free(off); free(mcount);
   return ns;
 }
 size_t orc_lz_parse(const u8 *src, u32 n, orc_seq_t *seq, u32 *last_lits) { return orc_lz_parse_pre(src, 0, n, seq, last_lits); }

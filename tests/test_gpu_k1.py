@@ -114,6 +114,32 @@ def test_k1_corpora_vs_oracle():
     _compare(datas, names)
 
 
+def test_k1_miss_skip_transitions_vs_oracle():
+    """Blocks that enter and leave the miss-skip mode (oracle orc_lz_parse_pre: a window after a
+    window without matches searches only its first tiles): random stretches between text,
+    random with a repeat of an earlier stretch, text inside random at window offsets."""
+    rng = np.random.default_rng(11)
+    text = T.gen(T.DG_TEXT, 1, 0x5EED0009, BLOCK)
+    rnd = rng.integers(0, 256, BLOCK, dtype=np.uint8)
+    datas, names = [], []
+
+    def add(nm, d):
+        names.append(nm)
+        datas.append(np.ascontiguousarray(d[:BLOCK], dtype=np.uint8))
+
+    add("rand16k+text", np.concatenate([rnd[:16384], text[:49152]]))
+    add("text8k+rand40k+text", np.concatenate([text[:8192], rnd[:40960], text[8192:24576]]))
+    rep = rnd.copy()
+    rep[40000:52000] = rep[1000:13000]
+    add("rand+repeat", rep)
+    for off in (9 * 2048 + 100, 9 * 2048 + 300, 20 * 2048 - 50):
+        d = rnd.copy()
+        d[off:off + 6000] = text[:6000]
+        add(f"rand+text@{off}", d)
+    add("rand_ragged", rnd[:30001])
+    _compare(datas, names)
+
+
 def test_k1_special_and_ragged_vs_oracle():
     items = T.special_inputs()
     names = sorted(k for k in items if 0 < len(items[k]) <= BLOCK)
