@@ -434,7 +434,7 @@ enum : u32 { LF_FL = 1u << 8, LF_FS = 1u << 9, LF_XL = 1u << 10, LF_XS = 1u << 1
 // match if it gets there (take_rule on the next positions' info: DPP within the round, the
 // round above by carry; la1 / la2 = the two positions above the span when it is the window's
 // top one) -> the rounds' take masks tm.  At the top of a span that is not the window's top the next positions
-// belong to another wave: those take bits stay clear and wave 0 decides them (span_tops).
+// belong to another wave: those take bits stay clear until the wave decides them after barrier X.
 template <bool LAZY2>
 __device__ __forceinline__ void span_lengths(const u32 *in32, u32 *ci, u64 *tm, u16 *xq, u32 r_lo, u32 r_hi, u32 wsb, u32 we, u32 n, u32 lim,
                                              u32 lane, bool top, u32 la1, u32 la2) {
@@ -653,7 +653,11 @@ __device__ __forceinline__ void inserter_loop(const u32 *in32, u16 *T, u8 *ci8, 
   u32 passed = 0;  // X barriers taken so far
   for (u32 k = 0; k < nwin + 1; k++) {
     u32 const wsb = wstart + k * ZH_WINDOW;
+#ifdef ZH_EXP_NODUMP
+    if (k < nwin && !skipc) {
+#else
     if (k < nwin) {
+#endif
       if (skipc) dump_window<LONG, ZH_SKIP_TILES>(ci8 + (k & 1u) * 4 * CI_WORDS, lane, creg, cwe);
       else dump_window<LONG, TILES>(ci8 + (k & 1u) * 4 * CI_WORDS, lane, creg, cwe);
     }
@@ -952,8 +956,8 @@ __device__ __forceinline__ u32 lz_block(const ZhBlockDesc *__restrict__ blocks, 
   //   phase A  lengths of window k (waves 1..13) | parse, catch-up and sequence records of
   //            window k - 1 (wave 0)
   //   X
-  //   phase B  take decisions at window k's span tops (wave 1), the literals of window k - 1
-  //            (lanes = positions, all worker waves)
+  //   phase B  take decisions at window k's span tops (each wave its own), the literals of
+  //            window k - 1 (lanes = positions, all worker waves)
   for (u32 k = 0; k < nwin + 1; k++) {
     u32 const wsb = wstart + k * ZH_WINDOW;
     u32 const we = min(wsb + ZH_WINDOW, n);
@@ -1068,17 +1072,16 @@ __device__ __forceinline__ u32 lz_block(const ZhBlockDesc *__restrict__ blocks, 
     if (lane == 0) atomicAdd(&misc[MISC_ARR], 1u);
     __syncthreads();  // X: window k's match info and take masks; window k - 1's records and literal bits
     ZH_STAMP(st_X);
-    if (wave == 1 && have) {
-      // ---- take decisions at window k's span tops (the next positions were another wave's)
+    if (have && wave != 0 && wave < (skipk ? RS : NWW - 1)) {
+      // ---- take decisions at this wave's span top (the next positions were the next wave's):
+      // every wave but the window's top one, its last one (LAZY2: two) positions
       constexpr u32 PER = LAZY2 ? 2u : 1u;
-      u32 const w = 1u + lane / PER;
-      u32 rh = 0;
-      for (u32 v = 0; v <= min(w, NWW - 1); v++) rh += rounds_of(v);
-      if (skipk) rh = w;  // (a miss-skip window: one round per wave)
-      bool const act = lane < PER * (skipk ? RS - 1 : NWW - 2);  // spans of waves 1..12 (1..RS-1)
-      u32 const i = act ? 64 * rh - 1 - lane % PER : 0u;
-      u32 const inf = ciK[cidx(i)], inf1 = ciK[cidx(i + 1)], inf2 = ciK[cidx(i + 2)];
-      if (act && i < we - wsb && (inf & 255u) && take_rule<LAZY2>(inf, inf1, inf2)) atomicOr((unsigned long long *)&tmK[i >> 6], 1ull << (i & 63));
+      u32 const hi = skipk ? wave : r_hi;
+      u32 const i = 64 * hi - 1 - (lane & (PER - 1));
+      if (lane < PER) {
+        u32 const inf = ciK[cidx(i)], inf1 = ciK[cidx(i + 1)], inf2 = ciK[cidx(i + 2)];
+        if (i < we - wsb && (inf & 255u) && take_rule<LAZY2>(inf, inf1, inf2)) atomicOr((unsigned long long *)&tmK[i >> 6], 1ull << (i & 63));
+      }
     }
     if (prev) {
       // ---- literals of window k - 1, lanes = positions (round r = segments 2r, 2r + 1)
@@ -1089,7 +1092,9 @@ __device__ __forceinline__ u32 lz_block(const ZhBlockDesc *__restrict__ blocks, 
         u32 const lbr = lane_value(lb, 2 * r);
         if ((lm >> lane) & 1ull) {
           u32 const rank = __builtin_amdgcn_mbcnt_hi((u32)(lm >> 32), __builtin_amdgcn_mbcnt_lo((u32)lm, 0u));
+#ifndef ZH_EXP_NOLIT
           lit_out[nlit_tot + lbr + rank] = in[wsp + 64 * r + lane];
+#endif
         }
       }
       nlit_tot += lane_value(lincl, 63);
@@ -1110,7 +1115,11 @@ __device__ __forceinline__ u32 lz_block(const ZhBlockDesc *__restrict__ blocks, 
   }
   if ((tid & 63) == 0 && tid < INS_TID) {  // each worker wave's length-phase cycles
     u32 const w = tid >> 6;
+#ifdef ZH_EXP_PWAIT
+    ws.dbg(b)[w < 12 ? 28 + w : 53 + (w - 12)] = st_A;
+#else
     ws.dbg(b)[w < 12 ? 28 + w : 53 + (w - 12)] = st_B;
+#endif
   }
 #endif
   return next_b;
