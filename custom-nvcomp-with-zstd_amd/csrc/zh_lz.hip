@@ -3,38 +3,36 @@
 // Replaces the reference's find_matches_kernel / greedy_parse_kernel /
 // build_sequences_gpu_kernel<<<1,1>>> (src/lz77_parallel.cu:26-70, 177-268)
 // and the literal gather kernels (src/cuda_zstd_manager.cu:602-723).
-// Output is identical to oracle/zstd_oracle.c orc_lz_parse (tile-lagged hash
-// insertion, longer of long/short candidate, greedy + lazy-1 parse).
+// Output is identical to oracle/zstd_oracle.c orc_lz_parse_pre (tile-lagged hash
+// insertion, longer of long/short candidate, greedy + lazy-1 (or LAZY2) parse, catch-up,
+// window-granular miss skip).
 //
-// One workgroup of 1024 threads (16 wave64, one workgroup per CU) per block,
-// everything in LDS:
-//   in[]   the block, staged once with 16-B loads (64 KiB)
+// One persistent workgroup of 1024 threads (16 wave64, one workgroup per CU), blocks taken
+// from a device counter, everything in LDS:
+//   in[]   the block (and its history prefix), staged once with 16-B loads (64 KiB)
 //   TL/TS  2 x 2^14 u16 hash tables, entry = position + 1 (0 = empty)
-//   cinfo  one 4096-position window: candidates -> match info (off<<8|len) in place
-//   tm     take masks (per 64-position round); per walk segment: the walk's literal and match
-//          bits, the literal bits after catch-up, the end of its last match
-//   mlist  the window's matches in position order, with their catch-up lengths
-// Wave roles (wave specialisation, synchronised with workgroup barriers):
-//   waves 14, 15  inserters: one wave per hash table walks the next window's
-//                 tiles of ZH_TILE positions.  A single wave needs no barrier
-//                 between a tile's lookups and its inserts because LDS executes
-//                 one wave's operations in order; lanes of one store that hit the
-//                 same slot are resolved to the latest position by a read-back.
-//                 Candidates are held in registers and dumped into cinfo at the
-//                 window switch, so the next window's insertion overlaps this
-//                 window's parse.
-//   waves 0..13   match lengths, lanes = positions: each candidate's common prefix
-//                 from its first 8 bytes, and along same-offset chains (the candidate
-//                 of p+1 is the candidate of p plus one) lcp(p) = 1 + lcp(p+1): a ballot
-//                 of the chain ends and one ds_bpermute give every position its length,
-//                 only chain ends past 8 bytes are extended.
-//   wave 0        the parse, lanes = 64-position segments: each lane walks its segment
-//                 (literal runs skipped through the has-match mask) from a guessed entry;
-//                 Jacobi rounds re-walk the segments whose entry changed until the walk
-//                 meets the previous one -- exactly the serial parse -- and lists the
-//                 window's matches.
-//   waves 0..13   lanes = matches: each match grows backwards over the literals before it
-//                 (catch-up), then the sequence records; lanes = positions: the literals.
+//   cinfo  two 2048-position windows: candidates -> match info (off<<8|len) in place
+//   tm     take masks (per 64-position round), two windows
+//   lm     per window parity, per 32-position walk segment: the literal bits
+//   mlist  per window parity: the window's matches in order (start, catch-up bound, length,
+//          offset, the walk's literals before it)
+// A three-stage window pipeline, step k:
+//   waves 14, 15  inserters (s_setprio 2): one wave per hash table inserts window k+1's tiles
+//                 of ZH_TILE positions, two per LDS round trip (program order = LDS order
+//                 within a wave; lanes of one store that hit the same slot are checked by a
+//                 read-back); candidates stay in registers and are dumped after barrier X.
+//   waves 1..13   window k's match lengths, lanes = positions: each candidate's common prefix
+//                 from its first 8 bytes, and along same-offset chains (the candidate of p+1
+//                 is the candidate of p plus one) lcp(p) = 1 + lcp(p+1): a ballot of the chain
+//                 ends and one ds_bpermute give every position its length, only chain ends
+//                 past 8 bytes are extended; then the parse's take decision per position.
+//   wave 0        window k-1's parse, lanes = 32-position segments: each lane walks its
+//                 segment (one literal run + one match per step, from the take mask) from a
+//                 guessed entry; Jacobi rounds re-walk the segments whose entry changed until
+//                 the walk meets the previous one -- exactly the serial parse; then the
+//                 window's match list.
+//   wave 1        after its lengths: window k-2's catch-up and sequence records.
+//   after X       span-top take decisions (each wave its own); window k-2's literals.
 #include "zh_common.h"
 
 #include <algorithm>
@@ -65,6 +63,7 @@ constexpr u32 TPL = ZH_TILE / 64;           // positions per inserter lane per t
 constexpr u32 NCR = TILES * TPL / 2;        // candidate registers per inserter lane (u16 pairs)
 static_assert(NSEG == 64, "one walk lane per segment");
 static_assert(INS_TID == 896 && NROUND == 32, "round split: waves 1..13 take 6 x 3 + 7 x 2 rounds");
+constexpr u32 REC_WAVE = 1;  // the worker wave that writes a window's records (after its length rounds)
 static_assert(ZH_WINDOW % ZH_TILE == 0 && ZH_TILE % 64 == 0 && TILES * TPL % 2 == 0, "tiles tile windows");
 
 constexpr u32 HL_SIZE = 1u << ZH_HASH_LOG_LONG;
@@ -84,11 +83,14 @@ constexpr u32 SEGM_WALK_LIT = 0, SEGM_MATCH = 1, SEGM_LIT = 2, SEGM_END = 3;  //
 // match starts, the literal bits left after catch-up, the end of the segment's last match
 __device__ __forceinline__ u32 segm(u32 par, u32 kind) { return (4 * par + kind) * NSEG; }
 constexpr u32 ML_CAP = ((ZH_WINDOW + ZH_MIN_MATCH_SHORT - 1) / ZH_MIN_MATCH_SHORT + 12 + 3) & ~3u;  // matches per window
-constexpr u32 OFF_ML = OFF_SEGM + 4 * 8 * NSEG;      // the parsed window's match starts, in order
+constexpr u32 OFF_ML = OFF_SEGM + 4 * 8 * NSEG;      // per window parity: the window's matches in order (u64,
+                                                     // ML_* fields) for the records one step later
 constexpr u32 XQ_CAP = 192;                          // chain-end queue entries per worker wave
-constexpr u32 OFF_XQ = OFF_ML + 4 * ML_CAP;          // u16 per entry: window index | S << 15
+constexpr u32 OFF_XQ = OFF_ML + 2 * 8 * ML_CAP;      // u16 per entry: window index | S << 15
 constexpr u32 OFF_MISC = OFF_XQ + 2 * XQ_CAP * NWW;  // [2 par + 0] matches, [2 par + 1] first parsed position
 constexpr u32 K1_LDS = OFF_MISC + 4 * 16;
+constexpr u32 ML_LO = 11, ML_LEN = 22, ML_OFF = 29, ML_CUM = 45;  // match-list entry: start [0, 11) | ...
+constexpr u32 MISC_WNM = 0;   // misc[par]: matches of the window of that parity (its match list's length)
 constexpr u32 MISC_ARR = 12;  // misc[12]: worker-wave barrier arrivals (cumulative)
 constexpr u32 MISC_NM = 4;    // misc[4 + (j & 3)]: matches the parse took in window j (miss skip)
 constexpr u32 MISC_ANY = 13;  // misc[13]: block_any's flag (0 between calls)
@@ -651,7 +653,7 @@ __device__ __forceinline__ void inserter_loop(const u32 *in32, u16 *T, u8 *ci8, 
 #endif
   u32 const nwin = (n - wstart + ZH_WINDOW - 1) / ZH_WINDOW;
   u32 passed = 0;  // X barriers taken so far
-  for (u32 k = 0; k < nwin + 1; k++) {
+  for (u32 k = 0; k < nwin + 2; k++) {
     u32 const wsb = wstart + k * ZH_WINDOW;
 #ifdef ZH_EXP_NODUMP
     if (k < nwin && !skipc) {
@@ -950,7 +952,7 @@ __device__ __forceinline__ u32 lz_block(const ZhBlockDesc *__restrict__ blocks, 
   u32 *const sgm = (u32 *)(smem + OFF_SEGM);
   u16 *const xq = (u16 *)(smem + OFF_XQ) + XQ_CAP * wave;
   u32 const nwin = (n - wstart + ZH_WINDOW - 1) / ZH_WINDOW;
-  u32 *const mlist = (u32 *)(smem + OFF_ML);
+  u64 *const mlist = (u64 *)(smem + OFF_ML);
   u32 nwalk_tot = 0;  // the walk's literal count before the parsed window (records carry it)
   // Step k (window j at wstart + j * ZH_WINDOW, parity j & 1):
   //   phase A  lengths of window k (waves 1..13) | parse, catch-up and sequence records of
@@ -958,13 +960,15 @@ __device__ __forceinline__ u32 lz_block(const ZhBlockDesc *__restrict__ blocks, 
   //   X
   //   phase B  take decisions at window k's span tops (each wave its own), the literals of
   //            window k - 1 (lanes = positions, all worker waves)
-  for (u32 k = 0; k < nwin + 1; k++) {
+  for (u32 k = 0; k < nwin + 2; k++) {
     u32 const wsb = wstart + k * ZH_WINDOW;
     u32 const we = min(wsb + ZH_WINDOW, n);
     u32 const kb = k & 1u;
     bool const have = k < nwin && we > pre;                    // window k: lengths
     u32 const wsp = wsb - ZH_WINDOW, wep = min(wsp + ZH_WINDOW, n);
-    bool const prev = k >= 1 && wep > pre;                     // window k - 1: parse, records, literals
+    bool const prev = k >= 1 && k <= nwin && wep > pre;        // window k - 1: parse, match list
+    u32 const wsq = wsb - 2 * ZH_WINDOW;
+    bool const prev2 = k >= 2 && min(wsq + ZH_WINDOW, n) > pre;  // window k - 2: records, literals
     // opaque per-step thread index: keeps the compiler from hoisting every LDS address
     // derived from it out of the loop (they would be spilled to scratch)
     u32 tid;
@@ -972,7 +976,9 @@ __device__ __forceinline__ u32 lz_block(const ZhBlockDesc *__restrict__ blocks, 
     u32 const lane = tid & 63;
     u32 *const ciK = ci0 + kb * CI_WORDS, *const ciP = ci0 + (kb ^ 1u) * CI_WORDS;
     u64 *const tmK = hm + kb * NROUND, *const tmP = hm + (kb ^ 1u) * NROUND;
-    u32 *const lmf = sgm + segm(0, SEGM_LIT);  // window k - 1's literal bits after catch-up
+    u32 *const lmP = sgm + segm(kb ^ 1u, SEGM_LIT);   // window k - 1's literal bits (the walk's)
+    u32 *const lmQ = sgm + segm(kb, SEGM_LIT);        // window k - 2's (after its catch-up)
+    u64 *const mlP = mlist + (kb ^ 1u) * ML_CAP, *const mlQ = mlist + kb * ML_CAP;
     __syncthreads();  // P: candidates of window k in buffer k & 1
     ZH_STAMP(st_A);
     // a miss-skip window has candidates in its first RS rounds only: waves 1..RS take one each
@@ -1026,48 +1032,61 @@ __device__ __forceinline__ u32 lz_block(const ZhBlockDesc *__restrict__ blocks, 
       }
       e_in = wsp + lane_value(ex, 63);
       ZH_STAMP(st_J1);
-      // the window's matches in position order
+      // the window's matches in position order, then their entries (lanes = matches): start |
+      // end of the match before it (the window's first parsed position for the first: the
+      // catch-up bound) | length | offset | the walk's literals before it
       u32 const ns = (u32)__popc(MM);
       u32 const is = wave_scan_incl(ns);
       u32 const nm = lane_value(is, 63);
-      lmf[lane] = LM;
+      lmP[lane] = LM;
       u32 const nwl = lane_value(wave_scan_incl((u32)__popc(LM)), 63);
       u32 mm = MM, q = is - ns;
       while (__ballot(mm != 0)) {
         if (mm) {
-          mlist[q++] = S + (u32)__builtin_ctz(mm);
+          mlP[q++] = S + (u32)__builtin_ctz(mm);
           mm &= mm - 1u;
         }
       }
       ZH_STAMP(st_J2);
-      // ---- catch-up and sequence records, lanes = matches.  A match's lower bound is the end
-      // of the match before it (the window's first parsed position for the first); it takes
-      // back e bytes of the literal run.  Record: the walk's literals before the match (its
-      // start - e0 - the lengths of the matches before it) | length | e | offset; K2 takes e off
-      // the literal run (zh_entropy.hip).
-      u32 covered = 0;  // walk lengths of the matches before this pass
+      u32 covered = 0, pend = e0;  // walk lengths of the matches before this pass; end of the last one
       for (u32 j0 = 0; j0 < nm; j0 += 64) {
         u32 const j = j0 + lane;
         bool const v = j < nm;
-        u32 const ms = v ? mlist[j] : 0u, inf = ciP[cidx(ms)];
-        u32 const pm = (v && j) ? mlist[j - 1] : 0u;
-        u32 const lo = (v && j) ? pm + (ciP[cidx(pm)] & 255u) : e0;
+        u32 const ms = v ? (u32)mlP[j] : 0u, inf = ciP[cidx(ms)];
         u32 const len = v ? inf & 255u : 0u, off = (inf >> 8) & 0xFFFFu;
-        u32 const e = catch_up(in32, wsp + ms, off, wsp + lo, v);
         u32 const incl = wave_scan_incl(len);
         u32 const cum = nwalk_tot + (ms - e0) - (covered + incl - len);
+        u32 lo = wave_shr1(ms + len);
+        if (lane == 0) lo = pend;
+        pend = lane_value(ms + len, min(63u, nm - 1u - j0));
         covered += lane_value(incl, 63);
+        if (v) mlP[j] = (u64)ms | ((u64)lo << ML_LO) | ((u64)len << ML_LEN) | ((u64)off << ML_OFF) | ((u64)cum << ML_CUM);
+      }
+      nwalk_tot += nwl;  // the window's walk literals (its last match may run past its end)
+      if (lane == 0) { misc[MISC_WNM + (kb ^ 1u)] = nm; misc[MISC_NM + ((k - 1) & 3)] = nm; }
+      ZH_STAMP(st_J);
+    }
+    if (wave == REC_WAVE && prev2) {
+      // ---- catch-up and sequence records of window k - 2, lanes = matches.  A match grows
+      // back over the literals down to the end of the match before it; it takes back e bytes of
+      // the literal run.  Record: the walk's literals before the match | length | e | offset;
+      // K2 takes e off the literal run (zh_entropy.hip).
+      u32 const nm = (u32)__builtin_amdgcn_readfirstlane(misc[MISC_WNM + kb]);
+      for (u32 j0 = 0; j0 < nm; j0 += 64) {
+        u32 const j = j0 + lane;
+        bool const v = j < nm;
+        u64 const en = v ? mlQ[j] : 0ull;
+        u32 const ms = (u32)en & 0x7FFu, lo = (u32)(en >> ML_LO) & 0x7FFu, len = (u32)(en >> ML_LEN) & 0x7Fu;
+        u32 const off = (u32)(en >> ML_OFF) & 0xFFFFu, cum = (u32)(en >> ML_CUM);
+        u32 const e = catch_up(in32, wsq + ms, off, wsq + lo, v);
         if (v) seq_out[nseq_tot + j] = (u64)cum | ((u64)len << 17) | ((u64)e << 24) | ((u64)off << 36);
         if (e) {
           for (u32 g = (ms - e) / SEGP; g <= (ms - 1) / SEGP; g++) {
             u32 const a = max(ms - e, SEGP * g) - SEGP * g, bnd = min(ms - SEGP * g, SEGP);
-            atomicAnd(&lmf[g], ~bit_range32(a, bnd));
+            atomicAnd(&lmQ[g], ~bit_range32(a, bnd));
           }
         }
       }
-      nwalk_tot += nwl;  // the window's walk literals (its last match may run past its end)
-      if (lane == 0) { misc[1] = nm; misc[MISC_NM + ((k - 1) & 3)] = nm; }
-      ZH_STAMP(st_J);
     }
     if (lane == 0) atomicAdd(&misc[MISC_ARR], 1u);
     __syncthreads();  // X: window k's match info and take masks; window k - 1's records and literal bits
@@ -1080,20 +1099,21 @@ __device__ __forceinline__ u32 lz_block(const ZhBlockDesc *__restrict__ blocks, 
       u32 const i = 64 * hi - 1 - (lane & (PER - 1));
       if (lane < PER) {
         u32 const inf = ciK[cidx(i)], inf1 = ciK[cidx(i + 1)], inf2 = ciK[cidx(i + 2)];
-        if (i < we - wsb && (inf & 255u) && take_rule<LAZY2>(inf, inf1, inf2)) atomicOr((unsigned long long *)&tmK[i >> 6], 1ull << (i & 63));
+        // (a 32-bit atomic on the mask's half: a hoisted 64-bit bit constant spilled)
+        if (i < we - wsb && (inf & 255u) && take_rule<LAZY2>(inf, inf1, inf2)) atomicOr((u32 *)&tmK[i >> 6] + ((i >> 5) & 1u), 1u << (i & 31));
       }
     }
-    if (prev) {
-      // ---- literals of window k - 1, lanes = positions (round r = segments 2r, 2r + 1)
-      u32 const nm = __builtin_amdgcn_readfirstlane(misc[1]);
-      u32 const lc = (u32)__popc(lmf[lane]), lincl = wave_scan_incl(lc), lb = lincl - lc;
+    if (prev2) {
+      // ---- literals of window k - 2, lanes = positions (round r = segments 2r, 2r + 1)
+      u32 const nm = __builtin_amdgcn_readfirstlane(misc[MISC_WNM + kb]);
+      u32 const lc = (u32)__popc(lmQ[lane]), lincl = wave_scan_incl(lc), lb = lincl - lc;
       for (u32 r = wave; r < NROUND; r += NWW) {
-        u64 const lm = ((u64)(u32)__builtin_amdgcn_readfirstlane(lmf[2 * r + 1]) << 32) | (u32)__builtin_amdgcn_readfirstlane(lmf[2 * r]);
+        u64 const lm = ((u64)(u32)__builtin_amdgcn_readfirstlane(lmQ[2 * r + 1]) << 32) | (u32)__builtin_amdgcn_readfirstlane(lmQ[2 * r]);
         u32 const lbr = lane_value(lb, 2 * r);
         if ((lm >> lane) & 1ull) {
           u32 const rank = __builtin_amdgcn_mbcnt_hi((u32)(lm >> 32), __builtin_amdgcn_mbcnt_lo((u32)lm, 0u));
 #ifndef ZH_EXP_NOLIT
-          lit_out[nlit_tot + lbr + rank] = in[wsp + 64 * r + lane];
+          lit_out[nlit_tot + lbr + rank] = in[wsq + 64 * r + lane];
 #endif
         }
       }
