@@ -397,11 +397,19 @@ __device__ __forceinline__ u32 ld4_before(const u32 *in32, u32 a) {
 //  C  (rounds high to low) lengths from the chain structure -> match info in place.
 constexpr u32 MAX_RW = 3;   // rounds per worker wave
 // Rounds (64-position segments) of worker wave w in a window's length phase: waves 1..13
-// (wave 0 parses), by SIMD (a CU's waves go to SIMDs by wave id mod 4): three for the waves on
-// SIMDs 0 and 1 but wave 13 (it takes the window's top span and the lookahead positions), two
-// for the waves sharing SIMDs 2 and 3 with the inserters.  3 x 6 + 2 x 7 = 32.
+// (wave 0 parses).  A CU's waves go to SIMDs by wave id mod 4 and the length phase saturates
+// VALU issue, so every SIMD gets 8 rounds -- SIMD 0 beside wave 0's parse, SIMD 1 beside wave
+// 1's records and wave 13's lookahead, SIMDs 2 and 3 beside an inserter each -- with the older
+// wave of a SIMD taking 3 (issue goes to the oldest ready wave).  Measured (C3 mix, K1 per
+// launch, one box): per-SIMD 9/11/6/6 rounds 12.30 ms, 9/9/7/7 11.86, 8/9/8/7 11.73,
+// 8/8/8/8 11.61, 8/7/8/9 12.29.
+constexpr u64 ROUND_TAB = 0xaabfbf8ull;  // 2 bits per wave: 0 2 3 3 3 2 3 3 3 2 2 2 2 2
 __device__ __forceinline__ u32 rounds_of(u32 w) {
-  return w == 0 ? 0u : (((w & 3u) == 1u && w != 13u) || (w & 3u) == 0u) ? 3u : 2u;
+#ifdef ZH_RTAB
+  return (u32)(((unsigned long long)(ZH_RTAB) >> (2 * w)) & 3u);
+#else
+  return (u32)((ROUND_TAB >> (2 * w)) & 3u);
+#endif
 }
 
 // Length of position p's candidate from the chain structure: T = ballot of the chain ends
@@ -655,11 +663,7 @@ __device__ __forceinline__ void inserter_loop(const u32 *in32, u16 *T, u8 *ci8, 
   u32 passed = 0;  // X barriers taken so far
   for (u32 k = 0; k < nwin + 2; k++) {
     u32 const wsb = wstart + k * ZH_WINDOW;
-#ifdef ZH_EXP_NODUMP
-    if (k < nwin && !skipc) {
-#else
     if (k < nwin) {
-#endif
       if (skipc) dump_window<LONG, ZH_SKIP_TILES>(ci8 + (k & 1u) * 4 * CI_WORDS, lane, creg, cwe);
       else dump_window<LONG, TILES>(ci8 + (k & 1u) * 4 * CI_WORDS, lane, creg, cwe);
     }
