@@ -21,7 +21,7 @@ struct ZhBlockDesc {
   u32 dst_cap;       // bytes available at dst
   u32 flags;         // ZH_F_* below
   const u8 *pre;     // ZH_F_DICT first block: dictionary content tail staged before the block
-  u32 pre_n;         // its length (pre_n + n <= ZH_BLOCK_MAX), 0 without a dictionary
+  u32 pre_n;         // its length (pre_n + n <= ZH_BLOCK_MAX; ZH_F_DEEP: pre_n <= ZH_DEEP_PRE), 0 without one
   u32 dict_id;       // Dictionary_ID written to the frame header (0: none)
 };
 
@@ -31,6 +31,8 @@ enum : u32 {
   ZH_F_DIRECT = 4u,  // single-block frame written straight into the item's output
   ZH_F_CHECKSUM = 8u,  // frame carries a content checksum (first block: FHD bit; zh_checksum_kernel appends it)
   ZH_F_DICT = 16u,     // dictionary frame: Dictionary_ID in the header, repcodes start unknown
+  ZH_F_DEEP = 32u,     // level >= ZH_DEEP_LEVEL (zh_lz_deep.hip): a dictionary frame's first block is staged
+                       // behind the last ZH_DEEP_PRE content bytes
 };
 
 // Per-block workspace carved from the caller's temp buffer.

@@ -1646,18 +1646,14 @@ constexpr u32 K3_LDS = K3_WAVES * K3_TAB_STRIDE;
 constexpr u32 K3_BATCH = 16;   // steps per code load / state store
 constexpr u32 K3_TABW = ZH_FSE_TAB_BYTES / 4;
 
-extern "C" __global__ __launch_bounds__(64 * K3_WAVES) __attribute__((amdgpu_waves_per_eu(8, 8))) void zh_fse_chain_kernel(const ZhBlockDesc *__restrict__ blocks, u32 nblocks, ZhWorkspace ws) {
-  extern __shared__ __attribute__((aligned(16))) u8 smem_all[];
-  u32 const lane = lane_id(), wv = threadIdx.x >> 6;
-  u32 const bb = blockIdx.x * K3_WAVES + wv;
-  u8 *const smem = smem_all + wv * K3_TAB_STRIDE;  // this wave's block tables
+// K3 of block bb (one wave; the caller checked that the block needs it); smem = the wave's
+// K3_TAB_STRIDE bytes of LDS
+__device__ __forceinline__ void k3_chain(ZhWorkspace ws, u32 bb, u8 *smem, u32 lane) {
 #ifdef ZH_STAMPS
   u64 const k3pre = __builtin_amdgcn_s_memtime();
   u64 const k3rt0 = __builtin_amdgcn_s_memrealtime();
 #endif
-  if (bb >= nblocks || blocks[bb].n == 0) return;
   u32 *ff = ws.fsef(bb);
-  if (ff[ZH_FF_NEED] == 0) return;
   {
     const u32 *src = (const u32 *)ws.fse(bb);
     u32 v[(K3_TABW + 63) / 64];
@@ -1779,6 +1775,15 @@ extern "C" __global__ __launch_bounds__(64 * K3_WAVES) __attribute__((amdgpu_wav
 #endif
 }
 
+extern "C" __global__ __launch_bounds__(64 * K3_WAVES) __attribute__((amdgpu_waves_per_eu(8, 8))) void zh_fse_chain_kernel(const ZhBlockDesc *__restrict__ blocks, u32 nblocks, ZhWorkspace ws) {
+  extern __shared__ __attribute__((aligned(16))) u8 smem_all[];
+  u32 const lane = lane_id(), wv = threadIdx.x >> 6;
+  u32 const bb = blockIdx.x * K3_WAVES + wv;
+  if (bb >= nblocks || blocks[bb].n == 0) return;
+  if (ws.fsef(bb)[ZH_FF_NEED] == 0) return;
+  k3_chain(ws, bb, smem_all + wv * K3_TAB_STRIDE, lane);  // this wave's block tables
+}
+
 // ======================= sequence bitstream packing (K2b) =======================
 // One wave per block left by the entropy kernel: FSE state bits and extra bits of 64
 // encode steps per bit-sink append, final state flush, then the block is finished
@@ -1788,17 +1793,10 @@ extern "C" __global__ __launch_bounds__(64 * K3_WAVES) __attribute__((amdgpu_wav
 constexpr u32 KP_SW = 0, KP_DNB = 4 * SW_WORDS, KP_LDS = (KP_DNB + 4 * 128 + 15) & ~15u;
 constexpr u32 K4_WAVES = 4;
 
-extern "C" __global__ __launch_bounds__(64 * K4_WAVES) void zh_seq_pack_kernel(const ZhBlockDesc *__restrict__ blocks, u32 nblocks, ZhWorkspace ws,
-                                                                               u64 *__restrict__ item_size, u32 *__restrict__ item_status,
-                                                                               u32 *__restrict__ blk_size) {
-  extern __shared__ __attribute__((aligned(16))) u8 smem_all[];
-  u32 const wv = threadIdx.x >> 6, b = blockIdx.x * K4_WAVES + wv, lane = lane_id();
-  u8 *const smem = smem_all + wv * KP_LDS;
-  if (b >= nblocks) return;
-  ZhBlockDesc const d = blocks[b];
-  if (d.n == 0) return;
+// K4 of block b (one wave; the caller checked that the block needs it); smem = KP_LDS bytes
+__device__ __forceinline__ void k4_pack(const ZhBlockDesc &d, ZhWorkspace ws, u32 b, u8 *smem, u32 lane, u64 *__restrict__ item_size,
+                                        u32 *__restrict__ item_status, u32 *__restrict__ blk_size) {
   const u32 *ff = ws.fsef(b);
-  if (ff[ZH_FF_NEED] == 0) return;
   u32 *sw = (u32 *)(smem + KP_SW);
   u32 *dNb = (u32 *)(smem + KP_DNB);  // LL [0, 36), OF [40, 72), ML [72, 125)
   const u8 *fz = ws.fse(b);
@@ -1812,6 +1810,8 @@ extern "C" __global__ __launch_bounds__(64 * K4_WAVES) void zh_seq_pack_kernel(c
   Out const o{d.dst, d.dst_cap};
   const u64 *seq = ws.seq(b);
   u32 const k3L = ZH_K3_SEGLEN(nbSeq), k3m = zh_k3_magic(k3L);
+  // K3's states in the chain layout (a step-linear layout, whole lines here but 32-B pieces for
+  // K3's stores, measured slower: entropy stage 3.05 -> 3.30 ms)
   const u16 *gLL = (const u16 *)ws.lits(b), *gOF = gLL + ZH_K3_TSTRIDE, *gML = gOF + ZH_K3_TSTRIDE;  // chain layout
   CodeTabs ct;
   ct.load();
@@ -1859,6 +1859,38 @@ extern "C" __global__ __launch_bounds__(64 * K4_WAVES) void zh_seq_pack_kernel(c
   write_status(d, b, total, item_size, item_status, blk_size);
 }
 
+extern "C" __global__ __launch_bounds__(64 * K4_WAVES) void zh_seq_pack_kernel(const ZhBlockDesc *__restrict__ blocks, u32 nblocks, ZhWorkspace ws,
+                                                                               u64 *__restrict__ item_size, u32 *__restrict__ item_status,
+                                                                               u32 *__restrict__ blk_size) {
+  extern __shared__ __attribute__((aligned(16))) u8 smem_all[];
+  u32 const wv = threadIdx.x >> 6, b = blockIdx.x * K4_WAVES + wv;
+  if (b >= nblocks) return;
+  ZhBlockDesc const d = blocks[b];
+  if (d.n == 0 || ws.fsef(b)[ZH_FF_NEED] == 0) return;
+  k4_pack(d, ws, b, smem_all + wv * KP_LDS, lane_id(), item_size, item_status, blk_size);
+}
+
+// K3 + K4 fused (ZH_K34_FUSED builds): one wave runs its block's state chains, then packs the
+// bitstream from the states it just wrote (L2-resident, not re-fetched from HBM by a second
+// kernel), with no launch boundary between the two.
+static_assert(KP_LDS <= K3_TAB_STRIDE, "K4's LDS fits the wave's K3 region");
+extern "C" __global__ __launch_bounds__(64 * K3_WAVES) __attribute__((amdgpu_waves_per_eu(8, 8))) void zh_fse_chain_pack_kernel(
+    const ZhBlockDesc *__restrict__ blocks, u32 nblocks, ZhWorkspace ws, u64 *__restrict__ item_size, u32 *__restrict__ item_status,
+    u32 *__restrict__ blk_size) {
+  extern __shared__ __attribute__((aligned(16))) u8 smem_all[];
+  u32 const lane = lane_id(), wv = threadIdx.x >> 6;
+  u32 const b = blockIdx.x * K3_WAVES + wv;
+  if (b >= nblocks) return;
+  ZhBlockDesc const d = blocks[b];
+  if (d.n == 0 || ws.fsef(b)[ZH_FF_NEED] == 0) return;
+  u8 *const smem = smem_all + wv * K3_TAB_STRIDE;
+  k3_chain(ws, b, smem, lane);
+  // the states other lanes stored, visible to this wave's loads (stores complete, L1 invalidated)
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "agent");
+  __builtin_amdgcn_wave_barrier();
+  k4_pack(d, ws, b, smem, lane, item_size, item_status, blk_size);
+}
+
 extern "C" u32 zh_entropy_lds_bytes() { return K2_LDS; }
 #ifdef ZH_STAMPS
 extern "C" __global__ void zh_read_hst(u32 *out) { for (int k = 0; k < 6; k++) { out[k] = g_hst[k]; g_hst[k] = 0; } }
@@ -1875,14 +1907,20 @@ namespace zh {
 hipError_t entropy_init() {
   hipError_t e = hipFuncSetAttribute((const void *)zh_entropy_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)K2_LDS);
   if (e == hipSuccess) e = hipFuncSetAttribute((const void *)zh_fse_chain_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)K3_LDS);
+  if (e == hipSuccess) e = hipFuncSetAttribute((const void *)zh_fse_chain_pack_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)K3_LDS);
   return e;
 }
 void entropy_launch(const ZhBlockDesc *d_descs, u32 nblocks, ZhWorkspace ws, u32 window_log, u32 cfg_block_size, u64 *d_item_size,
                     u32 *d_item_status, u32 *d_blk_size, hipStream_t stream) {
   hipLaunchKernelGGL(zh_entropy_kernel, dim3(nblocks), dim3(K2_THREADS), K2_LDS, stream, d_descs, ws, window_log, cfg_block_size, d_item_size,
                      d_item_status, d_blk_size);
+#ifdef ZH_K34_FUSED
+  hipLaunchKernelGGL(zh_fse_chain_pack_kernel, dim3((nblocks + K3_WAVES - 1) / K3_WAVES), dim3(64 * K3_WAVES), K3_LDS, stream, d_descs, nblocks, ws,
+                     d_item_size, d_item_status, d_blk_size);
+#else
   hipLaunchKernelGGL(zh_fse_chain_kernel, dim3((nblocks + K3_WAVES - 1) / K3_WAVES), dim3(64 * K3_WAVES), K3_LDS, stream, d_descs, nblocks, ws);
   hipLaunchKernelGGL(zh_seq_pack_kernel, dim3((nblocks + K4_WAVES - 1) / K4_WAVES), dim3(64 * K4_WAVES), K4_WAVES * KP_LDS, stream, d_descs, nblocks, ws, d_item_size,
                      d_item_status, d_blk_size);
+#endif
 }
 }  // namespace zh

@@ -139,7 +139,6 @@ namespace {
 constexpr u32 kSkippableMagic = 0x184D2A50u;  // RFC 8878 skippable frames 0x184D2A50..5F
 constexpr u32 kMetadataMagic = 0x444D5A43u;   // "CZMD": this library's metadata frame
 constexpr size_t kMetadataFrameBytes = 16;
-constexpr int kLazy2Level = 9;  // levels >= 9 (LAZY and up, reference src/cuda_zstd_types.cpp:172-182) parse LAZY2 on the device
 struct LibZstd {
   size_t (*compress)(void *, size_t, const void *, size_t, int) = nullptr;
   size_t (*decompress)(void *, size_t, const void *, size_t) = nullptr;
@@ -392,7 +391,7 @@ struct DevDict {
 // Descriptor fields of a block: a dictionary frame's first block gets the content tail that
 // fits in front of it in K1's 64 KiB of LDS; a later block of a history frame gets the 32 KiB
 // of input before it (when the window reaches that far)
-void set_dict_block(ZhBlockDesc &d, const DevDict *dd, bool first, bool hist) {
+void set_dict_block(ZhBlockDesc &d, const DevDict *dd, bool first, bool hist, bool deep) {
   d.pre = nullptr;
   d.pre_n = 0;
   d.dict_id = 0;
@@ -405,7 +404,9 @@ void set_dict_block(ZhBlockDesc &d, const DevDict *dd, bool first, bool hist) {
   d.dict_id = dd->id;
   if (!first) return;
   size_t const cn = dd->content_n();
-  d.pre_n = (u32)std::min(cn, (size_t)ZH_BLOCK_MAX - d.n);
+  // (the deep matcher of levels >= ZH_DEEP_LEVEL stages up to ZH_DEEP_PRE content bytes: it keeps
+  // the staged bytes in global memory, not in K1's 64 KiB of LDS)
+  d.pre_n = (u32)std::min(cn, deep ? (size_t)ZH_DEEP_PRE : (size_t)ZH_BLOCK_MAX - d.n);
   d.pre = dd->content() + cn - d.pre_n;
 }
 
@@ -482,8 +483,9 @@ class ZstdBatchManager::Impl {
         d.n = (u32)std::min(bs, n - k * bs);
         d.item = (u32)i;
         d.flags = (k == 0 ? ZH_F_FIRST : 0u) | (k + 1 == nb ? ZH_F_LAST : 0u) | (nb == 1 ? ZH_F_DIRECT : 0u) |
-                  (config.checksum != ChecksumPolicy::NO_COMPUTE_NO_VERIFY ? ZH_F_CHECKSUM : 0u);
-        set_dict_block(d, dd, k == 0, hist);
+                  (config.checksum != ChecksumPolicy::NO_COMPUTE_NO_VERIFY ? ZH_F_CHECKSUM : 0u) |
+                  (config.level >= ZH_DEEP_LEVEL ? ZH_F_DEEP : 0u);
+        set_dict_block(d, dd, k == 0, hist, config.level >= ZH_DEEP_LEVEL);
         if (nb == 1) {
           d.dst = (u8 *)out_ptrs[i];
           d.dst_cap = (u32)std::min(out_sizes[i], (size_t)0xFFFFFFFFu);
@@ -498,7 +500,7 @@ class ZstdBatchManager::Impl {
     hipError_t e = zh::launch_compress((const ZhBlockDesc *)(base + L.descs), (u32)nblocks, ws, config.window_log, config.block_size,
                                        (u64 *)(base + L.item_size), (u32 *)(base + L.item_status), (u32 *)(base + L.blk_size),
                                        (const ZhItemDesc *)(base + L.items), (u32)count, staged,
-                                       config.checksum != ChecksumPolicy::NO_COMPUTE_NO_VERIFY, config.level >= kLazy2Level, stream);
+                                       config.checksum != ChecksumPolicy::NO_COMPUTE_NO_VERIFY, config.level, stream);
     if (e != hipSuccess) return Status::ERROR_CUDA_ERROR;
     u64 *h_size = (u64 *)(h + up_bytes);
     u32 *h_status = (u32 *)(h_size + count);
@@ -883,13 +885,14 @@ Status ZstdBatchManager::compress_batch_device(const void *const *d_in_ptrs, con
   bool const ck = pimpl_->config.checksum != ChecksumPolicy::NO_COMPUTE_NO_VERIFY;
   u32 const hist = pimpl_->config.window_log >= ZH_HIST_WINDOW_LOG ? 1u : 0u;
   hipError_t e = zh::launch_plan(d_in_ptrs, d_in_sizes, (u32)count, (u32)bpi, d_out_ptrs, cap, base + L.staging, (ZhBlockDesc *)(base + L.descs),
-                                 (ZhItemDesc *)(base + L.items), item_size, item_status, ck ? ZH_F_CHECKSUM : 0u,
+                                 (ZhItemDesc *)(base + L.items), item_size, item_status,
+                                 (ck ? ZH_F_CHECKSUM : 0u) | (pimpl_->config.level >= ZH_DEEP_LEVEL ? ZH_F_DEEP : 0u),
                                  dd ? dd->content() : nullptr, dd ? (u32)dd->content_n() : 0u, dd ? dd->id : 0u, hist, stream);
   if (e != hipSuccess) return Status::ERROR_CUDA_ERROR;
   ZhWorkspace ws{base + L.blocks, (u32 *)(base + L.counter), dd && dd->tabs_P ? dd->tabs : nullptr, dd ? dd->tabs_P : 0u};
   e = zh::launch_compress((const ZhBlockDesc *)(base + L.descs), (u32)nblocks, ws, pimpl_->config.window_log, pimpl_->config.block_size, item_size,
                           item_status, (u32 *)(base + L.blk_size), (const ZhItemDesc *)(base + L.items), (u32)count, bpi > 1, ck,
-                          pimpl_->config.level >= kLazy2Level, stream);
+                          pimpl_->config.level, stream);
   return e == hipSuccess ? Status::SUCCESS : Status::ERROR_CUDA_ERROR;
 }
 

@@ -51,7 +51,7 @@ u32 entropy_lds_bytes();
 // out = 2^15 u16, tmp32 = 2^15 u32 scratch; P = the tail length covered (0: none)
 hipError_t lz_dict_tables(const u8 *content, size_t cn, u16 *out, u32 *tmp32, u32 &P, hipStream_t stream);
 hipError_t launch_compress(const ZhBlockDesc *d_descs, u32 nblocks, ZhWorkspace ws, u32 window_log, u32 cfg_block_size, u64 *d_item_size,
-                           u32 *d_item_status, u32 *d_blk_size, const ZhItemDesc *d_items, u32 nitems, bool gather, bool checksum, bool lazy2,
+                           u32 *d_item_status, u32 *d_blk_size, const ZhItemDesc *d_items, u32 nitems, bool gather, bool checksum, int level,
                            hipStream_t stream);
 void profile_enable(bool on);
 int profile_collect(double *totals);

@@ -34,6 +34,7 @@
 //   wave 1        after its lengths: window k-2's catch-up and sequence records.
 //   after X       span-top take decisions (each wave its own); window k-2's literals.
 #include "zh_common.h"
+#include "zh_hash.h"
 
 #include <algorithm>
 #include <vector>
@@ -97,20 +98,6 @@ constexpr u32 MISC_ANY = 13;  // misc[13]: block_any's flag (0 between calls)
 static_assert(K1_LDS <= 163840 - 256, "K1 LDS budget");
 static_assert(OFF_TL % 16 == 0 && OFF_CI % 16 == 0 && OFF_HM % 16 == 0 && OFF_MISC % 4 == 0, "alignment");
 
-// Hashes of include/zstd_hip_params.h: full-rate v_mad_u32_u24 sums (the 24-bit multiplies
-// take the low 24 bits of each operand, so byte groups need no masking but the short hash's
-// bytes 3-4)
-__device__ __forceinline__ u32 hash_long(u32 lo, u32 hi) {
-  u32 t = __umul24(lo, ZH_HK_L0);
-  t += __umul24(__builtin_amdgcn_alignbyte(hi, lo, 3), ZH_HK_L1);
-  t += __umul24(hi >> 16, ZH_HK_L2);
-  return t >> (32 - ZH_HASH_LOG_LONG);
-}
-__device__ __forceinline__ u32 hash_short(u32 lo, u32 hi) {
-  u32 t = __umul24(lo, ZH_HK_S0);
-  t += __umul24(__builtin_amdgcn_alignbyte(hi, lo, 3) & 0xFFFFu, ZH_HK_S1);
-  return t >> (32 - ZH_HASH_LOG_SHORT);
-}
 
 // 8 bytes at p from LDS as (lo, hi): three aligned dwords + v_alignbyte
 __device__ __forceinline__ void ld64u(const u32 *in32, u32 p, u32 &lo, u32 &hi) {

@@ -19,6 +19,8 @@ extern "C" u32 zh_entropy_lds_bytes();
 namespace zh {
 hipError_t lz_init();
 void lz_launch(const ZhBlockDesc *d_descs, u32 nblocks, ZhWorkspace ws, bool lazy2, hipStream_t stream);
+hipError_t lz_deep_init();
+hipError_t lz_deep_launch(const ZhBlockDesc *d_descs, u32 nblocks, ZhWorkspace ws, int level, hipStream_t stream);
 hipError_t entropy_init();
 void entropy_launch(const ZhBlockDesc *d_descs, u32 nblocks, ZhWorkspace ws, u32 window_log, u32 cfg_block_size, u64 *d_item_size,
                     u32 *d_item_status, u32 *d_blk_size, hipStream_t stream);
@@ -51,7 +53,7 @@ extern "C" __global__ void zh_plan_kernel(const void *const *__restrict__ in_ptr
     d.flags |= ZH_F_DICT;
     d.dict_id = dict_id;
     if (k == 0) {
-      d.pre_n = min(dict_n, (u32)ZH_BLOCK_MAX - d.n);
+      d.pre_n = (extra_flags & ZH_F_DEEP) ? min(dict_n, (u32)ZH_DEEP_PRE) : min(dict_n, (u32)ZH_BLOCK_MAX - d.n);
       d.pre = dict + dict_n - d.pre_n;
     }
   }
@@ -145,6 +147,8 @@ namespace zh {
 hipError_t init_kernels() {
   hipError_t e = lz_init();
   if (e != hipSuccess) return e;
+  e = lz_deep_init();
+  if (e != hipSuccess) return e;
   return entropy_init();
 }
 
@@ -198,7 +202,7 @@ int profile_collect(double *totals) {
 }
 
 hipError_t launch_compress(const ZhBlockDesc *d_descs, u32 nblocks, ZhWorkspace ws, u32 window_log, u32 cfg_block_size, u64 *d_item_size,
-                           u32 *d_item_status, u32 *d_blk_size, const ZhItemDesc *d_items, u32 nitems, bool gather, bool checksum, bool lazy2,
+                           u32 *d_item_status, u32 *d_blk_size, const ZhItemDesc *d_items, u32 nitems, bool gather, bool checksum, int level,
                            hipStream_t stream) {
   if (nblocks == 0) return hipSuccess;
   std::vector<hipEvent_t> ev;
@@ -208,7 +212,13 @@ hipError_t launch_compress(const ZhBlockDesc *d_descs, u32 nblocks, ZhWorkspace 
   }
   if (!ev.empty()) (void)hipEventRecord(ev[0], stream);
   (void)hipMemsetAsync(ws.ctr, 0, 4, stream);  // K1's block counter
-  lz_launch(d_descs, nblocks, ws, lazy2, stream);
+  // levels >= ZH_DEEP_LEVEL: the deep chain matcher; below: K1's dual-hash parse
+  if (level >= ZH_DEEP_LEVEL) {
+    hipError_t const e = lz_deep_launch(d_descs, nblocks, ws, level, stream);
+    if (e != hipSuccess) return e;
+  } else {
+    lz_launch(d_descs, nblocks, ws, false, stream);
+  }
   if (!ev.empty()) (void)hipEventRecord(ev[1], stream);
   entropy_launch(d_descs, nblocks, ws, window_log, cfg_block_size, d_item_size, d_item_status, d_blk_size, stream);
   if (!ev.empty()) (void)hipEventRecord(ev[2], stream);

@@ -42,6 +42,17 @@
 #define ZH_HK_L2 0xC2B2AEu
 #define ZH_HK_S0 0x27D4EBu
 #define ZH_HK_S1 0x165667u
+/* Deep matcher, levels >= ZH_DEEP_LEVEL (reference level table
+ * src/cuda_zstd_types.cpp:172-183, matcher src/lz77_parallel.cu:26-70): exact hash chains over
+ * the whole staged buffer (a dictionary frame's first block is staged behind the last
+ * ZH_DEEP_PRE bytes of the dictionary content), keyed by the 5-byte short hash; per position the
+ * longest of the first ZH_DEEP_DEPTH(level) chain candidates within ZH_DEEP_MAXOFF (>=
+ * ZH_MIN_MATCH_SHORT bytes, capped at ZH_MAX_MATCH, nearest on ties); LAZY2 parse on those
+ * matches, no catch-up. */
+#define ZH_DEEP_LEVEL 9
+#define ZH_DEEP_PRE 65536
+#define ZH_DEEP_MAXOFF 131068      /* offset + 3 fits the 17-bit offset field of a sequence record */
+#define ZH_DEEP_DEPTH(level) ((level) <= 9 ? 32 : (level) == 10 ? 64 : 128)
 #define ZH_COMPRESS_LITERALS_SIZE_MIN 63
 #define ZH_LONGNBSEQ 0x7F00
 #define ZH_MAGIC 0xFD2FB528u

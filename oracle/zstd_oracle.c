@@ -858,8 +858,67 @@ void orc_lz_match_info(const u8 *src, u32 n, u8 *len, u16 *off) {
  * match at p is deferred when the match at p+1 gains more than 4, or the one at p+2 more than 7,
  * with gain = 4 x length - bit length of (offset + 1).  Set by orc_compress_frame_lv. */
 static int orc_parse_lazy2 = 0;
+static int orc_parse_level = 3; /* levels >= ZH_DEEP_LEVEL: the deep matcher (orc_lz_parse_deep) */
 static int match_gain(const u8 *len, const u16 *off, u32 p) {
   return len[p] ? 4 * (int)len[p] - (31 - __builtin_clz((u32)off[p] + 1u)) : -1000;
+}
+static int match_gain32(const u8 *len, const u32 *off, u32 p) {
+  return len[p] ? 4 * (int)len[p] - (31 - __builtin_clz(off[p] + 1u)) : -1000;
+}
+
+/* Deep matcher (levels >= ZH_DEEP_LEVEL; the reference's level table gives level 9
+ * a 32-candidate chain search, src/cuda_zstd_types.cpp:172-183, walked per position by
+ * find_matches_kernel, src/lz77_parallel.cu:26-70, whose atomicExch chain insert makes it
+ * nondeterministic).  Deterministic restatement, what zh_lz_deep_kernel computes:
+ *   - exact hash chains over the whole staged buffer buf[0, n) (history/dictionary prefix
+ *     [0, pre) + block): prev[p] = the latest q < p with the same 5-byte short hash, positions
+ *     [0, lim) with lim = n - ZH_HASH_READ;
+ *   - per block position p in [pre, lim): the first `depth` chain candidates at offsets up to
+ *     ZH_DEEP_MAXOFF (the walk ends at the first one further away), each's common
+ *     prefix with p (capped at ZH_MAX_MATCH and at n); the longest with >= ZH_MIN_MATCH_SHORT
+ *     bytes wins, the nearest on ties; the walk stops early at a capped match;
+ *   - LAZY2 parse from pre (libzstd ZSTD_compressBlock_lazy_generic's depth-2 rule, as
+ *     orc_lz_parse_pre), no catch-up, a directly following same-offset match merged. */
+size_t orc_lz_parse_deep(const u8 *buf, u32 pre, u32 n, u32 depth, orc_seq_t *seq, u32 *last_lits) {
+  u32 const lim = n > ZH_HASH_READ ? n - ZH_HASH_READ : 0;
+  u32 *prev = malloc(sizeof(u32) * (lim + 1));
+  u32 *head = calloc((size_t)1 << ZH_HASH_LOG_SHORT, sizeof(u32));
+  u8 *len = calloc(n + 3, 1);
+  u32 *off = calloc(n + 3, sizeof(u32));
+  for (u32 p = 0; p < lim; p++) {
+    u32 const h = zh_hash_short(rd64(buf + p));
+    prev[p] = head[h]; /* q + 1, 0 = none */
+    head[h] = p + 1;
+  }
+  for (u32 p = pre; p < lim; p++) {
+    u32 best = 0, bo = 0, c = prev[p];
+    for (u32 d = 0; d < depth && c && p - (c - 1) <= ZH_DEEP_MAXOFF; d++) {
+      u32 const q = c - 1, l = common_prefix(buf, p, q, n, ZH_MAX_MATCH);
+      if (l >= ZH_MIN_MATCH_SHORT && l > best) {
+        best = l;
+        bo = p - q;
+        if (best >= ZH_MAX_MATCH) break;
+      }
+      c = prev[q];
+    }
+    len[p] = (u8)best;
+    off[p] = bo;
+  }
+  size_t ns = 0;
+  u32 p = pre, anchor = pre;
+  while (p < lim) {
+    if (len[p] == 0) { p++; continue; }
+    int const g0 = match_gain32(len, off, p);
+    if (match_gain32(len, off, p + 1) > g0 + 4 || match_gain32(len, off, p + 2) > g0 + 7) { p++; continue; }
+    u32 const ll = p - anchor, of = off[p];
+    if (ns && ll == 0 && seq[ns - 1].off == of) seq[ns - 1].ml += len[p];
+    else { seq[ns].ll = ll; seq[ns].ml = len[p]; seq[ns].off = of; ns++; }
+    p += len[p];
+    anchor = p;
+  }
+  *last_lits = n - anchor;
+  free(prev); free(head); free(len); free(off);
+  return ns;
 }
 /* Miss skip (libzstd dfast's kSearchStrength idea at window granularity): the matcher and the
  * parse run window by window (ZH_WINDOW positions, aligned in the staged buffer, as K1's
@@ -868,6 +927,7 @@ static int match_gain(const u8 *len, const u16 *off, u32 p) {
  * catch-up) searches and inserts only its first ZH_SKIP_TILES tiles; the rest of it has no
  * candidates.  Windows up to three past the one holding `pre` never skip. */
 size_t orc_lz_parse_pre(const u8 *src, u32 pre, u32 n, orc_seq_t *seq, u32 *last_lits) {
+  if (orc_parse_level >= ZH_DEEP_LEVEL) return orc_lz_parse_deep(src, pre, n, ZH_DEEP_DEPTH(orc_parse_level), seq, last_lits);
   u8 *len = malloc(n + 2);
   u16 *off = malloc(sizeof(u16) * (n + 2));
   match_info_reset(n, len, off);
@@ -1126,7 +1186,8 @@ size_t orc_compress_frame_dict(u8 *dst, size_t cap, const u8 *src, u64 n, u32 bl
     size_t w;
     if (b == 0 && dict_n) {
       size_t cn = dict_n - co;
-      u32 pre = (u32)(cn < (size_t)(ZH_BLOCK_MAX - bn) ? cn : (size_t)(ZH_BLOCK_MAX - bn));
+      size_t const room = orc_parse_level >= ZH_DEEP_LEVEL ? (size_t)ZH_DEEP_PRE : (size_t)(ZH_BLOCK_MAX - bn);
+      u32 pre = (u32)(cn < room ? cn : room);
       u8 *buf = malloc((size_t)pre + bn + 16);
       memcpy(buf, dict + dict_n - pre, pre);
       memcpy(buf + pre, src, bn);
@@ -1152,13 +1213,16 @@ size_t orc_compress_frame_dict(u8 *dst, size_t cap, const u8 *src, u64 n, u32 bl
 size_t orc_compress_frame_ck(u8 *dst, size_t cap, const u8 *src, u64 n, u32 block_size, u32 window_log, int checksum) {
   return orc_compress_frame_dict(dst, cap, src, n, block_size, window_log, checksum, NULL, 0);
 }
-/* The frame at a compression level: levels >= 9 parse LAZY2 (the device's zh_lz_lazy2_kernel). */
+/* The frame at a compression level: levels >= ZH_DEEP_LEVEL run the deep matcher (the device's
+ * zh_lz_deep_kernel); the dual-hash LAZY2 parse (orc_parse_lazy2) stays for the study tools. */
 size_t orc_compress_frame_lv(u8 *dst, size_t cap, const u8 *src, u64 n, u32 block_size, u32 window_log, int checksum, const u8 *dict,
                              size_t dict_n, int level) {
-  int const save = orc_parse_lazy2;
+  int const save = orc_parse_lazy2, save_lv = orc_parse_level;
   orc_parse_lazy2 = level >= 9;
+  orc_parse_level = level;
   size_t const r = orc_compress_frame_dict(dst, cap, src, n, block_size, window_log, checksum, dict, dict_n);
   orc_parse_lazy2 = save;
+  orc_parse_level = save_lv;
   return r;
 }
 

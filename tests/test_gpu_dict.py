@@ -123,8 +123,9 @@ def test_reference_dictionary_scenario(torch_cuda):
 def test_c5_level9_cover_64k(torch_cuda, libzstd):
     """Config C5 at test size: level 9, a 64 KiB COVER dictionary trained by
     cuda_zstd_train_dictionary on 256 JSON-like records of 16 KiB (seed 0x5EED0005); 256 other
-    records compressed in one batch.  GPU frames == the oracle's, libzstd decodes them with
-    the dictionary, and the ratio gains over no dictionary."""
+    records compressed in one batch.  GPU frames == the oracle's (the deep matcher: 32 chain
+    candidates, the whole 64 KiB dictionary staged), libzstd decodes them with the dictionary,
+    and the ratios reach the round-3 targets (libzstd L9 on the same records: ~7.2 / ~8.9)."""
     import cuda_zstd
 
     recs = T.gen(T.DG_JSON, 512, 0x5EED0005, 16384)
@@ -146,6 +147,7 @@ def test_c5_level9_cover_64k(torch_cuda, libzstd):
     ratio0 = total / sum(o.numel() for o in plain)
     print(f"C5 (256 x 16 KiB, level 9): ratio {ratio0:.3f} without -> {ratio:.3f} with the 64 KiB COVER dictionary")
     assert ratio > 1.15 * ratio0
+    assert ratio0 >= 6.6 and ratio >= 8.5, (ratio0, ratio)
 
 
 def test_dictionary_tables_ragged_sizes(torch_cuda):

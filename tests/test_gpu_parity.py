@@ -268,14 +268,16 @@ def test_full_size_blocks_match_libzstd(torch_cuda, mgr):
 
 
 @pytest.mark.parametrize("level", [9, 19])
-def test_lazy2_levels_match_oracle(torch_cuda, level):
-    """Levels >= 9 run the LAZY2 parse (zh_lz_lazy2_kernel): frames equal the
-    oracle's at that level and decode with libzstd; ragged and multi-block sizes included."""
+def test_deep_levels_match_oracle(torch_cuda, level):
+    """Levels >= 9 run the deep chain matcher (zh_lz_deep_kernel: exact hash chains, the level's
+    search depth, LAZY2 parse): frames equal the oracle's at that level and
+    decode with libzstd; ragged, multi-block (history) and RLE sizes included."""
     import cuda_zstd
 
     m = cuda_zstd.Manager(level)
     datas = [T.gen(k, 1, 40 + k, s) for k, s in ((T.DG_JSON, 65536), (T.DG_TEXT, 65536), (T.DG_MIX, 65536), (T.DG_SOURCE, 40000),
                                                 (T.DG_CSV, 300000), (T.DG_EXE, 777), (T.DG_SENSOR, 65535))]
+    datas += [np.zeros(5000, dtype=np.uint8), T.gen(T.DG_RANDOM, 1, 41, 70000), T.gen(T.DG_TEXT, 1, 42, 9)]
     outs = m.compress_batch([torch_cuda.from_numpy(d).cuda() for d in datas])
     for k, (o, d) in enumerate(zip(outs, datas)):
         got = o.cpu().numpy().tobytes()
