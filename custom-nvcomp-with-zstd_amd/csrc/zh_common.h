@@ -85,6 +85,12 @@ struct ZhWorkspace {
   // dtab_P content bytes, positions [0, dtab_P - ZH_DTAB_MARGIN) inserted
   const u16 *dtab;
   u32 dtab_P;
+  // The deep matcher's chains of the batch dictionary (levels >= ZH_DEEP_LEVEL; null: none):
+  // links of staged positions [0, dd_split) of a first block with dd_pre staged content bytes, and
+  // the head table after them (zh_lz_deep.hip zh_deep_dict_kernel)
+  const u32 *dd_prev;
+  const u32 *dd_head;
+  u32 dd_pre, dd_split;
   __device__ u64 *seq(u32 b) const { return (u64 *)(base + (size_t)b * ZH_WS_BLOCK_BYTES); }
   __device__ u8 *lits(u32 b) const { return base + (size_t)b * ZH_WS_BLOCK_BYTES + ZH_SEQ_BYTES; }
   __device__ u32 *meta(u32 b) const { return (u32 *)(base + (size_t)b * ZH_WS_BLOCK_BYTES + ZH_SEQ_BYTES + ZH_LIT_BYTES); }

@@ -1792,6 +1792,10 @@ extern "C" __global__ __launch_bounds__(64 * K3_WAVES) __attribute__((amdgpu_wav
 // most 16 workgroups.
 constexpr u32 KP_SW = 0, KP_DNB = 4 * SW_WORDS, KP_LDS = (KP_DNB + 4 * 128 + 15) & ~15u;
 constexpr u32 K4_WAVES = 4;
+#ifndef ZH_K4_PF
+#define ZH_K4_PF 3
+#endif
+constexpr u32 K4_PF = ZH_K4_PF;  // chunks in flight
 
 // K4 of block b (one wave; the caller checked that the block needs it); smem = KP_LDS bytes
 __device__ __forceinline__ void k4_pack(const ZhBlockDesc &d, ZhWorkspace ws, u32 b, u8 *smem, u32 lane, u64 *__restrict__ item_size,
@@ -1817,25 +1821,28 @@ __device__ __forceinline__ void k4_pack(const ZhBlockDesc &d, ZhWorkspace ws, u3
   ct.load();
   wave_sync();
   BitSink bs{ff[ZH_FF_OP], 0};
-  u64 nrec = lane < nbSeq ? seq[nbSeq - 1 - lane] : 0;
-  u32 nL = 0, nM = 0, nO = 0;
-  if (0 < lane && lane < nbSeq) {
-    u32 const x = zh_k3_index(lane, 0, k3L, k3m);
-    nL = gLL[x]; nM = gML[x]; nO = gOF[x];
-  }
+  // K4_PF 64-step chunks of records and states in flight (a chunk's work is shorter than a
+  // global round trip: with one chunk ahead a block's packing was latency-bound)
+  u64 rq[K4_PF];
+  u32 lq[K4_PF], mq[K4_PF], oq[K4_PF];
+  auto fetch = [&](u32 e, u64 &r, u32 &sl, u32 &sm, u32 &so) {
+    r = e < nbSeq ? seq[nbSeq - 1 - e] : 0;
+    sl = sm = so = 0;
+    if (0 < e && e < nbSeq) {
+      u32 const x = zh_k3_index(e, 0, k3L, k3m);
+      sl = gLL[x]; sm = gML[x]; so = gOF[x];
+    }
+  };
+#pragma unroll
+  for (u32 j = 0; j < K4_PF; j++) fetch(64 * j + lane, rq[j], lq[j], mq[j], oq[j]);
   for (u32 e0 = 0; e0 < nbSeq; e0 += 64) {
     u32 const e = e0 + lane;
     bool const valid = e < nbSeq;
-    u64 const rec = nrec;
-    u32 const s_L = nL, s_M = nM, s_O = nO;
-    u32 const en = e + 64;
-    nrec = en < nbSeq ? seq[nbSeq - 1 - en] : 0;  // next chunk in flight
-    if (en < nbSeq) {
-      u32 const x = zh_k3_index(en, 0, k3L, k3m);
-      nL = gLL[x]; nM = gML[x]; nO = gOF[x];
-    } else {
-      nL = nM = nO = 0;
-    }
+    u64 const rec = rq[0];
+    u32 const s_L = lq[0], s_M = mq[0], s_O = oq[0];
+#pragma unroll
+    for (u32 j = 0; j + 1 < K4_PF; j++) { rq[j] = rq[j + 1]; lq[j] = lq[j + 1]; mq[j] = mq[j + 1]; oq[j] = oq[j + 1]; }
+    fetch(e + 64 * K4_PF, rq[K4_PF - 1], lq[K4_PF - 1], mq[K4_PF - 1], oq[K4_PF - 1]);
     u32 const ll = (u32)(rec & 0x1FFFFu), mlb = (u32)((rec >> 17) & 0x1FFFFu), ob = (u32)(rec >> 34) & 0x1FFFFu;
     u32 const llc = valid ? (u32)(rec >> 51) & 63u : 0, mlc = valid ? (u32)(rec >> 57) & 63u : 0, ofc = valid ? highbit32(ob) : 0;
     u32 const llbits = ct.ll_bits(llc), mlbits = ct.ml_bits(mlc);
@@ -1870,27 +1877,6 @@ extern "C" __global__ __launch_bounds__(64 * K4_WAVES) void zh_seq_pack_kernel(c
   k4_pack(d, ws, b, smem_all + wv * KP_LDS, lane_id(), item_size, item_status, blk_size);
 }
 
-// K3 + K4 fused (ZH_K34_FUSED builds): one wave runs its block's state chains, then packs the
-// bitstream from the states it just wrote (L2-resident, not re-fetched from HBM by a second
-// kernel), with no launch boundary between the two.
-static_assert(KP_LDS <= K3_TAB_STRIDE, "K4's LDS fits the wave's K3 region");
-extern "C" __global__ __launch_bounds__(64 * K3_WAVES) __attribute__((amdgpu_waves_per_eu(8, 8))) void zh_fse_chain_pack_kernel(
-    const ZhBlockDesc *__restrict__ blocks, u32 nblocks, ZhWorkspace ws, u64 *__restrict__ item_size, u32 *__restrict__ item_status,
-    u32 *__restrict__ blk_size) {
-  extern __shared__ __attribute__((aligned(16))) u8 smem_all[];
-  u32 const lane = lane_id(), wv = threadIdx.x >> 6;
-  u32 const b = blockIdx.x * K3_WAVES + wv;
-  if (b >= nblocks) return;
-  ZhBlockDesc const d = blocks[b];
-  if (d.n == 0 || ws.fsef(b)[ZH_FF_NEED] == 0) return;
-  u8 *const smem = smem_all + wv * K3_TAB_STRIDE;
-  k3_chain(ws, b, smem, lane);
-  // the states other lanes stored, visible to this wave's loads (stores complete, L1 invalidated)
-  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "agent");
-  __builtin_amdgcn_wave_barrier();
-  k4_pack(d, ws, b, smem, lane, item_size, item_status, blk_size);
-}
-
 extern "C" u32 zh_entropy_lds_bytes() { return K2_LDS; }
 #ifdef ZH_STAMPS
 extern "C" __global__ void zh_read_hst(u32 *out) { for (int k = 0; k < 6; k++) { out[k] = g_hst[k]; g_hst[k] = 0; } }
@@ -1907,20 +1893,14 @@ namespace zh {
 hipError_t entropy_init() {
   hipError_t e = hipFuncSetAttribute((const void *)zh_entropy_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)K2_LDS);
   if (e == hipSuccess) e = hipFuncSetAttribute((const void *)zh_fse_chain_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)K3_LDS);
-  if (e == hipSuccess) e = hipFuncSetAttribute((const void *)zh_fse_chain_pack_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)K3_LDS);
   return e;
 }
 void entropy_launch(const ZhBlockDesc *d_descs, u32 nblocks, ZhWorkspace ws, u32 window_log, u32 cfg_block_size, u64 *d_item_size,
                     u32 *d_item_status, u32 *d_blk_size, hipStream_t stream) {
   hipLaunchKernelGGL(zh_entropy_kernel, dim3(nblocks), dim3(K2_THREADS), K2_LDS, stream, d_descs, ws, window_log, cfg_block_size, d_item_size,
                      d_item_status, d_blk_size);
-#ifdef ZH_K34_FUSED
-  hipLaunchKernelGGL(zh_fse_chain_pack_kernel, dim3((nblocks + K3_WAVES - 1) / K3_WAVES), dim3(64 * K3_WAVES), K3_LDS, stream, d_descs, nblocks, ws,
-                     d_item_size, d_item_status, d_blk_size);
-#else
   hipLaunchKernelGGL(zh_fse_chain_kernel, dim3((nblocks + K3_WAVES - 1) / K3_WAVES), dim3(64 * K3_WAVES), K3_LDS, stream, d_descs, nblocks, ws);
   hipLaunchKernelGGL(zh_seq_pack_kernel, dim3((nblocks + K4_WAVES - 1) / K4_WAVES), dim3(64 * K4_WAVES), K4_WAVES * KP_LDS, stream, d_descs, nblocks, ws, d_item_size,
                      d_item_status, d_blk_size);
-#endif
 }
 }  // namespace zh

@@ -325,6 +325,10 @@ struct DevDict {
   u16 *tabs = nullptr;
   u32 *tabs_tmp = nullptr;
   u32 tabs_P = 0;
+  // the deep matcher's chains of the content tail (levels >= ZH_DEEP_LEVEL), built at load
+  u32 *deep_prev = nullptr, *deep_head = nullptr;
+  u8 *deep_stg = nullptr;
+  u32 deep_P = 0, deep_split = 0;
   std::vector<u8> host;  // the loaded bytes (a reload of the same dictionary keeps everything)
   DevDict() = default;
   DevDict(const DevDict &) = delete;
@@ -333,6 +337,9 @@ struct DevDict {
     if (d && owned) (void)hipFree(d);
     if (tabs) (void)hipFree(tabs);
     if (tabs_tmp) (void)hipFree(tabs_tmp);
+    if (deep_prev) (void)hipFree(deep_prev);
+    if (deep_head) (void)hipFree(deep_head);
+    if (deep_stg) (void)hipFree(deep_stg);
   }
   // raw-content view of device-resident history (never freed here)
   static void view(DevDict &v, const void *p, size_t bytes) {
@@ -342,6 +349,7 @@ struct DevDict {
     v.off = 0;
     v.id = 0;
     v.tabs_P = 0;  // (a moving history window: hashed by every block)
+    v.deep_P = 0;
   }
   const u8 *content() const { return d + off; }
   size_t content_n() const { return n - off; }
@@ -376,6 +384,18 @@ struct DevDict {
       if (zh::lz_dict_tables(content(), content_n(), tabs, tabs_tmp, P, stream) == hipSuccess && hipStreamSynchronize(stream) == hipSuccess)
         tabs_P = P;
     }
+    deep_P = deep_split = 0;
+    if (!deep_prev && hipMalloc(&deep_prev, 4u * ZH_DEEP_PRE) != hipSuccess) deep_prev = nullptr;
+    if (!deep_head && hipMalloc(&deep_head, 4u << ZH_HASH_LOG_SHORT) != hipSuccess) deep_head = nullptr;
+    if (!deep_stg && hipMalloc(&deep_stg, ZH_DEEP_PRE + 256) != hipSuccess) deep_stg = nullptr;
+    if (deep_prev && deep_head && deep_stg) {
+      u32 P = 0, sp = 0;
+      if (zh::lz_deep_dict_tables(content(), content_n(), deep_stg, deep_prev, deep_head, P, sp, stream) == hipSuccess &&
+          hipStreamSynchronize(stream) == hipSuccess) {
+        deep_P = P;
+        deep_split = sp;
+      }
+    }
     host.swap(h);
     return Status::SUCCESS;
   }
@@ -408,6 +428,17 @@ void set_dict_block(ZhBlockDesc &d, const DevDict *dd, bool first, bool hist, bo
   // the staged bytes in global memory, not in K1's 64 KiB of LDS)
   d.pre_n = (u32)std::min(cn, deep ? (size_t)ZH_DEEP_PRE : (size_t)ZH_BLOCK_MAX - d.n);
   d.pre = dd->content() + cn - d.pre_n;
+}
+
+// the deep matcher's precomputed dictionary chains, when the dictionary has them
+void set_deep_dict(ZhWorkspace &ws, const DevDict *dd) {
+  ws.dd_prev = ws.dd_head = nullptr;
+  ws.dd_pre = ws.dd_split = 0;
+  if (!dd || !dd->deep_P) return;
+  ws.dd_prev = dd->deep_prev;
+  ws.dd_head = dd->deep_head;
+  ws.dd_pre = dd->deep_P;
+  ws.dd_split = dd->deep_split;
 }
 
 Status from_item_status(u32 s) {
@@ -497,6 +528,7 @@ class ZstdBatchManager::Impl {
     }
     if (hipMemcpyAsync(base, h, up_bytes, hipMemcpyHostToDevice, stream) != hipSuccess) return Status::ERROR_CUDA_ERROR;
     ZhWorkspace ws{base + L.blocks, (u32 *)(base + L.counter), dd && dd->tabs_P ? dd->tabs : nullptr, dd ? dd->tabs_P : 0u};
+    set_deep_dict(ws, dd);
     hipError_t e = zh::launch_compress((const ZhBlockDesc *)(base + L.descs), (u32)nblocks, ws, config.window_log, config.block_size,
                                        (u64 *)(base + L.item_size), (u32 *)(base + L.item_status), (u32 *)(base + L.blk_size),
                                        (const ZhItemDesc *)(base + L.items), (u32)count, staged,
@@ -890,6 +922,7 @@ Status ZstdBatchManager::compress_batch_device(const void *const *d_in_ptrs, con
                                  dd ? dd->content() : nullptr, dd ? (u32)dd->content_n() : 0u, dd ? dd->id : 0u, hist, stream);
   if (e != hipSuccess) return Status::ERROR_CUDA_ERROR;
   ZhWorkspace ws{base + L.blocks, (u32 *)(base + L.counter), dd && dd->tabs_P ? dd->tabs : nullptr, dd ? dd->tabs_P : 0u};
+  set_deep_dict(ws, dd);
   e = zh::launch_compress((const ZhBlockDesc *)(base + L.descs), (u32)nblocks, ws, pimpl_->config.window_log, pimpl_->config.block_size, item_size,
                           item_status, (u32 *)(base + L.blk_size), (const ZhItemDesc *)(base + L.items), (u32)count, bpi > 1, ck,
                           pimpl_->config.level, stream);

@@ -50,6 +50,7 @@ u32 entropy_lds_bytes();
 // K1 hash tables of a dictionary's content tail, built once per dictionary (zh_lz.hip):
 // out = 2^15 u16, tmp32 = 2^15 u32 scratch; P = the tail length covered (0: none)
 hipError_t lz_dict_tables(const u8 *content, size_t cn, u16 *out, u32 *tmp32, u32 &P, hipStream_t stream);
+hipError_t lz_deep_dict_tables(const u8 *content, size_t cn, u8 *stg, u32 *dprev, u32 *dhead, u32 &P, u32 &split, hipStream_t stream);
 hipError_t launch_compress(const ZhBlockDesc *d_descs, u32 nblocks, ZhWorkspace ws, u32 window_log, u32 cfg_block_size, u64 *d_item_size,
                            u32 *d_item_status, u32 *d_blk_size, const ZhItemDesc *d_items, u32 nitems, bool gather, bool checksum, int level,
                            hipStream_t stream);

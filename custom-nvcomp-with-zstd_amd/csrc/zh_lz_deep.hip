@@ -8,7 +8,7 @@
 // entropy stage, so K2-K4 are shared.
 //
 // One persistent 1024-thread workgroup per CU; blocks from the device counter.  Each workgroup
-// owns a slot of a library-held scratch buffer (deep_scratch below): the staged bytes (history or
+// owns a slot of a library-held scratch buffer (g_deep below): the staged bytes (history or
 // dictionary prefix + block, contiguous), prev[] and the per-position offsets.  Per block:
 //   1. stage the prefix + block into the slot (and probe RLE); hash every position into prev[]
 //   2. chains, wave 0: positions in order, 64 per LDS `ds_max_rtn_u32` on the head table (entry =
@@ -31,13 +31,15 @@ namespace {
 constexpr u32 DT = 1024;                          // threads per workgroup
 constexpr u32 HSIZE = 1u << ZH_HASH_LOG_SHORT;    // head table entries (+ a junk slot)
 constexpr u32 NSEG = ZH_BLOCK_MAX / 64;           // 64-position parse segments per block
+constexpr u32 HB = 8192;                          // positions per chain-building round
 static_assert(NSEG == DT, "one parse segment per thread");
 static_assert(ZH_DEEP_PRE <= ZH_BLOCK_MAX && ZH_HIST_BLOCK <= ZH_BLOCK_MAX, "staged prefix fits the slot");
 // scratch slot of one workgroup (global memory)
 constexpr u32 STG_BYTES = 2 * ZH_BLOCK_MAX + 256;           // staged bytes + zero pad
 constexpr u32 SLOT_PREV = STG_BYTES;                        // u32 prev[2 * ZH_BLOCK_MAX]: q + 1, 0 = none
-constexpr u32 SLOT_OFF = SLOT_PREV + 4 * 2 * ZH_BLOCK_MAX;  // u32 off[ZH_BLOCK_MAX] per block position
-constexpr size_t SLOT_BYTES = SLOT_OFF + 4 * ZH_BLOCK_MAX;
+constexpr u32 SLOT_OFF = SLOT_PREV + 4 * 2 * ZH_BLOCK_MAX;  // u32 off << 8 | len per block position
+constexpr u32 SLOT_P16 = SLOT_OFF + 4 * ZH_BLOCK_MAX;       // u16 link distances when LDS cannot hold them
+constexpr size_t SLOT_BYTES = SLOT_P16 + 2 * 2 * ZH_BLOCK_MAX;
 static_assert(SLOT_BYTES % 256 == 0, "slot alignment");
 // LDS
 constexpr u32 L_HEAD = 0;                  // u32 head[HSIZE + 4] (chains) / u8 len[ZH_BLOCK_MAX] (search, parse)
@@ -47,11 +49,13 @@ constexpr u32 L_MM = L_LM + 8 * NSEG;      // u64 match-start bits per segment
 constexpr u32 L_EX = L_MM + 8 * NSEG;      // u32 walk exit per segment
 constexpr u32 L_LP = L_EX + 4 * NSEG;      // u32 literals before the segment
 constexpr u32 L_MP = L_LP + 4 * NSEG;      // u32 matches before the segment
-constexpr u32 L_WS = L_MP + 4 * NSEG;      // u32[32] per-wave sums
+constexpr u32 DEEP_LDS = 160 * 1024;
+constexpr u32 L_WS = DEEP_LDS - 256;       // u32[32] per-wave sums
 constexpr u32 L_MISC = L_WS + 4 * 32;      // u32[8]: [0] block_any flag, [1] next block
-constexpr u32 DEEP_LDS = L_MISC + 4 * 8;
+constexpr u32 SEARCH_LDS = L_WS;           // search: u16 link distances, then (if they fit) the staged bytes
+static_assert(L_MP + 4 * NSEG <= L_WS, "parse arrays below the scan sums");
 static_assert(4 * (HSIZE + 4) >= ZH_BLOCK_MAX, "len[] reuses the head table");
-static_assert(DEEP_LDS <= 160 * 1024, "deep LDS budget");
+static_assert(L_TM + 2 * 2 * HB <= L_WS, "chain rounds' hash buffers fit below the scan sums");
 
 // the 8 bytes at staged position p (4-B aligned slot, zero padded)
 __device__ __forceinline__ void g64(const u32 *s32, u32 p, u32 &lo, u32 &hi) {
@@ -132,12 +136,203 @@ __device__ __forceinline__ void seg_walk64(const u8 *len, u64 tmk, u32 S, u32 SE
   }
 }
 
+#ifdef ZH_STAMPS
+__device__ u32 g_deep_fix;  // diagnostic: chain steps that needed the out-of-order fix-up
+#endif
+// Links of the staged positions [s0, lim) (s0 % 4 == 0): prev[p] = the latest q < p with p's
+// hash, + 1 (0: none), given a head table holding the latest of every position below s0.  Every
+// position's hash first (all threads), then rounds of HB positions: waves 1..15 copy round r + 1's
+// hashes into one LDS buffer (hb: 2 x HB u16) while wave 0 links round r from the other, 64
+// positions per LDS atomic, four in flight.  Ends with a barrier.
+__device__ void deep_chains(const u32 *s32, u32 *prev, u32 *head, u16 *hb, u32 s0, u32 lim, u32 tid) {
+  u32 const lane = tid & 63;
+  // every position's hash into prev[] (4 positions per thread from 3 dwords; overwritten by the
+  // links below)
+#pragma unroll 4
+  for (u32 g4 = (s0 >> 2) + tid; 4 * g4 < lim; g4 += DT) {
+    u32 const w0 = s32[g4], w1 = s32[g4 + 1], w2 = s32[g4 + 2];
+    uint4 h4;
+    u32 *hh = (u32 *)&h4;
+#pragma unroll
+    for (u32 k = 0; k < 4; k++) hh[k] = 4 * g4 + k < lim ? hash_short(__builtin_amdgcn_alignbyte(w1, w0, k), __builtin_amdgcn_alignbyte(w2, w1, k)) : HSIZE;
+    *(uint4 *)(prev + 4 * g4) = h4;
+  }
+  __threadfence_block();
+  __syncthreads();
+
+  // ---- 2. chains.  Rounds of HB positions: waves 1..15 copy round r + 1's hashes into one LDS
+  // buffer while wave 0 links round r from the other: 64 positions per LDS atomic, four in flight.
+  {
+    auto hash_round = [&](u32 r, u32 t0, u32 nt) {
+      u16 *const dst = hb + (r & 1u) * HB;
+#pragma unroll 4
+      for (u32 j = 4 * t0; j < HB; j += 4 * nt) {
+        u32 const p = s0 + r * HB + j;
+        uint4 const h4 = p < lim ? *(const uint4 *)(prev + p) : make_uint4(HSIZE, HSIZE, HSIZE, HSIZE);
+        u32 const a = p < lim ? h4.x : HSIZE, b = p + 1 < lim ? h4.y : HSIZE, c = p + 2 < lim ? h4.z : HSIZE, e = p + 3 < lim ? h4.w : HSIZE;
+        *(uint2 *)(dst + j) = make_uint2(a | (b << 16), c | (e << 16));
+      }
+    };
+    u32 const nr = lim > s0 ? (lim - s0 + HB - 1) / HB : 0u;
+    if (nr) hash_round(0, tid, DT);
+    for (u32 r = 0; r < nr; r++) {
+      __syncthreads();  // round r hashed; wave 0 is done with the buffer round r + 1 reuses
+      if (tid < 64) {
+        const u16 *const src = hb + (r & 1u) * HB;
+        constexpr u32 U = 4;
+        for (u32 j0 = 0; j0 < HB && s0 + r * HB + j0 < lim; j0 += 64 * U) {
+          u32 h[U], rv[U];
+#pragma unroll
+          for (u32 u = 0; u < U; u++) h[u] = src[j0 + 64 * u + lane];
+#pragma unroll
+          for (u32 u = 0; u < U; u++) rv[u] = atomicMax(&head[h[u]], s0 + r * HB + j0 + 64 * u + lane + 1);
+#pragma unroll
+          for (u32 u = 0; u < U; u++) {
+            u32 const p = s0 + r * HB + j0 + 64 * u + lane;
+            bool const v = p < lim;
+            if (__ballot(v && rv[u] >= p + 1)) {
+#ifdef ZH_STAMPS
+              if (lane == 0) atomicAdd(&g_deep_fix, 1u);
+#endif
+              // lanes of one atomic applied out of lane order: prev = the latest earlier lane with
+              // the same hash, else the head before the step (the smallest value any lane of the
+              // group got)
+              u32 mn = ~0u, pm = 0;
+              for (u32 k = 0; k < 64; k++) {
+                u32 const hk = (u32)__builtin_amdgcn_readlane((int)h[u], (int)k), rk = (u32)__builtin_amdgcn_readlane((int)rv[u], (int)k);
+                if (hk == h[u]) {
+                  mn = min(mn, rk);
+                  if (k < lane) pm = p - lane + k + 1;
+                }
+              }
+              rv[u] = pm ? pm : mn;
+            }
+            if (v) prev[p] = rv[u];
+          }
+        }
+      } else if (r + 1 < nr) {
+        hash_round(r + 1, tid - 64, DT - 64);
+      }
+    }
+  }
+  __threadfence_block();
+  __syncthreads();
+
+}
+
+// Step 3 of deep_block: per block position the chain's first `depth` candidates -> offg[i] =
+// off << 8 | len.  DL: the staged bytes in LDS at e16 (else gdata, the slot); PL: the link
+// distances in LDS at 0 (else gP16, the slot); positions below s0 link through dprev.
+template <bool DL, bool PL>
+__device__ __forceinline__ void deep_search(const u32 *gdata, const u16 *gP16, u32 e16, const u32 *dprev, u32 *offg, u32 pre, u32 nb, u32 n,
+                                            u32 lim, u32 s0, u32 depth, u32 tid) {
+  extern __shared__ __attribute__((aligned(16))) u8 smem[];
+  const u32 *const D32 = DL ? (const u32 *)(smem + e16) : gdata;
+  const u16 *const P16 = PL ? (const u16 *)smem : gP16;
+  // the next candidate after q (+ 1, 0 = none)
+  auto link = [&](u32 q) -> u32 {
+    if (q < s0) return dprev[q];
+    u32 const dl = P16[q - s0];
+    return dl ? q + 1u - dl : 0u;
+  };
+  // lanes = block positions, two independent chains per lane (i, i + DT)
+  struct Cur {
+    u32 i, p, olo, ohi, c, best, bo, dd;
+    bool act;
+  };
+  auto cur_init = [&](Cur &k, u32 i) {
+    k.i = i;
+    k.p = pre + i;
+    k.act = i < nb && k.p < lim;
+    k.olo = k.ohi = k.c = 0;
+    k.best = k.bo = k.dd = 0;
+    if (k.act) {
+      g64(D32, k.p, k.olo, k.ohi);
+      k.c = link(k.p);
+    }
+    k.act = k.act && k.c != 0 && k.p - (k.c - 1u) <= ZH_DEEP_MAXOFF;
+  };
+  auto cur_done = [&](Cur &k) {
+    if (k.i < nb) offg[k.i] = k.bo << 8 | k.best;
+  };
+  // common prefix of the bytes from p + 8 and q + 8 (<= 56): 15 dwords each, loaded together
+  auto ext = [&](u32 p, u32 q) {
+    u32 A[15], B[15];
+    u32 const wp = (p >> 2) + 2, wq = (q >> 2) + 2, sp = p & 3, sq = q & 3;
+#pragma unroll
+    for (u32 k = 0; k < 15; k++) { A[k] = D32[wp + k]; B[k] = D32[wq + k]; }
+    u32 l = 56;
+#pragma unroll
+    for (int j = 13; j >= 0; j--) {
+      u32 const x = __builtin_amdgcn_alignbyte(A[j + 1], A[j], sp) ^ __builtin_amdgcn_alignbyte(B[j + 1], B[j], sq);
+      if (x) l = 4 * (u32)j + ((u32)__builtin_ctz(x) >> 3);
+    }
+    return l;
+  };
+  for (u32 i0 = 0; i0 < nb; i0 += 2 * DT) {
+    Cur ka, kb;
+    cur_init(ka, i0 + tid);
+    cur_init(kb, i0 + DT + tid);
+    while (__ballot(ka.act || kb.act)) {
+      u32 const qa = ka.act ? ka.c - 1u : 0u, qb = kb.act ? kb.c - 1u : 0u;
+      u32 na = 0, nb2 = 0, alo = 0, ahi = 0, blo = 0, bhi = 0;
+      // a candidate can replace a best of >= 8 bytes only if its byte at `best` matches too
+      // (libzstd's match[ml] == ip[ml] pre-check): one byte compare instead of the whole prefix
+      auto may_win = [&](const Cur &k, u32 q) {
+        if (k.best < 8) return true;
+        u32 const a = k.p + k.best, b = q + k.best;
+        return ((D32[a >> 2] >> (8 * (a & 3))) & 255u) == ((D32[b >> 2] >> (8 * (b & 3))) & 255u);
+      };
+      bool const wa = ka.act && may_win(ka, qa), wb = kb.act && may_win(kb, qb);
+      if (ka.act) na = link(qa);
+      if (kb.act) nb2 = link(qb);
+      if (wa) g64(D32, qa, alo, ahi);
+      if (wb) g64(D32, qb, blo, bhi);
+      auto pre8 = [](u32 olo, u32 ohi, u32 clo, u32 chi) {
+        u32 const x = olo ^ clo, y = ohi ^ chi;
+        return x ? (u32)__builtin_ctz(x) >> 3 : y ? 4u + ((u32)__builtin_ctz(y) >> 3) : 8u;
+      };
+      u32 la = wa ? pre8(ka.olo, ka.ohi, alo, ahi) : 0u, lb = wb ? pre8(kb.olo, kb.ohi, blo, bhi) : 0u;
+      bool const xa = wa && la == 8 && ka.p + 8 < n, xb = wb && lb == 8 && kb.p + 8 < n;
+      if (xa) la = 8 + ext(ka.p, qa);
+      if (xb) lb = 8 + ext(kb.p, qb);
+      auto upd = [&](Cur &k, u32 l, u32 q, u32 nx) {
+        if (!k.act) return;
+        l = min(l, k.p < n ? n - k.p : 0u);
+        if (l >= ZH_MIN_MATCH_SHORT && l > k.best) {
+          k.best = l;
+          k.bo = k.p - q;
+        }
+        k.dd++;
+        k.c = nx;
+        k.act = k.best < ZH_MAX_MATCH && k.dd < depth && k.c != 0 && k.p - (k.c - 1u) <= ZH_DEEP_MAXOFF;
+      };
+      upd(ka, la, qa, na);
+      upd(kb, lb, qb, nb2);
+    }
+    cur_done(ka);
+    cur_done(kb);
+  }
+}
+
+#ifdef ZH_STAMPS
+#define DSTAMP(k)                                                           \
+  do {                                                                      \
+    u64 _t = __builtin_amdgcn_s_memtime();                                  \
+    if (tid == 0) ws.dbg(b)[30 + (k)] = (u32)(_t - dst0);                   \
+  } while (0)
+#else
+#define DSTAMP(k) do { } while (0)
+#endif
 __device__ void deep_block(const ZhBlockDesc &d, ZhWorkspace ws, u32 b, u8 *slot, u32 depth, u32 tid) {
+#ifdef ZH_STAMPS
+  u64 const dst0 = __builtin_amdgcn_s_memtime();
+#endif
   extern __shared__ __attribute__((aligned(16))) u8 smem[];
   u32 *head = (u32 *)(smem + L_HEAD);
   u8 *lenL = smem + L_HEAD;
-  u64 *tm = (u64 *)(smem + L_TM), *lmk = (u64 *)(smem + L_LM), *mmk = (u64 *)(smem + L_MM);
-  u32 *exL = (u32 *)(smem + L_EX), *lpL = (u32 *)(smem + L_LP), *mpL = (u32 *)(smem + L_MP);
+  u64 *tm = (u64 *)(smem + L_TM), *lmk = (u64 *)(smem + L_LM);
+  u32 *exL = (u32 *)(smem + L_EX), *lpL = (u32 *)(smem + L_LP);
   u32 *wsum = (u32 *)(smem + L_WS), *misc = (u32 *)(smem + L_MISC);
   u32 const lane = tid & 63;
   u32 const pre = d.pre_n, nb = d.n, n = pre + nb;
@@ -149,125 +344,98 @@ __device__ void deep_block(const ZhBlockDesc &d, ZhWorkspace ws, u32 b, u8 *slot
   // ---- 1. stage prefix + block (4 bytes per thread and step), RLE probe, head table cleared
   u8 const first = d.src[0];
   bool same = true;
-  for (u32 i = 4 * tid; i < n + 64; i += 4 * DT) {
-    u32 w = 0;
-#pragma unroll
-    for (u32 k = 0; k < 4; k++) {
-      u32 const j = i + k;
-      u8 const c = j < pre ? d.pre[j] : j < n ? d.src[j - pre] : (u8)0;
-      same &= j < pre || j >= n || c == first;
-      w |= (u32)c << (8 * k);
+  u32 const f4 = first * 0x01010101u;
+  if ((((uintptr_t)d.src | (uintptr_t)d.pre | pre) & 15) == 0) {
+    // 16-B loads: prefix and block both 16-B aligned (contiguous records, dictionary content)
+    u32 const nv = (n + 64 + 15) / 16;
+#pragma unroll 4
+    for (u32 v = tid; v < nv; v += DT) {
+      u32 const i = 16 * v;
+      uint4 w = make_uint4(0, 0, 0, 0);
+      if (i < pre) w = *(const uint4 *)(d.pre + i);
+      else if (i + 16 <= n) w = *(const uint4 *)(d.src + (i - pre));
+      else {
+        u32 t[4] = {0, 0, 0, 0};
+        for (u32 k = 0; k < 16 && i + k < n; k++) t[k >> 2] |= (u32)d.src[i + k - pre] << (8 * (k & 3));
+        w = make_uint4(t[0], t[1], t[2], t[3]);
+      }
+      *(uint4 *)(stg + i) = w;
+      if (i >= pre && i + 16 <= n) same &= (w.x == f4) & (w.y == f4) & (w.z == f4) & (w.w == f4);
+      else if (i >= pre && i < n) {
+        u32 const t4[4] = {w.x, w.y, w.z, w.w};
+        for (u32 k = 0; k < 16 && i + k < n; k++) same &= ((t4[k >> 2] >> (8 * (k & 3))) & 255u) == first;
+      }
     }
-    *(u32 *)(stg + i) = w;
+  } else {
+    for (u32 i = 4 * tid; i < n + 64; i += 4 * DT) {
+      u32 w = 0;
+#pragma unroll
+      for (u32 k = 0; k < 4; k++) {
+        u32 const j = i + k;
+        u8 const c = j < pre ? d.pre[j] : j < n ? d.src[j - pre] : (u8)0;
+        same &= j < pre || j >= n || c == first;
+        w |= (u32)c << (8 * k);
+      }
+      *(u32 *)(stg + i) = w;
+    }
   }
-  for (u32 i = tid; i < HSIZE + 4; i += DT) head[i] = 0;
+  // A dictionary frame's first block starts from the dictionary's precomputed chains (built once
+  // per dictionary, zh_deep_dict_kernel): the head table after its positions [0, dd_split), whose
+  // links stay in ws.dd_prev; the block links only [dd_split, lim) -- the same chains.
+  bool const use_dd = ws.dd_head && (d.flags & ZH_F_DICT) && (d.flags & ZH_F_FIRST) && pre == ws.dd_pre;
+  u32 const s0 = use_dd ? ws.dd_split : 0u;
+  const u32 *const dprev = ws.dd_prev;
+  for (u32 i = tid; i < HSIZE + 4; i += DT) head[i] = use_dd && i < HSIZE ? ws.dd_head[i] : 0u;
   if (wg_any(!same, &misc[0], tid) == false && nb >= 2) {
     if (tid == 0) { meta[0] = 0; meta[1] = 0; meta[2] = 1; }
     return;
   }
   u32 const lim = n > ZH_HASH_READ ? n - ZH_HASH_READ : 0u;
-  // hashes of every position into prev[] (overwritten by the chains below)
-  for (u32 p = tid; p < lim; p += DT) {
-    u32 lo, hi;
-    g64(s32, p, lo, hi);
-    prev[p] = hash_short(lo, hi);
-  }
-  __syncthreads();
 
-  // ---- 2. chains (wave 0): four 64-position steps of atomics in flight, then their checks
-  if (tid < 64) {
-    constexpr u32 U = 4;
-    for (u32 p0 = 0; p0 < lim; p0 += 64 * U) {
-      u32 h[U], r[U];
-#pragma unroll
-      for (u32 u = 0; u < U; u++) {
-        u32 const p = p0 + 64 * u + lane;
-        h[u] = p < lim ? prev[p] : HSIZE;
-      }
-#pragma unroll
-      for (u32 u = 0; u < U; u++) r[u] = atomicMax(&head[h[u]], p0 + 64 * u + lane + 1);
-#pragma unroll
-      for (u32 u = 0; u < U; u++) {
-        u32 const p = p0 + 64 * u + lane;
-        bool const v = p < lim;
-        if (__ballot(v && r[u] >= p + 1)) {
-          // lanes of one atomic applied out of lane order: prev = the latest earlier lane with the
-          // same hash, else the head before the step (the smallest value any lane of the group got)
-          u32 mn = ~0u, pm = 0;
-          for (u32 k = 0; k < 64; k++) {
-            u32 const hk = (u32)__builtin_amdgcn_readlane((int)h[u], (int)k), rk = (u32)__builtin_amdgcn_readlane((int)r[u], (int)k);
-            if (hk == h[u]) {
-              mn = min(mn, rk);
-              if (k < lane) pm = p0 + 64 * u + k + 1;
-            }
-          }
-          r[u] = pm ? pm : mn;
-        }
-        if (v) prev[p] = r[u];
-      }
-    }
+  __syncthreads();  // staged bytes visible to every wave
+  DSTAMP(0);
+  // ---- 2. chains of positions [s0, lim); below s0 (a dictionary's precomputed part) the head
+  // table already holds every position's latest
+  deep_chains(s32, prev, head, (u16 *)(smem + L_TM), s0, lim, tid);
+  DSTAMP(1);
+
+  // ---- 3. search.  The links become u16 distances (exact: offsets <= ZH_DEEP_MAXOFF = 65535) in
+  // LDS, followed by the staged bytes when both fit (C5's 16 KiB records, with or without the
+  // 64 KiB dictionary: every candidate step is LDS-only); otherwise the distances in LDS or the
+  // slot and the bytes from the slot (L2).  Generic pointers: one code path for both.
+  u32 const E = lim > s0 ? lim - s0 : 0u;  // linked positions [s0, lim)
+  u32 const e16 = (2 * E + 15) & ~15u;
+  bool const p_lds = e16 <= SEARCH_LDS;
+  bool const d_lds = p_lds && e16 + n + 96 <= SEARCH_LDS;
+  u16 *const P16w = p_lds ? (u16 *)smem : (u16 *)(slot + SLOT_P16);
+  for (u32 i = tid; i < E; i += DT) {
+    u32 const c = prev[s0 + i], dl = c ? s0 + i + 1u - c : 0u;
+    P16w[i] = (u16)(dl <= ZH_DEEP_MAXOFF ? dl : 0u);
   }
+  if (d_lds)
+    for (u32 v = tid; 16 * v < n + 80; v += DT) *(uint4 *)(smem + e16 + 16 * v) = *(const uint4 *)(stg + 16 * v);
   __threadfence_block();
   __syncthreads();
-
-  // ---- 3. search, lanes = block positions: the chain's first `depth` candidates
-  for (u32 i0 = 0; i0 < nb; i0 += DT) {
-    u32 const i = i0 + tid, p = pre + i;
-    bool act = i < nb && p < lim;
-    u32 olo = 0, ohi = 0, c = 0;
-    if (act) {
-      g64(s32, p, olo, ohi);
-      c = prev[p];
-    }
-    u32 best = 0, bo = 0, dd = 0;
-    act = act && c != 0 && p - (c - 1u) <= ZH_DEEP_MAXOFF;
-    while (__ballot(act)) {
-      if (act) {
-        u32 const q = c - 1u;
-        u32 const cn = prev[q];
-        u32 clo, chi;
-        g64(s32, q, clo, chi);
-        u32 const x = olo ^ clo, y = ohi ^ chi;
-        u32 l = x ? (u32)__builtin_ctz(x) >> 3 : y ? 4u + ((u32)__builtin_ctz(y) >> 3) : 8u;
-        if (l == 8) {
-          for (u32 k = 8; k < ZH_MAX_MATCH && p + k < n; k += 8) {
-            u32 alo, ahi, blo, bhi;
-            g64(s32, p + k, alo, ahi);
-            g64(s32, q + k, blo, bhi);
-            u32 const x2 = alo ^ blo, y2 = ahi ^ bhi;
-            if (x2 | y2) {
-              l = k + (x2 ? (u32)__builtin_ctz(x2) >> 3 : 4u + ((u32)__builtin_ctz(y2) >> 3));
-              break;
-            }
-            l = k + 8;
-          }
-        }
-        l = min(min(l, (u32)ZH_MAX_MATCH), n - p);
-        if (l >= ZH_MIN_MATCH_SHORT && l > best) {
-          best = l;
-          bo = p - q;
-        }
-        dd++;
-        c = cn;
-        act = best < ZH_MAX_MATCH && dd < depth && c != 0 && p - (c - 1u) <= ZH_DEEP_MAXOFF;
-      }
-    }
-    if (i < nb) {
-      lenL[i] = (u8)best;
-      offg[i] = bo;
-    }
-  }
+  // typed LDS / global variants (a generic pointer makes every access a flat one: measured slower
+  // than global memory)
+  if (d_lds) deep_search<true, true>(s32, (const u16 *)(slot + SLOT_P16), e16, dprev, offg, pre, nb, n, lim, s0, depth, tid);
+  else if (p_lds) deep_search<false, true>(s32, (const u16 *)(slot + SLOT_P16), e16, dprev, offg, pre, nb, n, lim, s0, depth, tid);
+  else deep_search<false, false>(s32, (const u16 *)(slot + SLOT_P16), e16, dprev, offg, pre, nb, n, lim, s0, depth, tid);
   __threadfence_block();
   __syncthreads();
+  // lengths into LDS for the parse (over the dead search arrays)
+  for (u32 i = tid; i < nb; i += DT) lenL[i] = (u8)(offg[i] & 255u);
+  __syncthreads();
 
+  DSTAMP(2);
   // ---- 4. take masks (LAZY2 rule on the positions i, i+1, i+2), then the segment walk
   for (u32 i0 = 0; i0 < nb; i0 += DT) {
     u32 const i = i0 + tid;
     u32 const l0 = i < nb ? lenL[i] : 0u, l1 = i + 1 < nb ? lenL[i + 1] : 0u, l2 = i + 2 < nb ? lenL[i + 2] : 0u;
     bool tk = false;
     if (l0) {
-      int const g0 = gain_of(l0, offg[i]);
-      int const g1 = l1 ? gain_of(l1, offg[i + 1]) : -1000, g2 = l2 ? gain_of(l2, offg[i + 2]) : -1000;
+      int const g0 = gain_of(l0, offg[i] >> 8);
+      int const g1 = l1 ? gain_of(l1, offg[i + 1] >> 8) : -1000, g2 = l2 ? gain_of(l2, offg[i + 2] >> 8) : -1000;
       tk = g1 <= g0 + 4 && g2 <= g0 + 7;
     }
     u64 const bm = __ballot(tk);
@@ -293,6 +461,7 @@ __device__ void deep_block(const ZhBlockDesc &d, ZhWorkspace ws, u32 b, u8 *slot
     }
   }
 
+  DSTAMP(3);
   // ---- 5. records and literals
   u32 nm_tot, nl_tot;
   u32 const mbase = wg_excl_scan(sv ? (u32)__popcll(MM) : 0u, wsum, tid, nm_tot);
@@ -300,7 +469,6 @@ __device__ void deep_block(const ZhBlockDesc &d, ZhWorkspace ws, u32 b, u8 *slot
   if (sv) {
     lmk[g] = LM;
     lpL[g] = lbase;
-    mpL[g] = mbase;
   }
   u64 *seq_out = ws.seq(b);
   u64 mm = MM;
@@ -310,7 +478,7 @@ __device__ void deep_block(const ZhBlockDesc &d, ZhWorkspace ws, u32 b, u8 *slot
     mm &= mm - 1ull;
     u32 const m = S + o;
     u32 const cum = lbase + (u32)__popcll(LM & ~bits_from(o));
-    seq_out[j++] = (u64)cum | ((u64)lenL[m] << 17) | ((u64)offg[m] << 36);
+    seq_out[j++] = (u64)cum | ((u64)lenL[m] << 17) | ((u64)(offg[m] >> 8) << 36);
   }
   __syncthreads();
   u8 *lit_out = ws.lits(b);
@@ -320,7 +488,7 @@ __device__ void deep_block(const ZhBlockDesc &d, ZhWorkspace ws, u32 b, u8 *slot
     if ((lm >> o) & 1ull) lit_out[lpL[i >> 6] + (u32)__popcll(lm & ~bits_from(o))] = stg[pre + i];
   }
   if (tid == 0) { meta[0] = nm_tot; meta[1] = nl_tot; meta[2] = 0; }
-  (void)mpL;
+  DSTAMP(4);
 }
 
 }  // namespace
@@ -344,37 +512,88 @@ extern "C" __global__ __launch_bounds__(DT) void zh_lz_deep_kernel(const ZhBlock
   }
 }
 
-namespace zh {
-// Library-held scratch of the deep matcher: one slot per workgroup (one per CU), allocated on a
-// device's first deep launch and kept (~0.9 MB per CU).  Not part of the caller's workspace:
-// the temp size of the reference API does not depend on the level.
-static u8 *deep_scratch(int dev, u32 slots) {
-  static std::mutex mu;
-  static u8 *ptr[64] = {};
-  static u32 have[64] = {};
-  if (dev < 0 || dev >= 64) return nullptr;
-  std::lock_guard<std::mutex> g(mu);
-  if (have[dev] < slots) {
-    if (ptr[dev]) (void)hipFree(ptr[dev]);
-    ptr[dev] = nullptr;
-    have[dev] = 0;
-    if (hipMalloc(&ptr[dev], SLOT_BYTES * slots) != hipSuccess) return nullptr;
-    have[dev] = slots;
-  }
-  return ptr[dev];
+#ifdef ZH_STAMPS
+extern "C" __global__ void zh_read_deep_fix(u32 *out) { *out = g_deep_fix; g_deep_fix = 0; }
+extern "C" u32 zh_deep_fix_host() {
+  u32 *d = nullptr, h = 0;
+  if (hipMalloc(&d, 4) != hipSuccess) return ~0u;
+  hipLaunchKernelGGL(zh_read_deep_fix, dim3(1), dim3(1), 0, 0, d);
+  (void)hipMemcpy(&h, d, 4, hipMemcpyDeviceToHost);
+  (void)hipFree(d);
+  return h;
+}
+#endif
+// A dictionary's deep-matcher chains, built once per dictionary (one workgroup): the last P =
+// min(content, ZH_DEEP_PRE) content bytes staged as a record's first block stages them, the links
+// of positions [0, split) (split = (P - ZH_HASH_READ) & ~3: every byte they hash is dictionary
+// content) into dprev and the head table after them into dhead.
+extern "C" __global__ __launch_bounds__(DT) void zh_deep_dict_kernel(const u8 *__restrict__ tail, u32 P, u8 *stg, u32 *dprev, u32 *dhead) {
+  extern __shared__ __attribute__((aligned(16))) u8 smem[];
+  u32 *head = (u32 *)(smem + L_HEAD);
+  u32 const tid = threadIdx.x;
+  for (u32 i = tid; i < P + 64; i += DT) stg[i] = i < P ? tail[i] : (u8)0;
+  for (u32 i = tid; i < HSIZE + 4; i += DT) head[i] = 0;
+  __syncthreads();
+  u32 const split = (P > ZH_HASH_READ ? P - ZH_HASH_READ : 0u) & ~3u;
+  deep_chains((const u32 *)stg, dprev, head, (u16 *)(smem + L_TM), 0, split, tid);
+  for (u32 i = tid; i < HSIZE; i += DT) dhead[i] = head[i];
 }
 
-hipError_t lz_deep_init() { return hipFuncSetAttribute((const void *)zh_lz_deep_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)DEEP_LDS); }
+namespace zh {
+// chains of a dictionary's last min(cn, ZH_DEEP_PRE) content bytes: dprev u32[ZH_DEEP_PRE],
+// dhead u32[2^ZH_HASH_LOG_SHORT], stg >= ZH_DEEP_PRE + 64 bytes; P = 0: none (too short)
+hipError_t lz_deep_dict_tables(const u8 *content, size_t cn, u8 *stg, u32 *dprev, u32 *dhead, u32 &P, u32 &split, hipStream_t stream) {
+  P = (u32)std::min(cn, (size_t)ZH_DEEP_PRE);
+  split = (P > ZH_HASH_READ ? P - ZH_HASH_READ : 0u) & ~3u;
+  if (split < 64) { P = split = 0; return hipSuccess; }
+  hipLaunchKernelGGL(zh_deep_dict_kernel, dim3(1), dim3(DT), DEEP_LDS, stream, content + cn - P, P, stg, dprev, dhead);
+  return hipGetLastError();
+}
+
+// Library-held scratch of the deep matcher: one slot per workgroup (one per CU), allocated on a
+// device's first deep launch and kept (~1.2 MB per CU).  Not part of the caller's workspace: the
+// temp size of the reference API does not depend on the level.  Launches on one device share the
+// slots, so each deep launch waits (on its stream, no host sync) for the previous one on that
+// device, whatever stream it ran on.
+struct DeepDev {
+  u8 *ptr = nullptr;
+  u32 slots = 0;
+  hipEvent_t last = nullptr;
+  bool pending = false;
+};
+static std::mutex g_deep_mu;
+static DeepDev g_deep[64];
+hipError_t lz_deep_init() {
+  hipError_t e = hipFuncSetAttribute((const void *)zh_lz_deep_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)DEEP_LDS);
+  if (e == hipSuccess) e = hipFuncSetAttribute((const void *)zh_deep_dict_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)DEEP_LDS);
+  return e;
+}
 
 hipError_t lz_deep_launch(const ZhBlockDesc *d_descs, u32 nblocks, ZhWorkspace ws, int level, hipStream_t stream) {
   int dev = 0, cus = 0;
   if (stream) (void)hipStreamGetDevice(stream, &dev);
   else (void)hipGetDevice(&dev);
+  if (dev < 0 || dev >= 64) return hipErrorInvalidDevice;
   if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) cus = 256;
   u32 const grid = std::min(nblocks, (u32)cus);
-  u8 *scr = deep_scratch(dev, (u32)cus);
-  if (!scr) return hipErrorOutOfMemory;
-  hipLaunchKernelGGL(zh_lz_deep_kernel, dim3(grid), dim3(DT), DEEP_LDS, stream, d_descs, nblocks, ws, scr, (u32)ZH_DEEP_DEPTH(level));
-  return hipGetLastError();
+  std::lock_guard<std::mutex> g(g_deep_mu);
+  DeepDev &D = g_deep[dev];
+  if (D.pending && hipStreamWaitEvent(stream, D.last, 0) != hipSuccess) return hipErrorUnknown;
+  if (D.slots < (u32)cus) {
+    // (re)allocation: every earlier deep launch on the device must be done with the old slots
+    if (D.pending && hipEventSynchronize(D.last) != hipSuccess) return hipErrorUnknown;
+    if (D.ptr) (void)hipFree(D.ptr);
+    D.ptr = nullptr;
+    D.slots = 0;
+    if (hipMalloc(&D.ptr, SLOT_BYTES * (size_t)cus) != hipSuccess) { D.ptr = nullptr; return hipErrorOutOfMemory; }
+    D.slots = (u32)cus;
+  }
+  if (!D.last && hipEventCreateWithFlags(&D.last, hipEventDisableTiming) != hipSuccess) { D.last = nullptr; return hipErrorUnknown; }
+  hipLaunchKernelGGL(zh_lz_deep_kernel, dim3(grid), dim3(DT), DEEP_LDS, stream, d_descs, nblocks, ws, D.ptr, (u32)ZH_DEEP_DEPTH(level));
+  hipError_t const e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  if (hipEventRecord(D.last, stream) != hipSuccess) return hipErrorUnknown;
+  D.pending = true;
+  return hipSuccess;
 }
 }  // namespace zh

@@ -51,7 +51,7 @@
  * matches, no catch-up. */
 #define ZH_DEEP_LEVEL 9
 #define ZH_DEEP_PRE 65536
-#define ZH_DEEP_MAXOFF 131068      /* offset + 3 fits the 17-bit offset field of a sequence record */
+#define ZH_DEEP_MAXOFF 65535       /* links stored as u16 distances (zh_lz_deep.hip) are exact */
 #define ZH_DEEP_DEPTH(level) ((level) <= 9 ? 32 : (level) == 10 ? 64 : 128)
 #define ZH_COMPRESS_LITERALS_SIZE_MIN 63
 #define ZH_LONGNBSEQ 0x7F00

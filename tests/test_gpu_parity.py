@@ -283,3 +283,36 @@ def test_deep_levels_match_oracle(torch_cuda, level):
         got = o.cpu().numpy().tobytes()
         assert got == T.oracle_frame(d, level=level), k
         assert T.zstd_decompress(got, len(d)) == d.tobytes(), k
+
+
+def test_deep_concurrent_streams(torch_cuda):
+    """Two level-9 batches enqueued on two streams without a host sync between them: the deep
+    matcher's library-held scratch slots are shared per device, so its launches are ordered by an
+    event (zh_lz_deep.hip lz_deep_launch); both batches' frames equal the oracle's."""
+    import cuda_zstd
+
+    torch = torch_cuda
+    n, cs = 96, 16384
+    datas = [T.gen(T.DG_JSON, n, 0x5EED0A01, cs), T.gen(T.DG_TEXT, n, 0x5EED0A02, cs)]
+    runs = []
+    for k, d in enumerate(datas):
+        bc = cuda_zstd.BatchedCompressor(9, cs)
+        dev = torch.from_numpy(d).cuda()
+        slot = (bc.max_out(cs) + 255) // 256 * 256
+        out = torch.empty(n * slot, dtype=torch.uint8, device="cuda")
+        ar = torch.arange(n, dtype=torch.int64, device="cuda")
+        args = (dev.data_ptr() + ar * cs, torch.full((n,), cs, dtype=torch.int64, device="cuda"), cs, out.data_ptr() + ar * slot,
+                torch.zeros(n, dtype=torch.int64, device="cuda"), torch.zeros(n, dtype=torch.int32, device="cuda"))
+        temp = torch.empty(bc.temp_size(n, cs), dtype=torch.uint8, device="cuda")
+        runs.append((bc, dev, out, slot, args, temp, torch.cuda.Stream()))
+    torch.cuda.synchronize()
+    for bc, dev, out, slot, args, temp, s in runs:
+        bc.compress_async(*args, temp, stream=s)
+    torch.cuda.synchronize()
+    for (bc, dev, out, slot, args, temp, s), d in zip(runs, datas):
+        assert int((args[5] != 0).sum()) == 0
+        sz = args[4].cpu().numpy()
+        ob = out.cpu().numpy()
+        for i in range(n):
+            f = ob[i * slot:i * slot + int(sz[i])].tobytes()
+            assert f == T.oracle_frame(d[i * cs:(i + 1) * cs], level=9), i
