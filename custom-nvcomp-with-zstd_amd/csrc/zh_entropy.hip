@@ -1020,7 +1020,10 @@ __device__ __forceinline__ void copy_bytes(const Out &o, u32 pos, const u8 *src,
   u32 const sa = (u32)((uintptr_t)s0 & 3u);
   const u32 *const s32 = (const u32 *)(s0 - sa);
   u32 *const d32 = (u32 *)(d0 + h);
-  constexpr u32 U = 8;
+#ifndef ZH_COPY_U
+#define ZH_COPY_U 8
+#endif
+  constexpr u32 U = ZH_COPY_U;  // dwords per lane in flight (16: no change on random data, 1.33 ms)
   for (u32 w0 = 0; w0 < lim; w0 += 64 * U) {
     u32 v[U];
 #pragma unroll
@@ -1793,9 +1796,10 @@ extern "C" __global__ __launch_bounds__(64 * K3_WAVES) __attribute__((amdgpu_wav
 constexpr u32 KP_SW = 0, KP_DNB = 4 * SW_WORDS, KP_LDS = (KP_DNB + 4 * 128 + 15) & ~15u;
 constexpr u32 K4_WAVES = 4;
 #ifndef ZH_K4_PF
-#define ZH_K4_PF 3
+#define ZH_K4_PF 1
 #endif
-constexpr u32 K4_PF = ZH_K4_PF;  // chunks in flight
+constexpr u32 K4_PF = ZH_K4_PF;  // chunks in flight (3 measured slower: entropy 3.05 -> 3.20 ms at 16,384
+                                 // blocks, no change at 2,048)
 
 // K4 of block b (one wave; the caller checked that the block needs it); smem = KP_LDS bytes
 __device__ __forceinline__ void k4_pack(const ZhBlockDesc &d, ZhWorkspace ws, u32 b, u8 *smem, u32 lane, u64 *__restrict__ item_size,
@@ -1821,8 +1825,7 @@ __device__ __forceinline__ void k4_pack(const ZhBlockDesc &d, ZhWorkspace ws, u3
   ct.load();
   wave_sync();
   BitSink bs{ff[ZH_FF_OP], 0};
-  // K4_PF 64-step chunks of records and states in flight (a chunk's work is shorter than a
-  // global round trip: with one chunk ahead a block's packing was latency-bound)
+  // K4_PF 64-step chunks of records and states in flight
   u64 rq[K4_PF];
   u32 lq[K4_PF], mq[K4_PF], oq[K4_PF];
   auto fetch = [&](u32 e, u64 &r, u32 &sl, u32 &sm, u32 &so) {
