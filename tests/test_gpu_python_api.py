@@ -104,24 +104,27 @@ def test_metadata_frame_on_device(cz):
     assert m.decompress(blob).cpu().numpy().tobytes() == d.tobytes()
 
 
-def test_streaming_with_history(cz, libzstd):
+@pytest.mark.parametrize("level", [3, 9])
+def test_streaming_with_history(cz, libzstd, level):
     """F4: a 600 KiB JSON-like stream in chunks of mixed sizes; chunk k with history equals
     the oracle frame of chunk k with the last <= 64 KiB of the stream before it as a raw-content
     dictionary, decodes with libzstd using that history, and the streaming decoder returns the
-    stream in order.  With history the stream compresses better than chunk by chunk."""
+    stream in order.  With history the stream compresses better than chunk by chunk.  Level 9
+    (the deep matcher) stages up to 64 KiB of history + a 64 KiB block: its links stay in the
+    global scratch slot (the search's slot-only variant)."""
     import torch
 
     stream = T.gen(T.DG_JSON, 1, 0x5EED0005, 600_000)
     sizes = [10_000, 30_000, 65_536, 100_000, 1, 40_000, 200_000, 16_384]
     sizes.append(len(stream) - sum(sizes))
-    s = cz.StreamingManager(3)
-    plain = cz.StreamingManager(3)
+    s = cz.StreamingManager(level)
+    plain = cz.StreamingManager(level)
     frames, pos, tot_h, tot_p = [], 0, 0, 0
     for n in sizes:
         chunk = stream[pos:pos + n]
         hist = stream[max(0, pos - 65536):pos].tobytes()
         f = s.compress_chunk(torch.from_numpy(chunk.copy()).cuda(), with_history=True).cpu().numpy().tobytes()
-        assert f == T.oracle_frame(chunk, dictionary=hist if hist else None), (pos, n)
+        assert f == T.oracle_frame(chunk, dictionary=hist if hist else None, level=level), (pos, n)
         assert T.zstd_decompress(f, n, dictionary=hist if hist else None) == chunk.tobytes()
         tot_h += len(f)
         tot_p += plain.compress_chunk(torch.from_numpy(chunk.copy()).cuda(), with_history=False).numel()
