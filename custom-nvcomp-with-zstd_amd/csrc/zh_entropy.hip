@@ -16,6 +16,9 @@
 
 namespace {
 
+#ifndef ZH_HIST_PF
+#define ZH_HIST_PF 1  // literal histogram: next step's loads before this step's atomics
+#endif
 constexpr u32 K2_THREADS = 128;  // wave 0: literals section; wave 1: frame/sequences section, finish
 constexpr u32 SW_WORDS = 184;  // >= 512 literal codes of <= 11 bits per append (+ pending bits)
 
@@ -1198,9 +1201,9 @@ extern "C" __global__ __launch_bounds__(K2_THREADS) void zh_entropy_kernel(const
       u32 const nl = nlit;
       if (wave == 0) for (u32 i = lane; i < 256; i += 64) hist0[i] = 0;
       __syncthreads();
-      // 16 literals per lane per load (lits is 16-B aligned), two loads in flight
-      for (u32 i0 = 32 * lane + 2048 * wave; i0 < nl; i0 += 4096) {
-        uint4 q[2];
+      // 16 literals per lane per load (lits is 16-B aligned), two loads per step, the next step's
+      // loads issued before this step's LDS atomics
+      auto load2 = [&](u32 i0, uint4 (&q)[2]) {
 #pragma unroll
         for (u32 g = 0; g < 2; g++) {
           u32 const i = i0 + 16 * g;
@@ -1211,6 +1214,15 @@ extern "C" __global__ __launch_bounds__(K2_THREADS) void zh_entropy_kernel(const
             q[g] = make_uint4(t[0], t[1], t[2], t[3]);
           }
         }
+      };
+      u32 const i00 = 32 * lane + 2048 * wave;
+      uint4 q[2];
+      if (i00 < nl) load2(i00, q);
+      for (u32 i0 = i00; i0 < nl; i0 += 4096) {
+        uint4 qn[2];
+#if ZH_HIST_PF
+        if (i0 + 4096 < nl) load2(i0 + 4096, qn);
+#endif
 #pragma unroll
         for (u32 g = 0; g < 2; g++) {
           u32 const i = i0 + 16 * g;
@@ -1220,6 +1232,11 @@ extern "C" __global__ __launch_bounds__(K2_THREADS) void zh_entropy_kernel(const
           for (u32 k = 0; k < 16; k++)
             if (k < cnt) atomicAdd(&hist0[(w[k >> 2] >> (8 * (k & 3))) & 255u], 1u);
         }
+#if !ZH_HIST_PF
+        if (i0 + 4096 < nl) load2(i0 + 4096, qn);
+#endif
+        q[0] = qn[0];
+        q[1] = qn[1];
       }
       __syncthreads();
     }
