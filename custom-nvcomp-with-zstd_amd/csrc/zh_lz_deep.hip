@@ -15,8 +15,9 @@
 //      position + 1): LDS executes one wave's operations in order and a store's lanes one after
 //      another, so each lane gets the latest earlier position with its hash -- checked (a lane
 //      that got a position >= its own saw a later lane first) with an exact fix-up otherwise
-//   3. search, lanes = block positions (all 16 waves): the chain's candidates from global memory
-//      (L2: the slot is re-read by its own CU only), the longest common prefix within the cap
+//   3. search, lanes = block positions (all 16 waves): the chain's candidates, links as u16
+//      distances and the staged bytes in LDS when they fit (else the slot, L2), the longest
+//      common prefix within the cap
 //   4. take mask per position (the LAZY2 rule on p, p+1, p+2), then the parse as 64-position
 //      segments, one per thread, walked from a guessed entry with Jacobi rounds across the
 //      workgroup until every segment's entry is its left neighbour's exit (the serial parse)
@@ -32,6 +33,9 @@ constexpr u32 DT = 1024;                          // threads per workgroup
 constexpr u32 HSIZE = 1u << ZH_HASH_LOG_SHORT;    // head table entries (+ a junk slot)
 constexpr u32 NSEG = ZH_BLOCK_MAX / 64;           // 64-position parse segments per block
 constexpr u32 HB = 8192;                          // positions per chain-building round
+#ifndef ZH_DEEP_FORCE_FIXUP
+#define ZH_DEEP_FORCE_FIXUP 0  // test builds: every chain step takes the out-of-order fix-up path
+#endif
 static_assert(NSEG == DT, "one parse segment per thread");
 static_assert(ZH_DEEP_PRE <= ZH_BLOCK_MAX && ZH_HIST_BLOCK <= ZH_BLOCK_MAX, "staged prefix fits the slot");
 // scratch slot of one workgroup (global memory)
@@ -190,7 +194,7 @@ __device__ void deep_chains(const u32 *s32, u32 *prev, u32 *head, u16 *hb, u32 s
           for (u32 u = 0; u < U; u++) {
             u32 const p = s0 + r * HB + j0 + 64 * u + lane;
             bool const v = p < lim;
-            if (__ballot(v && rv[u] >= p + 1)) {
+            if (ZH_DEEP_FORCE_FIXUP || __ballot(v && rv[u] >= p + 1)) {
 #ifdef ZH_STAMPS
               if (lane == 0) atomicAdd(&g_deep_fix, 1u);
 #endif
@@ -235,7 +239,7 @@ __device__ __forceinline__ void deep_search(const u32 *gdata, const u16 *gP16, u
     u32 const dl = P16[q - s0];
     return dl ? q + 1u - dl : 0u;
   };
-  // lanes = block positions, two independent chains per lane (i, i + DT)
+  // lanes = block positions
   struct Cur {
     u32 i, p, olo, ohi, c, best, bo, dd;
     bool act;
@@ -255,49 +259,50 @@ __device__ __forceinline__ void deep_search(const u32 *gdata, const u16 *gP16, u
   auto cur_done = [&](Cur &k) {
     if (k.i < nb) offg[k.i] = k.bo << 8 | k.best;
   };
-  // common prefix of the bytes from p + 8 and q + 8 (<= 56): 15 dwords each, loaded together
-  auto ext = [&](u32 p, u32 q) {
-    u32 A[15], B[15];
-    u32 const wp = (p >> 2) + 2, wq = (q >> 2) + 2, sp = p & 3, sq = q & 3;
+  // one chain per lane, the position's own 64 bytes held in registers (aligned to p): a
+  // candidate's extension loads only its own 15 dwords (two chains per lane, both loading the
+  // whole 112 bytes per extension: C5 8.5 / 6.7 GB/s vs 9.1 / 7.3 this way)
+  for (u32 i = tid; i < nb + (DT - 1) - (nb + DT - 1) % DT; i += DT) {
+    Cur k;
+    cur_init(k, i);
+    u32 O[16];
+    {
+      u32 const w = k.p >> 2, sh = k.p & 3;
+      u32 R[17];
 #pragma unroll
-    for (u32 k = 0; k < 15; k++) { A[k] = D32[wp + k]; B[k] = D32[wq + k]; }
-    u32 l = 56;
+      for (u32 j = 0; j < 17; j++) R[j] = k.i < nb ? D32[w + j] : 0u;
 #pragma unroll
-    for (int j = 13; j >= 0; j--) {
-      u32 const x = __builtin_amdgcn_alignbyte(A[j + 1], A[j], sp) ^ __builtin_amdgcn_alignbyte(B[j + 1], B[j], sq);
-      if (x) l = 4 * (u32)j + ((u32)__builtin_ctz(x) >> 3);
+      for (u32 j = 0; j < 16; j++) O[j] = __builtin_amdgcn_alignbyte(R[j + 1], R[j], sh);
     }
-    return l;
-  };
-  for (u32 i0 = 0; i0 < nb; i0 += 2 * DT) {
-    Cur ka, kb;
-    cur_init(ka, i0 + tid);
-    cur_init(kb, i0 + DT + tid);
-    while (__ballot(ka.act || kb.act)) {
-      u32 const qa = ka.act ? ka.c - 1u : 0u, qb = kb.act ? kb.c - 1u : 0u;
-      u32 na = 0, nb2 = 0, alo = 0, ahi = 0, blo = 0, bhi = 0;
-      // a candidate can replace a best of >= 8 bytes only if its byte at `best` matches too
-      // (libzstd's match[ml] == ip[ml] pre-check): one byte compare instead of the whole prefix
-      auto may_win = [&](const Cur &k, u32 q) {
-        if (k.best < 8) return true;
-        u32 const a = k.p + k.best, b = q + k.best;
-        return ((D32[a >> 2] >> (8 * (a & 3))) & 255u) == ((D32[b >> 2] >> (8 * (b & 3))) & 255u);
-      };
-      bool const wa = ka.act && may_win(ka, qa), wb = kb.act && may_win(kb, qb);
-      if (ka.act) na = link(qa);
-      if (kb.act) nb2 = link(qb);
-      if (wa) g64(D32, qa, alo, ahi);
-      if (wb) g64(D32, qb, blo, bhi);
-      auto pre8 = [](u32 olo, u32 ohi, u32 clo, u32 chi) {
-        u32 const x = olo ^ clo, y = ohi ^ chi;
-        return x ? (u32)__builtin_ctz(x) >> 3 : y ? 4u + ((u32)__builtin_ctz(y) >> 3) : 8u;
-      };
-      u32 la = wa ? pre8(ka.olo, ka.ohi, alo, ahi) : 0u, lb = wb ? pre8(kb.olo, kb.ohi, blo, bhi) : 0u;
-      bool const xa = wa && la == 8 && ka.p + 8 < n, xb = wb && lb == 8 && kb.p + 8 < n;
-      if (xa) la = 8 + ext(ka.p, qa);
-      if (xb) lb = 8 + ext(kb.p, qb);
-      auto upd = [&](Cur &k, u32 l, u32 q, u32 nx) {
-        if (!k.act) return;
+    while (__ballot(k.act)) {
+      if (k.act) {
+        u32 const q = k.c - 1u;
+        bool w = true;
+        if (k.best >= 8) {
+          u32 const a = k.p + k.best, b = q + k.best;
+          w = ((D32[a >> 2] >> (8 * (a & 3))) & 255u) == ((D32[b >> 2] >> (8 * (b & 3))) & 255u);
+        }
+        u32 const nx = link(q);
+        u32 l = 0;
+        if (w) {
+          u32 clo, chi;
+          g64(D32, q, clo, chi);
+          u32 const x = O[0] ^ clo, y = O[1] ^ chi;
+          l = x ? (u32)__builtin_ctz(x) >> 3 : y ? 4u + ((u32)__builtin_ctz(y) >> 3) : 8u;
+          if (l == 8 && k.p + 8 < n) {
+            u32 B[15];
+            u32 const wq = (q >> 2) + 2, sq = q & 3;
+#pragma unroll
+            for (u32 j = 0; j < 15; j++) B[j] = D32[wq + j];
+            u32 e = 56;
+#pragma unroll
+            for (int j = 13; j >= 0; j--) {
+              u32 const xx = O[j + 2] ^ __builtin_amdgcn_alignbyte(B[j + 1], B[j], sq);
+              if (xx) e = 4 * (u32)j + ((u32)__builtin_ctz(xx) >> 3);
+            }
+            l = 8 + e;
+          }
+        }
         l = min(l, k.p < n ? n - k.p : 0u);
         if (l >= ZH_MIN_MATCH_SHORT && l > k.best) {
           k.best = l;
@@ -306,12 +311,9 @@ __device__ __forceinline__ void deep_search(const u32 *gdata, const u16 *gP16, u
         k.dd++;
         k.c = nx;
         k.act = k.best < ZH_MAX_MATCH && k.dd < depth && k.c != 0 && k.p - (k.c - 1u) <= ZH_DEEP_MAXOFF;
-      };
-      upd(ka, la, qa, na);
-      upd(kb, lb, qb, nb2);
+      }
     }
-    cur_done(ka);
-    cur_done(kb);
+    cur_done(k);
   }
 }
 
