@@ -274,13 +274,14 @@ __device__ __forceinline__ void deep_search(const u32 *gdata, const u16 *gP16, u
 #pragma unroll
       for (u32 j = 0; j < 16; j++) O[j] = __builtin_amdgcn_alignbyte(R[j + 1], R[j], sh);
     }
+    u32 ownb = 0;  // own byte at p + best (best >= 8)
     while (__ballot(k.act)) {
       if (k.act) {
         u32 const q = k.c - 1u;
         bool w = true;
         if (k.best >= 8) {
-          u32 const a = k.p + k.best, b = q + k.best;
-          w = ((D32[a >> 2] >> (8 * (a & 3))) & 255u) == ((D32[b >> 2] >> (8 * (b & 3))) & 255u);
+          u32 const b = q + k.best;
+          w = ownb == ((D32[b >> 2] >> (8 * (b & 3))) & 255u);
         }
         u32 const nx = link(q);
         u32 l = 0;
@@ -307,6 +308,8 @@ __device__ __forceinline__ void deep_search(const u32 *gdata, const u16 *gP16, u
         if (l >= ZH_MIN_MATCH_SHORT && l > k.best) {
           k.best = l;
           k.bo = k.p - q;
+          u32 const a = k.p + l;  // the own byte a candidate must match to beat the new best
+          ownb = (D32[a >> 2] >> (8 * (a & 3))) & 255u;
         }
         k.dd++;
         k.c = nx;
