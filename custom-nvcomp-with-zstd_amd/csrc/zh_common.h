@@ -77,6 +77,13 @@ enum : u32 {
   ZH_FF_SLL = 5, ZH_FF_SOF = 6, ZH_FF_SML = 7,  // final FSE states (chain kernel)
 };
 
+// Deep matcher (zh_lz_deep.hip) scratch slot of one persistent workgroup: staged bytes (prefix +
+// block, zero padded) | u32 prev[2 x 64 Ki] | u32 off/len per block position | u16 link distances
+// (when LDS cannot hold them).  Slots per call = min(blocks, ZH_DEEP_SLOTS_MAX): the grid.
+#define ZH_DEEP_STG_BYTES (2u * ZH_BLOCK_MAX + 256u)
+#define ZH_DEEP_SLOT_BYTES ((size_t)ZH_DEEP_STG_BYTES + 4u * 2u * ZH_BLOCK_MAX + 4u * ZH_BLOCK_MAX + 2u * 2u * ZH_BLOCK_MAX)
+#define ZH_DEEP_SLOTS_MAX 256u
+
 struct ZhWorkspace {
   u8 *base;          // nblocks * ZH_WS_BLOCK_BYTES
   u32 *ctr;          // K1's block counter (persistent workgroups take the next block from it)
@@ -91,6 +98,10 @@ struct ZhWorkspace {
   const u32 *dd_prev;
   const u32 *dd_head;
   u32 dd_pre, dd_split;
+  // The deep matcher's per-workgroup scratch slots (ZH_DEEP_SLOT_BYTES each; levels >=
+  // ZH_DEEP_LEVEL only): part of the caller's workspace, so independent calls never share them
+  u8 *deep_slots;
+  u32 deep_nslots;
   __device__ u64 *seq(u32 b) const { return (u64 *)(base + (size_t)b * ZH_WS_BLOCK_BYTES); }
   __device__ u8 *lits(u32 b) const { return base + (size_t)b * ZH_WS_BLOCK_BYTES + ZH_SEQ_BYTES; }
   __device__ u32 *meta(u32 b) const { return (u32 *)(base + (size_t)b * ZH_WS_BLOCK_BYTES + ZH_SEQ_BYTES + ZH_LIT_BYTES); }

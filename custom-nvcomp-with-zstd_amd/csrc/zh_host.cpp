@@ -62,6 +62,54 @@ const char *status_to_string(Status s) {
 }
 
 // ============================================================================
+// error context / last error (reference src/cuda_zstd_types.cpp:81-141)
+// ============================================================================
+namespace {
+std::recursive_mutex &error_mutex() {
+  static std::recursive_mutex m;
+  return m;
+}
+ErrorContext g_last_error;
+ErrorCallback g_error_callback = nullptr;
+}  // namespace
+const char *get_detailed_error_message(const ErrorContext &ctx) {
+  static thread_local char buf[512];
+  const char *const file = ctx.file ? ctx.file : "unknown", *const fn = ctx.function ? ctx.function : "unknown";
+  const char *const sep = ctx.message ? " - " : "", *const msg = ctx.message ? ctx.message : "";
+  if (ctx.cuda_error != hipSuccess)
+    snprintf(buf, sizeof(buf), "%s at %s:%d in %s() - HIP Error: %s (%d)%s%s", status_to_string(ctx.status), file, ctx.line, fn,
+             hipGetErrorString(ctx.cuda_error), (int)ctx.cuda_error, sep, msg);
+  else
+    snprintf(buf, sizeof(buf), "%s at %s:%d in %s()%s%s", status_to_string(ctx.status), file, ctx.line, fn, sep, msg);
+  return buf;
+}
+void set_error_callback(ErrorCallback cb) {
+  std::lock_guard<std::recursive_mutex> g(error_mutex());
+  g_error_callback = cb;
+}
+void log_error(const ErrorContext &ctx) {
+  std::lock_guard<std::recursive_mutex> g(error_mutex());
+  g_last_error = ctx;
+  if (g_error_callback) g_error_callback(ctx);
+}
+ErrorContext get_last_error() {
+  std::lock_guard<std::recursive_mutex> g(error_mutex());
+  return g_last_error;
+}
+void clear_last_error() {
+  std::lock_guard<std::recursive_mutex> g(error_mutex());
+  g_last_error = ErrorContext();
+}
+namespace {
+// a public entry point's result: failures go to the last-error slot (and the callback)
+inline Status noted(Status s, const char *fn, int line) {
+  if (s != Status::SUCCESS) log_error(ErrorContext(s, __FILE__, line, fn));
+  return s;
+}
+}  // namespace
+#define ZH_NOTED(s) noted((s), __func__, __LINE__)
+
+// ============================================================================
 // CompressionConfig (reference src/cuda_zstd_types.cpp:147-210, 860-950)
 // ============================================================================
 Strategy CompressionConfig::level_to_strategy(int level) {
@@ -229,8 +277,10 @@ inline size_t align256(size_t v) { return (v + 255) & ~(size_t)255; }
 
 // Workspace layout inside the caller's temp buffer
 struct WsLayout {
-  size_t descs, items, blk_size, item_size, item_status, staging, counter, blocks, total;
-  static WsLayout make(size_t nblocks, size_t nitems, bool staged) {
+  size_t descs, items, blk_size, item_size, item_status, staging, counter, blocks, deep, deep_slots, total;
+  // deep: a level >= ZH_DEEP_LEVEL call (the deep matcher's scratch slots, one per persistent
+  // workgroup, follow the block areas)
+  static WsLayout make(size_t nblocks, size_t nitems, bool staged, bool deep = false) {
     WsLayout L{};
     size_t o = 0;
     L.descs = o; o = align256(o + nblocks * sizeof(ZhBlockDesc));
@@ -241,16 +291,19 @@ struct WsLayout {
     L.staging = o; o = align256(o + (staged ? nblocks * (size_t)ZH_STAGE_SLOT : 0));
     L.counter = o; o = align256(o + 4);
     L.blocks = o; o = align256(o + nblocks * (size_t)ZH_WS_BLOCK_BYTES);
+    L.deep_slots = deep ? std::min(nblocks, (size_t)ZH_DEEP_SLOTS_MAX) : 0;
+    L.deep = o; o = align256(o + L.deep_slots * ZH_DEEP_SLOT_BYTES);
     L.total = o + 256;  // slack for base alignment
     return L;
   }
 };
 
 // Device blocks of a frame of n bytes (ZH_FRAME_BLOCK: 64 KiB, or 32 KiB history blocks for
-// larger frames and for dictionary frames over 32 KiB)
-inline size_t block_size_of(size_t n, bool dict) { return ZH_FRAME_BLOCK(n, dict); }
-inline size_t blocks_of(size_t n, bool dict = false) {
-  size_t const bs = block_size_of(n, dict);
+// larger frames and for dictionary frames over 32 KiB below ZH_DEEP_LEVEL: split_dict)
+inline size_t block_size_of(size_t n, bool split_dict) { return ZH_FRAME_BLOCK(n, split_dict); }
+inline bool split_dict_of(bool has_dict, int level) { return has_dict && level < ZH_DEEP_LEVEL; }
+inline size_t blocks_of(size_t n, bool split_dict = false) {
+  size_t const bs = block_size_of(n, split_dict);
   return (n + bs - 1) / bs;
 }
 
@@ -330,10 +383,15 @@ struct DevDict {
   u8 *deep_stg = nullptr;
   u32 deep_P = 0, deep_split = 0;
   std::vector<u8> host;  // the loaded bytes (a reload of the same dictionary keeps everything)
+  // stream-ordered launches that may still read the buffers: one event per stream, recorded
+  // after each launch (the blocking entry points have finished reading when they return)
+  std::vector<std::pair<hipStream_t, hipEvent_t>> uses;
   DevDict() = default;
   DevDict(const DevDict &) = delete;
   DevDict &operator=(const DevDict &) = delete;
   ~DevDict() {
+    wait_uses();
+    for (auto &u : uses) (void)hipEventDestroy(u.second);
     if (d && owned) (void)hipFree(d);
     if (tabs) (void)hipFree(tabs);
     if (tabs_tmp) (void)hipFree(tabs_tmp);
@@ -353,6 +411,23 @@ struct DevDict {
   }
   const u8 *content() const { return d + off; }
   size_t content_n() const { return n - off; }
+  // a stream-ordered launch on `stream` reads this dictionary
+  Status note_use(hipStream_t stream) const {
+    auto *self = const_cast<DevDict *>(this);
+    for (auto &u : self->uses)
+      if (u.first == stream) return hipEventRecord(u.second, stream) == hipSuccess ? Status::SUCCESS : Status::ERROR_CUDA_ERROR;
+    hipEvent_t e;
+    if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return Status::ERROR_CUDA_ERROR;
+    self->uses.emplace_back(stream, e);
+    return hipEventRecord(e, stream) == hipSuccess ? Status::SUCCESS : Status::ERROR_CUDA_ERROR;
+  }
+  // every stream-ordered launch that read the dictionary has finished (before it is replaced)
+  Status wait_uses() {
+    Status s = Status::SUCCESS;
+    for (auto &u : uses)
+      if (hipEventSynchronize(u.second) != hipSuccess) s = Status::ERROR_CUDA_ERROR;
+    return s;
+  }
   // raw content or a formatted dictionary (host or device buffer); replaces the previous one
   Status load(const void *p, size_t bytes, hipStream_t stream) {
     if (!p || !bytes || bytes > zh::kDictMaxBytes) return Status::ERROR_INVALID_PARAMETER;
@@ -363,7 +438,7 @@ struct DevDict {
     u32 did = 0;
     size_t co = 0;
     if (!zh::dict_layout(h.data(), bytes, did, co)) return Status::ERROR_DICTIONARY_FAILED;
-    if (d && hipDeviceSynchronize() != hipSuccess) return Status::ERROR_CUDA_ERROR;  // launches still reading it
+    if (d && wait_uses() != Status::SUCCESS) return Status::ERROR_CUDA_ERROR;  // stream-ordered launches still reading it
     if (bytes > cap) {
       if (d) (void)hipFree(d);
       d = nullptr;
@@ -485,11 +560,11 @@ class ZstdBatchManager::Impl {
     bool const has_dict = dd && dd->n;
     bool const hist = config.window_log >= ZH_HIST_WINDOW_LOG;
     for (size_t i = 0; i < count; i++) {
-      size_t nb = blocks_of(in_sizes[i], has_dict);
+      size_t nb = blocks_of(in_sizes[i], split_dict_of(has_dict, config.level));
       nblocks += nb;
       staged |= nb > 1;
     }
-    WsLayout L = WsLayout::make(nblocks, count, staged);
+    WsLayout L = WsLayout::make(nblocks, count, staged, config.level >= ZH_DEEP_LEVEL);
     if (!temp || temp_size < L.total) return Status::ERROR_BUFFER_TOO_SMALL;
     u8 *base = (u8 *)(((uintptr_t)temp + 255) & ~(uintptr_t)255);
 
@@ -502,7 +577,8 @@ class ZstdBatchManager::Impl {
     u8 *staging = base + L.staging;
     size_t b = 0;
     for (size_t i = 0; i < count; i++) {
-      size_t const n = in_sizes[i], nb = blocks_of(n, has_dict), bs = block_size_of(n, has_dict);
+      bool const sd = split_dict_of(has_dict, config.level);
+      size_t const n = in_sizes[i], nb = blocks_of(n, sd), bs = block_size_of(n, sd);
       hi[i].dst = (u8 *)out_ptrs[i];
       hi[i].cap = out_sizes[i];
       hi[i].first_block = (u32)b;
@@ -529,6 +605,8 @@ class ZstdBatchManager::Impl {
     if (hipMemcpyAsync(base, h, up_bytes, hipMemcpyHostToDevice, stream) != hipSuccess) return Status::ERROR_CUDA_ERROR;
     ZhWorkspace ws{base + L.blocks, (u32 *)(base + L.counter), dd && dd->tabs_P ? dd->tabs : nullptr, dd ? dd->tabs_P : 0u};
     set_deep_dict(ws, dd);
+    ws.deep_slots = L.deep_slots ? base + L.deep : nullptr;
+    ws.deep_nslots = (u32)L.deep_slots;
     hipError_t e = zh::launch_compress((const ZhBlockDesc *)(base + L.descs), (u32)nblocks, ws, config.window_log, config.block_size,
                                        (u64 *)(base + L.item_size), (u32 *)(base + L.item_status), (u32 *)(base + L.blk_size),
                                        (const ZhItemDesc *)(base + L.items), (u32)count, staged,
@@ -649,7 +727,7 @@ CompressionConfig ZstdBatchManager::get_config() const { return pimpl_->config; 
 // sized for the dictionary layout as well (a per-call dictionary is only known at compress())
 size_t ZstdBatchManager::get_compress_temp_size(size_t n) const {
   size_t nb = std::max<size_t>(1, blocks_of(n, true));
-  return WsLayout::make(nb, 1, nb > 1).total;
+  return WsLayout::make(nb, 1, nb > 1, pimpl_->config.level >= ZH_DEEP_LEVEL).total;
 }
 // one slot for 128 KiB blocks (reference src/cuda_zstd_manager.cu:1373-1408 also sizes for one block)
 size_t ZstdBatchManager::get_decompress_temp_size(size_t) const { return DecLayout::make(1, DecLayout::kBlockMax).total; }
@@ -768,9 +846,12 @@ void ZstdBatchManager::reset_stats() { pimpl_->stats = CompressionStats{}; }
 size_t ZstdBatchManager::get_batch_compress_temp_size(const std::vector<size_t> &sizes) const {
   size_t nb = 0;
   bool staged = false;
-  // (the block layout does not depend on a dictionary: ZH_FRAME_BLOCK)
-  for (size_t s : sizes) { size_t k = blocks_of(s); nb += k; staged |= k > 1; }
-  return WsLayout::make(nb, sizes.size(), staged).total;
+  // (for the manager's dictionary as set now -- compress_batch takes no per-call dictionary; a
+  // dictionary set later may need more: ZH_FRAME_BLOCK, and the call then fails with
+  // ERROR_BUFFER_TOO_SMALL)
+  bool const sd = split_dict_of(pimpl_->active() != nullptr, pimpl_->config.level);
+  for (size_t s : sizes) { size_t k = blocks_of(s, sd); nb += k; staged |= k > 1; }
+  return WsLayout::make(nb, sizes.size(), staged, pimpl_->config.level >= ZH_DEEP_LEVEL).total;
 }
 size_t ZstdBatchManager::get_batch_decompress_temp_size(const std::vector<size_t> &sizes) const {
   return DecLayout::make(std::max<size_t>(1, sizes.size()), DecLayout::kBlockMax).total;
@@ -892,9 +973,15 @@ Status ZstdBatchManager::allocate_inference_workspace(size_t a, size_t b, void *
 }
 Status ZstdBatchManager::free_inference_workspace(void *ptr) { return hipFree(ptr) == hipSuccess ? Status::SUCCESS : Status::ERROR_CUDA_ERROR; }
 
+// (static: no dictionary, levels below ZH_DEEP_LEVEL; get_batch_device_temp_size_for covers the
+// manager's level and dictionary)
 size_t ZstdBatchManager::get_batch_device_temp_size(size_t count, size_t max_chunk) {
   size_t const bpi = std::max<size_t>(1, blocks_of(max_chunk));
   return WsLayout::make(count * bpi, count, bpi > 1).total;
+}
+size_t ZstdBatchManager::get_batch_device_temp_size_for(size_t count, size_t max_chunk) const {
+  size_t const bpi = std::max<size_t>(1, blocks_of(max_chunk, split_dict_of(pimpl_->active() != nullptr, pimpl_->config.level)));
+  return WsLayout::make(count * bpi, count, bpi > 1, pimpl_->config.level >= ZH_DEEP_LEVEL).total;
 }
 
 Status ZstdBatchManager::compress_batch_device(const void *const *d_in_ptrs, const size_t *d_in_sizes, size_t max_chunk, size_t count,
@@ -907,8 +994,8 @@ Status ZstdBatchManager::compress_batch_device(const void *const *d_in_ptrs, con
   const DevDict *dd = pimpl_->active();
   // (with a dictionary set, chunks over 32 KiB take two history blocks: a larger workspace
   // than get_batch_device_temp_size's, from nvcomp_zstd_batch_get_compress_temp_size_v5)
-  size_t const bpi = blocks_of(max_chunk, dd != nullptr), nblocks = count * bpi;
-  WsLayout L = WsLayout::make(nblocks, count, bpi > 1);
+  size_t const bpi = blocks_of(max_chunk, split_dict_of(dd != nullptr, pimpl_->config.level)), nblocks = count * bpi;
+  WsLayout L = WsLayout::make(nblocks, count, bpi > 1, pimpl_->config.level >= ZH_DEEP_LEVEL);
   if (!temp || temp_size < L.total) return Status::ERROR_BUFFER_TOO_SMALL;
   u8 *base = (u8 *)(((uintptr_t)temp + 255) & ~(uintptr_t)255);
   u64 const cap = estimate_compressed_size(max_chunk, pimpl_->config.level);
@@ -923,10 +1010,13 @@ Status ZstdBatchManager::compress_batch_device(const void *const *d_in_ptrs, con
   if (e != hipSuccess) return Status::ERROR_CUDA_ERROR;
   ZhWorkspace ws{base + L.blocks, (u32 *)(base + L.counter), dd && dd->tabs_P ? dd->tabs : nullptr, dd ? dd->tabs_P : 0u};
   set_deep_dict(ws, dd);
+  ws.deep_slots = L.deep_slots ? base + L.deep : nullptr;
+  ws.deep_nslots = (u32)L.deep_slots;
   e = zh::launch_compress((const ZhBlockDesc *)(base + L.descs), (u32)nblocks, ws, pimpl_->config.window_log, pimpl_->config.block_size, item_size,
                           item_status, (u32 *)(base + L.blk_size), (const ZhItemDesc *)(base + L.items), (u32)count, bpi > 1, ck,
                           pimpl_->config.level, stream);
-  return e == hipSuccess ? Status::SUCCESS : Status::ERROR_CUDA_ERROR;
+  if (e != hipSuccess) return Status::ERROR_CUDA_ERROR;
+  return dd ? dd->note_use(stream) : Status::SUCCESS;
 }
 
 size_t ZstdBatchManager::get_batch_device_decompress_temp_size(size_t count, size_t max_out) {
@@ -953,7 +1043,8 @@ Status ZstdBatchManager::decompress_batch_device(const void *const *d_in_ptrs, c
   a.out_sizes = d_out_sizes;
   a.statuses = d_statuses ? (u32 *)d_statuses : (u32 *)(base + L.statuses);
   a.nvcomp_codes = 1;
-  return zh::launch_decompress(a, (u32)count, stream) == hipSuccess ? Status::SUCCESS : Status::ERROR_CUDA_ERROR;
+  if (zh::launch_decompress(a, (u32)count, stream) != hipSuccess) return Status::ERROR_CUDA_ERROR;
+  return pimpl_->mgr_dict.n ? pimpl_->mgr_dict.note_use(stream) : Status::SUCCESS;
 }
 
 // ============================================================================
@@ -965,6 +1056,14 @@ Status ZstdBatchManager::decompress_batch_device(const void *const *d_in_ptrs, c
 // chunks of either kind decode in stream order.
 // ============================================================================
 namespace {
+struct FrameProbe {
+  u64 content = 0;
+  bool has_content = false, checksum = false;
+  u32 dict_id = 0, window_log = 0;
+  int meta_level = -1;
+  size_t frame_offset = 0;
+};
+Status probe_frame(const void *data, size_t n, FrameProbe &f);
 constexpr size_t kStreamWindow = 64 * 1024;
 // a device window of the last kStreamWindow stream bytes (double-buffered: no overlapping copies)
 struct HistWindow {
@@ -981,18 +1080,32 @@ struct HistWindow {
     return Status::SUCCESS;
   }
   const u8 *data() const { return buf[cur]; }
-  Status append(const void *src, size_t len, hipStream_t stream) {
+  // Enqueue the window's next state (its last bytes + src) into the other buffer on `stream`,
+  // without waiting: the chunk call's own stream synchronisation (its compress / decompress,
+  // which is blocking on return) covers it.  The current buffer stays valid until commit().
+  size_t pend_n = 0;
+  Status stage(const void *src, size_t len, hipStream_t stream) {
     Status s = ensure();
     if (s != Status::SUCCESS) return s;
     u8 *const dst = buf[cur ^ 1];
     size_t const take = std::min(len, kStreamWindow), keep = std::min(n, kStreamWindow - take);
     if (keep && hipMemcpyAsync(dst, buf[cur] + n - keep, keep, hipMemcpyDeviceToDevice, stream) != hipSuccess) return Status::ERROR_CUDA_ERROR;
     if (hipMemcpyAsync(dst + keep, (const u8 *)src + len - take, take, hipMemcpyDefault, stream) != hipSuccess) return Status::ERROR_CUDA_ERROR;
+    pend_n = keep + take;
+    return Status::SUCCESS;
+  }
+  void commit() {
     cur ^= 1;
-    n = keep + take;
-    // the chunk calls return with the caller's buffer free for reuse: the copy must have read
-    // it (a refill on another stream would otherwise race with it)
-    return hipStreamSynchronize(stream) == hipSuccess ? Status::SUCCESS : Status::ERROR_CUDA_ERROR;
+    n = pend_n;
+  }
+  // stage + a wait of its own (decompress_chunk: the window takes the decoded bytes, which exist
+  // only after the call's synchronisation)
+  Status append(const void *src, size_t len, hipStream_t stream) {
+    Status s = stage(src, len, stream);
+    if (s != Status::SUCCESS) return s;
+    if (hipStreamSynchronize(stream) != hipSuccess) return Status::ERROR_CUDA_ERROR;
+    commit();
+    return Status::SUCCESS;
   }
   void clear() { n = 0; }
 };
@@ -1037,6 +1150,11 @@ Status ZstdStreamingManager::init_compression_with_history(hipStream_t st, size_
   if (s == Status::SUCCESS) pimpl_->hist_mode = true;
   return s;
 }
+Status ZstdStreamingManager::init_decompression_with_history(hipStream_t st) {
+  Status s = init_decompression(st);
+  if (s == Status::SUCCESS) pimpl_->hist_mode = true;
+  return s;
+}
 Status ZstdStreamingManager::init_decompression(hipStream_t) {
   Status s = pimpl_->ensure_ws(pimpl_->mgr.get_decompress_temp_size(0));
   if (s == Status::SUCCESS) s = pimpl_->dhist.ensure();
@@ -1048,9 +1166,16 @@ Status ZstdStreamingManager::compress_chunk(const void *in, size_t n, void *out,
   if (!pimpl_->comp) return Status::ERROR_NOT_INITIALIZED;
   Status s = pimpl_->ensure_ws(pimpl_->mgr.get_compress_temp_size(n));
   if (s != Status::SUCCESS) return s;
+  // the stream window follows every chunk, so a later chunk_with_history sees these bytes (the
+  // window copy is enqueued first: compress()'s final synchronisation covers it)
+  bool const win = pimpl_->chist.buf[0] != nullptr;
+  if (win) {
+    s = pimpl_->chist.stage(in, n, stream);
+    if (s != Status::SUCCESS) return s;
+  }
   s = pimpl_->mgr.compress(in, n, out, out_size, pimpl_->ws, pimpl_->ws_size, nullptr, 0, stream);
-  // the stream window follows every chunk, so a later chunk_with_history sees these bytes
-  if (s == Status::SUCCESS && pimpl_->chist.buf[0]) s = pimpl_->chist.append(in, n, stream);
+  if (s == Status::SUCCESS && win) pimpl_->chist.commit();
+  else if (win) (void)hipStreamSynchronize(stream);  // (an early error return: the copy still reads `in`)
   return s;
 }
 Status ZstdStreamingManager::compress_chunk_with_history(const void *in, size_t n, void *out, size_t *out_size, bool, hipStream_t stream) {
@@ -1061,8 +1186,13 @@ Status ZstdStreamingManager::compress_chunk_with_history(const void *in, size_t 
   }
   Status s = pimpl_->ensure_ws(pimpl_->mgr.get_compress_temp_size(n));
   if (s != Status::SUCCESS) return s;
+  // the next window state goes to the other buffer while this chunk reads the current one;
+  // compress_with_history's synchronisation covers the copy
+  s = pimpl_->chist.stage(in, n, stream);
+  if (s != Status::SUCCESS) return s;
   s = pimpl_->mgr.compress_with_history(in, n, out, out_size, pimpl_->ws, pimpl_->ws_size, pimpl_->chist.data(), pimpl_->chist.n, stream);
-  if (s == Status::SUCCESS) s = pimpl_->chist.append(in, n, stream);
+  if (s == Status::SUCCESS) pimpl_->chist.commit();
+  else (void)hipStreamSynchronize(stream);  // (an early error return: the copy still reads `in`)
   return s;
 }
 Status ZstdStreamingManager::decompress_chunk(const void *in, size_t n, void *out, size_t *out_size, bool *is_last, hipStream_t stream) {
@@ -1074,12 +1204,24 @@ Status ZstdStreamingManager::decompress_chunk(const void *in, size_t n, void *ou
   if (is_last) *is_last = true;  // every chunk is a complete frame
   Status s = pimpl_->ensure_ws(pimpl_->mgr.get_decompress_temp_size(n));
   if (s != Status::SUCCESS) return s;
-  // the decoded window is the chunk's history only in a history session, or when no
-  // dictionary is set (an independent frame never reaches before its start, so the window is
-  // harmless there); with a dictionary, a frame of its own decodes with the dictionary
+  // Per frame: the decoded window is the frame's history unless the frame was compressed with
+  // the manager's dictionary.  A formatted dictionary names itself in the frame header, so a
+  // frame without its ID is a history frame; a raw-content dictionary has ID 0 like a history
+  // frame, so there the session decides (compression with history in this manager, or
+  // init_decompression_with_history).  Without a dictionary the window is harmless (a frame of
+  // its own never reaches before its start).
   dictionary::Dictionary dct;
   (void)pimpl_->mgr.get_dictionary(dct);
-  bool const use_hist = pimpl_->dhist.n && (pimpl_->hist_mode || dct.raw_content.empty());
+  bool hist_frame = true;
+  if (!dct.raw_content.empty()) {
+    if (dct.dict_id) {
+      FrameProbe fp;
+      hist_frame = probe_frame(in, n, fp) == Status::SUCCESS && fp.dict_id == 0;
+    } else {
+      hist_frame = pimpl_->hist_mode;
+    }
+  }
+  bool const use_hist = pimpl_->dhist.n && hist_frame;
   s = pimpl_->mgr.decompress_with_history(in, n, out, out_size, pimpl_->ws, pimpl_->ws_size, use_hist ? pimpl_->dhist.data() : nullptr,
                                           use_hist ? pimpl_->dhist.n : 0, stream);
   if (s == Status::SUCCESS) s = pimpl_->dhist.append(out, *out_size, stream);
@@ -1120,8 +1262,15 @@ std::unique_ptr<ZstdBatchManager> create_batch_manager(int level) {
 std::unique_ptr<ZstdStreamingManager> create_streaming_manager(int level) {
   return std::unique_ptr<ZstdStreamingManager>(new ZstdStreamingManager(CompressionConfig::from_level(level)));
 }
-Status compress_simple(const void *in, size_t n, void *out, size_t *out_size, int level, hipStream_t stream) {
+namespace {
+// one frame through a temporary manager (level, optional dictionary), workspace allocated here
+Status oneshot_compress(const void *in, size_t n, void *out, size_t *out_size, int level, const dictionary::Dictionary *dict, hipStream_t stream) {
+  if (!is_valid_compression_level(level)) return Status::ERROR_INVALID_PARAMETER;
   ZstdBatchManager m(CompressionConfig::from_level(level));
+  if (dict) {
+    Status const sd = m.set_dictionary(*dict);
+    if (sd != Status::SUCCESS) return sd;
+  }
   size_t need = m.get_compress_temp_size(n);
   void *ws = nullptr;
   if (hipMalloc(&ws, need) != hipSuccess) return Status::ERROR_OUT_OF_MEMORY;
@@ -1129,8 +1278,12 @@ Status compress_simple(const void *in, size_t n, void *out, size_t *out_size, in
   (void)hipFree(ws);
   return s;
 }
-Status decompress_simple(const void *in, size_t n, void *out, size_t *out_size, hipStream_t stream) {
+Status oneshot_decompress(const void *in, size_t n, void *out, size_t *out_size, const dictionary::Dictionary *dict, hipStream_t stream) {
   ZstdBatchManager m;
+  if (dict) {
+    Status const sd = m.set_dictionary(*dict);
+    if (sd != Status::SUCCESS) return sd;
+  }
   size_t need = m.get_decompress_temp_size(n);
   void *ws = nullptr;
   if (hipMalloc(&ws, need) != hipSuccess) return Status::ERROR_OUT_OF_MEMORY;
@@ -1138,18 +1291,52 @@ Status decompress_simple(const void *in, size_t n, void *out, size_t *out_size, 
   (void)hipFree(ws);
   return s;
 }
+}  // namespace
+Status compress_simple(const void *in, size_t n, void *out, size_t *out_size, int level, hipStream_t stream) {
+  return ZH_NOTED(oneshot_compress(in, n, out, out_size, level, nullptr, stream));
+}
+Status decompress_simple(const void *in, size_t n, void *out, size_t *out_size, hipStream_t stream) {
+  return ZH_NOTED(oneshot_decompress(in, n, out, out_size, nullptr, stream));
+}
+Status compress_with_dict(const void *in, size_t n, void *out, size_t *out_size, const dictionary::Dictionary &dict, int level, hipStream_t stream) {
+  return ZH_NOTED(oneshot_compress(in, n, out, out_size, level, &dict, stream));
+}
+Status decompress_with_dict(const void *in, size_t n, void *out, size_t *out_size, const dictionary::Dictionary &dict, hipStream_t stream) {
+  return ZH_NOTED(oneshot_decompress(in, n, out, out_size, &dict, stream));
+}
+
+// reference src/cuda_zstd_types.cpp:271-560 (per-stage pool buffers) -> one region here
+Status allocate_compression_workspace(CompressionWorkspace &w, size_t max_block_size, const CompressionConfig &config) {
+  if (w.is_allocated || max_block_size == 0) return ZH_NOTED(Status::ERROR_INVALID_PARAMETER);
+  Status const sv = config.validate();
+  if (sv != Status::SUCCESS) return ZH_NOTED(sv);
+  ZstdBatchManager m(config);
+  size_t const need = m.get_compress_temp_size(max_block_size);
+  void *p = nullptr;
+  if (hipMalloc(&p, need) != hipSuccess) return ZH_NOTED(Status::ERROR_OUT_OF_MEMORY);
+  w = CompressionWorkspace{};
+  w.d_workspace = p;
+  w.total_size = w.total_size_bytes = need;
+  w.is_allocated = true;
+  w.hash_table_size = 1u << config.hash_log;
+  w.chain_table_size = 1u << config.chain_log;
+  w.max_matches = (u32)std::min<size_t>(max_block_size, 0xFFFFFFFFu);
+  w.max_costs = w.max_matches + 1;
+  w.max_sequences = w.max_matches / 3;
+  w.num_blocks = (u32)((max_block_size + ZH_BLOCK_MAX - 1) / ZH_BLOCK_MAX);
+  return Status::SUCCESS;
+}
+Status free_compression_workspace(CompressionWorkspace &w) {
+  Status s = Status::SUCCESS;
+  if (w.d_workspace && hipFree(w.d_workspace) != hipSuccess) s = Status::ERROR_CUDA_ERROR;
+  w = CompressionWorkspace{};
+  return ZH_NOTED(s);
+}
 
 // Frame header fields of the first zstd frame in a buffer, after any skippable frames (the
 // reference parse_zstd_frame_header skips them the same way, src/cuda_zstd_manager.cu:875-900);
 // *meta_level = the level of a metadata frame written by write_metadata_frame, else -1.
 namespace {
-struct FrameProbe {
-  u64 content = 0;
-  bool has_content = false, checksum = false;
-  u32 dict_id = 0, window_log = 0;
-  int meta_level = -1;
-  size_t frame_offset = 0;
-};
 Status probe_frame(const void *data, size_t n, FrameProbe &f) {
   if (!data || n < 4) return Status::ERROR_INVALID_PARAMETER;
   size_t off = 0;
@@ -1419,16 +1606,59 @@ Status get_chunk_sizes(const void *d, size_t n, size_t *sizes, size_t max_chunks
 // ============================================================================
 // HybridEngine (reference src/cuda_zstd_hybrid.cu)
 // ============================================================================
+// Throughput history for ADAPTIVE routing (reference src/cuda_zstd_hybrid.cu:46-136): a
+// 64-sample ring per (CPU | GPU, compress | decompress), MB/s = MiB of input (compress) or of
+// output (decompress) per second of the call.
+struct ThroughputHistory {
+  static constexpr size_t kMax = 64;
+  double ring[4][kMax] = {};
+  size_t count[4] = {};
+  static size_t slot(ExecutionBackend b, bool comp) {
+    bool const cpu = b == ExecutionBackend::CPU_LIBZSTD || b == ExecutionBackend::CPU_PARALLEL;
+    return (cpu ? 0u : 2u) + (comp ? 0u : 1u);
+  }
+  void record(ExecutionBackend b, bool comp, double mbps) {
+    size_t const k = slot(b, comp);
+    ring[k][count[k] % kMax] = mbps;
+    count[k]++;
+  }
+  double average(ExecutionBackend b, bool comp) const {
+    size_t const k = slot(b, comp), n = std::min(count[k], kMax);
+    if (!n) return 0.0;
+    double s = 0;
+    for (size_t i = 0; i < n; i++) s += ring[k][i];
+    return s / (double)n;
+  }
+  void reset() { for (size_t &c : count) c = 0; }
+};
+
 class HybridEngine::Impl {
  public:
   HybridConfig config;
   CompressionStats stats;
+  ThroughputHistory prof;
+  mutable std::mutex mu;  // guards prof (get_observed_throughput may run beside a call)
   ZstdBatchManager mgr;
   explicit Impl(const HybridConfig &c) : config(c), mgr(CompressionConfig::from_level(c.compression_level)) {}
+  void profile(ExecutionBackend b, bool comp, size_t bytes, double ms) {
+    if (!config.enable_profiling) return;
+    std::lock_guard<std::mutex> g(mu);
+    prof.record(b, comp, ms > 0 ? ((double)bytes / (1024.0 * 1024.0)) / (ms / 1000.0) : 0.0);
+  }
 };
 HybridEngine::HybridEngine() : pimpl_(new Impl(HybridConfig{})) {}
 HybridEngine::HybridEngine(const HybridConfig &c) : pimpl_(new Impl(c)) {}
 HybridEngine::~HybridEngine() = default;
+HybridEngine::HybridEngine(HybridEngine &&) noexcept = default;
+HybridEngine &HybridEngine::operator=(HybridEngine &&) noexcept = default;
+double HybridEngine::get_observed_throughput(ExecutionBackend b, bool comp) const {
+  std::lock_guard<std::mutex> g(pimpl_->mu);
+  return pimpl_->prof.average(b, comp);
+}
+void HybridEngine::reset_profiling() {
+  std::lock_guard<std::mutex> g(pimpl_->mu);
+  pimpl_->prof.reset();
+}
 Status HybridEngine::configure(const HybridConfig &c) {
   if (!is_valid_compression_level(c.compression_level)) return Status::ERROR_INVALID_PARAMETER;
   pimpl_->config = c;
@@ -1441,14 +1671,21 @@ Status HybridEngine::set_compression_level(int level) {
   return pimpl_->mgr.set_compression_level(level);
 }
 DataLocation HybridEngine::detect_location(const void *p) { return is_device_ptr(p) ? DataLocation::DEVICE : DataLocation::HOST; }
-ExecutionBackend HybridEngine::query_routing(size_t n, DataLocation il, DataLocation ol, bool) const {
+ExecutionBackend HybridEngine::query_routing(size_t n, DataLocation il, DataLocation ol, bool is_compression) const {
   HybridMode m = pimpl_->config.mode;
   if (m == HybridMode::FORCE_CPU) return ExecutionBackend::CPU_LIBZSTD;
   if (m == HybridMode::FORCE_GPU) return ExecutionBackend::GPU_KERNELS;
   bool const dev = il == DataLocation::DEVICE && ol == DataLocation::DEVICE;
   if (m == HybridMode::PREFER_GPU) return (il == DataLocation::HOST && ol == DataLocation::HOST) ? ExecutionBackend::CPU_LIBZSTD : ExecutionBackend::GPU_KERNELS;
   if (m == HybridMode::PREFER_CPU) return dev ? ExecutionBackend::GPU_KERNELS : ExecutionBackend::CPU_LIBZSTD;
-  // AUTO / ADAPTIVE: device-resident data stays on the device; host data goes to libzstd
+  if (m == HybridMode::ADAPTIVE) {
+    // reference src/cuda_zstd_hybrid.cu:215-240: with samples of both, the GPU when > 1.2x the CPU
+    double const cpu = get_observed_throughput(ExecutionBackend::CPU_LIBZSTD, is_compression);
+    double const gpu = get_observed_throughput(ExecutionBackend::GPU_KERNELS, is_compression);
+    if (cpu > 0.0 && gpu > 0.0) return gpu > 1.2 * cpu ? ExecutionBackend::GPU_KERNELS : ExecutionBackend::CPU_LIBZSTD;
+  }
+  // AUTO (and ADAPTIVE without history): device-resident data stays on the device; host data
+  // goes to libzstd
   (void)n;
   return dev ? ExecutionBackend::GPU_KERNELS : ExecutionBackend::CPU_LIBZSTD;
 }
@@ -1498,6 +1735,7 @@ Status HybridEngine::compress(const void *in, size_t n, void *out, size_t *out_s
     pimpl_->stats.input_bytes += n;
     pimpl_->stats.output_bytes += *out_size;
     pimpl_->stats.compression_time_ms += ms;
+    pimpl_->profile(be, true, n, ms);
   }
   if (res) {
     res->backend_used = be;
@@ -1511,7 +1749,7 @@ Status HybridEngine::compress(const void *in, size_t n, void *out, size_t *out_s
     res->throughput_mbps = ms > 0 ? n / 1e6 / (ms / 1e3) : 0;
     res->routing_reason = be == ExecutionBackend::CPU_LIBZSTD ? "cpu (libzstd)" : "gpu (gfx950 kernels)";
   }
-  return s;
+  return ZH_NOTED(s);
 }
 
 // same routing as compress (reference src/cuda_zstd_hybrid.cu:836-905): libzstd for host data /
@@ -1549,6 +1787,11 @@ Status HybridEngine::decompress(const void *in, size_t n, void *out, size_t *out
     if (ws) (void)hipFree(ws);
   }
   double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  if (s == Status::SUCCESS) {
+    pimpl_->stats.bytes_decompressed += *out_size;
+    pimpl_->stats.decompression_time_ms += ms;
+    pimpl_->profile(be, false, *out_size, ms);
+  }
   if (res) {
     res->backend_used = be;
     res->input_location = il;
@@ -1557,7 +1800,7 @@ Status HybridEngine::decompress(const void *in, size_t n, void *out, size_t *out
     res->input_bytes = n;
     res->output_bytes = s == Status::SUCCESS ? *out_size : 0;
   }
-  return s;
+  return ZH_NOTED(s);
 }
 
 Status HybridEngine::compress_batch(const void *const *inputs, const size_t *sizes, void **outputs, size_t *out_sizes, size_t count,
@@ -1571,7 +1814,23 @@ Status HybridEngine::compress_batch(const void *const *inputs, const size_t *siz
   }
   return ok ? Status::SUCCESS : Status::ERROR_GENERIC;
 }
+Status HybridEngine::decompress_batch(const void *const *inputs, const size_t *sizes, void **outputs, size_t *out_sizes, size_t count,
+                                      DataLocation il, DataLocation ol, BatchRoutingResult *results, hipStream_t stream) {
+  if (count && (!inputs || !sizes || !outputs || !out_sizes)) return ZH_NOTED(Status::ERROR_INVALID_PARAMETER);
+  bool ok = true;
+  for (size_t i = 0; i < count; i++) {
+    HybridResult r;
+    Status s = decompress(inputs[i], sizes[i], outputs[i], &out_sizes[i], il, ol, &r, stream);
+    if (results) { results[i].backend_used = r.backend_used; results[i].status = s; results[i].output_size = s == Status::SUCCESS ? out_sizes[i] : 0; }
+    ok &= s == Status::SUCCESS;
+  }
+  return ok ? Status::SUCCESS : Status::ERROR_GENERIC;
+}
 
+Status hybrid_decompress(const void *in, size_t n, void *out, size_t *out_size, DataLocation il, DataLocation ol, HybridResult *res, hipStream_t stream) {
+  HybridEngine e;
+  return e.decompress(in, n, out, out_size, il, ol, res, stream);
+}
 Status hybrid_compress(const void *in, size_t n, void *out, size_t *out_size, DataLocation il, DataLocation ol, int level, HybridResult *res,
                        hipStream_t stream) {
   HybridConfig c;
@@ -1599,6 +1858,9 @@ struct cuda_zstd_dict_t { std::unique_ptr<dictionary::Dictionary> dict; };
 struct nvcomp_zstd_batch_manager_t { std::unique_ptr<nvcomp_v5::NvcompV5BatchManager> mgr; };
 struct cuda_zstd_hybrid_engine_t { std::unique_ptr<HybridEngine> engine; };
 
+// every C entry's Status -> the reference's int codes; failures also go to the last-error slot
+static int c_err(Status s) { return status_to_nvcomp_error(s == Status::SUCCESS ? s : noted(s, "C API", 0)); }
+
 extern "C" {
 
 cuda_zstd_manager_t *cuda_zstd_create_manager(int level) {
@@ -1614,12 +1876,12 @@ cuda_zstd_manager_t *cuda_zstd_create_manager(int level) {
 void cuda_zstd_destroy_manager(cuda_zstd_manager_t *m) { delete m; }
 
 int cuda_zstd_compress(cuda_zstd_manager_t *m, const void *src, size_t n, void *dst, size_t *dst_size, void *ws, size_t ws_size, hipStream_t stream) {
-  if (!m || !m->manager) return status_to_nvcomp_error(Status::ERROR_INVALID_PARAMETER);
-  return status_to_nvcomp_error(m->manager->compress(src, n, dst, dst_size, ws, ws_size, nullptr, 0, stream));
+  if (!m || !m->manager) return c_err(Status::ERROR_INVALID_PARAMETER);
+  return c_err(m->manager->compress(src, n, dst, dst_size, ws, ws_size, nullptr, 0, stream));
 }
 int cuda_zstd_decompress(cuda_zstd_manager_t *m, const void *src, size_t n, void *dst, size_t *dst_size, void *ws, size_t ws_size, hipStream_t stream) {
-  if (!m || !m->manager) return status_to_nvcomp_error(Status::ERROR_INVALID_PARAMETER);
-  return status_to_nvcomp_error(m->manager->decompress(src, n, dst, dst_size, ws, ws_size, stream));
+  if (!m || !m->manager) return c_err(Status::ERROR_INVALID_PARAMETER);
+  return c_err(m->manager->decompress(src, n, dst, dst_size, ws, ws_size, stream));
 }
 size_t cuda_zstd_get_compress_workspace_size(cuda_zstd_manager_t *m, size_t n) { return (m && m->manager) ? m->manager->get_compress_temp_size(n) : 0; }
 size_t cuda_zstd_get_decompress_workspace_size(cuda_zstd_manager_t *m, size_t n) { return (m && m->manager) ? m->manager->get_decompress_temp_size(n) : 0; }
@@ -1670,21 +1932,21 @@ size_t cuda_zstd_get_dictionary_content(const cuda_zstd_dict_t *d, void *out, si
   return n;
 }
 int cuda_zstd_get_dictionary_layout(const cuda_zstd_dict_t *d, unsigned int *dict_id, size_t *content_offset) {
-  if (!d || !d->dict) return status_to_nvcomp_error(Status::ERROR_INVALID_PARAMETER);
+  if (!d || !d->dict) return c_err(Status::ERROR_INVALID_PARAMETER);
   u32 id = 0;
   size_t off = 0;
-  if (!zh::dict_layout(d->dict->raw_content.data(), d->dict->raw_content.size(), id, off)) return status_to_nvcomp_error(Status::ERROR_DICTIONARY_FAILED);
+  if (!zh::dict_layout(d->dict->raw_content.data(), d->dict->raw_content.size(), id, off)) return c_err(Status::ERROR_DICTIONARY_FAILED);
   if (dict_id) *dict_id = id;
   if (content_offset) *content_offset = off;
   return 0;
 }
 int cuda_zstd_clear_dictionary(cuda_zstd_manager_t *m) {
-  if (!m || !m->manager) return status_to_nvcomp_error(Status::ERROR_INVALID_PARAMETER);
-  return status_to_nvcomp_error(m->manager->clear_dictionary());
+  if (!m || !m->manager) return c_err(Status::ERROR_INVALID_PARAMETER);
+  return c_err(m->manager->clear_dictionary());
 }
 int cuda_zstd_set_dictionary(cuda_zstd_manager_t *m, cuda_zstd_dict_t *d) {
-  if (!m || !m->manager || !d || !d->dict) return status_to_nvcomp_error(Status::ERROR_INVALID_PARAMETER);
-  return status_to_nvcomp_error(m->manager->set_dictionary(*d->dict));
+  if (!m || !m->manager || !d || !d->dict) return c_err(Status::ERROR_INVALID_PARAMETER);
+  return c_err(m->manager->set_dictionary(*d->dict));
 }
 const char *cuda_zstd_get_error_string(int code) { return status_to_string(nvcomp_v5::nvcomp_error_to_status(code)); }
 int cuda_zstd_is_error(int code) { return code != 0; }
@@ -1695,7 +1957,7 @@ size_t cuda_zstd_get_batch_compress_workspace_size(cuda_zstd_manager_t *m, const
 }
 int cuda_zstd_compress_batch(cuda_zstd_manager_t *m, const void *const *in_ptrs, const size_t *in_sizes, size_t count, void *const *out_ptrs,
                              size_t *out_sizes, int *statuses, void *ws, size_t ws_size, hipStream_t stream) {
-  if (!m || !m->manager || (count && (!in_ptrs || !in_sizes || !out_ptrs || !out_sizes))) return status_to_nvcomp_error(Status::ERROR_INVALID_PARAMETER);
+  if (!m || !m->manager || (count && (!in_ptrs || !in_sizes || !out_ptrs || !out_sizes))) return c_err(Status::ERROR_INVALID_PARAMETER);
   std::vector<BatchItem> items(count);
   for (size_t i = 0; i < count; i++) {
     items[i].input_ptr = (void *)in_ptrs[i];
@@ -1706,9 +1968,9 @@ int cuda_zstd_compress_batch(cuda_zstd_manager_t *m, const void *const *in_ptrs,
   Status s = m->manager->compress_batch(items, ws, ws_size, stream);
   for (size_t i = 0; i < count; i++) {
     if (items[i].status == Status::SUCCESS) out_sizes[i] = items[i].output_size;
-    if (statuses) statuses[i] = status_to_nvcomp_error(items[i].status);
+    if (statuses) statuses[i] = c_err(items[i].status);
   }
-  return status_to_nvcomp_error(s);
+  return c_err(s);
 }
 size_t cuda_zstd_get_batch_decompress_workspace_size(cuda_zstd_manager_t *m, const size_t *sizes, size_t count) {
   if (!m || !m->manager || (!sizes && count)) return 0;
@@ -1716,7 +1978,7 @@ size_t cuda_zstd_get_batch_decompress_workspace_size(cuda_zstd_manager_t *m, con
 }
 int cuda_zstd_decompress_batch(cuda_zstd_manager_t *m, const void *const *in_ptrs, const size_t *in_sizes, size_t count, void *const *out_ptrs,
                                size_t *out_sizes, int *statuses, void *ws, size_t ws_size, hipStream_t stream) {
-  if (!m || !m->manager || (count && (!in_ptrs || !in_sizes || !out_ptrs || !out_sizes))) return status_to_nvcomp_error(Status::ERROR_INVALID_PARAMETER);
+  if (!m || !m->manager || (count && (!in_ptrs || !in_sizes || !out_ptrs || !out_sizes))) return c_err(Status::ERROR_INVALID_PARAMETER);
   std::vector<BatchItem> items(count);
   for (size_t i = 0; i < count; i++) {
     items[i].input_ptr = (void *)in_ptrs[i];
@@ -1727,9 +1989,9 @@ int cuda_zstd_decompress_batch(cuda_zstd_manager_t *m, const void *const *in_ptr
   Status s = m->manager->decompress_batch(items, ws, ws_size, stream);
   for (size_t i = 0; i < count; i++) {
     out_sizes[i] = items[i].status == Status::SUCCESS ? items[i].output_size : 0;
-    if (statuses) statuses[i] = status_to_nvcomp_error(items[i].status);
+    if (statuses) statuses[i] = c_err(items[i].status);
   }
-  return status_to_nvcomp_error(s);
+  return c_err(s);
 }
 
 nvcompZstdManagerHandle nvcomp_zstd_create_manager_v5(int level) {
@@ -1743,18 +2005,18 @@ nvcompZstdManagerHandle nvcomp_zstd_create_manager_v5(int level) {
 void nvcomp_zstd_destroy_manager_v5(nvcompZstdManagerHandle h) { delete static_cast<ZstdBatchManager *>(h); }
 int nvcomp_zstd_compress_async_v5(nvcompZstdManagerHandle h, const void *in, size_t n, void *out, size_t *out_size, void *t, size_t ts, hipStream_t s) {
   auto *m = static_cast<ZstdBatchManager *>(h);
-  if (!m) return status_to_nvcomp_error(Status::ERROR_INVALID_PARAMETER);
-  return status_to_nvcomp_error(m->compress(in, n, out, out_size, t, ts, nullptr, 0, s));
+  if (!m) return c_err(Status::ERROR_INVALID_PARAMETER);
+  return c_err(m->compress(in, n, out, out_size, t, ts, nullptr, 0, s));
 }
 int nvcomp_zstd_decompress_async_v5(nvcompZstdManagerHandle h, const void *in, size_t n, void *out, size_t *out_size, void *t, size_t ts, hipStream_t s) {
   auto *m = static_cast<ZstdBatchManager *>(h);
-  if (!m) return status_to_nvcomp_error(Status::ERROR_INVALID_PARAMETER);
-  return status_to_nvcomp_error(m->decompress(in, n, out, out_size, t, ts, s));
+  if (!m) return c_err(Status::ERROR_INVALID_PARAMETER);
+  return c_err(m->decompress(in, n, out, out_size, t, ts, s));
 }
 size_t nvcomp_zstd_get_compress_temp_size_v5(nvcompZstdManagerHandle h, size_t n) { return h ? static_cast<ZstdBatchManager *>(h)->get_compress_temp_size(n) : 0; }
 size_t nvcomp_zstd_get_decompress_temp_size_v5(nvcompZstdManagerHandle h, size_t n) { return h ? static_cast<ZstdBatchManager *>(h)->get_decompress_temp_size(n) : 0; }
 int nvcomp_zstd_get_metadata_v5(const void *d, size_t n, nvcomp_v5::NvcompV5Metadata *m, hipStream_t s) {
-  return status_to_nvcomp_error(nvcomp_v5::get_metadata_async(d, n, m, s));
+  return c_err(nvcomp_v5::get_metadata_async(d, n, m, s));
 }
 
 nvcomp_zstd_batch_manager_t *nvcomp_zstd_batch_create_v5(int level, unsigned int chunk_size, int enable_checksum) {
@@ -1780,26 +2042,29 @@ size_t nvcomp_zstd_batch_get_max_compressed_chunk_size_v5(nvcomp_zstd_batch_mana
 }
 int nvcomp_zstd_batch_compress_async_v5(nvcomp_zstd_batch_manager_t *m, const void *const *in, const size_t *in_sizes, size_t n, void *const *out,
                                         size_t *out_sizes, void *t, size_t tb, hipStream_t s) {
-  if (!m || !m->mgr) return status_to_nvcomp_error(Status::ERROR_INVALID_PARAMETER);
-  return status_to_nvcomp_error(m->mgr->compress_async(in, in_sizes, n, out, out_sizes, t, tb, s));
+  if (!m || !m->mgr) return c_err(Status::ERROR_INVALID_PARAMETER);
+  return c_err(m->mgr->compress_async(in, in_sizes, n, out, out_sizes, t, tb, s));
 }
 size_t nvcomp_zstd_batched_compress_get_temp_size_v5(size_t n, size_t max_chunk) { return ZstdBatchManager::get_batch_device_temp_size(n, max_chunk); }
+size_t nvcomp_zstd_batch_get_batched_temp_size_v5(nvcomp_zstd_batch_manager_t *m, size_t n, size_t max_chunk) {
+  return (m && m->mgr) ? m->mgr->batch_manager().get_batch_device_temp_size_for(n, max_chunk) : 0;
+}
 int nvcomp_zstd_batch_set_dictionary_v5(nvcomp_zstd_batch_manager_t *m, cuda_zstd_dict_t *d) {
-  if (!m || !m->mgr || !d || !d->dict) return status_to_nvcomp_error(Status::ERROR_INVALID_PARAMETER);
-  return status_to_nvcomp_error(m->mgr->batch_manager().set_dictionary(*d->dict));
+  if (!m || !m->mgr || !d || !d->dict) return c_err(Status::ERROR_INVALID_PARAMETER);
+  return c_err(m->mgr->batch_manager().set_dictionary(*d->dict));
 }
 int nvcomp_zstd_batched_compress_async_v5(nvcomp_zstd_batch_manager_t *m, const void *const *d_in, const size_t *d_in_sizes, size_t max_chunk,
                                           size_t n, void *const *d_out, size_t *d_out_sizes, int *d_statuses, void *t, size_t tb, hipStream_t s) {
-  if (!m || !m->mgr) return status_to_nvcomp_error(Status::ERROR_INVALID_PARAMETER);
-  return status_to_nvcomp_error(m->mgr->batch_manager().compress_batch_device(d_in, d_in_sizes, max_chunk, n, d_out, d_out_sizes, d_statuses, t, tb, s));
+  if (!m || !m->mgr) return c_err(Status::ERROR_INVALID_PARAMETER);
+  return c_err(m->mgr->batch_manager().compress_batch_device(d_in, d_in_sizes, max_chunk, n, d_out, d_out_sizes, d_statuses, t, tb, s));
 }
 size_t nvcomp_zstd_batch_get_decompress_temp_size_v5(nvcomp_zstd_batch_manager_t *m, const size_t *sizes, size_t n) {
   return (m && m->mgr) ? m->mgr->get_decompress_temp_size(sizes, n) : 0;
 }
 int nvcomp_zstd_batch_decompress_async_v5(nvcomp_zstd_batch_manager_t *m, const void *const *in, const size_t *in_sizes, size_t n, void *const *out,
                                           size_t *out_sizes, void *t, size_t tb, hipStream_t s) {
-  if (!m || !m->mgr) return status_to_nvcomp_error(Status::ERROR_INVALID_PARAMETER);
-  return status_to_nvcomp_error(m->mgr->decompress_async(in, in_sizes, n, out, out_sizes, t, tb, s));
+  if (!m || !m->mgr) return c_err(Status::ERROR_INVALID_PARAMETER);
+  return c_err(m->mgr->decompress_async(in, in_sizes, n, out, out_sizes, t, tb, s));
 }
 size_t nvcomp_zstd_batched_decompress_get_temp_size_v5(size_t n, size_t max_out) {
   return ZstdBatchManager::get_batch_device_decompress_temp_size(n, max_out);
@@ -1807,8 +2072,8 @@ size_t nvcomp_zstd_batched_decompress_get_temp_size_v5(size_t n, size_t max_out)
 int nvcomp_zstd_batched_decompress_async_v5(nvcomp_zstd_batch_manager_t *m, const void *const *d_in, const size_t *d_in_sizes,
                                             const size_t *d_out_caps, size_t max_out, size_t n, void *const *d_out, size_t *d_out_sizes,
                                             int *d_statuses, void *t, size_t tb, hipStream_t s) {
-  if (!m || !m->mgr) return status_to_nvcomp_error(Status::ERROR_INVALID_PARAMETER);
-  return status_to_nvcomp_error(
+  if (!m || !m->mgr) return c_err(Status::ERROR_INVALID_PARAMETER);
+  return c_err(
       m->mgr->batch_manager().decompress_batch_device(d_in, d_in_sizes, d_out_caps, max_out, n, d_out, d_out_sizes, d_statuses, t, tb, s));
 }
 
@@ -1848,19 +2113,19 @@ static void fill_result(cuda_zstd_hybrid_result_t *r, const HybridResult &h) {
 }
 int cuda_zstd_hybrid_compress(cuda_zstd_hybrid_engine_t *e, const void *in, size_t n, void *out, size_t *out_size, unsigned il, unsigned ol,
                               cuda_zstd_hybrid_result_t *r, hipStream_t s) {
-  if (!e || !e->engine || il > 3 || ol > 3) return status_to_nvcomp_error(Status::ERROR_INVALID_PARAMETER);
+  if (!e || !e->engine || il > 3 || ol > 3) return c_err(Status::ERROR_INVALID_PARAMETER);
   HybridResult h;
   Status st = e->engine->compress(in, n, out, out_size, (DataLocation)il, (DataLocation)ol, &h, s);
   fill_result(r, h);
-  return status_to_nvcomp_error(st);
+  return c_err(st);
 }
 int cuda_zstd_hybrid_decompress(cuda_zstd_hybrid_engine_t *e, const void *in, size_t n, void *out, size_t *out_size, unsigned il, unsigned ol,
                                 cuda_zstd_hybrid_result_t *r, hipStream_t s) {
-  if (!e || !e->engine || il > 3 || ol > 3) return status_to_nvcomp_error(Status::ERROR_INVALID_PARAMETER);
+  if (!e || !e->engine || il > 3 || ol > 3) return c_err(Status::ERROR_INVALID_PARAMETER);
   HybridResult h;
   Status st = e->engine->decompress(in, n, out, out_size, (DataLocation)il, (DataLocation)ol, &h, s);
   fill_result(r, h);
-  return status_to_nvcomp_error(st);
+  return c_err(st);
 }
 size_t cuda_zstd_hybrid_max_compressed_size(cuda_zstd_hybrid_engine_t *e, size_t n) { return (e && e->engine) ? e->engine->get_max_compressed_size(n) : 0; }
 unsigned int cuda_zstd_hybrid_query_routing(cuda_zstd_hybrid_engine_t *e, size_t n, unsigned il, unsigned ol, int is_c) {
@@ -1887,26 +2152,26 @@ cuda_zstd_stream_t *cuda_zstd_stream_create(int level) {
 void cuda_zstd_stream_destroy(cuda_zstd_stream_t *s) { delete s; }
 int cuda_zstd_stream_compress_chunk(cuda_zstd_stream_t *s, const void *src, size_t n, void *dst, size_t *dst_size, int with_history, int last,
                                     hipStream_t stream) {
-  if (!s || !s->m) return status_to_nvcomp_error(Status::ERROR_INVALID_PARAMETER);
+  if (!s || !s->m) return c_err(Status::ERROR_INVALID_PARAMETER);
   if (!with_history && !s->m->is_compression_initialized()) {
     Status st = s->m->init_compression(stream, n);
-    if (st != Status::SUCCESS) return status_to_nvcomp_error(st);
+    if (st != Status::SUCCESS) return c_err(st);
   }
-  return status_to_nvcomp_error(with_history ? s->m->compress_chunk_with_history(src, n, dst, dst_size, last != 0, stream)
+  return c_err(with_history ? s->m->compress_chunk_with_history(src, n, dst, dst_size, last != 0, stream)
                                              : s->m->compress_chunk(src, n, dst, dst_size, last != 0, stream));
 }
 int cuda_zstd_stream_decompress_chunk(cuda_zstd_stream_t *s, const void *src, size_t n, void *dst, size_t *dst_size, int *is_last,
                                       hipStream_t stream) {
-  if (!s || !s->m) return status_to_nvcomp_error(Status::ERROR_INVALID_PARAMETER);
+  if (!s || !s->m) return c_err(Status::ERROR_INVALID_PARAMETER);
   bool l = false;
   Status st = s->m->decompress_chunk(src, n, dst, dst_size, &l, stream);
   if (is_last) *is_last = l ? 1 : 0;
-  return status_to_nvcomp_error(st);
+  return c_err(st);
 }
-int cuda_zstd_stream_reset(cuda_zstd_stream_t *s) { return s && s->m ? status_to_nvcomp_error(s->m->reset()) : 2; }
+int cuda_zstd_stream_reset(cuda_zstd_stream_t *s) { return s && s->m ? c_err(s->m->reset()) : 2; }
 
 int cuda_zstd_write_metadata_frame(void *dst, size_t capacity, int level, size_t *written, hipStream_t stream) {
-  return status_to_nvcomp_error(write_metadata_frame(dst, capacity, level, written, stream));
+  return c_err(write_metadata_frame(dst, capacity, level, written, stream));
 }
 int cuda_zstd_extract_metadata(const void *src, size_t size, unsigned int *level, unsigned long long *usize, unsigned int *dict_id, int *has_ck) {
   NvcompMetadata m;
@@ -1917,7 +2182,7 @@ int cuda_zstd_extract_metadata(const void *src, size_t size, unsigned int *level
     if (dict_id) *dict_id = m.dictionary_id;
     if (has_ck) *has_ck = m.checksum_policy != ChecksumPolicy::NO_COMPUTE_NO_VERIFY;
   }
-  return status_to_nvcomp_error(s);
+  return c_err(s);
 }
 
 const char *cuda_zstd_hip_version(void) { return "cuda_zstd_hip 0.2.0 (gfx950)"; }

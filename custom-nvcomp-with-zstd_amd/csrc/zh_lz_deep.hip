@@ -8,8 +8,9 @@
 // entropy stage, so K2-K4 are shared.
 //
 // One persistent 1024-thread workgroup per CU; blocks from the device counter.  Each workgroup
-// owns a slot of a library-held scratch buffer (g_deep below): the staged bytes (history or
-// dictionary prefix + block, contiguous), prev[] and the per-position offsets.  Per block:
+// owns a slot of the deep scratch in the caller's workspace (ZhWorkspace::deep_slots): the staged
+// bytes (history or dictionary prefix + block, contiguous), prev[] and the per-position offsets.
+// Per block:
 //   1. stage the prefix + block into the slot (and probe RLE); hash every position into prev[]
 //   2. chains, wave 0: positions in order, 64 per LDS `ds_max_rtn_u32` on the head table (entry =
 //      position + 1): LDS executes one wave's operations in order and a store's lanes one after
@@ -25,8 +26,6 @@
 #include "zh_common.h"
 #include "zh_hash.h"
 
-#include <mutex>
-
 namespace {
 
 constexpr u32 DT = 1024;                          // threads per workgroup
@@ -39,12 +38,12 @@ constexpr u32 HB = 8192;                          // positions per chain-buildin
 static_assert(NSEG == DT, "one parse segment per thread");
 static_assert(ZH_DEEP_PRE <= ZH_BLOCK_MAX && ZH_HIST_BLOCK <= ZH_BLOCK_MAX, "staged prefix fits the slot");
 // scratch slot of one workgroup (global memory)
-constexpr u32 STG_BYTES = 2 * ZH_BLOCK_MAX + 256;           // staged bytes + zero pad
+constexpr u32 STG_BYTES = ZH_DEEP_STG_BYTES;                // staged bytes + zero pad
 constexpr u32 SLOT_PREV = STG_BYTES;                        // u32 prev[2 * ZH_BLOCK_MAX]: q + 1, 0 = none
 constexpr u32 SLOT_OFF = SLOT_PREV + 4 * 2 * ZH_BLOCK_MAX;  // u32 off << 8 | len per block position
 constexpr u32 SLOT_P16 = SLOT_OFF + 4 * ZH_BLOCK_MAX;       // u16 link distances when LDS cannot hold them
 constexpr size_t SLOT_BYTES = SLOT_P16 + 2 * 2 * ZH_BLOCK_MAX;
-static_assert(SLOT_BYTES % 256 == 0, "slot alignment");
+static_assert(SLOT_BYTES % 256 == 0 && SLOT_BYTES == ZH_DEEP_SLOT_BYTES, "slot alignment / host size");
 // LDS
 constexpr u32 L_HEAD = 0;                  // u32 head[HSIZE + 4] (chains) / u8 len[ZH_BLOCK_MAX] (search, parse)
 constexpr u32 L_TM = 4 * (HSIZE + 4);      // u64 take masks per segment
@@ -555,19 +554,6 @@ hipError_t lz_deep_dict_tables(const u8 *content, size_t cn, u8 *stg, u32 *dprev
   return hipGetLastError();
 }
 
-// Library-held scratch of the deep matcher: one slot per workgroup (one per CU), allocated on a
-// device's first deep launch and kept (~1.2 MB per CU).  Not part of the caller's workspace: the
-// temp size of the reference API does not depend on the level.  Launches on one device share the
-// slots, so each deep launch waits (on its stream, no host sync) for the previous one on that
-// device, whatever stream it ran on.
-struct DeepDev {
-  u8 *ptr = nullptr;
-  u32 slots = 0;
-  hipEvent_t last = nullptr;
-  bool pending = false;
-};
-static std::mutex g_deep_mu;
-static DeepDev g_deep[64];
 hipError_t lz_deep_init() {
   hipError_t e = hipFuncSetAttribute((const void *)zh_lz_deep_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)DEEP_LDS);
   if (e == hipSuccess) e = hipFuncSetAttribute((const void *)zh_deep_dict_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)DEEP_LDS);
@@ -580,25 +566,10 @@ hipError_t lz_deep_launch(const ZhBlockDesc *d_descs, u32 nblocks, ZhWorkspace w
   else (void)hipGetDevice(&dev);
   if (dev < 0 || dev >= 64) return hipErrorInvalidDevice;
   if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) cus = 256;
-  u32 const grid = std::min(nblocks, (u32)cus);
-  std::lock_guard<std::mutex> g(g_deep_mu);
-  DeepDev &D = g_deep[dev];
-  if (D.pending && hipStreamWaitEvent(stream, D.last, 0) != hipSuccess) return hipErrorUnknown;
-  if (D.slots < (u32)cus) {
-    // (re)allocation: every earlier deep launch on the device must be done with the old slots
-    if (D.pending && hipEventSynchronize(D.last) != hipSuccess) return hipErrorUnknown;
-    if (D.ptr) (void)hipFree(D.ptr);
-    D.ptr = nullptr;
-    D.slots = 0;
-    if (hipMalloc(&D.ptr, SLOT_BYTES * (size_t)cus) != hipSuccess) { D.ptr = nullptr; return hipErrorOutOfMemory; }
-    D.slots = (u32)cus;
-  }
-  if (!D.last && hipEventCreateWithFlags(&D.last, hipEventDisableTiming) != hipSuccess) { D.last = nullptr; return hipErrorUnknown; }
-  hipLaunchKernelGGL(zh_lz_deep_kernel, dim3(grid), dim3(DT), DEEP_LDS, stream, d_descs, nblocks, ws, D.ptr, (u32)ZH_DEEP_DEPTH(level));
-  hipError_t const e = hipGetLastError();
-  if (e != hipSuccess) return e;
-  if (hipEventRecord(D.last, stream) != hipSuccess) return hipErrorUnknown;
-  D.pending = true;
-  return hipSuccess;
+  // one persistent workgroup per CU, at most one per scratch slot of the caller's workspace
+  if (!ws.deep_slots || !ws.deep_nslots) return hipErrorInvalidValue;
+  u32 const grid = std::min(std::min(nblocks, (u32)cus), ws.deep_nslots);
+  hipLaunchKernelGGL(zh_lz_deep_kernel, dim3(grid), dim3(DT), DEEP_LDS, stream, d_descs, nblocks, ws, ws.deep_slots, (u32)ZH_DEEP_DEPTH(level));
+  return hipGetLastError();
 }
 }  // namespace zh

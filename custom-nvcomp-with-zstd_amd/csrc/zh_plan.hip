@@ -34,7 +34,7 @@ extern "C" __global__ void zh_plan_kernel(const void *const *__restrict__ in_ptr
   if (b >= nitems * bpi) return;
   u32 const it = b / bpi, k = b % bpi;
   u64 const size = in_sizes[it];
-  u64 const bs = ZH_FRAME_BLOCK(size, dict != nullptr);
+  u64 const bs = ZH_FRAME_BLOCK(size, dict != nullptr && !(extra_flags & ZH_F_DEEP));
   u64 const nb = (size + bs - 1) / bs;
   ZhBlockDesc d;
   d.src = (const u8 *)in_ptrs[it] + (u64)k * bs;

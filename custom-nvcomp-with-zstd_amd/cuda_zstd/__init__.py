@@ -69,6 +69,7 @@ def lib() -> ctypes.CDLL:
             "nvcomp_zstd_batch_get_max_compressed_chunk_size_v5": (sz, [vp, sz]),
             "nvcomp_zstd_batch_compress_async_v5": (i, [vp, vp, vp, sz, vp, vp, vp, sz, vp]),
             "nvcomp_zstd_batched_compress_get_temp_size_v5": (sz, [sz, sz]),
+            "nvcomp_zstd_batch_get_batched_temp_size_v5": (sz, [vp, sz, sz]),
             "nvcomp_zstd_batch_set_dictionary_v5": (i, [vp, vp]),
             "nvcomp_zstd_batched_compress_async_v5": (i, [vp, vp, vp, sz, sz, vp, vp, vp, vp, sz, vp]),
             "cuda_zstd_get_batch_decompress_workspace_size": (sz, [vp, psz, sz]),
@@ -432,9 +433,9 @@ class BatchedCompressor:
         except Exception:
             pass
 
-    @staticmethod
-    def temp_size(num_chunks: int, max_chunk: int) -> int:
-        return lib().nvcomp_zstd_batched_compress_get_temp_size_v5(num_chunks, max_chunk)
+    def temp_size(self, num_chunks: int, max_chunk: int) -> int:
+        """Workspace of compress_async for this handle's level and dictionary."""
+        return lib().nvcomp_zstd_batch_get_batched_temp_size_v5(self._h, num_chunks, max_chunk)
 
     def temp_size_for(self, chunk_sizes) -> int:
         """Workspace for these chunk sizes under the handle's current dictionary."""

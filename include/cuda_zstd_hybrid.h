@@ -20,6 +20,8 @@ class HybridEngine {
   ~HybridEngine();
   HybridEngine(const HybridEngine &) = delete;
   HybridEngine &operator=(const HybridEngine &) = delete;
+  HybridEngine(HybridEngine &&) noexcept;             // reference :82-83
+  HybridEngine &operator=(HybridEngine &&) noexcept;
 
   Status configure(const HybridConfig &config);
   HybridConfig get_config() const;
@@ -32,12 +34,23 @@ class HybridEngine {
   Status compress_batch(const void *const *inputs, const size_t *input_sizes, void **outputs, size_t *output_sizes, size_t count,
                         DataLocation input_loc = DataLocation::HOST, DataLocation output_loc = DataLocation::HOST,
                         BatchRoutingResult *results = nullptr, hipStream_t stream = 0);
+  // reference :180-186: each item routed like decompress(); output_sizes in = capacity, out = bytes
+  Status decompress_batch(const void *const *inputs, const size_t *input_sizes, void **outputs, size_t *output_sizes, size_t count,
+                          DataLocation input_loc = DataLocation::HOST, DataLocation output_loc = DataLocation::HOST,
+                          BatchRoutingResult *results = nullptr, hipStream_t stream = 0);
 
   size_t get_max_compressed_size(size_t input_size) const;
   ExecutionBackend query_routing(size_t data_size, DataLocation input_loc, DataLocation output_loc, bool is_compression) const;
   CompressionStats get_stats() const;
   void reset_stats();
   static DataLocation detect_location(const void *ptr);
+
+  // reference :229-235 (src/cuda_zstd_hybrid.cu:46-136, 1029-1038): the mean of the last 64
+  // MB/s samples of a backend (CPU_* share one history, GPU_* the other), recorded by
+  // compress/decompress when HybridConfig::enable_profiling is set; ADAPTIVE routing picks the
+  // GPU once both have samples and it is > 1.2x the CPU's. 0 = no samples.
+  double get_observed_throughput(ExecutionBackend backend, bool is_compression) const;
+  void reset_profiling();
 
  private:
   class Impl;
@@ -47,6 +60,9 @@ class HybridEngine {
 Status hybrid_compress(const void *input, size_t input_size, void *output, size_t *output_size, DataLocation input_loc = DataLocation::HOST,
                        DataLocation output_loc = DataLocation::HOST, int compression_level = 3, HybridResult *result = nullptr,
                        hipStream_t stream = 0);
+// reference :263-268: a temporary engine with the default configuration
+Status hybrid_decompress(const void *input, size_t input_size, void *output, size_t *output_size, DataLocation input_loc = DataLocation::HOST,
+                         DataLocation output_loc = DataLocation::HOST, HybridResult *result = nullptr, hipStream_t stream = 0);
 std::unique_ptr<HybridEngine> create_hybrid_engine(const HybridConfig &config = HybridConfig{});
 std::unique_ptr<HybridEngine> create_hybrid_engine(int compression_level);
 

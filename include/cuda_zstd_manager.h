@@ -104,6 +104,9 @@ class ZstdBatchManager : public ZstdManager {
                                void *const *d_out_ptrs, size_t *d_out_sizes, int *d_statuses, void *temp_workspace, size_t temp_size,
                                hipStream_t stream);
   static size_t get_batch_device_temp_size(size_t count, size_t max_chunk_bytes);
+  // the same for this manager's level and dictionary (levels >= 9 add the deep matcher's scratch
+  // slots, ~1.2 MB per persistent workgroup; a dictionary over 32 KiB chunks adds history blocks)
+  size_t get_batch_device_temp_size_for(size_t count, size_t max_chunk_bytes) const;
 
   // Stream-ordered batched decompression over device arrays (no host sync; GPU decoder,
   // any RFC 8878 frames); used by nvcomp_zstd_batched_decompress_async_v5.
@@ -137,6 +140,10 @@ class ZstdStreamingManager {
   Status init_compression(hipStream_t stream = 0, size_t max_chunk_size = 0);
   Status init_compression_with_history(hipStream_t stream = 0, size_t max_chunk_size = 0);
   Status init_decompression(hipStream_t stream = 0);
+  // (not in the reference) a decode-only session whose frames came from
+  // compress_chunk_with_history: with a raw-content dictionary set, decompress_chunk cannot tell
+  // a history frame from a dictionary frame by its header (both carry Dictionary_ID 0)
+  Status init_decompression_with_history(hipStream_t stream = 0);
   Status compress_chunk(const void *input, size_t input_size, void *output, size_t *output_size, bool is_last_chunk, hipStream_t stream = 0);
   Status compress_chunk_with_history(const void *input, size_t input_size, void *output, size_t *output_size, bool is_last_chunk,
                                      hipStream_t stream = 0);
@@ -167,6 +174,13 @@ Status compress_simple(const void *uncompressed_data, size_t uncompressed_size, 
                        int compression_level = 3, hipStream_t stream = 0);
 Status decompress_simple(const void *compressed_data, size_t compressed_size, void *uncompressed_data, size_t *uncompressed_size,
                          hipStream_t stream = 0);
+// reference include/cuda_zstd_manager.h:377-386 (declared there, never defined): one frame
+// compressed against / decompressed with `dict` (raw content or RFC 8878 §5 formatted), the
+// workspace allocated and freed inside the call, output valid on return
+Status compress_with_dict(const void *uncompressed_data, size_t uncompressed_size, void *compressed_data, size_t *compressed_size,
+                          const dictionary::Dictionary &dict, int compression_level = 3, hipStream_t stream = 0);
+Status decompress_with_dict(const void *compressed_data, size_t compressed_size, void *uncompressed_data, size_t *uncompressed_size,
+                            const dictionary::Dictionary &dict, hipStream_t stream = 0);
 
 Status get_decompressed_size(const void *compressed_data, size_t compressed_size, size_t *decompressed_size);
 Status validate_compressed_data(const void *compressed_data, size_t compressed_size, bool check_checksum = true);

@@ -61,6 +61,29 @@ enum class Status : u32 {
 
 const char *status_to_string(Status status);
 
+// Error context and the process-wide last-error slot (reference include/cuda_zstd_types.h:132-156,
+// src/cuda_zstd_types.cpp:81-141).  The library records every failing Status of its public
+// entry points here (log_error) and hands it to the callback, if one is set.
+struct ErrorContext {
+  Status status = Status::SUCCESS;
+  const char *file = nullptr;
+  int line = 0;
+  const char *function = nullptr;
+  const char *message = nullptr;
+  hipError_t cuda_error = hipSuccess;  // HIP runtime error (the reference's cudaError_t field)
+
+  ErrorContext() = default;
+  ErrorContext(Status s, const char *f, int l, const char *fn, const char *msg = nullptr)
+      : status(s), file(f), line(l), function(fn), message(msg) {}
+};
+// "<status> at <file>:<line> in <function>()[ - HIP Error: ...][ - message]", thread-local buffer
+const char *get_detailed_error_message(const ErrorContext &ctx);
+typedef void (*ErrorCallback)(const ErrorContext &ctx);
+void set_error_callback(ErrorCallback callback);
+void log_error(const ErrorContext &ctx);
+ErrorContext get_last_error();
+void clear_last_error();
+
 enum class Strategy : u32 { FAST = 0, DFAST = 1, GREEDY = 2, LAZY = 3, LAZY2 = 4, BTLAZY2 = 5, BTOPT = 6, BTULTRA = 7 };
 enum class CompressionMode : u32 { LEVEL_BASED = 0, STRATEGY_BASED = 1 };
 enum class ChecksumPolicy : u32 { NO_COMPUTE_NO_VERIFY = 0, COMPUTE_NO_VERIFY = 1, COMPUTE_AND_VERIFY = 2 };
@@ -178,6 +201,51 @@ struct BatchRoutingResult {
 inline bool is_valid_compression_level(int level) {
   return level >= (int)MIN_COMPRESSION_LEVEL && level <= (int)MAX_COMPRESSION_LEVEL;
 }
+inline float get_compression_ratio(size_t uncompressed, size_t compressed) {
+  return compressed > 0 ? static_cast<float>(uncompressed) / compressed : 0.0f;
+}
+
+// Pre-sized compression workspace (reference include/cuda_zstd_types.h:456-499, 523-527).  The
+// reference carves ~20 per-stage buffers out of a memory pool; this library's kernels use one
+// contiguous region (`d_workspace`, `total_size` bytes = ZstdBatchManager::get_compress_temp_size
+// of max_block_size, which covers every level and the dictionary layout) that is passed as the
+// temp workspace of compress().  The per-stage pointer fields are kept for source compatibility
+// and stay null; the size fields report the configured search parameters.
+struct CompressionWorkspace {
+  u32 *d_hash_table = nullptr;
+  u32 hash_table_size = 0;
+  u32 *d_chain_table = nullptr;
+  u32 chain_table_size = 0;
+  void *d_matches = nullptr;
+  u32 max_matches = 0;
+  void *d_costs = nullptr;
+  u32 max_costs = 0;
+  u32 *d_literal_lengths_reverse = nullptr;
+  u32 *d_match_lengths_reverse = nullptr;
+  u32 *d_offsets_reverse = nullptr;
+  u32 max_sequences = 0;
+  u32 *d_frequencies = nullptr;
+  u32 *d_code_lengths = nullptr;
+  u32 *d_bit_offsets = nullptr;
+  u32 *d_block_sums = nullptr;
+  u32 *d_scanned_block_sums = nullptr;
+  u32 num_blocks = 0;
+  void *d_workspace = nullptr;
+  size_t total_size = 0;
+  size_t total_size_bytes = 0;
+  bool is_allocated = false;
+  hipStream_t stream = nullptr;
+  hipEvent_t event_complete = nullptr;
+  u32 *d_lz77_temp = nullptr;
+  void *d_sequences = nullptr;
+  void *d_fse_tables = nullptr;
+  void *d_huffman_table = nullptr;
+  void *d_bitstream = nullptr;
+};
+// hipMalloc of the whole region (ERROR_OUT_OF_MEMORY on failure, ERROR_INVALID_PARAMETER for a
+// size of 0 or an already allocated workspace); free releases it and resets the struct.
+Status allocate_compression_workspace(CompressionWorkspace &workspace, size_t max_block_size, const CompressionConfig &config);
+Status free_compression_workspace(CompressionWorkspace &workspace);
 
 }  // namespace cuda_zstd
 #endif  // __cplusplus

@@ -16,13 +16,16 @@
 #define ZH_HIST_BLOCK 32768         /* device block of a history frame (below) */
 #define ZH_HIST_WINDOW_LOG 16       /* history needs a window of >= 64 KiB */
 /* Device block size of a frame of n bytes: frames up to 64 KiB are one
- * block (a dictionary frame's block staged behind the last 64 KiB - n bytes of the dictionary
- * content); larger frames are cut into 32 KiB blocks that are each staged behind the 32 KiB
- * before them (the previous block, or the dictionary's tail for the first), so matches reach
- * across block boundaries within the 64 KiB of LDS.  The layout -- and so the workspace size --
- * does not depend on whether a dictionary is set (the reference's temp size does not,
+ * block; larger frames are cut into 32 KiB blocks that are each staged behind the 32 KiB before
+ * them (the previous block), so matches reach across block boundaries within the 64 KiB of LDS.
+ * split_dict = a dictionary (or stream history) frame below ZH_DEEP_LEVEL: its first block is
+ * staged behind the last 64 KiB - block bytes of the dictionary content, so frames over 32 KiB
+ * are cut into 32 KiB blocks too (the first sees 32 KiB of dictionary, not 64 KiB - n).  The
+ * deep matcher (levels >= ZH_DEEP_LEVEL) stages its prefix outside LDS and never splits.
+ * Workspace sizes are taken for the split layout (a dictionary is not known when the temp size
+ * is asked for; the reference's temp size does not depend on it either,
  * src/cuda_zstd_manager.cu:5661). */
-#define ZH_FRAME_BLOCK(n, dict) ((void)(dict), ((n) <= ZH_BLOCK_MAX ? ZH_BLOCK_MAX : ZH_HIST_BLOCK))
+#define ZH_FRAME_BLOCK(n, split_dict) ((n) <= ((split_dict) ? ZH_HIST_BLOCK : ZH_BLOCK_MAX) ? ZH_BLOCK_MAX : ZH_HIST_BLOCK)
 #define ZH_TILE 128                 /* hash insertion granularity (positions) */
 #define ZH_WINDOW 2048              /* parse window (positions); catch-up stays inside one */
 #define ZH_SKIP_TILES 2             /* tiles a window searches after a window without matches (miss skip) */

@@ -1178,7 +1178,7 @@ size_t orc_compress_frame_dict(u8 *dst, size_t cap, const u8 *src, u64 n, u32 bl
   if (checksum) dst[4] |= 0x04;
   u64 pos = 0;
   u32 b = 0;
-  u32 const bs = ZH_FRAME_BLOCK(n, dict_n != 0);
+  u32 const bs = ZH_FRAME_BLOCK(n, dict_n != 0 && orc_parse_level < ZH_DEEP_LEVEL);
   do {
     u32 bn = (u32)((n - pos) < bs ? (n - pos) : bs);
     u32 rep[3] = {1, 4, 8};

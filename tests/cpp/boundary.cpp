@@ -22,6 +22,14 @@
 //                                  (raw content or a formatted dictionary): every chunk through
 //                                  compress_chunk (h = 0) or compress_chunk_with_history (h = 1),
 //                                  then every frame through decompress_chunk in order
+//   boundary stream_split <dir> <f>  compress_chunk_with_history in one streaming manager,
+//                                  decompress_chunk in a second, decode-only one; both with
+//                                  set_dictionary(<dir>/dict.bin); f = 1: the decoder calls
+//                                  init_decompression_with_history first
+//   boundary cxx_extra <dir>       compress_with_dict / decompress_with_dict with <dir>/dict.bin,
+//                                  allocate_/free_compression_workspace, the ErrorContext API,
+//                                  HybridEngine move ops / decompress_batch / profiling and
+//                                  hybrid_decompress (frames.bin = compress_with_dict's frames)
 //
 // <dir>/in.bin = the chunks back to back, <dir>/sizes.bin = u64 sizes.  Writes
 // <dir>/frames.bin (frames back to back), <dir>/fsizes.bin (u64), and for `nvcomp`
@@ -36,6 +44,7 @@
 #include <string>
 #include <vector>
 
+#include "cuda_zstd_hybrid.h"
 #include "cuda_zstd_manager.h"
 #include "cuda_zstd_nvcomp.h"
 
@@ -223,6 +232,178 @@ int main(int argc, char **argv) {
       CK(hipMemcpy(back.data() + offs[i], d_o, sizes[i], hipMemcpyDeviceToHost));
     }
     dump(dir + "/back.bin", back.data(), back.size());
+  } else if (mode == "stream_split") {
+    // advisor r3: frames from compress_chunk_with_history in one manager (dictionary set),
+    // decoded by a SECOND, decode-only manager with the same dictionary set.  <flag> = 1: the
+    // decoder calls init_decompression_with_history (needed for a raw-content dictionary, whose
+    // frames carry Dictionary_ID 0 like history frames); 0: a formatted dictionary's frames are
+    // told apart by their header alone.
+    if (argc < 4) return 1;
+    bool const flag = std::stoul(argv[3]) != 0;
+    std::vector<char> db = slurp(dir + "/dict.bin");
+    dictionary::Dictionary dct;
+    dct.raw_content.assign(db.begin(), db.end());
+    ZstdStreamingManager enc(CompressionConfig::from_level(3)), dec(CompressionConfig::from_level(3));
+    Status st = enc.set_dictionary(dct);
+    if (st == Status::SUCCESS) st = dec.set_dictionary(dct);
+    if (st == Status::SUCCESS) st = enc.init_compression_with_history(0, 0);
+    if (st == Status::SUCCESS) st = flag ? dec.init_decompression_with_history(0) : dec.init_decompression(0);
+    if (st != Status::SUCCESS) { fprintf(stderr, "init: %s\n", status_to_string(st)); return 3; }
+    for (size_t i = 0; i < n; i++) {
+      fsz[i] = cap;
+      st = enc.compress_chunk_with_history(d_in[i], sizes[i], d_out[i], &fsz[i], i + 1 == n, 0);
+      if (st != Status::SUCCESS) { fprintf(stderr, "compress_chunk_with_history %zu: %s\n", i, status_to_string(st)); return 3; }
+    }
+    std::vector<char> back(in.size());
+    void *d_o;
+    CK(hipMalloc(&d_o, std::max<size_t>(*std::max_element(sizes.begin(), sizes.end()), 1)));
+    for (size_t i = 0; i < n; i++) {
+      size_t got = sizes[i];
+      bool last = false;
+      st = dec.decompress_chunk(d_out[i], fsz[i], d_o, &got, &last, 0);
+      if (st != Status::SUCCESS || got != sizes[i]) { fprintf(stderr, "decompress_chunk %zu: %s, %zu B\n", i, status_to_string(st), got); return 4; }
+      CK(hipMemcpy(back.data() + offs[i], d_o, sizes[i], hipMemcpyDeviceToHost));
+    }
+    dump(dir + "/back.bin", back.data(), back.size());
+  } else if (mode == "cxx_extra") {
+    // the rest of the reference's C++ surface (VERDICT r3 missing #1):
+    //  * compress_with_dict / decompress_with_dict (include/cuda_zstd_manager.h:377-386) with
+    //    <dir>/dict.bin -> frames.bin, back.bin
+    //  * allocate_/free_compression_workspace (include/cuda_zstd_types.h:523-527): the region as
+    //    ZstdManager::compress's temp workspace, the frames must equal compress_with_dict's
+    //  * ErrorContext / set_error_callback / log_error / get_last_error / clear_last_error /
+    //    get_detailed_error_message (include/cuda_zstd_types.h:132-156)
+    //  * HybridEngine move construction / assignment, decompress_batch, get_observed_throughput,
+    //    reset_profiling, hybrid_decompress (include/cuda_zstd_hybrid.h:82-83,180-186,229-235,263-268)
+    std::vector<char> db = slurp(dir + "/dict.bin");
+    dictionary::Dictionary dct;
+    dct.raw_content.assign(db.begin(), db.end());
+    for (size_t i = 0; i < n; i++) {
+      fsz[i] = cap;
+      Status st = compress_with_dict(d_in[i], sizes[i], d_out[i], &fsz[i], dct, 3, 0);
+      if (st != Status::SUCCESS) { fprintf(stderr, "compress_with_dict %zu: %s\n", i, status_to_string(st)); return 3; }
+    }
+    std::vector<char> back(in.size());
+    void *d_o;
+    size_t const maxn = std::max<size_t>(*std::max_element(sizes.begin(), sizes.end()), 1);
+    CK(hipMalloc(&d_o, maxn));
+    for (size_t i = 0; i < n; i++) {
+      size_t got = sizes[i];
+      Status st = decompress_with_dict(d_out[i], fsz[i], d_o, &got, dct, 0);
+      if (st != Status::SUCCESS || got != sizes[i]) { fprintf(stderr, "decompress_with_dict %zu: %s\n", i, status_to_string(st)); return 4; }
+      CK(hipMemcpy(back.data() + offs[i], d_o, sizes[i], hipMemcpyDeviceToHost));
+    }
+    dump(dir + "/back.bin", back.data(), back.size());
+    // pre-sized workspace
+    {
+      CompressionConfig cfg = CompressionConfig::from_level(3);
+      CompressionWorkspace w;
+      Status st = allocate_compression_workspace(w, maxn, cfg);
+      if (st != Status::SUCCESS || !w.is_allocated || !w.d_workspace) { fprintf(stderr, "allocate_compression_workspace: %s\n", status_to_string(st)); return 5; }
+      if (allocate_compression_workspace(w, maxn, cfg) != Status::ERROR_INVALID_PARAMETER) { fprintf(stderr, "double allocate accepted\n"); return 5; }
+      ZstdBatchManager m(cfg);
+      if (m.set_dictionary(dct) != Status::SUCCESS) return 5;
+      void *d_f;
+      CK(hipMalloc(&d_f, cap));
+      for (size_t i = 0; i < n; i++) {
+        size_t fs = cap;
+        st = m.compress(d_in[i], sizes[i], d_f, &fs, w.d_workspace, w.total_size, nullptr, 0, 0);
+        std::vector<char> a(fs), b(fsz[i]);
+        CK(hipMemcpy(a.data(), d_f, fs, hipMemcpyDeviceToHost));
+        CK(hipMemcpy(b.data(), d_out[i], fsz[i], hipMemcpyDeviceToHost));
+        if (st != Status::SUCCESS || a != b) { fprintf(stderr, "workspace compress %zu: %s\n", i, status_to_string(st)); return 5; }
+      }
+      CK(hipFree(d_f));
+      if (free_compression_workspace(w) != Status::SUCCESS || w.is_allocated || w.d_workspace) { fprintf(stderr, "free_compression_workspace\n"); return 5; }
+    }
+    // error API
+    {
+      static int calls = 0;
+      static Status seen = Status::SUCCESS;
+      clear_last_error();
+      set_error_callback([](const ErrorContext &c) { calls++; seen = c.status; });
+      size_t os = cap;
+      Status st = compress_simple(nullptr, 100, d_out[0], &os, 3, 0);
+      ErrorContext const e = get_last_error();
+      if (st != Status::ERROR_INVALID_PARAMETER || e.status != st || calls != 1 || seen != st || !e.function) {
+        fprintf(stderr, "error API: st %s last %s calls %d\n", status_to_string(st), status_to_string(e.status), calls);
+        return 6;
+      }
+      std::string const msg = get_detailed_error_message(e);
+      if (msg.find(status_to_string(st)) == std::string::npos) { fprintf(stderr, "detailed message: %s\n", msg.c_str()); return 6; }
+      log_error(ErrorContext(Status::ERROR_TIMEOUT, "f.cpp", 7, "fn", "note"));
+      if (get_last_error().status != Status::ERROR_TIMEOUT || calls != 2) return 6;
+      if (std::string(get_detailed_error_message(get_last_error())) != "Timeout at f.cpp:7 in fn() - note") {
+        fprintf(stderr, "detailed message: %s\n", get_detailed_error_message(get_last_error()));
+        return 6;
+      }
+      set_error_callback(nullptr);
+      clear_last_error();
+      if (get_last_error().status != Status::SUCCESS) return 6;
+    }
+    // HybridEngine: moved engines keep working; host-buffer batch decompress (libzstd route) and
+    // device-buffer batch decompress (GPU route) of the dictionary-free frames; profiling
+    {
+      HybridConfig hc;
+      hc.enable_profiling = true;
+      HybridEngine e0(hc);
+      HybridEngine e1(std::move(e0));
+      HybridEngine e(HybridConfig{});
+      e = std::move(e1);
+      std::vector<std::vector<char>> hf(n), hb(n);
+      std::vector<const void *> ip(n), dip(n);
+      std::vector<void *> op(n), dop(n);
+      std::vector<size_t> is(n), os(n), dos(n);
+      for (size_t i = 0; i < n; i++) {
+        hf[i].resize(cap);
+        size_t fs = cap;
+        Status st = e.compress(in.data() + offs[i], sizes[i], hf[i].data(), &fs, DataLocation::HOST, DataLocation::HOST, nullptr, 0);
+        if (st != Status::SUCCESS) { fprintf(stderr, "hybrid compress %zu: %s\n", i, status_to_string(st)); return 7; }
+        hf[i].resize(fs);
+        hb[i].resize(sizes[i] + 1);
+        ip[i] = hf[i].data(); is[i] = fs; op[i] = hb[i].data(); os[i] = sizes[i] + 1;
+        fsz[i] = cap;
+        st = e.compress(d_in[i], sizes[i], d_out[i], &fsz[i], DataLocation::DEVICE, DataLocation::DEVICE, nullptr, 0);
+        if (st != Status::SUCCESS) { fprintf(stderr, "hybrid device compress %zu: %s\n", i, status_to_string(st)); return 7; }
+        dip[i] = d_out[i];
+        CK(hipMalloc(&dop[i], sizes[i] + 1));
+        dos[i] = sizes[i] + 1;
+      }
+      std::vector<BatchRoutingResult> rr(n), dr(n);
+      Status st = e.decompress_batch(ip.data(), is.data(), op.data(), os.data(), n, DataLocation::HOST, DataLocation::HOST, rr.data(), 0);
+      if (st != Status::SUCCESS) { fprintf(stderr, "hybrid decompress_batch: %s\n", status_to_string(st)); return 7; }
+      st = e.decompress_batch(dip.data(), fsz.data(), dop.data(), dos.data(), n, DataLocation::DEVICE, DataLocation::DEVICE, dr.data(), 0);
+      if (st != Status::SUCCESS) { fprintf(stderr, "hybrid device decompress_batch: %s\n", status_to_string(st)); return 7; }
+      for (size_t i = 0; i < n; i++) {
+        std::vector<char> g(sizes[i]);
+        CK(hipMemcpy(g.data(), dop[i], sizes[i], hipMemcpyDeviceToHost));
+        if (os[i] != sizes[i] || memcmp(hb[i].data(), in.data() + offs[i], sizes[i]) || rr[i].backend_used != ExecutionBackend::CPU_LIBZSTD ||
+            rr[i].output_size != sizes[i] || dos[i] != sizes[i] || memcmp(g.data(), in.data() + offs[i], sizes[i]) ||
+            dr[i].backend_used != ExecutionBackend::GPU_KERNELS) {
+          fprintf(stderr, "hybrid decompress_batch item %zu\n", i);
+          return 7;
+        }
+        CK(hipFree(dop[i]));
+      }
+      if (e.get_observed_throughput(ExecutionBackend::CPU_LIBZSTD, true) <= 0 || e.get_observed_throughput(ExecutionBackend::GPU_KERNELS, true) <= 0 ||
+          e.get_observed_throughput(ExecutionBackend::CPU_LIBZSTD, false) <= 0 || e.get_observed_throughput(ExecutionBackend::GPU_KERNELS, false) <= 0) {
+        fprintf(stderr, "no throughput samples\n");
+        return 7;
+      }
+      e.reset_profiling();
+      if (e.get_observed_throughput(ExecutionBackend::GPU_KERNELS, true) != 0.0) return 7;
+      size_t got = sizes[0] + 1;
+      std::vector<char> g(got);
+      HybridResult res;
+      st = hybrid_decompress(hf[0].data(), hf[0].size(), g.data(), &got, DataLocation::HOST, DataLocation::HOST, &res, 0);
+      if (st != Status::SUCCESS || got != sizes[0] || memcmp(g.data(), in.data(), sizes[0])) { fprintf(stderr, "hybrid_decompress: %s\n", status_to_string(st)); return 7; }
+      // the device frames of the GPU route are what frames.bin carries below: recompress with
+      // the dictionary so frames.bin holds compress_with_dict's output as documented
+      for (size_t i = 0; i < n; i++) {
+        fsz[i] = cap;
+        if (compress_with_dict(d_in[i], sizes[i], d_out[i], &fsz[i], dct, 3, 0) != Status::SUCCESS) return 3;
+      }
+    }
   } else {
     return 1;
   }

