@@ -21,13 +21,15 @@ the committed rocprofv3 SQ summary (profiles/*_sq_summary.json); `limiter` compa
 two fractions.  cpu_baseline = libzstd level 3 (the reference's own CPU route,
 src/cuda_zstd_manager.cu:1604-1668) through tools/libcpubench.so: one ZSTD_CCtx per
 POSIX thread, ZSTD_compressCCtx over the same chunks, a 1, 2, 4, ... thread curve up to
-the box's host share (--cpu-threads all: every thread of the affinity).  vs_baseline = GPU
-GB/s / the all-core libzstd figure (the north star's ">= 10x all-core" ratio; BASELINE.md
-publishes no GPU number for this metric): measured when the process may use every core,
-otherwise the larger of the measured rate and the 1-thread rate x physical cores x the
-measured parallel efficiency (the conservative denominator).
-Extra legs at N=1 (not `value`): C3 on uniform random bytes, C2 (one 64 MiB frame through
-ZstdManager::compress), and GPU decompression of the C3 frames.
+the box's host share (--cpu-threads all: every thread of the affinity).  vs_baseline is null:
+BASELINE.md publishes no number for this metric.  cpu_baseline.gpu_speedup gives GPU GB/s over
+the measured thread count, one thread and all cores (the north star's ">= 10x all-core" ratio,
+also the line's `vs_cpu_all_core`): all-core is measured when the process may use every core,
+otherwise the larger of the measured rate and the 1-thread rate x physical cores x the measured
+parallel efficiency (the conservative denominator).
+Extra legs at N=1 (not `value`): C3 on uniform random bytes and C2 (one 64 MiB frame through
+ZstdManager::compress), each with its roofline and libzstd beside it, and GPU decompression of
+the C3 frames.
 """
 import argparse
 import ctypes
@@ -119,7 +121,7 @@ def _cpubench():
     return L
 
 
-def cpu_run(mode, data, nchunks, threads, passes=5, sizes=None, slot=0):
+def cpu_run(mode, data, nchunks, threads, passes=5, sizes=None, slot=0, chunk=CHUNK):
     """Median wall time of `passes` sweeps over nchunks chunks (after one warm-up sweep)."""
     L = _cpubench()
     if L is None:
@@ -127,7 +129,7 @@ def cpu_run(mode, data, nchunks, threads, passes=5, sizes=None, slot=0):
     secs = (ctypes.c_double * (passes + 1))()
     outb = ctypes.c_size_t()
     sz = sizes.ctypes.data if sizes is not None else None
-    rc = L.cpub_run(mode, data.ctypes.data, sz, nchunks, CHUNK, slot, 3, threads, passes + 1, secs, ctypes.byref(outb))
+    rc = L.cpub_run(mode, data.ctypes.data, sz, nchunks, chunk, slot, 3, threads, passes + 1, secs, ctypes.byref(outb))
     if rc:
         return None
     t = statistics.median(list(secs)[1:])
@@ -164,6 +166,7 @@ def cpu_baseline(host, threads, gpu_gbs):
     return {"value": round(gm, 3), "unit": "GB/s", "cores": threads, "kind": "reference",
             "sample": f"libzstd {r['version']} ZSTD_compressCCtx level 3 (one CCtx per POSIX thread, tools/cpubench.c) over the same 64 KiB "
                       f"chunks: {threads} threads x {n} chunks ({n * CHUNK >> 20} MiB), median of 5 sweeps; ratio {n * CHUNK / r['out_bytes']:.4f}",
+            "ratio": round(n * CHUNK / r["out_bytes"], 4),
             "single_thread": {"value": g1, "unit": "GB/s", "sample": f"{curve[0]['chunks']} chunks, median of 5 sweeps"},
             "thread_curve": curve,
             "host": info,
@@ -232,6 +235,18 @@ class Batch:
             self.bc.compress_async(self.in_ptrs, self.in_sizes, CHUNK, self.out_ptrs, self.out_sizes, self.status, self.temp, self.stream)
 
 
+def leg_roofline(per_launch_bytes, kms, launches):
+    """Roofline of a leg's dominant kernel (K1 or the entropy stage), as the main line's: algorithmic
+    bytes per launch (input + compressed output) over its average HIP-event duration on the launch
+    stream (cuda_zstd.profile_*); no PMC traffic is taken for the legs."""
+    k1, k2 = kms[0] / max(launches, 1), kms[1] / max(launches, 1)
+    dom, ms = ("zh_lz_kernel", k1) if k1 >= k2 else ("entropy_stage", k2)
+    ach = per_launch_bytes / (ms / 1e3) / 1e9 if ms > 0 else 0.0
+    return {"kernel": dom, "bound": "hbm" if ach / HBM_PEAK_GBS > 0.5 else "issue", "achieved": round(ach, 2), "peak": HBM_PEAK_GBS,
+            "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 5), "traffic": None, "algorithmic_bytes_per_launch": int(per_launch_bytes),
+            "kernel_ms": {"zh_lz_kernel": round(k1, 3), "entropy_stage": round(k2, 3)}}
+
+
 def timed_events(fn, steps):
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record()
@@ -242,25 +257,40 @@ def timed_events(fn, steps):
     return e0.elapsed_time(e1) / steps
 
 
-def random_leg(dev, steps):
-    """C3 on uniform random bytes (seed 0x5EED0004): raw-block fallbacks everywhere."""
-    b = Batch(gen_chunks("random", CHUNKS, 0), dev)
+def random_leg(dev, steps, threads):
+    """C3 on uniform random bytes (seed 0x5EED0004): every block dies at K1's incompressibility
+    probe and goes out raw.  Roofline of its dominant kernel and libzstd on the same chunks."""
+    import cuda_zstd
+
+    host = gen_chunks("random", CHUNKS, 0)
+    b = Batch(host, dev)
     b.compress()
     torch.cuda.synchronize()
+    cuda_zstd.profile_enable(True)
     ms = timed_events(b.compress, steps)
+    cuda_zstd.profile_enable(False)
+    launches, kms = cuda_zstd.profile_collect()
     ok = int((b.status != 0).sum().item()) == 0
     comp = int(b.out_sizes.sum().item())
-    res = {"value": round(CHUNKS * CHUNK / (ms / 1e3) / 1e9, 3), "unit": "GB/s", "ms_per_step": round(ms, 3), "ratio": round(CHUNKS * CHUNK / comp, 4),
-           "status_ok": ok, "workload": "C3-random: 16384 x 64 KiB uniform random chunks, level 3"}
+    gbs = CHUNKS * CHUNK / (ms / 1e3) / 1e9
+    res = {"value": round(gbs, 3), "unit": "GB/s", "ms_per_step": round(ms, 3), "ratio": round(CHUNKS * CHUNK / comp, 4),
+           "status_ok": ok, "workload": "C3-random: 16384 x 64 KiB uniform random chunks, level 3",
+           "roofline": leg_roofline(CHUNKS * CHUNK + comp, kms, launches)}
+    verified = libzstd_roundtrip(b.d_out.cpu().numpy(), b.out_sizes.cpu().numpy(), b.slot, host)
+    res["libzstd_verified"] = verified
     del b
     torch.cuda.empty_cache()
+    if threads:
+        res["cpu_baseline"] = cpu_baseline(host, threads, gbs)
     return res
 
 
-def c2_leg(dev, steps):
+def c2_leg(dev, steps, threads):
     """C2: one 64 MiB buffer (iid over a seeded 16-symbol alphabet) -> one frame through
     ZstdManager::compress (cuda_zstd_compress); libzstd decodes the frame; libzstd level-3
-    ratio of the same buffer beside ours."""
+    ratio of the same buffer beside ours, and libzstd's time for the same single 64 MiB frame
+    (ZSTD_compressCCtx, one thread: one frame is one thread's work in libzstd without its
+    multi-threaded frame mode)."""
     import cuda_zstd
     import zh_testlib as T
 
@@ -269,10 +299,20 @@ def c2_leg(dev, steps):
     m = cuda_zstd.Manager(3)
     f = m.compress(d)
     torch.cuda.synchronize()
+    cuda_zstd.profile_enable(True)
     ms = timed_events(lambda: m.compress(d), steps)
+    cuda_zstd.profile_enable(False)
+    launches, kms = cuda_zstd.profile_collect()
     frame = f.cpu().numpy().tobytes()
     res = {"value": round(C2_BYTES / (ms / 1e3) / 1e9, 3), "unit": "GB/s", "ms_per_call": round(ms, 3), "ratio": round(C2_BYTES / len(frame), 4),
-           "workload": "C2: 64 MiB iid 16-symbol buffer, one frame (2048 x 32 KiB blocks, each matched against the 32 KiB before it), ZstdManager::compress incl. its host sync"}
+           "workload": "C2: 64 MiB iid 16-symbol buffer, one frame (2048 x 32 KiB blocks, each matched against the 32 KiB before it), ZstdManager::compress incl. its host sync",
+           "roofline": leg_roofline(C2_BYTES + len(frame), kms, launches)}
+    if threads:
+        r = cpu_run(0, host, 1, 1, passes=3, chunk=C2_BYTES)
+        if r:
+            res["cpu_baseline"] = {"value": round(C2_BYTES / r["seconds"] / 1e9, 3), "unit": "GB/s", "cores": 1, "kind": "reference",
+                                   "sample": f"libzstd {r['version']} ZSTD_compressCCtx level 3 of the same 64 MiB buffer as one frame, "
+                                             "median of 3 after a warm-up", "ratio": round(C2_BYTES / r["out_bytes"], 4)}
     z = T.zstd()
     if z is not None:
         res["libzstd_verified"] = T.zstd_decompress(frame, C2_BYTES) == host.tobytes()
@@ -473,10 +513,18 @@ def main():
     if not args.no_decompress:
         dec = decompress_leg(b, min(args.steps, 5), world)
 
+    aff = len(os.sched_getaffinity(0))
+    if args.cpu_threads == "all":
+        threads = aff
+    elif args.cpu_threads:
+        threads = max(1, min(aff, int(args.cpu_threads)))
+    else:
+        threads = host_share()
     legs = {}
     if world == 1 and not args.no_legs and args.dataset == "mix" and args.chunks == CHUNKS:
-        legs["c3_random"] = random_leg(dev, 5)
-        legs["c2_64mib"] = c2_leg(dev, 5)
+        leg_threads = None if args.no_cpu_baseline else threads
+        legs["c3_random"] = random_leg(dev, 5, leg_threads)
+        legs["c2_64mib"] = c2_leg(dev, 5, leg_threads)
 
     if rank == 0:
         total_in = float(n_total * CHUNK)
@@ -524,13 +572,6 @@ def main():
         }
         if gather:
             line["payload_gather"] = gather
-        aff = len(os.sched_getaffinity(0))
-        if args.cpu_threads == "all":
-            threads = aff
-        elif args.cpu_threads:
-            threads = max(1, min(aff, int(args.cpu_threads)))
-        else:
-            threads = host_share()
         if dec is not None:
             if not args.no_cpu_baseline and world == 1:
                 dec["cpu_baseline"] = cpu_decompress_baseline(b, threads)
@@ -540,11 +581,10 @@ def main():
         if not args.no_cpu_baseline and world == 1:
             cb = cpu_baseline(host, threads, gbs)
             line["cpu_baseline"] = cb
+            # vs_baseline stays null: BASELINE.md publishes no number for this metric (the driver
+            # contract); the GPU / libzstd ratios are cpu_baseline.gpu_speedup
             if cb:
-                line["vs_baseline"] = cb["gpu_speedup"]["vs_all_core"]
-                line["vs_baseline_basis"] = (f"GPU / all-core libzstd L3 ({cb['all_core']['value']} GB/s, "
-                                             f"{'measured' if cb['all_core']['measured'] else 'extrapolated from the measured thread curve'}); "
-                                             "BASELINE.md publishes no GPU number for this metric")
+                line["vs_cpu_all_core"] = cb["gpu_speedup"]["vs_all_core"]
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()

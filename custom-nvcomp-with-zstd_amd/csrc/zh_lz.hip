@@ -323,6 +323,19 @@ __device__ __forceinline__ bool skip_window(const u32 *misc, u32 k, u32 kskip0) 
   return k >= kskip0 && (u32)__builtin_amdgcn_readfirstlane(__atomic_load_n(&misc[MISC_NM + ((k - 3) & 3)], __ATOMIC_RELAXED)) == 0;
 }
 
+// Incompressibility probe (oracle orc_lz_parse_pre): at the top of loop step kprobe (the
+// parses of the ZH_PROBE_WINDOWS probe windows from the one holding `pre` are done) a block
+// whose parse took no match in them stops -- it takes no sequences, every byte is a literal.
+// Wave-uniform; every wave (inserters too) evaluates it at the same step, before barrier P.
+__device__ __forceinline__ bool probe_dead(const u32 *misc, u32 k, u32 kprobe) {
+  if (k != kprobe) return false;
+  u32 m = 0;
+#pragma unroll
+  for (u32 j = 1; j <= ZH_PROBE_WINDOWS; j++) m |= __atomic_load_n(&misc[MISC_NM + ((k - 1 - j) & 3)], __ATOMIC_RELAXED);
+  return (u32)__builtin_amdgcn_readfirstlane(m) == 0;
+}
+static_assert(ZH_PROBE_WINDOWS >= 1 && ZH_PROBE_WINDOWS <= 3, "probe windows fit the match-count ring");
+
 // Dump an inserter's candidates into its half of the cinfo words (LONG: low half).
 template <bool LONG, u32 NT>
 __device__ __forceinline__ void dump_window(u8 *ci8, u32 lane_, const u32 (&creg)[NCR], u32 cwe) {
@@ -637,7 +650,7 @@ __device__ __forceinline__ void seg_walk(const u32 *ci, u32 tmk, u32 S, u32 SE, 
 constexpr u32 WIN_BARRIERS = 1;  // X
 template <bool LONG>
 __device__ __forceinline__ void inserter_loop(const u32 *in32, u16 *T, u8 *ci8, u32 *misc_, u32 n, u32 lim, u32 lane, u32 *dbg, u32 wstart,
-                                              u32 pmin, u32 span_s, u32 span_e, u32 kskip0) {
+                                              u32 pmin, u32 span_s, u32 span_e, u32 kskip0, u32 kprobe) {
   u32 creg[NCR];
   u32 cwe = 0;
   if (span_s < span_e) insert_span<LONG>(in32, T, span_s, span_e, lane);
@@ -649,6 +662,7 @@ __device__ __forceinline__ void inserter_loop(const u32 *in32, u16 *T, u8 *ci8, 
   u32 const nwin = (n - wstart + ZH_WINDOW - 1) / ZH_WINDOW;
   u32 passed = 0;  // X barriers taken so far
   for (u32 k = 0; k < nwin + 2; k++) {
+    if (probe_dead(misc_, k, kprobe)) break;
     u32 const wsb = wstart + k * ZH_WINDOW;
     if (k < nwin) {
       if (skipc) dump_window<LONG, ZH_SKIP_TILES>(ci8 + (k & 1u) * 4 * CI_WORDS, lane, creg, cwe);
@@ -919,6 +933,10 @@ __device__ __forceinline__ u32 lz_block(const ZhBlockDesc *__restrict__ blocks, 
   u64 *seq_out = ws.seq(b);
   u8 *lit_out = ws.lits(b);
   u32 const lim = n > ZH_HASH_READ ? n - ZH_HASH_READ : 0;
+  // the probe's step: the oracle checks once the parse of windows [a0, a0 + ZH_PROBE_WINDOWS) is
+  // done, when the block has a window past them (windows counted up to lim, as the oracle does)
+  u32 const a0 = pre / ZH_WINDOW, nwl = (lim + ZH_WINDOW - 1) / ZH_WINDOW;
+  u32 const kprobe = a0 + ZH_PROBE_WINDOWS + 1 <= nwl ? a0 + ZH_PROBE_WINDOWS + 1 - wstart / ZH_WINDOW : ~0u;
   u32 nseq_tot = 0, nlit_tot = 0, e_in = pre;
   // ---- inserter waves: their own loop with the same barrier sequence as the workers'
   // (separate code, so their registers never add to the workers' pressure)
@@ -928,8 +946,8 @@ __device__ __forceinline__ u32 lz_block(const ZhBlockDesc *__restrict__ blocks, 
     // gate the workers' next window, so they take priority (MI355X_MICROARCH.md, "VALU issue
     // is arbitrated ... by priority, then age").
     __builtin_amdgcn_s_setprio(2);
-    if (tid < INS_TID + 64) inserter_loop<true>(in32, TL, ci8, misc, n, lim, lane, ws.dbg(b), wstart, pmin, span_s, span_e, kskip0);
-    else inserter_loop<false>(in32, TS, ci8, misc, n, lim, lane, ws.dbg(b), wstart, pmin, span_s, span_e, kskip0);
+    if (tid < INS_TID + 64) inserter_loop<true>(in32, TL, ci8, misc, n, lim, lane, ws.dbg(b), wstart, pmin, span_s, span_e, kskip0, kprobe);
+    else inserter_loop<false>(in32, TS, ci8, misc, n, lim, lane, ws.dbg(b), wstart, pmin, span_s, span_e, kskip0, kprobe);
     __builtin_amdgcn_s_setprio(0);
     return next_b;
   }
@@ -951,7 +969,12 @@ __device__ __forceinline__ u32 lz_block(const ZhBlockDesc *__restrict__ blocks, 
   //   X
   //   phase B  take decisions at window k's span tops (each wave its own), the literals of
   //            window k - 1 (lanes = positions, all worker waves)
+  bool dead = false;
   for (u32 k = 0; k < nwin + 2; k++) {
+    if (probe_dead(misc, k, kprobe)) {
+      dead = true;
+      break;
+    }
     u32 const wsb = wstart + k * ZH_WINDOW;
     u32 const we = min(wsb + ZH_WINDOW, n);
     u32 const kb = k & 1u;
@@ -1113,7 +1136,26 @@ __device__ __forceinline__ u32 lz_block(const ZhBlockDesc *__restrict__ blocks, 
     }
     ZH_STAMP(st_E);
   }
-  if (tid == 0) { meta[0] = nseq_tot; meta[1] = nlit_tot; meta[2] = 0; }
+  if (dead) {
+    // the probe found no match: no sequences, the whole block is literals (K2 decides Huffman /
+    // raw / RLE literals as for any block); the block's bytes go out of LDS in 16-B stores
+    u32 const nv = (d.n + 15) >> 4, sh = pre & 3;
+    const u32 *const src32 = in32 + (pre >> 2);
+    for (u32 i = tid_; i < nv; i += INS_TID) {
+      u32 w[5];
+#pragma unroll
+      for (u32 k = 0; k < 5; k++) w[k] = src32[4 * i + k];
+      uint4 v;
+      v.x = __builtin_amdgcn_alignbyte(w[1], w[0], sh);
+      v.y = __builtin_amdgcn_alignbyte(w[2], w[1], sh);
+      v.z = __builtin_amdgcn_alignbyte(w[3], w[2], sh);
+      v.w = __builtin_amdgcn_alignbyte(w[4], w[3], sh);
+      ((uint4 *)lit_out)[i] = v;
+    }
+    nseq_tot = 0;
+    nlit_tot = d.n;
+  }
+  if (tid_ == 0) { meta[0] = nseq_tot; meta[1] = nlit_tot; meta[2] = 0; }
 #ifdef ZH_STAMPS
   if (tid == 0) {
     u32 *dbg = ws.dbg(b);

@@ -29,6 +29,9 @@
 #define ZH_TILE 128                 /* hash insertion granularity (positions) */
 #define ZH_WINDOW 2048              /* parse window (positions); catch-up stays inside one */
 #define ZH_SKIP_TILES 2             /* tiles a window searches after a window without matches (miss skip) */
+#ifndef ZH_PROBE_WINDOWS
+#define ZH_PROBE_WINDOWS 2          /* a block whose parse takes no match in its first windows is all literals */
+#endif
 #define ZH_HASH_LOG_LONG 14         /* 8-byte hash table: 2^14 u16 entries */
 #define ZH_HASH_LOG_SHORT 14        /* 5-byte hash table: 2^14 u16 entries */
 #define ZH_HASH_READ 8              /* bytes read per hashed position */
@@ -52,10 +55,15 @@
  * longest of the first ZH_DEEP_DEPTH(level) chain candidates within ZH_DEEP_MAXOFF (>=
  * ZH_MIN_MATCH_SHORT bytes, capped at ZH_MAX_MATCH, nearest on ties); LAZY2 parse on those
  * matches, no catch-up. */
-#define ZH_DEEP_LEVEL 9
+/* Levels 5-8 take the deep matcher at a smaller depth (the reference's level table gives them
+ * 4-32 search steps, src/cuda_zstd_types.cpp:147-210): oracle on the C3 mix (256 chunks; libzstd
+ * at that level in brackets): depth 4 2.810 (L5 2.817), 8 2.847 (L6 2.871), 16 2.881 (L7 2.890),
+ * 32 2.910 (L8 2.923, L9 2.950).  Levels 1-4 run the dual-hash K1 (level 3's parse: 2.796, libzstd
+ * L3/L4 2.791). */
+#define ZH_DEEP_LEVEL 5
 #define ZH_DEEP_PRE 65536
 #define ZH_DEEP_MAXOFF 65535       /* links stored as u16 distances (zh_lz_deep.hip) are exact */
-#define ZH_DEEP_DEPTH(level) ((level) <= 9 ? 32 : (level) == 10 ? 64 : 128)
+#define ZH_DEEP_DEPTH(level) ((level) <= 5 ? 4 : (level) == 6 ? 8 : (level) == 7 ? 16 : (level) <= 9 ? 32 : (level) == 10 ? 64 : 128)
 #define ZH_COMPRESS_LITERALS_SIZE_MIN 63
 #define ZH_LONGNBSEQ 0x7F00
 #define ZH_MAGIC 0xFD2FB528u

@@ -942,6 +942,19 @@ size_t orc_lz_parse_pre(const u8 *src, u32 pre, u32 n, orc_seq_t *seq, u32 *last
       int const skip = a >= a0 + 3 && mcount[a - 3] == 0;
       match_info_tiles(src, n, t0, t1, skip ? t0 + ZH_SKIP_TILES * ZH_TILE : 0xFFFFFFFFu, len, off);
     }
+    /* incompressibility probe: once the parse of the probe windows [a0, a0 + ZH_PROBE_WINDOWS)
+     * is done (in the iteration after the one that inserted window a0 + ZH_PROBE_WINDOWS) and
+     * it took no match there, the block takes no sequences at all -- the whole block is
+     * literals (K1 stops; K2 reads them from the source, orc_compress_block_pre) */
+    if (a == a0 + ZH_PROBE_WINDOWS + 1 && a <= nwin) {
+      u32 m = 0;
+      for (u32 j = a0; j < a0 + ZH_PROBE_WINDOWS; j++) m += mcount[j];
+      if (m == 0) {
+        ns = 0;
+        anchor = pre;
+        break;
+      }
+    }
     /* the parse of every window before a (its lookahead p + 1, p + 2 is in window a's first tile) */
     u32 const pe = a < nwin ? a * ZH_WINDOW : lim;
     while (p < lim && p < pe) {

@@ -140,6 +140,32 @@ def test_k1_miss_skip_transitions_vs_oracle():
     _compare(datas, names)
 
 
+def test_k1_probe_vs_oracle():
+    """The incompressibility probe (ZH_PROBE_WINDOWS, oracle orc_lz_parse_pre): a block whose
+    parse takes no match in its first windows takes no sequences at all.  Blocks that die at the
+    probe, blocks whose probe windows just reach compressible bytes, text with a random stretch
+    after the probe (the miss skip, not the probe), and short blocks with no window past the probe."""
+    rng = np.random.default_rng(12)
+    text = T.gen(T.DG_TEXT, 1, 0x5EED0019, BLOCK)
+    rnd = rng.integers(0, 256, BLOCK, dtype=np.uint8)
+    W = 2048
+    datas, names = [], []
+
+    def add(nm, d):
+        names.append(nm)
+        datas.append(np.ascontiguousarray(d, dtype=np.uint8))
+
+    for cut in (W - 1, 2 * W - 200, 2 * W, 2 * W + 1, 3 * W):
+        add(f"rand{cut}+text", np.concatenate([rnd[:cut], text[:BLOCK - cut]]))
+    add("text4k+rand+text", np.concatenate([text[:4096], rnd[:40960], text[4096:24576]]))
+    half = rnd[:2 * W].copy()
+    half[W + 100:W + 400] = half[100:400]  # one repeat inside the probe windows
+    add("rand+repeat_in_probe", np.concatenate([half, rnd[2 * W:]]))
+    for n in (2 * W + 8, 2 * W + 9, 3 * W + 8, 3 * W + 9, 5000):
+        add(f"rand_{n}", rnd[:n])
+    _compare(datas, names)
+
+
 def test_k1_special_and_ragged_vs_oracle():
     items = T.special_inputs()
     names = sorted(k for k in items if 0 < len(items[k]) <= BLOCK)

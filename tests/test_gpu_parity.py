@@ -267,11 +267,12 @@ def test_full_size_blocks_match_libzstd(torch_cuda, mgr):
         assert fr[hs:].hex() == c["libzstd_block"], c["name"]
 
 
-@pytest.mark.parametrize("level", [9, 19])
+@pytest.mark.parametrize("level", [5, 6, 7, 8, 9, 19])
 def test_deep_levels_match_oracle(torch_cuda, level):
-    """Levels >= 9 run the deep chain matcher (zh_lz_deep_kernel: exact hash chains, the level's
-    search depth, LAZY2 parse): frames equal the oracle's at that level and
-    decode with libzstd; ragged, multi-block (history) and RLE sizes included."""
+    """Levels >= ZH_DEEP_LEVEL (5) run the deep chain matcher (zh_lz_deep_kernel: exact hash
+    chains, the level's search depth 4 / 8 / 16 / 32 / .. 128, LAZY2 parse):
+    frames equal the oracle's at that level and decode with libzstd; ragged, multi-block
+    (history) and RLE sizes included."""
     import cuda_zstd
 
     m = cuda_zstd.Manager(level)
@@ -286,9 +287,9 @@ def test_deep_levels_match_oracle(torch_cuda, level):
 
 
 def test_deep_concurrent_streams(torch_cuda):
-    """Two level-9 batches enqueued on two streams without a host sync between them: the deep
-    matcher's library-held scratch slots are shared per device, so its launches are ordered by an
-    event (zh_lz_deep.hip lz_deep_launch); both batches' frames equal the oracle's."""
+    """Two level-9 batches enqueued on two streams without a host sync between them: each call's
+    deep-matcher scratch slots live in its own workspace (ZhWorkspace::deep_slots), so the
+    launches run concurrently with nothing shared; both batches' frames equal the oracle's."""
     import cuda_zstd
 
     torch = torch_cuda
