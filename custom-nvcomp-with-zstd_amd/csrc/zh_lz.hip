@@ -4,8 +4,10 @@
 // build_sequences_gpu_kernel<<<1,1>>> (src/lz77_parallel.cu:26-70, 177-268)
 // and the literal gather kernels (src/cuda_zstd_manager.cu:602-723).
 // Output is identical to oracle/zstd_oracle.c orc_lz_parse_pre (tile-lagged hash
-// insertion, longer of long/short candidate, greedy + lazy-1 (or LAZY2) parse, catch-up,
-// window-granular miss skip).
+// insertion, longer of long/short candidate, greedy + lazy-1 parse, catch-up, window-granular
+// miss skip, incompressibility probe).  Three instantiations by level (ZH_K1_MODE): mode 0 (levels
+// 3-4) both tables + the lazy-1 check; mode 1 (level 2) the short table only; mode 2 (level 1) the
+// short table only, greedy -- the long inserter wave then only keeps the step barriers.
 //
 // One persistent workgroup of 1024 threads (16 wave64, one workgroup per CU), blocks taken
 // from a device counter, everything in LDS:
@@ -80,11 +82,10 @@ __device__ __forceinline__ u32 cidx(u32 i) { return i; }
 // overlaps the lengths of window k + 1)
 constexpr u32 OFF_HM = OFF_CI + 2 * 4 * CI_WORDS;    // per buffer u64 per round: take masks (see span_lengths)
 constexpr u32 OFF_SEGM = OFF_HM + 2 * 8 * NROUND;    // per window parity, per walk segment (u32 each):
-constexpr u32 SEGM_WALK_LIT = 0, SEGM_MATCH = 1, SEGM_LIT = 2, SEGM_END = 3;  // the walk's literal bits, its
-// match starts, the literal bits left after catch-up, the end of the segment's last match
-__device__ __forceinline__ u32 segm(u32 par, u32 kind) { return (4 * par + kind) * NSEG; }
+// the literal bits left after catch-up
+__device__ __forceinline__ u32 segm(u32 par) { return par * NSEG; }
 constexpr u32 ML_CAP = ((ZH_WINDOW + ZH_MIN_MATCH_SHORT - 1) / ZH_MIN_MATCH_SHORT + 12 + 3) & ~3u;  // matches per window
-constexpr u32 OFF_ML = OFF_SEGM + 4 * 8 * NSEG;      // per window parity: the window's matches in order (u64,
+constexpr u32 OFF_ML = OFF_SEGM + 4 * 2 * NSEG;      // per window parity: the window's matches in order (u64,
                                                      // ML_* fields) for the records one step later
 constexpr u32 XQ_CAP = 192;                          // chain-end queue entries per worker wave
 constexpr u32 OFF_XQ = OFF_ML + 2 * 8 * ML_CAP;      // u16 per entry: window index | S << 15
@@ -285,7 +286,7 @@ __device__ __forceinline__ void insert_window(const u32 *in32, u16 *T, u32 wsb, 
   // the next window's first position (lazy rule at this window's end): looked up
   // after all of this window's tiles, before any of the next window's
   cwe = 0;
-  if (lane < 2 && we + lane < lim) {  // (lane 1: we + 1, the second lookahead of LAZY2)
+  if (lane < 2 && we + lane < lim) {  // (lane 1: we + 1, kept for the span-top rule)
     u32 lo, hi;
     ld64u(in32, we + lane, lo, hi);
     cwe = T[hash_of<LONG>(lo, hi)];
@@ -365,22 +366,16 @@ __device__ __forceinline__ u32 bit_range32(u32 a, u32 b) {
 
 // ---- the parse step rule ---------------------------------------------------------------------
 // Match info words: off << 8 | len (off < 2^16).
-// Parse cost of a match: libzstd's lazy "gain" (4 per byte, minus the offset's bit length)
-__device__ __forceinline__ int match_gain(u32 inf) {
-  return (inf & 255u) ? 4 * (int)(inf & 255u) - (31 - (int)__builtin_clz(((inf >> 8) & 0xFFFFu) + 1u)) : -1000;
-}
 // The serial parse at a position with a match (inf) takes it unless the match at the next
-// position is longer (levels < 9) -- or, LAZY2 (levels >= 9), unless the match at
-// the next position gains more than 4 over it or the one after more than 7 (libzstd
-// ZSTD_compressBlock_lazy_generic, depth 2).
-template <bool LAZY2>
-__device__ __forceinline__ bool take_rule(u32 inf, u32 inf1, u32 inf2) {
-  if (LAZY2) {
-    int const g0 = match_gain(inf);
-    return match_gain(inf1) <= g0 + 4 && match_gain(inf2) <= g0 + 7;
-  }
+// position is longer (modes 0, 1: the lazy-1 check of levels 2-4) -- mode 2 (level 1) is greedy.
+template <u32 MODE>
+__device__ __forceinline__ bool take_rule(u32 inf, u32 inf1) {
+  if (MODE == 2) return true;
   return (inf1 & 255u) <= (inf & 255u);
 }
+// modes 1, 2 search the short table only
+template <u32 MODE>
+constexpr bool two_tables() { return MODE == 0; }
 
 // The 4 bytes in[a-4, a) (a >= 1; bytes before the buffer start read as 0s shifted out)
 __device__ __forceinline__ u32 ld4_before(const u32 *in32, u32 a) {
@@ -412,17 +407,6 @@ __device__ __forceinline__ u32 rounds_of(u32 w) {
 #endif
 }
 
-// Length of position p's candidate from the chain structure: T = ballot of the chain ends
-// (lanes whose lcp is their own: fewer than 8 bytes, or the next position does not continue
-// the candidate), e = their lcp.  A lane inside a chain is 1 + its successor's: the distance
-// to its chain end plus that end's lcp; a chain running past the round takes the carry.
-__device__ __forceinline__ u32 chain_lcp(u64 T, u32 e, u32 carry, u32 lane) {
-  u64 const rest = T >> lane;
-  u32 const q = rest ? ctz64(rest) : 64u - lane;
-  u32 const v = bperm(e, min(lane + q, 63u));
-  return min((u32)ZH_MAX_MATCH, q + (rest ? v : carry));
-}
-
 // Pass B: extend queue entries [0, k) (k <= 64) of xq, one per lane; the extension (<= 64)
 // goes to byte 0 (long candidate) or byte 2 (short) of the position's cinfo word.
 __device__ __forceinline__ void xq_flush(const u32 *in32, u32 *ci, const u16 *xq, u32 k, u32 wsb, u32 lane) {
@@ -442,12 +426,13 @@ enum : u32 { LF_FL = 1u << 8, LF_FS = 1u << 9, LF_XL = 1u << 10, LF_XS = 1u << 1
 // orc_lz_match_info: lcp capped at ZH_MAX_MATCH and at the block end, long candidates from 8
 // bytes, short from 5, the longer (long on ties).  Then per position whether the parse takes its
 // match if it gets there (take_rule on the next positions' info: DPP within the round, the
-// round above by carry; la1 / la2 = the two positions above the span when it is the window's
+// round above by carry; la1 = the position above the span when it is the window's
 // top one) -> the rounds' take masks tm.  At the top of a span that is not the window's top the next positions
 // belong to another wave: those take bits stay clear until the wave decides them after barrier X.
-template <bool LAZY2>
+template <u32 MODE>
 __device__ __forceinline__ void span_lengths(const u32 *in32, u32 *ci, u64 *tm, u16 *xq, u32 r_lo, u32 r_hi, u32 wsb, u32 we, u32 n, u32 lim,
-                                             u32 lane, bool top, u32 la1, u32 la2) {
+                                             u32 lane, bool top, u32 la1) {
+  constexpr bool TWO = two_tables<MODE>();
   u32 cwr[MAX_RW], flg[MAX_RW];
   // pass A, rounds high to low: a round's candidates, own bytes and candidate bytes are loaded
   // at the top of the round (hoisting every round's loads to the top of the pass was slower:
@@ -460,10 +445,13 @@ __device__ __forceinline__ void span_lengths(const u32 *in32, u32 *ci, u64 *tm, 
     u32 const cw = hv ? cw0 : 0u;
     cwr[k] = cw;
     ld64u(in32, p, olo[k], ohi[k]);
-    u32 const cL = cw & 0xFFFFu, cS = cw >> 16;
+    u32 const cL = TWO ? cw & 0xFFFFu : 0u, cS = cw >> 16;
     u32 const aL = (cL ? cL - 1u : 0u) >> 2, aS = (cS ? cS - 1u : 0u) >> 2;
 #pragma unroll
-    for (u32 t = 0; t < 3; t++) { Lw[k][t] = in32[aL + t]; Sw[k][t] = in32[aS + t]; }
+    for (u32 t = 0; t < 3; t++) {
+      if constexpr (TWO) Lw[k][t] = in32[aL + t];
+      Sw[k][t] = in32[aS + t];
+    }
   };
   u32 ccL = 0, ccS = 0;  // candidates of the position above the round being processed
   u32 nq = 0;            // queued entries (wave-uniform)
@@ -474,14 +462,14 @@ __device__ __forceinline__ void span_lengths(const u32 *in32, u32 *ci, u64 *tm, 
     loadA(k);
     u32 const r = r_hi - 1 - k, i = 64 * r + lane;
     u32 const cw = cwr[k];
-    u32 const cL = cw & 0xFFFFu, cS = cw >> 16;
+    u32 const cL = TWO ? cw & 0xFFFFu : 0u, cS = cw >> 16;
     auto pref = [&](u32 c, const u32 (&w)[3]) {
       u32 const sh = (c ? c - 1u : 0u) & 3u;
       u32 const x = olo[k] ^ __builtin_amdgcn_alignbyte(w[1], w[0], sh), y = ohi[k] ^ __builtin_amdgcn_alignbyte(w[2], w[1], sh);
       u32 const cx = __builtin_ctzg(x, 32), cy = __builtin_ctzg(y, 32);
       return c ? (x ? cx : 32u + cy) >> 3 : 0u;
     };
-    u32 const pL = pref(cL, Lw[k]), pS = pref(cS, Sw[k]);
+    u32 const pL = TWO ? pref(cL, Lw[k]) : 0u, pS = pref(cS, Sw[k]);
     u32 cLn = wave_shl1(cL), cSn = wave_shl1(cS);
     cLn = lane == 63 ? ccL : cLn;
     cSn = lane == 63 ? ccS : cSn;
@@ -493,7 +481,7 @@ __device__ __forceinline__ void span_lengths(const u32 *in32, u32 *ci, u64 *tm, 
     ccL = lane_value(cL, 0);
     ccS = lane_value(cS, 0);
     // queue the chain ends to extend (L then S), flushing 64 at a time from the top
-    u64 const bL = __ballot(xL), bS = __ballot(xS);
+    u64 const bL = TWO ? __ballot(xL) : 0ull, bS = __ballot(xS);
     u32 const rL = __builtin_amdgcn_mbcnt_hi((u32)(bL >> 32), __builtin_amdgcn_mbcnt_lo((u32)bL, 0u));
     u32 const rS = __builtin_amdgcn_mbcnt_hi((u32)(bS >> 32), __builtin_amdgcn_mbcnt_lo((u32)bS, 0u));
     u32 const nL = (u32)__popcll(bL);
@@ -517,23 +505,31 @@ __device__ __forceinline__ void span_lengths(const u32 *in32, u32 *ci, u64 *tm, 
     u32 const pL = f & 15u, pS = (f >> 4) & 15u;
     u32 const eL = (f & LF_XL) ? (ce & 255u) : pL;
     u32 const eS = (f & LF_XS) ? ((ce >> 16) & 255u) : ((f & LF_SL) ? eL : pS);
-    u64 const RL = __ballot(!(f & LF_FL)) >> lane, RS = __ballot(!(f & LF_FS)) >> lane;
-    u32 const qL = RL ? ctz64(RL) : 64u - lane, qS = RS ? ctz64(RS) : 64u - lane;
-    u32 const vL = bperm(eL, min(lane + qL, 63u)), vS = bperm(eS, min(lane + qS, 63u));
-    lLr[k] = RL ? min((u32)ZH_MAX_MATCH, qL + vL) : qL;  // (a chain running past: + carry in C2)
-    lSr[k] = RS ? min((u32)ZH_MAX_MATCH, qS + vS) : qS;
-    runs[k] = (RL ? 0u : 1u) | (RS ? 0u : 2u);
+    u64 const RS = __ballot(!(f & LF_FS)) >> lane;
+    u32 const qS = RS ? ctz64(RS) : 64u - lane;
+    u32 const vS = bperm(eS, min(lane + qS, 63u));
+    lSr[k] = RS ? min((u32)ZH_MAX_MATCH, qS + vS) : qS;  // (a chain running past: + carry in C2)
+    runs[k] = RS ? 0u : 2u;
+    if constexpr (TWO) {
+      u64 const RL = __ballot(!(f & LF_FL)) >> lane;
+      u32 const qL = RL ? ctz64(RL) : 64u - lane;
+      u32 const vL = bperm(eL, min(lane + qL, 63u));
+      lLr[k] = RL ? min((u32)ZH_MAX_MATCH, qL + vL) : qL;
+      runs[k] |= RL ? 0u : 1u;
+    } else {
+      lLr[k] = 0;
+    }
   };
 #pragma unroll
   for (u32 k = 0; k < MAX_RW; k++) c1(k);
   u32 clL = 0, clS = 0;  // lcps of the position above the round
-  u32 cv1 = la1, cv2 = la2;  // infos of the two positions above the round
+  u32 cv1 = la1;         // info of the position above the round
 #pragma unroll
   for (u32 k = 0; k < MAX_RW; k++) {
     if (r_lo + k >= r_hi) continue;
     u32 const r = r_hi - 1 - k, i = 64 * r + lane, p = wsb + i;
     u32 const cw = cwr[k];
-    u32 const cL = cw & 0xFFFFu, cS = cw >> 16;
+    u32 const cL = TWO ? cw & 0xFFFFu : 0u, cS = cw >> 16;
     u32 const lL = (runs[k] & 1u) ? min((u32)ZH_MAX_MATCH, lLr[k] + clL) : lLr[k];
     u32 const lS = (runs[k] & 2u) ? min((u32)ZH_MAX_MATCH, lSr[k] + clS) : lSr[k];
     clL = lane_value(lL, 0);
@@ -547,12 +543,9 @@ __device__ __forceinline__ void span_lengths(const u32 *in32, u32 *ci, u64 *tm, 
     u32 const v = ml ? ((p - (cm - 1u)) << 8) | ml : 0u;
     u32 v1 = wave_shl1(v);
     v1 = lane == 63 ? cv1 : v1;
-    u32 v2 = wave_shl1(v1);
-    v2 = lane == 63 ? cv2 : v2;
     cv1 = lane_value(v, 0);
-    cv2 = lane_value(v, 1);
-    bool const unk = k == 0 && !top && (lane == 63 || (LAZY2 && lane == 62));
-    bool const tk = v != 0 && !unk && take_rule<LAZY2>(v, v1, v2);
+    bool const unk = MODE != 2 && k == 0 && !top && lane == 63;
+    bool const tk = v != 0 && !unk && take_rule<MODE>(v, v1);
     ci[cidx(i)] = v;
     u64 const tb = __ballot(tk);
     if (lane == 0) tm[r] = tb;
@@ -561,9 +554,10 @@ __device__ __forceinline__ void span_lengths(const u32 *in32, u32 *ci, u64 *tm, 
 
 // Match info of one position from scratch (the lookahead positions `we`, `we + 1` of the
 // next window, which the next window's rounds compute again): c = candidate word.
+template <u32 MODE>
 __device__ __forceinline__ u32 info_one(const u32 *in32, u32 p, u32 cw, u32 n, u32 lim, bool act) {
   bool const hv = act && p < lim;
-  u32 const cL = hv ? (cw & 0xFFFFu) : 0u, cS = hv ? (cw >> 16) : 0u;
+  u32 const cL = (hv && two_tables<MODE>()) ? (cw & 0xFFFFu) : 0u, cS = hv ? (cw >> 16) : 0u;
   u32 lo, hi;
   ld64u(in32, hv ? p : 0u, lo, hi);
   u32 const tL = prefix8(in32, cL ? cL - 1u : 0u, lo, hi), tS = prefix8(in32, cS ? cS - 1u : 0u, lo, hi);
@@ -648,6 +642,16 @@ __device__ __forceinline__ void seg_walk(const u32 *ci, u32 tmk, u32 S, u32 SE, 
 // all 14 worker waves have arrived there (an LDS arrival counter), between two tiles, so the
 // insertion spreads over the whole step.
 constexpr u32 WIN_BARRIERS = 1;  // X
+// The long table's wave in modes 1, 2 (the short table only): no insertion, only the step's two
+// barriers (P, X) and the probe exit, so the workgroup's barrier sequence stays the same.
+__device__ __forceinline__ void idle_inserter_loop(u32 *misc_, u32 n, u32 wstart, u32 kprobe) {
+  u32 const nwin = (n - wstart + ZH_WINDOW - 1) / ZH_WINDOW;
+  for (u32 k = 0; k < nwin + 2; k++) {
+    if (probe_dead(misc_, k, kprobe)) break;
+    __syncthreads();  // P
+    __syncthreads();  // X
+  }
+}
 template <bool LONG>
 __device__ __forceinline__ void inserter_loop(const u32 *in32, u16 *T, u8 *ci8, u32 *misc_, u32 n, u32 lim, u32 lane, u32 *dbg, u32 wstart,
                                               u32 pmin, u32 span_s, u32 span_e, u32 kskip0, u32 kprobe) {
@@ -779,7 +783,7 @@ __device__ __forceinline__ u32 k1_tid(u32 w) {
   return (u32)((K1_WAVE_MAP >> (4 * w)) & 15u) << 6 | lane;
 }
 
-template <bool LAZY2>
+template <u32 MODE>
 __device__ __forceinline__ u32 lz_block(const ZhBlockDesc *__restrict__ blocks, ZhWorkspace ws, u32 b, u32 nblocks, u32 *s_take, Prefetch &pf, u32 wv) {
   extern __shared__ __attribute__((aligned(16))) u8 smem[];
   u8 *in = smem + OFF_IN;
@@ -946,8 +950,9 @@ __device__ __forceinline__ u32 lz_block(const ZhBlockDesc *__restrict__ blocks, 
     // gate the workers' next window, so they take priority (MI355X_MICROARCH.md, "VALU issue
     // is arbitrated ... by priority, then age").
     __builtin_amdgcn_s_setprio(2);
-    if (tid < INS_TID + 64) inserter_loop<true>(in32, TL, ci8, misc, n, lim, lane, ws.dbg(b), wstart, pmin, span_s, span_e, kskip0, kprobe);
-    else inserter_loop<false>(in32, TS, ci8, misc, n, lim, lane, ws.dbg(b), wstart, pmin, span_s, span_e, kskip0, kprobe);
+    if (tid >= INS_TID + 64) inserter_loop<false>(in32, TS, ci8, misc, n, lim, lane, ws.dbg(b), wstart, pmin, span_s, span_e, kskip0, kprobe);
+    else if (two_tables<MODE>()) inserter_loop<true>(in32, TL, ci8, misc, n, lim, lane, ws.dbg(b), wstart, pmin, span_s, span_e, kskip0, kprobe);
+    else idle_inserter_loop(misc, n, wstart, kprobe);
     __builtin_amdgcn_s_setprio(0);
     return next_b;
   }
@@ -990,8 +995,8 @@ __device__ __forceinline__ u32 lz_block(const ZhBlockDesc *__restrict__ blocks, 
     u32 const lane = tid & 63;
     u32 *const ciK = ci0 + kb * CI_WORDS, *const ciP = ci0 + (kb ^ 1u) * CI_WORDS;
     u64 *const tmK = hm + kb * NROUND, *const tmP = hm + (kb ^ 1u) * NROUND;
-    u32 *const lmP = sgm + segm(kb ^ 1u, SEGM_LIT);   // window k - 1's literal bits (the walk's)
-    u32 *const lmQ = sgm + segm(kb, SEGM_LIT);        // window k - 2's (after its catch-up)
+    u32 *const lmP = sgm + segm(kb ^ 1u);   // window k - 1's literal bits (the walk's)
+    u32 *const lmQ = sgm + segm(kb);        // window k - 2's (after its catch-up)
     u64 *const mlP = mlist + (kb ^ 1u) * ML_CAP, *const mlQ = mlist + kb * ML_CAP;
     __syncthreads();  // P: candidates of window k in buffer k & 1
     ZH_STAMP(st_A);
@@ -1002,25 +1007,24 @@ __device__ __forceinline__ u32 lz_block(const ZhBlockDesc *__restrict__ blocks, 
     static_assert(RS < NWW && (RS & 1) == 0, "miss-skip rounds");
     bool const skipk = have && skip_window(misc, k, kskip0);
     if (skipk && wave != 0) {
-      if (wave <= RS) span_lengths<LAZY2>(in32, ciK, tmK, xq, wave - 1, wave, wsb, we, n, lim, lane, wave == RS, 0u, 0u);
+      if (wave <= RS) span_lengths<MODE>(in32, ciK, tmK, xq, wave - 1, wave, wsb, we, n, lim, lane, wave == RS, 0u);
       for (u32 r = RS + wave - 1; r < NROUND; r += NWW - 1) {
         ciK[cidx(64 * r + lane)] = 0;
         if (lane == 0) tmK[r] = 0;
       }
       ZH_STAMP(st_B);
     } else if (have && wave != 0) {
-      // the window's top span (wave 13) first takes the lookahead positions `we`, `we + 1`:
-      // the take decisions at the window's end need their info
-      u32 la1 = 0, la2 = 0;
+      // the window's top span (wave 13) first takes the lookahead position `we`: the take
+      // decision at the window's end needs its info (not in greedy mode 2)
+      u32 la1 = 0;
       if (wave == NWW - 1) {
         u32 const p = we + lane;
         u32 const cw = ciK[cidx(ZH_WINDOW + (lane & 1))];
-        u32 const li = info_one(in32, p, cw, n, lim, lane < 2 && p < n);
+        u32 const li = info_one<MODE>(in32, p, cw, n, lim, MODE != 2 && lane == 0 && p < n);
         if (lane < 2) ciK[cidx(ZH_WINDOW + lane)] = li;
         la1 = lane_value(li, 0);
-        la2 = lane_value(li, 1);
       }
-      span_lengths<LAZY2>(in32, ciK, tmK, xq, r_lo, r_hi, wsb, we, n, lim, lane, wave == NWW - 1, la1, la2);
+      span_lengths<MODE>(in32, ciK, tmK, xq, r_lo, r_hi, wsb, we, n, lim, lane, wave == NWW - 1, la1);
       ZH_STAMP(st_B);
     }
     if (wave == 0 && prev) {
@@ -1105,16 +1109,15 @@ __device__ __forceinline__ u32 lz_block(const ZhBlockDesc *__restrict__ blocks, 
     if (lane == 0) atomicAdd(&misc[MISC_ARR], 1u);
     __syncthreads();  // X: window k's match info and take masks; window k - 1's records and literal bits
     ZH_STAMP(st_X);
-    if (have && wave != 0 && wave < (skipk ? RS : NWW - 1)) {
-      // ---- take decisions at this wave's span top (the next positions were the next wave's):
-      // every wave but the window's top one, its last one (LAZY2: two) positions
-      constexpr u32 PER = LAZY2 ? 2u : 1u;
+    if (MODE != 2 && have && wave != 0 && wave < (skipk ? RS : NWW - 1)) {
+      // ---- take decision at this wave's span top (the next position was the next wave's):
+      // every wave but the window's top one, its last position
       u32 const hi = skipk ? wave : r_hi;
-      u32 const i = 64 * hi - 1 - (lane & (PER - 1));
-      if (lane < PER) {
-        u32 const inf = ciK[cidx(i)], inf1 = ciK[cidx(i + 1)], inf2 = ciK[cidx(i + 2)];
+      u32 const i = 64 * hi - 1;
+      if (lane == 0) {
+        u32 const inf = ciK[cidx(i)], inf1 = ciK[cidx(i + 1)];
         // (a 32-bit atomic on the mask's half: a hoisted 64-bit bit constant spilled)
-        if (i < we - wsb && (inf & 255u) && take_rule<LAZY2>(inf, inf1, inf2)) atomicOr((u32 *)&tmK[i >> 6] + ((i >> 5) & 1u), 1u << (i & 31));
+        if (i < we - wsb && (inf & 255u) && take_rule<MODE>(inf, inf1)) atomicOr((u32 *)&tmK[i >> 6] + ((i >> 5) & 1u), 1u << (i & 31));
       }
     }
     if (prev2) {
@@ -1181,7 +1184,7 @@ __device__ __forceinline__ u32 lz_block(const ZhBlockDesc *__restrict__ blocks, 
 // Persistent workgroups (grid = one per CU, the LDS footprint allows no second): workgroup g
 // takes blocks g, g + grid, ... and stages each block from registers loaded while the previous
 // one was processed, so the HBM latency of staging and the per-block launch gap overlap work.
-template <bool LAZY2>
+template <u32 MODE>
 __device__ __forceinline__ void lz_blocks(const ZhBlockDesc *__restrict__ blocks, u32 nblocks, ZhWorkspace ws) {
   extern __shared__ __attribute__((aligned(16))) u8 smem[];
   __shared__ u32 s_take;  // block index taken from the counter, broadcast to the workgroup
@@ -1195,16 +1198,19 @@ __device__ __forceinline__ void lz_blocks(const ZhBlockDesc *__restrict__ blocks
   u32 const wv = (u32)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   prefetch_block(blocks, b, nblocks, k1_tid(wv), pf);
   while (b < nblocks) {
-    b = lz_block<LAZY2>(blocks, ws, b, nblocks, &s_take, pf, wv);  // returns the next block taken
+    b = lz_block<MODE>(blocks, ws, b, nblocks, &s_take, pf, wv);  // returns the next block taken
     __syncthreads();  // every wave is done with this block's LDS before the next is staged
   }
 }
-// level < 9: greedy + lazy-1; level >= 9: LAZY2 (the same kernel body, one instantiation each)
+// one instantiation per parse mode (ZH_K1_MODE: levels 3-4 / 2 / 1)
 extern "C" __global__ __launch_bounds__(K1_THREADS) void zh_lz_kernel(const ZhBlockDesc *__restrict__ blocks, u32 nblocks, ZhWorkspace ws) {
-  lz_blocks<false>(blocks, nblocks, ws);
+  lz_blocks<0>(blocks, nblocks, ws);
 }
-extern "C" __global__ __launch_bounds__(K1_THREADS) void zh_lz_lazy2_kernel(const ZhBlockDesc *__restrict__ blocks, u32 nblocks, ZhWorkspace ws) {
-  lz_blocks<true>(blocks, nblocks, ws);
+extern "C" __global__ __launch_bounds__(K1_THREADS) void zh_lz_short_kernel(const ZhBlockDesc *__restrict__ blocks, u32 nblocks, ZhWorkspace ws) {
+  lz_blocks<1>(blocks, nblocks, ws);
+}
+extern "C" __global__ __launch_bounds__(K1_THREADS) void zh_lz_greedy_kernel(const ZhBlockDesc *__restrict__ blocks, u32 nblocks, ZhWorkspace ws) {
+  lz_blocks<2>(blocks, nblocks, ws);
 }
 
 extern "C" u32 zh_lz_lds_bytes() { return K1_LDS; }
@@ -1227,9 +1233,11 @@ extern "C" __global__ void zh_dict_pack_kernel(const u32 *__restrict__ t32, u16 
 
 namespace zh {
 hipError_t lz_init() {
-  hipError_t e = hipFuncSetAttribute((const void *)zh_lz_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)K1_LDS);
-  if (e != hipSuccess) return e;
-  return hipFuncSetAttribute((const void *)zh_lz_lazy2_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)K1_LDS);
+  for (const void *f : {(const void *)zh_lz_kernel, (const void *)zh_lz_short_kernel, (const void *)zh_lz_greedy_kernel}) {
+    hipError_t const e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)K1_LDS);
+    if (e != hipSuccess) return e;
+  }
+  return hipSuccess;
 }
 // tables for the last P = min(cn, 65535) content bytes (positions [0, P - ZH_DTAB_MARGIN));
 // out: 2^15 u16 (long table, then short), tmp32: 2^15 u32 scratch.  P = 0: none (too short).
@@ -1243,22 +1251,24 @@ hipError_t lz_dict_tables(const u8 *content, size_t cn, u16 *out, u32 *tmp32, u3
   hipLaunchKernelGGL(zh_dict_pack_kernel, dim3((HL_SIZE + HS_SIZE + 255) / 256), dim3(256), 0, stream, tmp32, out);
   return hipGetLastError();
 }
-void lz_launch(const ZhBlockDesc *d_descs, u32 nblocks, ZhWorkspace ws, bool lazy2, hipStream_t stream) {
+// mode = ZH_K1_MODE(level)
+void lz_launch(const ZhBlockDesc *d_descs, u32 nblocks, ZhWorkspace ws, u32 mode, hipStream_t stream) {
   // one persistent workgroup per CU of the stream's device
   int dev = 0, cus = 0;
   if (stream) (void)hipStreamGetDevice(stream, &dev);
   else (void)hipGetDevice(&dev);
   if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) cus = 256;
   u32 const grid = std::min(nblocks, (u32)cus);
-  if (lazy2) hipLaunchKernelGGL(zh_lz_lazy2_kernel, dim3(grid), dim3(K1_THREADS), K1_LDS, stream, d_descs, nblocks, ws);
-  else hipLaunchKernelGGL(zh_lz_kernel, dim3(grid), dim3(K1_THREADS), K1_LDS, stream, d_descs, nblocks, ws);
+  auto *const k = mode == 2 ? zh_lz_greedy_kernel : mode == 1 ? zh_lz_short_kernel : zh_lz_kernel;
+  hipLaunchKernelGGL(k, dim3(grid), dim3(K1_THREADS), K1_LDS, stream, d_descs, nblocks, ws);
 }
 }  // namespace zh
 
-// Test hook (tests/test_gpu_k1.py, not a product entry point): K1 alone over single-block items
-// in[i * stride, + sizes[i]) (each <= ZH_BLOCK_MAX, no dictionary), its raw output copied back:
-// per item ZH_SEQ_CAP records, ZH_LIT_BYTES of the literal area and meta {nseq, nlit, rle}.
-extern "C" int zh_test_lz(const u8 *d_in, u32 nitems, u32 stride, const u32 *h_sizes, int lazy2, u64 *h_recs, u8 *h_lits, u32 *h_meta) {
+// Test hook (tests/test_gpu_k1.py, not a product entry point): K1 alone (parse mode `mode`,
+// ZH_K1_MODE) over single-block items in[i * stride, + sizes[i]) (each <= ZH_BLOCK_MAX, no
+// dictionary), its raw output copied back: per item ZH_SEQ_CAP records, ZH_LIT_BYTES of the
+// literal area and meta {nseq, nlit, rle}.
+extern "C" int zh_test_lz(const u8 *d_in, u32 nitems, u32 stride, const u32 *h_sizes, int mode, u64 *h_recs, u8 *h_lits, u32 *h_meta) {
   if (!nitems) return 0;
   std::vector<ZhBlockDesc> descs(nitems);
   for (u32 i = 0; i < nitems; i++) {
@@ -1282,7 +1292,7 @@ extern "C" int zh_test_lz(const u8 *d_in, u32 nitems, u32 stride, const u32 *h_s
     (void)hipMemcpy(dd, descs.data(), sizeof(ZhBlockDesc) * nitems, hipMemcpyHostToDevice);
     (void)hipMemset(ctr, 0, 4);
     ZhWorkspace ws{base, ctr, nullptr, 0u};
-    zh::lz_launch(dd, nitems, ws, lazy2 != 0, nullptr);
+    zh::lz_launch(dd, nitems, ws, (u32)mode, nullptr);
     if (hipDeviceSynchronize() != hipSuccess) rc = 1;
     for (u32 i = 0; i < nitems && !rc; i++) {
       u8 *const b = base + (size_t)i * ZH_WS_BLOCK_BYTES;

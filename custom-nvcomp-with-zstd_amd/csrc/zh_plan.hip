@@ -18,7 +18,7 @@ extern "C" u32 zh_lz_lds_bytes();
 extern "C" u32 zh_entropy_lds_bytes();
 namespace zh {
 hipError_t lz_init();
-void lz_launch(const ZhBlockDesc *d_descs, u32 nblocks, ZhWorkspace ws, bool lazy2, hipStream_t stream);
+void lz_launch(const ZhBlockDesc *d_descs, u32 nblocks, ZhWorkspace ws, u32 mode, hipStream_t stream);
 hipError_t lz_deep_init();
 hipError_t lz_deep_launch(const ZhBlockDesc *d_descs, u32 nblocks, ZhWorkspace ws, int level, hipStream_t stream);
 hipError_t entropy_init();
@@ -217,7 +217,7 @@ hipError_t launch_compress(const ZhBlockDesc *d_descs, u32 nblocks, ZhWorkspace 
     hipError_t const e = lz_deep_launch(d_descs, nblocks, ws, level, stream);
     if (e != hipSuccess) return e;
   } else {
-    lz_launch(d_descs, nblocks, ws, false, stream);
+    lz_launch(d_descs, nblocks, ws, (u32)ZH_K1_MODE(level), stream);
   }
   if (!ev.empty()) (void)hipEventRecord(ev[1], stream);
   entropy_launch(d_descs, nblocks, ws, window_log, cfg_block_size, d_item_size, d_item_status, d_blk_size, stream);

@@ -35,6 +35,12 @@
 #define ZH_HASH_LOG_LONG 14         /* 8-byte hash table: 2^14 u16 entries */
 #define ZH_HASH_LOG_SHORT 14        /* 5-byte hash table: 2^14 u16 entries */
 #define ZH_HASH_READ 8              /* bytes read per hashed position */
+/* K1's parse mode by level (levels 1-4; SURVEY.md §8f F2, reference level table
+ * src/cuda_zstd_types.cpp:147-210): 0 = both tables + lazy-1 check (levels 3-4), 1 = the short
+ * table only + lazy-1 (level 2), 2 = the short table only, greedy (level 1).  Oracle on the C3
+ * mix (256 chunks; libzstd at that level): mode 2 2.647 (L1 2.534), mode 1 2.682 (L2 2.673),
+ * mode 0 2.796 (L3 2.791). */
+#define ZH_K1_MODE(level) ((level) <= 1 ? 2 : (level) == 2 ? 1 : 0)
 #define ZH_MIN_MATCH_LONG 8
 #define ZH_MIN_MATCH_SHORT 5
 #define ZH_MAX_MATCH 64             /* per-position length cap; continuations are merged */

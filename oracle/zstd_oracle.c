@@ -816,6 +816,10 @@ static u32 common_prefix(const u8 *src, u32 a, u32 b, u32 n, u32 cap) {
  * earlier tile's insertions (K1's inserter waves: zh_lz.hip insert_window).  `skip_from`:
  * tiles at or above it are neither looked up nor inserted (len 0), see orc_lz_parse_pre. */
 static u32 g_TL[1 << ZH_HASH_LOG_LONG], g_TS[1 << ZH_HASH_LOG_SHORT];
+/* K1's parse mode of the level (ZH_K1_MODE): 0 = both tables, lazy-1 check (levels 3-4);
+ * 1 = the short (5-byte) table only, lazy-1 (level 2); 2 = the short table only, greedy (level 1).
+ * Set by orc_compress_frame_lv. */
+static int orc_lz_mode = 0;
 static void match_info_tiles(const u8 *src, u32 n, u32 t0, u32 t1, u32 skip_from, u8 *len, u16 *off) {
   const u32 EMPTY = 0xFFFFFFFFu;
   u32 const lim = n - ZH_HASH_READ;
@@ -824,7 +828,7 @@ static void match_info_tiles(const u8 *src, u32 n, u32 t0, u32 t1, u32 skip_from
     for (u32 p = t; p < e; p++) {
       u64 v = rd64(src + p);
       u32 qL = g_TL[zh_hash_long(v)], qS = g_TS[zh_hash_short(v)];
-      u32 lL = qL != EMPTY ? common_prefix(src, p, qL, n, ZH_MAX_MATCH) : 0;
+      u32 lL = (qL != EMPTY && orc_lz_mode == 0) ? common_prefix(src, p, qL, n, ZH_MAX_MATCH) : 0;
       u32 lS = qS != EMPTY ? common_prefix(src, p, qS, n, ZH_MAX_MATCH) : 0;
       if (lL < ZH_MIN_MATCH_LONG) lL = 0;
       if (lS < ZH_MIN_MATCH_SHORT) lS = 0;
@@ -963,7 +967,7 @@ size_t orc_lz_parse_pre(const u8 *src, u32 pre, u32 n, orc_seq_t *seq, u32 *last
       else if (orc_parse_lazy2) {
         int const g0 = match_gain(len, off, p);
         defer = match_gain(len, off, p + 1) > g0 + 4 || match_gain(len, off, p + 2) > g0 + 7;
-      } else defer = len[p + 1] > len[p];
+      } else defer = orc_lz_mode != 2 && len[p + 1] > len[p];
       if (defer) { p++; continue; }
       /* catch-up (libzstd 1.4.9 ZSTD_compressBlock_doubleFast_generic / lazy_generic "catch
        * up"): the match grows backwards over the literals since the last sequence while the
@@ -1230,12 +1234,14 @@ size_t orc_compress_frame_ck(u8 *dst, size_t cap, const u8 *src, u64 n, u32 bloc
  * zh_lz_deep_kernel); the dual-hash LAZY2 parse (orc_parse_lazy2) stays for the study tools. */
 size_t orc_compress_frame_lv(u8 *dst, size_t cap, const u8 *src, u64 n, u32 block_size, u32 window_log, int checksum, const u8 *dict,
                              size_t dict_n, int level) {
-  int const save = orc_parse_lazy2, save_lv = orc_parse_level;
+  int const save = orc_parse_lazy2, save_lv = orc_parse_level, save_m = orc_lz_mode;
   orc_parse_lazy2 = level >= 9;
   orc_parse_level = level;
+  orc_lz_mode = ZH_K1_MODE(level);
   size_t const r = orc_compress_frame_dict(dst, cap, src, n, block_size, window_log, checksum, dict, dict_n);
   orc_parse_lazy2 = save;
   orc_parse_level = save_lv;
+  orc_lz_mode = save_m;
   return r;
 }
 

@@ -267,6 +267,25 @@ def test_full_size_blocks_match_libzstd(torch_cuda, mgr):
         assert fr[hs:].hex() == c["libzstd_block"], c["name"]
 
 
+@pytest.mark.parametrize("level", [1, 2, 4])
+def test_k1_levels_match_oracle(torch_cuda, level):
+    """Levels 1-4 run K1 in the level's parse mode (ZH_K1_MODE: level 1 the short table only,
+    greedy; level 2 the short table only, lazy-1; levels 3-4 both tables): frames equal the
+    oracle's at that level and decode with libzstd; ragged, multi-block (history), random and RLE
+    sizes included."""
+    import cuda_zstd
+
+    m = cuda_zstd.Manager(level)
+    datas = [T.gen(k, 1, 60 + k, s) for k, s in ((T.DG_MIX, 65536), (T.DG_TEXT, 65536), (T.DG_JSON, 65536), (T.DG_SOURCE, 40000),
+                                                (T.DG_CSV, 300000), (T.DG_EXE, 777), (T.DG_SENSOR, 65535), (T.DG_SYM16, 65536))]
+    datas += [np.zeros(5000, dtype=np.uint8), T.gen(T.DG_RANDOM, 1, 61, 70000), T.gen(T.DG_TEXT, 1, 62, 9)]
+    outs = m.compress_batch([torch_cuda.from_numpy(d).cuda() for d in datas])
+    for k, (o, d) in enumerate(zip(outs, datas)):
+        got = o.cpu().numpy().tobytes()
+        assert got == T.oracle_frame(d, level=level), k
+        assert T.zstd_decompress(got, len(d)) == d.tobytes(), k
+
+
 @pytest.mark.parametrize("level", [5, 6, 7, 8, 9, 19])
 def test_deep_levels_match_oracle(torch_cuda, level):
     """Levels >= ZH_DEEP_LEVEL (5) run the deep chain matcher (zh_lz_deep_kernel: exact hash
