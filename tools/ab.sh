@@ -21,15 +21,23 @@ fi
 TAG=${2:-ab}
 K=${3:-"k1 or levels or c3 or corpora or special"}
 mkdir -p $R/gpurun_out
-CUDA_ZSTD_HIP_LIB=$R/tools/libB.so timeout -k 10 400 python3 -u -m pytest $R/tests/test_gpu_k1.py $R/tests/test_gpu_parity.py -x -q --timeout 120 --timeout-method thread -k "$K" > $R/gpurun_out/${TAG}_testsB.log 2>&1 || { tail -30 $R/gpurun_out/${TAG}_testsB.log; exit 1; }
-tail -1 $R/gpurun_out/${TAG}_testsB.log
+# extra variants: tools/libV_<X>.so (+ tools/libVS_<X>.so stamps), named in $VARIANTS
+VS="A B $VARIANTS"
+for v in B $VARIANTS; do
+  L=$R/tools/lib$v.so; [ $v = B ] || L=$R/tools/libV_$v.so
+  CUDA_ZSTD_HIP_LIB=$L timeout -k 10 400 python3 -u -m pytest $R/tests/test_gpu_k1.py $R/tests/test_gpu_parity.py -x -q --timeout 120 --timeout-method thread -k "$K" > $R/gpurun_out/${TAG}_tests$v.log 2>&1 || { tail -30 $R/gpurun_out/${TAG}_tests$v.log; exit 1; }
+  echo "tests $v: $(tail -1 $R/gpurun_out/${TAG}_tests$v.log)"
+done
 for k in 1 2 3; do
-  for v in A B; do
-    if [ $v = A ]; then L=$P/libcuda_zstd_hip.so; else L=$R/tools/libB.so; fi
+  for v in $VS; do
+    if [ $v = A ]; then L=$P/libcuda_zstd_hip.so; elif [ $v = B ]; then L=$R/tools/libB.so; else L=$R/tools/libV_$v.so; fi
     CUDA_ZSTD_HIP_LIB=$L timeout -k 10 200 python3 $R/bench.py --steps 8 --warmup 2 --no-cpu-baseline --no-verify --no-decompress --no-legs > $R/gpurun_out/${TAG}_${v}${k}.json 2>/dev/null
     python3 -c "import json; d=json.loads(open('$R/gpurun_out/${TAG}_${v}${k}.json').read().strip().splitlines()[-1]); print('$v', d['value'], d['ms_per_step'], d['config']['kernel_ms'], d['config']['ratio'])"
   done
 done
 STAMPS_LIB=$R/tools/libcuda_zstd_hip_stamps.so timeout -k 10 200 python3 $R/tools/stamps.py mix 4096 > $R/gpurun_out/${TAG}_stampsA.log 2>&1
 STAMPS_LIB=$R/tools/libBS.so timeout -k 10 200 python3 $R/tools/stamps.py mix 4096 > $R/gpurun_out/${TAG}_stampsB.log 2>&1
+for v in $VARIANTS; do
+  STAMPS_LIB=$R/tools/libVS_$v.so timeout -k 10 200 python3 $R/tools/stamps.py mix 4096 > $R/gpurun_out/${TAG}_stamps$v.log 2>&1
+done
 echo ab-done
