@@ -83,6 +83,13 @@ enum : u32 {
 #define ZH_DEEP_STG_BYTES (2u * ZH_BLOCK_MAX + 256u)
 #define ZH_DEEP_SLOT_BYTES ((size_t)ZH_DEEP_STG_BYTES + 4u * 2u * ZH_BLOCK_MAX + 4u * ZH_BLOCK_MAX + 2u * 2u * ZH_BLOCK_MAX)
 #define ZH_DEEP_SLOTS_MAX 256u
+// K1's per-block meta word 2: 0 normal (records + literal area), 1 RLE block, ZH_META_K1HIST: no
+// sequences, the literals are the block's source bytes (16-B aligned) and K1 left the literal
+// histogram as ZH_K1_HIST_WAVES 256-bin u32 sub-histograms at lits + ZH_K1_HIST_OFF
+#define ZH_META_K1HIST 2u
+#define ZH_K1_HIST_OFF 65536u
+#define ZH_K1_HIST_WAVES 14u
+static_assert(ZH_K1_HIST_OFF + ZH_K1_HIST_WAVES * 1024u <= ZH_LIT_BYTES, "K1 sub-histograms fit the literal area");
 
 struct ZhWorkspace {
   u8 *base;          // nblocks * ZH_WS_BLOCK_BYTES

@@ -1141,7 +1141,7 @@ extern "C" __global__ __launch_bounds__(K2_THREADS) void zh_entropy_kernel(const
   u32 const n = d.n;
   if (n == 0) return;
   const u32 *meta = ws.meta(b);
-  u32 const nseq_raw = meta[0], nlit = meta[1], rle = meta[2];
+  u32 const nseq_raw = meta[0], nlit = meta[1], rle = meta[2] == 1u, k1hist = meta[2] == ZH_META_K1HIST;
   Out const o{d.dst, d.dst_cap};
   if (wave == 0 && lane == 0) sw[0] = 0;  // (wave 1's SW overlaps wave 0's layout: never touched)
 #ifdef ZH_STAMPS
@@ -1192,14 +1192,27 @@ extern "C" __global__ __launch_bounds__(K2_THREADS) void zh_entropy_kernel(const
     if (wave == 1 && lane == 0) { o.put(blk, (u8)hdr); o.put(blk + 1, (u8)(hdr >> 8)); o.put(blk + 2, (u8)(hdr >> 16)); o.put(blk + 3, d.src[0]); }
     total = blk + 4;
   } else {
-    const u8 *lits = ws.lits(b);
+    // (ZH_META_K1HIST: no sequences, the literals are the block's own bytes -- read from the
+    // source -- and K1 counted their histogram)
+    const u8 *lits = k1hist ? d.src : ws.lits(b);
     u64 *seq = ws.seq(b);
     u32 op = body0;
     // the literal histogram, both waves (wave 1 before its sequence work), into wave 0's hist
     if (nlit > ZH_COMPRESS_LITERALS_SIZE_MIN) {
       u32 *const hist0 = (u32 *)(smem_all + OFF_HIST);
       u32 const nl = nlit;
-      if (wave == 0) for (u32 i = lane; i < 256; i += 64) hist0[i] = 0;
+      if (k1hist) {
+        // the sum of K1's per-wave sub-histograms, both waves (two bins per lane)
+        const u32 *const kh = (const u32 *)(ws.lits(b) + ZH_K1_HIST_OFF);
+        u32 const i = lane + 64u * wave, i2 = i + 128u;
+        u32 s1 = 0, s2 = 0;
+#pragma unroll
+        for (u32 w = 0; w < ZH_K1_HIST_WAVES; w++) { s1 += kh[256u * w + i]; s2 += kh[256u * w + i2]; }
+        hist0[i] = s1;
+        hist0[i2] = s2;
+      } else if (wave == 0) {
+        for (u32 i = lane; i < 256; i += 64) hist0[i] = 0;
+      }
       __syncthreads();
       // 16 literals per lane per load (lits is 16-B aligned), two loads per step, the next step's
       // loads issued before this step's LDS atomics
@@ -1215,7 +1228,7 @@ extern "C" __global__ __launch_bounds__(K2_THREADS) void zh_entropy_kernel(const
           }
         }
       };
-      u32 const i00 = 32 * lane + 2048 * wave;
+      u32 const i00 = k1hist ? nl : 32 * lane + 2048 * wave;  // (K1's histogram: nothing to count)
       uint4 q[2];
       if (i00 < nl) load2(i00, q);
       for (u32 i0 = i00; i0 < nl; i0 += 4096) {

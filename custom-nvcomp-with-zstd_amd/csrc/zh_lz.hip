@@ -55,6 +55,12 @@ extern "C" u32 zh_fixups_host() {
 #endif
 namespace {
 
+#ifndef ZH_PARSE_PRIO
+#define ZH_PARSE_PRIO 0
+#endif
+#ifndef ZH_FIRST_WALK_PLAIN
+#define ZH_FIRST_WALK_PLAIN 0
+#endif
 constexpr u32 K1_THREADS = 1024;
 constexpr u32 NROUND = ZH_WINDOW / 64;      // 64-position length rounds per window
 constexpr u32 SEGP = 32;                    // positions per walk segment (one lane of wave 0)
@@ -599,8 +605,10 @@ __device__ __forceinline__ u32 catch_up(const u32 *in32, u32 P, u32 off, u32 lo,
 // segment's literal and match-start bits, ex: the exit (first position >= SE).  With old
 // visited bits (a Jacobi re-walk from a new entry), the walk stops where it meets a position
 // the old walk visited -- from there on both are the same -- and keeps the old bits above it.
+template <bool REWALK>
 __device__ __forceinline__ void seg_walk(const u32 *ci, u32 tmk, u32 S, u32 SE, u32 p, bool act0, u32 &LM, u32 &MM, u32 &ex) {
-  u32 const old = act0 ? (LM | MM) : 0u;
+  // (the first walk has no old trajectory: REWALK = false drops the merge test from the step)
+  u32 const old = (REWALK && act0) ? (LM | MM) : 0u;
   u32 nl = 0, nm = 0;
   bool act = act0 && p < SE, merged = false;
   u32 mpos = 0;
@@ -1029,13 +1037,16 @@ __device__ __forceinline__ u32 lz_block(const ZhBlockDesc *__restrict__ blocks, 
     }
     if (wave == 0 && prev) {
       // ---- the parse of window k - 1, lanes = 32-position segments
+#if ZH_PARSE_PRIO
+      __builtin_amdgcn_s_setprio(ZH_PARSE_PRIO);  // the parse's dependent chain before the length waves' issue
+#endif
       u32 const wn = wep - wsp;
       u32 const S = SEGP * lane, SE = min(S + SEGP, wn);
       u32 const tmk = (u32)(tmP[lane >> 1] >> (32 * (lane & 1)));
       u32 const e0 = e_in - wsp;  // first parsed position (< 64 except in the window holding `pre`)
       u32 entry = lane == 0 ? e0 : max(S, e0), ex = entry;
       u32 LM = 0, MM = 0;
-      seg_walk(ciP, tmk, S, SE, entry, true, LM, MM, ex);
+      seg_walk<!ZH_FIRST_WALK_PLAIN>(ciP, tmk, S, SE, entry, true, LM, MM, ex);
       // Jacobi rounds: a segment's entry is its predecessor's exit
       for (;;) {
         u32 const pe = wave_shr1(ex);
@@ -1045,7 +1056,7 @@ __device__ __forceinline__ u32 lz_block(const ZhBlockDesc *__restrict__ blocks, 
         st_rounds++;
 #endif
         if (!__ballot(ch)) break;
-        seg_walk(ciP, tmk, S, SE, ne, ch, LM, MM, ex);
+        seg_walk<true>(ciP, tmk, S, SE, ne, ch, LM, MM, ex);
         entry = ne;
       }
       e_in = wsp + lane_value(ex, 63);
@@ -1082,6 +1093,9 @@ __device__ __forceinline__ u32 lz_block(const ZhBlockDesc *__restrict__ blocks, 
       }
       nwalk_tot += nwl;  // the window's walk literals (its last match may run past its end)
       if (lane == 0) { misc[MISC_WNM + (kb ^ 1u)] = nm; misc[MISC_NM + ((k - 1) & 3)] = nm; }
+#if ZH_PARSE_PRIO
+      __builtin_amdgcn_s_setprio(0);
+#endif
       ZH_STAMP(st_J);
     }
     if (wave == REC_WAVE && prev2) {
@@ -1139,9 +1153,31 @@ __device__ __forceinline__ u32 lz_block(const ZhBlockDesc *__restrict__ blocks, 
     }
     ZH_STAMP(st_E);
   }
+  if (dead && (((uintptr_t)d.src) & 15) == 0) {
+    // the probe found no match: no sequences, the whole block is literals, and they are the
+    // block's own bytes -- K2 reads them from the source (16-B aligned).  K1 leaves K2 the
+    // literal histogram instead: one 256-bin sub-histogram per worker wave, counted in LDS (the
+    // hash tables are dead) and stored after the first 64 KiB of the literal area (ZH_K1_HIST_OFF).
+    u32 *const hw = (u32 *)(smem + OFF_TL) + 256u * wave;
+    for (u32 i = lane; i < 256; i += 64) hw[i] = 0;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    u32 const per = (((d.n + NWW - 1) / NWW) + 63) & ~63u;  // this wave's bytes: [per * wave, + per)
+    u32 const a = per * wave, e = min(a + per, d.n);
+    for (u32 i = a + lane; i < e; i += 64) atomicAdd(&hw[in[pre + i]], 1u);
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    u32 *const gh = (u32 *)(lit_out + ZH_K1_HIST_OFF) + 256u * wave;
+    for (u32 i = lane; i < 256; i += 64) gh[i] = hw[i];
+    if (tid_ == 0) {
+      u32 two;  // (opaque: a constant {0, n, 2} vector would be hoisted out of the block loop and spilled)
+      __asm__ volatile("v_mov_b32 %0, 2" : "=v"(two));
+      meta[0] = two - 2u; meta[1] = d.n; meta[2] = two;
+    }
+    return next_b;
+  }
   if (dead) {
-    // the probe found no match: no sequences, the whole block is literals (K2 decides Huffman /
-    // raw / RLE literals as for any block); the block's bytes go out of LDS in 16-B stores
+    // (unaligned source) the block's bytes go out of LDS to the literal area in 16-B stores
     u32 const nv = (d.n + 15) >> 4, sh = pre & 3;
     const u32 *const src32 = in32 + (pre >> 2);
     for (u32 i = tid_; i < nv; i += INS_TID) {

@@ -223,6 +223,78 @@ __device__ void deep_chains(const u32 *s32, u32 *prev, u32 *head, u16 *hb, u32 s
 
 }
 
+// The chain search of block position i (lanes `valid`; all lanes of the wave call it together):
+// the longest of the chain's first `depth` candidates -> off << 8 | len (0: none).  D32: the
+// staged bytes (LDS or the slot), P16: link distances of positions [s0, lim) (LDS or the slot),
+// positions below s0 link through dprev.  One chain per lane, the position's own 64 bytes held in
+// registers (aligned to p): a candidate's extension loads only its own 15 dwords (two chains per
+// lane, both loading the whole 112 bytes per extension: C5 8.5 / 6.7 GB/s vs 9.1 / 7.3 this way).
+__device__ __forceinline__ u32 deep_search_one(const u32 *D32, const u16 *P16, const u32 *dprev, u32 i, bool valid, u32 pre, u32 nb, u32 n,
+                                               u32 lim, u32 s0, u32 depth) {
+  // the next candidate after q (+ 1, 0 = none)
+  auto link = [&](u32 q) -> u32 {
+    if (q < s0) return dprev[q];
+    u32 const dl = P16[q - s0];
+    return dl ? q + 1u - dl : 0u;
+  };
+  u32 const p = pre + i;
+  bool act = valid && i < nb && p < lim;
+  u32 c = act ? link(p) : 0u, best = 0, bo = 0, dd = 0;
+  act = act && c != 0 && p - (c - 1u) <= ZH_DEEP_MAXOFF;
+  u32 O[16];
+  {
+    u32 const w = p >> 2, sh = p & 3;
+    u32 R[17];
+#pragma unroll
+    for (u32 j = 0; j < 17; j++) R[j] = (valid && i < nb) ? D32[w + j] : 0u;
+#pragma unroll
+    for (u32 j = 0; j < 16; j++) O[j] = __builtin_amdgcn_alignbyte(R[j + 1], R[j], sh);
+  }
+  u32 ownb = 0;  // own byte at p + best (best >= 8)
+  while (__ballot(act)) {
+    if (act) {
+      u32 const q = c - 1u;
+      bool w = true;
+      if (best >= 8) {
+        u32 const b = q + best;
+        w = ownb == ((D32[b >> 2] >> (8 * (b & 3))) & 255u);
+      }
+      u32 const nx = link(q);
+      u32 l = 0;
+      if (w) {
+        u32 clo, chi;
+        g64(D32, q, clo, chi);
+        u32 const x = O[0] ^ clo, y = O[1] ^ chi;
+        l = x ? (u32)__builtin_ctz(x) >> 3 : y ? 4u + ((u32)__builtin_ctz(y) >> 3) : 8u;
+        if (l == 8 && p + 8 < n) {
+          u32 B[15];
+          u32 const wq = (q >> 2) + 2, sq = q & 3;
+#pragma unroll
+          for (u32 j = 0; j < 15; j++) B[j] = D32[wq + j];
+          u32 e = 56;
+#pragma unroll
+          for (int j = 13; j >= 0; j--) {
+            u32 const xx = O[j + 2] ^ __builtin_amdgcn_alignbyte(B[j + 1], B[j], sq);
+            if (xx) e = 4 * (u32)j + ((u32)__builtin_ctz(xx) >> 3);
+          }
+          l = 8 + e;
+        }
+      }
+      l = min(l, p < n ? n - p : 0u);
+      if (l >= ZH_MIN_MATCH_SHORT && l > best) {
+        best = l;
+        bo = p - q;
+        u32 const a = p + l;  // the own byte a candidate must match to beat the new best
+        ownb = (D32[a >> 2] >> (8 * (a & 3))) & 255u;
+      }
+      dd++;
+      c = nx;
+      act = best < ZH_MAX_MATCH && dd < depth && c != 0 && p - (c - 1u) <= ZH_DEEP_MAXOFF;
+    }
+  }
+  return bo << 8 | best;
+}
+
 // Step 3 of deep_block: per block position the chain's first `depth` candidates -> offg[i] =
 // off << 8 | len.  DL: the staged bytes in LDS at e16 (else gdata, the slot); PL: the link
 // distances in LDS at 0 (else gP16, the slot); positions below s0 link through dprev.
@@ -232,90 +304,173 @@ __device__ __forceinline__ void deep_search(const u32 *gdata, const u16 *gP16, u
   extern __shared__ __attribute__((aligned(16))) u8 smem[];
   const u32 *const D32 = DL ? (const u32 *)(smem + e16) : gdata;
   const u16 *const P16 = PL ? (const u16 *)smem : gP16;
-  // the next candidate after q (+ 1, 0 = none)
-  auto link = [&](u32 q) -> u32 {
-    if (q < s0) return dprev[q];
-    u32 const dl = P16[q - s0];
-    return dl ? q + 1u - dl : 0u;
-  };
-  // lanes = block positions
-  struct Cur {
-    u32 i, p, olo, ohi, c, best, bo, dd;
-    bool act;
-  };
-  auto cur_init = [&](Cur &k, u32 i) {
-    k.i = i;
-    k.p = pre + i;
-    k.act = i < nb && k.p < lim;
-    k.olo = k.ohi = k.c = 0;
-    k.best = k.bo = k.dd = 0;
-    if (k.act) {
-      g64(D32, k.p, k.olo, k.ohi);
-      k.c = link(k.p);
-    }
-    k.act = k.act && k.c != 0 && k.p - (k.c - 1u) <= ZH_DEEP_MAXOFF;
-  };
-  auto cur_done = [&](Cur &k) {
-    if (k.i < nb) offg[k.i] = k.bo << 8 | k.best;
-  };
-  // one chain per lane, the position's own 64 bytes held in registers (aligned to p): a
-  // candidate's extension loads only its own 15 dwords (two chains per lane, both loading the
-  // whole 112 bytes per extension: C5 8.5 / 6.7 GB/s vs 9.1 / 7.3 this way)
   for (u32 i = tid; i < nb + (DT - 1) - (nb + DT - 1) % DT; i += DT) {
-    Cur k;
-    cur_init(k, i);
-    u32 O[16];
-    {
-      u32 const w = k.p >> 2, sh = k.p & 3;
-      u32 R[17];
-#pragma unroll
-      for (u32 j = 0; j < 17; j++) R[j] = k.i < nb ? D32[w + j] : 0u;
-#pragma unroll
-      for (u32 j = 0; j < 16; j++) O[j] = __builtin_amdgcn_alignbyte(R[j + 1], R[j], sh);
-    }
-    u32 ownb = 0;  // own byte at p + best (best >= 8)
-    while (__ballot(k.act)) {
-      if (k.act) {
-        u32 const q = k.c - 1u;
-        bool w = true;
-        if (k.best >= 8) {
-          u32 const b = q + k.best;
-          w = ownb == ((D32[b >> 2] >> (8 * (b & 3))) & 255u);
-        }
-        u32 const nx = link(q);
-        u32 l = 0;
-        if (w) {
-          u32 clo, chi;
-          g64(D32, q, clo, chi);
-          u32 const x = O[0] ^ clo, y = O[1] ^ chi;
-          l = x ? (u32)__builtin_ctz(x) >> 3 : y ? 4u + ((u32)__builtin_ctz(y) >> 3) : 8u;
-          if (l == 8 && k.p + 8 < n) {
-            u32 B[15];
-            u32 const wq = (q >> 2) + 2, sq = q & 3;
-#pragma unroll
-            for (u32 j = 0; j < 15; j++) B[j] = D32[wq + j];
-            u32 e = 56;
-#pragma unroll
-            for (int j = 13; j >= 0; j--) {
-              u32 const xx = O[j + 2] ^ __builtin_amdgcn_alignbyte(B[j + 1], B[j], sq);
-              if (xx) e = 4 * (u32)j + ((u32)__builtin_ctz(xx) >> 3);
+    u32 const r = deep_search_one(D32, P16, dprev, i, true, pre, nb, n, lim, s0, depth);
+    if (i < nb) offg[i] = r;
+  }
+}
+
+// ---- demand-driven search + parse -------------------------------------------
+// The serial LAZY2 parse reads the match at a position only when it gets there, plus the two
+// after it.  So instead of searching every position and then walking (steps 3-4 of deep_block),
+// the segment walks run first and search on demand: every segment's lane walks as far as the
+// memo of searched positions allows; a lane that needs an unsearched position posts it and the
+// next two to a queue; all threads then search the queue (lanes = entries) and the walks go on.
+// Jacobi rounds as before (a re-walk stops where it meets its old trajectory).  The positions the
+// walks consult are the ones the serial parse consults, so records, literals and frames are
+// unchanged -- only fewer positions are searched.  Used when the link distances, staged bytes and
+// the memo fit in LDS (C5's 16 KiB records with or without the 64 KiB dictionary).
+//   memo[i] (u16): 0xFFFF unsearched; else len | (bit length of off + 1) << 8 (the LAZY2 gain)
+constexpr u32 MEMO_UNK = 0xFFFFu;
+constexpr u32 DQ_PER = 3;  // positions posted per blocked lane
+__device__ __forceinline__ int memo_gain(u32 m) { return (m & 255u) ? 4 * (int)(m & 255u) - (int)(m >> 8) : -1000; }
+__device__ __forceinline__ u32 demand_segl(u32 nb) { return nb <= 16384u ? 16u : nb <= 32768u ? 32u : 64u; }
+// LDS bytes the demand path needs above the staged bytes (memo, queue, exits), for nb positions
+__device__ __forceinline__ u32 demand_lds(u32 nb) { return ((2u * nb + 15u) & ~15u) + 2u * DQ_PER * DT + 4u * DT; }
+
+// Returns through meta / seq_out / lit_out like step 5 of deep_block.  lds = the free LDS above the
+// staged bytes (demand_lds(nb) bytes); misc = deep_block's LDS scalars ([0] the wg_any flag,
+// [2] the queue count).
+__device__ void deep_parse_demand(const u32 *D32, const u16 *P16, const u32 *dprev, u32 *offg, u8 *lds, u32 *misc, u32 *wsum, u32 pre, u32 nb,
+                                  u32 n, u32 lim, u32 s0, u32 depth, u32 tid, ZhWorkspace ws, u32 b, const u8 *stg) {
+  u16 *const memo = (u16 *)lds;
+  u16 *const q = (u16 *)(lds + ((2u * nb + 15u) & ~15u));
+  u32 *const exL = (u32 *)((u8 *)q + 2u * DQ_PER * DT);
+  u32 const SEGL = demand_segl(nb), nseg = (nb + SEGL - 1) / SEGL;
+  // unsearched below lim, no match at or past it (the oracle's len[] is 0 there)
+  for (u32 i = tid; i < nb; i += DT) memo[i] = pre + i < lim ? (u16)MEMO_UNK : (u16)0;
+  if (tid == 0) misc[2] = 0;
+  __syncthreads();
+  u32 const g = tid, S = SEGL * g, SE = min(S + SEGL, nb);
+  bool const sv = g < nseg;
+  u64 LM = 0, MM = 0;
+  u32 entry = S, ex = S;
+  // one walk (first or Jacobi re-walk) of every lane with act0 set; all threads take part in the
+  // search rounds.  old: the visited bits of the previous walk (re-walks).
+  auto walk = [&](u32 p0, bool act0) {
+    u64 const old = act0 ? (LM | MM) : 0ull;
+    u64 nl = 0, nm = 0;
+    bool act = act0 && p0 < SE, merged = false;
+    u32 p = p0, mpos = 0;
+    for (;;) {
+      // advance as far as the memo allows
+      u32 need = ~0u;
+      bool adv = act;
+      while (__ballot(adv)) {
+        if (adv) {
+          if (p >= SE) {
+            act = adv = false;
+          } else if ((old >> (p - S)) & 1ull) {  // met the old trajectory: the rest is the old walk's
+            merged = true;
+            mpos = p - S;
+            act = adv = false;
+          } else {
+            u32 const m0 = memo[p];
+            if (m0 == MEMO_UNK) {
+              need = p;
+              adv = false;
+            } else if ((m0 & 255u) == 0) {
+              nl |= 1ull << (p - S);
+              p++;
+            } else {
+              u32 const m1 = p + 1 < nb ? (u32)memo[p + 1] : 0u, m2 = p + 2 < nb ? (u32)memo[p + 2] : 0u;
+              if (m1 == MEMO_UNK || m2 == MEMO_UNK) {
+                need = m1 == MEMO_UNK ? p + 1 : p + 2;
+                adv = false;
+              } else {
+                int const g0 = memo_gain(m0);
+                if (memo_gain(m1) > g0 + 4 || memo_gain(m2) > g0 + 7) {  // deferred: p is a literal
+                  nl |= 1ull << (p - S);
+                  p++;
+                } else {
+                  nm |= 1ull << (p - S);
+                  p += m0 & 255u;
+                }
+              }
             }
-            l = 8 + e;
           }
         }
-        l = min(l, k.p < n ? n - k.p : 0u);
-        if (l >= ZH_MIN_MATCH_SHORT && l > k.best) {
-          k.best = l;
-          k.bo = k.p - q;
-          u32 const a = k.p + l;  // the own byte a candidate must match to beat the new best
-          ownb = (D32[a >> 2] >> (8 * (a & 3))) & 255u;
+      }
+      // post the needed position and the two after it (the lazy check's lookahead)
+      if (need != ~0u) {
+#pragma unroll
+        for (u32 t = 0; t < DQ_PER; t++) {
+          u32 const x = need + t;
+          if (x < nb && memo[x] == MEMO_UNK) q[atomicAdd(&misc[2], 1u)] = (u16)x;
         }
-        k.dd++;
-        k.c = nx;
-        k.act = k.best < ZH_MAX_MATCH && k.dd < depth && k.c != 0 && k.p - (k.c - 1u) <= ZH_DEEP_MAXOFF;
+      }
+      __syncthreads();
+      u32 const nq = misc[2];
+      if (nq == 0) break;  // (every lane has finished: no lane needed anything)
+      // search the queue, lanes = entries (a position queued twice is searched twice, same result)
+      for (u32 j0 = 0; j0 < nq; j0 += DT) {
+        u32 const j = j0 + tid;
+        bool const v = j < nq;
+        u32 const x = v ? q[j] : 0u;
+        u32 const r = deep_search_one(D32, P16, dprev, x, v, pre, nb, n, lim, s0, depth);
+        if (v) {
+          offg[x] = r;
+          u32 const l = r & 255u;
+          memo[x] = (u16)(l ? l | ((31u - (u32)__builtin_clz((r >> 8) + 1u)) << 8) : 0u);
+        }
+      }
+      __syncthreads();
+      if (tid == 0) misc[2] = 0;
+      __syncthreads();
+    }
+    if (act0) {
+      if (merged) {
+        u64 const keep = bits_from(mpos);
+        LM = nl | (LM & keep);
+        MM = nm | (MM & keep);
+      } else {
+        LM = nl;
+        MM = nm;
+        ex = p;
       }
     }
-    cur_done(k);
+  };
+  walk(entry, sv);
+  for (;;) {
+    if (sv) exL[g] = ex;
+    __syncthreads();
+    u32 const ne = g == 0 ? 0u : (sv ? exL[g - 1] : entry);
+    bool const ch = sv && ne != entry;
+    if (!wg_any(ch, &misc[0], tid)) break;
+    walk(ne, ch);
+    if (ch) entry = ne;
+  }
+  // ---- records and literals (step 5 of deep_block)
+  u32 nm_tot, nl_tot;
+  u32 const mbase = wg_excl_scan(sv ? (u32)__popcll(MM) : 0u, wsum, tid, nm_tot);
+  u32 const lbase = wg_excl_scan(sv ? (u32)__popcll(LM) : 0u, wsum, tid, nl_tot);
+  u64 *seq_out = ws.seq(b);
+  u64 mm = MM;
+  u32 j = mbase;
+  while (mm) {
+    u32 const o = (u32)__builtin_ctzll(mm);
+    mm &= mm - 1ull;
+    u32 const m = S + o;
+    u32 const cum = lbase + (u32)__popcll(LM & ~bits_from(o));
+    u32 const r = offg[m];
+    seq_out[j++] = (u64)cum | ((u64)(r & 255u) << 17) | ((u64)(r >> 8) << 36);
+  }
+  // literals: every lane its segment's literal bytes (SEGL <= 64 positions)
+  u8 *lit_out = ws.lits(b);
+  if (sv) {
+    u64 lm = LM;
+    u32 k = lbase;
+    while (lm) {
+      u32 const o = (u32)__builtin_ctzll(lm);
+      lm &= lm - 1ull;
+      lit_out[k++] = stg[pre + S + o];
+    }
+  }
+  if (tid == 0) {
+    u32 *meta = ws.meta(b);
+    meta[0] = nm_tot;
+    meta[1] = nl_tot;
+    meta[2] = 0;
   }
 }
 
@@ -420,6 +575,16 @@ __device__ void deep_block(const ZhBlockDesc &d, ZhWorkspace ws, u32 b, u8 *slot
     for (u32 v = tid; 16 * v < n + 80; v += DT) *(uint4 *)(smem + e16 + 16 * v) = *(const uint4 *)(stg + 16 * v);
   __threadfence_block();
   __syncthreads();
+#ifndef ZH_DEEP_NO_DEMAND
+  // demand-driven search + parse when the memo fits beside the links and bytes in LDS
+  u32 const dbase = e16 + ((n + 96 + 15) & ~15u);
+  if (d_lds && dbase + demand_lds(nb) <= SEARCH_LDS) {
+    deep_parse_demand((const u32 *)(smem + e16), (const u16 *)smem, dprev, offg, smem + dbase, misc, wsum, pre, nb, n, lim, s0, depth, tid, ws, b,
+                      stg);
+    DSTAMP(4);
+    return;
+  }
+#endif
   // typed LDS / global variants (a generic pointer makes every access a flat one: measured slower
   // than global memory)
   if (d_lds) deep_search<true, true>(s32, (const u16 *)(slot + SLOT_P16), e16, dprev, offg, pre, nb, n, lim, s0, depth, tid);

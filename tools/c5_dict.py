@@ -20,7 +20,8 @@ sys.path.insert(0, os.path.join(ROOT, "custom-nvcomp-with-zstd_amd"))
 import cuda_zstd  # noqa: E402
 import zh_testlib as T  # noqa: E402
 
-REC, N, SEED, LEVEL, DICT = 16384, 4096, 0x5EED0005, 9, 65536
+REC, N, SEED, DICT = 16384, 4096, 0x5EED0005, 65536
+LEVEL = int(os.environ.get("C5_LEVEL", "9"))
 vp = ctypes.c_void_p
 
 
