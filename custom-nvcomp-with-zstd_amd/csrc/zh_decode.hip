@@ -386,7 +386,7 @@ __device__ __forceinline__ u32 umod(u32 m, u32 d) {
 // ---- Huffman ------------------------------------------------------------------------------
 // HUF_readStats (libzstd lib/common/entropy_common.c) on lane 0: weights -> L.hufw, L.hlog,
 // L.hnsym.  Returns the header bytes consumed, 0 on error.
-__device__ u32 huf_read_weights(DecLds &L, const u8 *p, u32 avail) {
+__device__ __noinline__ u32 huf_read_weights(DecLds &L, const u8 *p, u32 avail) {
   if (avail < 1) return 0;
   u32 const hb = p[0];
   u32 nw = 0, used;
@@ -447,7 +447,7 @@ __device__ u32 huf_read_weights(DecLds &L, const u8 *p, u32 avail) {
 
 // HUF_readDTableX1 fill, lane-parallel: weight classes in ascending weight order, symbols
 // ascending inside a class, 2^(w-1) entries per symbol.
-__device__ void huf_build_dtable(DecLds &L) {
+__device__ __forceinline__ void huf_build_dtable(DecLds &L) {
   u32 const lane = lane_id();
   u32 const tlog = uni(L.hlog);
   u32 w4[4];
@@ -701,7 +701,7 @@ __device__ u32 decode_literals(DecLds &L, const u8 *bp, u32 bsz, const Slot &sl,
 
 // One sequence table (mode 0 predefined, 1 RLE, 2 FSE, 3 repeat) on lane 0.
 // Returns bytes consumed (>= 0) or -1 on error.
-__device__ s32 seq_table(DecLds &L, u32 t, u32 mode, const u8 *p, u32 avail) {
+__device__ __noinline__ s32 seq_table(DecLds &L, u32 t, u32 mode, const u8 *p, u32 avail) {
   u32 *T = L.fse + tab_off(t);
   u32 const maxSV = tab_maxsv(t);
   if (mode == 0) {
@@ -739,7 +739,7 @@ __device__ s32 seq_table(DecLds &L, u32 t, u32 mode, const u8 *p, u32 avail) {
 // Formatted dictionary (RFC 8878 §5): its Huffman table and OF / ML / LL FSE tables become
 // the frame's previous tables (treeless literals and repeat modes use them).  Lane 0; false
 // when they do not parse.  d = the dictionary, off = its content offset.
-__device__ bool load_dict_entropy(DecLds &L, const u8 *d, u32 off) {
+__device__ __forceinline__ bool load_dict_entropy(DecLds &L, const u8 *d, u32 off) {
   if (off < 8 + 12) return false;
   const u8 *const p = d + 8;
   u32 const avail = off - 8 - 12;

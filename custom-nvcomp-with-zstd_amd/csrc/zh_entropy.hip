@@ -1012,7 +1012,7 @@ __device__ u32 huf_write_ctable_wave(u8 *hbuf, u8 *w, const u8 *hnb, u32 maxSV, 
 // Wave copy of n bytes to o[pos..]: byte head up to a 4-B aligned destination, then
 // dword stores (source realigned with alignbyte, 8 independent loads per lane in
 // flight), byte tail; bytes at or past o.cap are dropped like Out::put does.
-__device__ __forceinline__ void copy_bytes(const Out &o, u32 pos, const u8 *src, u32 n) {
+__device__ __forceinline__ void copy_bytes4(const Out &o, u32 pos, const u8 *src, u32 n) {
   u32 const lane = lane_id();
   u8 *const d0 = o.dst + pos;
   u32 const h = min((u32)((4u - ((uintptr_t)d0 & 3u)) & 3u), n);
@@ -1046,6 +1046,62 @@ __device__ __forceinline__ void copy_bytes(const Out &o, u32 pos, const u8 *src,
   }
   if (lane < h) o.put(pos + lane, src[lane]);
   for (u32 i = h + 4 * lim + lane; i < n; i += 64) o.put(pos + i, src[i]);
+}
+
+// Large copies (raw blocks, raw literals): 16-B aligned stores, each from the one or two
+// aligned 16-B source chunks holding its bytes (a chunk holding a needed byte never crosses a
+// page), funnel-shifted by the source's offset; CP16_U stores per lane in flight.
+#ifndef ZH_CP16_U
+#define ZH_CP16_U 4
+#endif
+__device__ __forceinline__ uint4 funnel16(uint4 a, uint4 b, u32 sa) {
+  // bytes [sa, sa + 16) of the 32-byte a:b (sa wave-uniform; selects, no indexed array)
+  u32 const q = sa >> 2, r = sa & 3u;
+  u32 const w0 = q == 0 ? a.x : q == 1 ? a.y : q == 2 ? a.z : a.w;
+  u32 const w1 = q == 0 ? a.y : q == 1 ? a.z : q == 2 ? a.w : b.x;
+  u32 const w2 = q == 0 ? a.z : q == 1 ? a.w : q == 2 ? b.x : b.y;
+  u32 const w3 = q == 0 ? a.w : q == 1 ? b.x : q == 2 ? b.y : b.z;
+  u32 const w4 = q == 0 ? b.x : q == 1 ? b.y : q == 2 ? b.z : b.w;
+  return make_uint4(__builtin_amdgcn_alignbyte(w1, w0, r), __builtin_amdgcn_alignbyte(w2, w1, r), __builtin_amdgcn_alignbyte(w3, w2, r),
+                    __builtin_amdgcn_alignbyte(w4, w3, r));
+}
+__device__ __forceinline__ void copy_bytes16(const Out &o, u32 pos, const u8 *src, u32 n) {
+  u32 const lane = lane_id();
+  u8 *const d0 = o.dst + pos;
+  u32 const hb = min((u32)((16u - ((uintptr_t)d0 & 15u)) & 15u), n);  // bytes before a 16-B boundary
+  u32 const nc = (n - hb) >> 4;
+  u32 const capc = o.cap > pos + hb ? (o.cap - pos - hb) >> 4 : 0u;
+  u32 const lim = min(nc, capc);
+  const u8 *const s = src + hb;
+  u32 const sa = (u32)((uintptr_t)s & 15u);
+  const uint4 *const s16 = (const uint4 *)(s - sa);
+  uint4 *const dd = (uint4 *)(d0 + hb);
+  constexpr u32 U = ZH_CP16_U;
+  for (u32 c0 = 0; c0 < lim; c0 += 64 * U) {
+    uint4 a[U], b2[U];
+#pragma unroll
+    for (u32 u = 0; u < U; u++) {
+      u32 const c = c0 + 64 * u + lane;
+      if (c < lim) {
+        a[u] = s16[c];
+        b2[u] = sa ? s16[c + 1] : a[u];
+      }
+    }
+#pragma unroll
+    for (u32 u = 0; u < U; u++) {
+      u32 const c = c0 + 64 * u + lane;
+      if (c < lim) dd[c] = sa ? funnel16(a[u], b2[u], sa) : a[u];
+    }
+  }
+  if (lane < hb) o.put(pos + lane, src[lane]);
+  for (u32 i = hb + 16 * lim + lane; i < n; i += 64) o.put(pos + i, src[i]);
+}
+#ifndef ZH_COPY16
+#define ZH_COPY16 1
+#endif
+__device__ __forceinline__ void copy_bytes(const Out &o, u32 pos, const u8 *src, u32 n) {
+  if (ZH_COPY16) copy_bytes16(o, pos, src, n);
+  else copy_bytes4(o, pos, src, n);
 }
 
 }  // namespace

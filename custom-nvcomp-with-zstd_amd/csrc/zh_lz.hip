@@ -61,6 +61,9 @@ namespace {
 #ifndef ZH_FIRST_WALK_PLAIN
 #define ZH_FIRST_WALK_PLAIN 0
 #endif
+#ifndef ZH_WALK_V2
+#define ZH_WALK_V2 0
+#endif
 constexpr u32 K1_THREADS = 1024;
 constexpr u32 NROUND = ZH_WINDOW / 64;      // 64-position length rounds per window
 constexpr u32 SEGP = 32;                    // positions per walk segment (one lane of wave 0)
@@ -612,6 +615,28 @@ __device__ __forceinline__ void seg_walk(const u32 *ci, u32 tmk, u32 S, u32 SE, 
   u32 nl = 0, nm = 0;
   bool act = act0 && p < SE, merged = false;
   u32 mpos = 0;
+#if ZH_WALK_V2
+  if constexpr (!REWALK) {
+    // the first walk: the shortest dependent chain per step (shift, ctz, the length's LDS read,
+    // add); a lane's state stops changing once it leaves the segment
+    while (__ballot(act)) {
+      u32 const o = p - S;                          // (< 32 on active lanes)
+      u32 const q = p + __builtin_ctzg(tmk >> o, 32);  // next take position (>= SE: none)
+      bool const st = act && q < SE;
+      u32 const len = ci[cidx(q)] & 255u;           // (q <= S + 63: inside the cinfo buffers)
+      nl |= act ? bit_range32(o, min(q, SE) - S) : 0u;
+      nm |= st ? 1u << (q - S) : 0u;
+      p = act ? (st ? q + len : SE) : p;
+      act = act && p < SE;
+    }
+    if (act0) {
+      LM = nl;
+      MM = nm;
+      ex = p;
+    }
+    return;
+  }
+#endif
   // branch-free steps (selects, no exec-mask branches): each is one literal run and the
   // position after it, or the point where the walk meets the old one
   while (__ballot(act)) {

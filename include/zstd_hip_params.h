@@ -30,7 +30,7 @@
 #define ZH_WINDOW 2048              /* parse window (positions); catch-up stays inside one */
 #define ZH_SKIP_TILES 2             /* tiles a window searches after a window without matches (miss skip) */
 #ifndef ZH_PROBE_WINDOWS
-#define ZH_PROBE_WINDOWS 2          /* a block whose parse takes no match in its first windows is all literals */
+#define ZH_PROBE_WINDOWS 1          /* a block whose parse takes no match in its first windows is all literals */
 #endif
 #define ZH_HASH_LOG_LONG 14         /* 8-byte hash table: 2^14 u16 entries */
 #define ZH_HASH_LOG_SHORT 14        /* 5-byte hash table: 2^14 u16 entries */

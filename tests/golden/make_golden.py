@@ -133,7 +133,8 @@ def block_cases():
     out = []
     for name, kind, size, seed in [("text", T.DG_TEXT, 8192, 1), ("csv", T.DG_CSV, 6000, 2), ("json", T.DG_JSON, 8192, 3),
                                    ("exe", T.DG_EXE, 5000, 4), ("sensor", T.DG_SENSOR, 8192, 5), ("source", T.DG_SOURCE, 7000, 6),
-                                   ("sym16", T.DG_SYM16, 4096, 7), ("text_small", T.DG_TEXT, 700, 8)]:
+                                   ("sym16", T.DG_SYM16, 4096, 7), ("text_small", T.DG_TEXT, 700, 8),
+                                   ("sym16_seq", T.DG_SYM16, 4096, 10)]:  # (sym16 seed 7: no match in the probe window)
         out.append(_block_case(o, cc, name, T.gen(kind, 1, seed, size), False))
     for kname in ("mix", "text", "exe", "sensor", "json", "csv", "source", "sym16"):
         for first in (0, 5):

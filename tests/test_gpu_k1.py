@@ -168,13 +168,15 @@ def test_k1_probe_vs_oracle():
         names.append(nm)
         datas.append(np.ascontiguousarray(d, dtype=np.uint8))
 
-    for cut in (W - 1, 2 * W - 200, 2 * W, 2 * W + 1, 3 * W):
+    # (boundaries of one and of two probe windows)
+    for cut in (W - 200, W - 1, W, W + 1, 2 * W - 200, 2 * W, 2 * W + 1, 3 * W):
         add(f"rand{cut}+text", np.concatenate([rnd[:cut], text[:BLOCK - cut]]))
     add("text4k+rand+text", np.concatenate([text[:4096], rnd[:40960], text[4096:24576]]))
-    half = rnd[:2 * W].copy()
-    half[W + 100:W + 400] = half[100:400]  # one repeat inside the probe windows
-    add("rand+repeat_in_probe", np.concatenate([half, rnd[2 * W:]]))
-    for n in (2 * W + 8, 2 * W + 9, 3 * W + 8, 3 * W + 9, 5000):
+    for at in (1100, W + 100):  # one repeat inside the first window / inside the second
+        half = rnd[:2 * W].copy()
+        half[at:at + 300] = half[100:400]
+        add(f"rand+repeat@{at}", np.concatenate([half, rnd[2 * W:]]))
+    for n in (W + 8, W + 9, 2 * W + 8, 2 * W + 9, 3 * W + 8, 3 * W + 9, 5000):
         add(f"rand_{n}", rnd[:n])
     _compare(datas, names)
 
