@@ -16,6 +16,9 @@
 
 namespace {
 
+#ifndef ZH_K2_PAIR
+#define ZH_K2_PAIR 1  // the record pass two chunks per iteration
+#endif
 #ifndef ZH_HIST_PF
 #define ZH_HIST_PF 1  // literal histogram: next step's loads before this step's atomics
 #endif
@@ -49,7 +52,10 @@ constexpr u32 U_FSE_END = OFF_WTS + 256;
 constexpr u32 K2_WAVE_LDS = (U_HUF_END > U_FSE_END ? U_HUF_END : U_FSE_END);  // one wave's layout
 static_assert(K2_WAVE_LDS < 16384, "K2 LDS budget");
 constexpr u32 K2_W1 = (K2_WAVE_LDS - OFF_MISC + 15) & ~15u;  // wave 1's layout base
-constexpr u32 K2_LDS = K2_W1 + K2_WAVE_LDS;
+#ifndef ZH_K2_LDS_PAD
+#define ZH_K2_LDS_PAD 0  // (occupancy experiments: extra LDS per block)
+#endif
+constexpr u32 K2_LDS = K2_W1 + K2_WAVE_LDS + ZH_K2_LDS_PAD;
 
 __constant__ u8 c_LL_bits[36] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 1, 1, 1, 1, 2, 2, 3, 3, 4, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16};
 __constant__ u8 c_ML_bits[53] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0,
@@ -1457,7 +1463,7 @@ extern "C" __global__ __launch_bounds__(K2_THREADS) void zh_entropy_kernel(const
       CodeTabs ct;
       ct.load();
       // sequences nbSeq + [0, m) in lanes [0, m)
-      auto sequences = [&](u32 m, u32 ll, u32 ml, u32 off) {
+      auto sequences_c = [&](u32 m, u32 ll, u32 ml, u32 off, u32 llc, u32 mlc) {
         u32 const i = nbSeq + lane;
         bool const valid = lane < m;
         u32 r0 = wave_shr1(off);
@@ -1484,7 +1490,6 @@ extern "C" __global__ __launch_bounds__(K2_THREADS) void zh_entropy_kernel(const
         cr1 = lane_value(n1, lastLane);
         cr2 = lane_value(n2, lastLane);
         u32 const mlb = ml - 3;
-        u32 const llc = ct.ll_code(ll), mlc = ct.ml_code(mlb);
         if (valid) {
           atomicAdd(&hLL[llc], 1u);
           atomicAdd(&hML[mlc], 1u);
@@ -1494,10 +1499,84 @@ extern "C" __global__ __launch_bounds__(K2_THREADS) void zh_entropy_kernel(const
         }
         nbSeq += m;
       };
+      auto sequences = [&](u32 m, u32 ll, u32 ml, u32 off) { sequences_c(m, ll, ml, off, ct.ll_code(ll), ct.ml_code(ml - 3)); };
       u32 carryCum = 0, carryOff = 0, openLL = 0, openMl = 0, openOff = 0;
       bool open = false;
       RecRing ring;  // records loaded RING_DEPTH chunks ahead (a chunk writes only indices < its end)
       ring.init(seq, nseq_raw, lane);
+#if ZH_K2_PAIR
+      // Two chunks per iteration: the second chunk's run analysis, its permutes and both
+      // chunks' code lookups depend only on records (not on the first chunk's results), so
+      // their LDS round trips overlap; the open run and the repcodes pass on in order.
+      struct Chunk { u32 ll, off, runMl, incl, cum; u64 hm; bool head; };
+      auto analyse = [&](u64 rec, u32 i, u32 pc0, u32 po0, Chunk &c) {
+        bool const valid = i < nseq_raw;
+        u32 const cum = (u32)(rec & 0x1FFFFu), ce = (u32)((rec >> 24) & 0xFFFu);
+        u32 const ml = (u32)((rec >> 17) & 0x7Fu) + ce, off = (u32)((rec >> 36) & 0x1FFFFu);
+        u32 pc = wave_shr1(cum), po = wave_shr1(off);
+        if (lane == 0) { pc = pc0; po = po0; }
+        u32 const ll = cum - pc - ce;
+        bool const flag = valid && i > 0 && ll == 0 && off == po;
+        bool const head = valid && !flag;
+        u64 const hm = __ballot(head);
+        u32 const mlv = valid ? ml : 0u;
+        u32 const incl = wave_scan_incl(mlv);
+        u64 const headBitsAfter = hm & ~((lane == 63) ? ~0ull : ((2ull << lane) - 1));
+        u32 const runEnd = headBitsAfter ? (u32)__builtin_ctzll(headBitsAfter) - 1u : 63u;
+        u32 const inclEnd = (u32)__builtin_amdgcn_ds_bpermute((int)(runEnd << 2), (int)incl);
+        c.runMl = inclEnd - (incl - mlv);
+        c.ll = ll; c.off = off; c.incl = incl; c.cum = cum; c.hm = hm; c.head = head;
+      };
+      // the chunk's runs to lanes hp + rank (ds_permute, as in the single-chunk step below)
+      auto gather = [&](const Chunk &c, u32 hp, u32 &sll, u32 &sml, u32 &soff) {
+        u32 const hcount = (u32)__popcll(c.hm), rank = (u32)__popcll(c.hm & below);
+        u32 const dest = c.head ? rank + hp : (hcount + hp + (lane - rank)) & 63u;
+        sll = (u32)__builtin_amdgcn_ds_permute((int)(dest << 2), (int)c.ll);
+        sml = (u32)__builtin_amdgcn_ds_permute((int)(dest << 2), (int)c.runMl);
+        soff = (u32)__builtin_amdgcn_ds_permute((int)(dest << 2), (int)c.off);
+      };
+      // open-run state through the chunk; returns the sequences it closes (lanes [0, m))
+      auto advance = [&](const Chunk &c, u32 &sll, u32 &sml, u32 &soff) {
+        u32 const hcount = (u32)__popcll(c.hm);
+        u32 const firstH = c.hm ? (u32)__builtin_ctzll(c.hm) : 64u;
+        openMl += firstH ? lane_value(c.incl, firstH - 1u) : 0u;
+        if (!hcount) return 0u;
+        u32 const hp = open ? 1u : 0u;
+        if (hp && lane == 0) { sll = openLL; sml = openMl; soff = openOff; }
+        int const lastH = 63 - __builtin_clzll(c.hm);
+        openLL = lane_value(c.ll, (u32)lastH);
+        openOff = lane_value(c.off, (u32)lastH);
+        openMl = lane_value(c.runMl, (u32)lastH);
+        open = true;
+        return hp + hcount - 1;
+      };
+      for (u32 base = 0; base < nseq_raw; base += 128) {
+        bool const two = base + 64 < nseq_raw;  // (then chunk A is full)
+        u64 const recA = ring.next(seq, nseq_raw, base + lane);
+        u64 const recB = two ? ring.next(seq, nseq_raw, base + 64 + lane) : 0ull;
+        Chunk A, B;
+        analyse(recA, base + lane, carryCum, carryOff, A);
+        u32 const cA = lane_value(A.cum, 63), oA = lane_value(A.off, 63);
+        if (two) analyse(recB, base + 64 + lane, cA, oA, B);
+        u32 const lastLane = two ? min(63u, nseq_raw - 1 - (base + 64)) : min(63u, nseq_raw - 1 - base);
+        carryCum = two ? lane_value(B.cum, lastLane) : lane_value(A.cum, lastLane);
+        carryOff = two ? lane_value(B.off, lastLane) : lane_value(A.off, lastLane);
+        u32 const hpA = open ? 1u : 0u, hpB = (open || A.hm) ? 1u : 0u;
+        u32 aL = 0, aM = 0, aO = 0, bL = 0, bM = 0, bO = 0;
+        if (A.hm) gather(A, hpA, aL, aM, aO);
+        if (two && B.hm) gather(B, hpB, bL, bM, bO);
+        u32 const mA = advance(A, aL, aM, aO);
+        u32 const aLc = ct.ll_code(aL), aMc = ct.ml_code(aM - 3);
+        u32 mB = 0, bLc = 0, bMc = 0;
+        if (two) {
+          mB = advance(B, bL, bM, bO);
+          bLc = ct.ll_code(bL);
+          bMc = ct.ml_code(bM - 3);
+        }
+        if (mA) sequences_c(mA, aL, aM, aO, aLc, aMc);
+        if (mB) sequences_c(mB, bL, bM, bO, bLc, bMc);
+      }
+#else
       for (u32 base = 0; base < nseq_raw; base += 64) {
         u32 const i = base + lane;
         bool const valid = i < nseq_raw;
@@ -1546,6 +1625,7 @@ extern "C" __global__ __launch_bounds__(K2_THREADS) void zh_entropy_kernel(const
         carryCum = lane_value(cum, lastLane);
         carryOff = lane_value(off, lastLane);
       }
+#endif
       if (open) sequences(1, openLL, openMl, openOff);
       wave_sync();
     }

@@ -28,7 +28,7 @@ for v in B $VARIANTS; do
   CUDA_ZSTD_HIP_LIB=$L timeout -k 10 400 python3 -u -m pytest $R/tests/test_gpu_k1.py $R/tests/test_gpu_parity.py -x -q --timeout 120 --timeout-method thread -k "$K" > $R/gpurun_out/${TAG}_tests$v.log 2>&1 || { tail -30 $R/gpurun_out/${TAG}_tests$v.log; exit 1; }
   echo "tests $v: $(tail -1 $R/gpurun_out/${TAG}_tests$v.log)"
 done
-for k in 1 2 3; do
+for k in $(seq 1 ${ROUNDS:-3}); do
   for v in $VS; do
     if [ $v = A ]; then L=$P/libcuda_zstd_hip.so; elif [ $v = B ]; then L=$R/tools/libB.so; else L=$R/tools/libV_$v.so; fi
     CUDA_ZSTD_HIP_LIB=$L timeout -k 10 200 python3 $R/bench.py --steps 8 --warmup 2 --no-cpu-baseline --no-verify --no-decompress --no-legs > $R/gpurun_out/${TAG}_${v}${k}.json 2>/dev/null
