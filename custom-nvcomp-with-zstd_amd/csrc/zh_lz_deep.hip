@@ -343,6 +343,10 @@ __device__ void deep_parse_demand(const u32 *D32, const u16 *P16, const u32 *dpr
   __syncthreads();
   u32 const g = tid, S = SEGL * g, SE = min(S + SEGL, nb);
   bool const sv = g < nseg;
+#ifdef ZH_STAMPS
+  u64 const dm0 = __builtin_amdgcn_s_memtime();
+  u32 st_rounds = 0, st_searched = 0, st_walk = 0, st_jac = 0;
+#endif
   u64 LM = 0, MM = 0;
   u32 entry = S, ex = S;
   // one walk (first or Jacobi re-walk) of every lane with act0 set; all threads take part in the
@@ -402,6 +406,10 @@ __device__ void deep_parse_demand(const u32 *D32, const u16 *P16, const u32 *dpr
       __syncthreads();
       u32 const nq = misc[2];
       if (nq == 0) break;  // (every lane has finished: no lane needed anything)
+#ifdef ZH_STAMPS
+      st_rounds++;
+      st_searched += nq;
+#endif
       // search the queue, lanes = entries (a position queued twice is searched twice, same result)
       for (u32 j0 = 0; j0 < nq; j0 += DT) {
         u32 const j = j0 + tid;
@@ -431,6 +439,9 @@ __device__ void deep_parse_demand(const u32 *D32, const u16 *P16, const u32 *dpr
     }
   };
   walk(entry, sv);
+#ifdef ZH_STAMPS
+  st_walk = (u32)(__builtin_amdgcn_s_memtime() - dm0);
+#endif
   for (;;) {
     if (sv) exL[g] = ex;
     __syncthreads();
@@ -440,6 +451,10 @@ __device__ void deep_parse_demand(const u32 *D32, const u16 *P16, const u32 *dpr
     walk(ne, ch);
     if (ch) entry = ne;
   }
+#ifdef ZH_STAMPS
+  st_jac = (u32)(__builtin_amdgcn_s_memtime() - dm0) - st_walk;
+  if (tid == 0) { u32 *dbg = ws.dbg(b); dbg[20] = st_rounds; dbg[21] = st_searched; dbg[22] = st_walk; dbg[23] = st_jac; }
+#endif
   // ---- records and literals (step 5 of deep_block)
   u32 nm_tot, nl_tot;
   u32 const mbase = wg_excl_scan(sv ? (u32)__popcll(MM) : 0u, wsum, tid, nm_tot);
@@ -579,6 +594,7 @@ __device__ void deep_block(const ZhBlockDesc &d, ZhWorkspace ws, u32 b, u8 *slot
   // demand-driven search + parse when the memo fits beside the links and bytes in LDS
   u32 const dbase = e16 + ((n + 96 + 15) & ~15u);
   if (d_lds && dbase + demand_lds(nb) <= SEARCH_LDS) {
+    DSTAMP(2);  // (search set-up: link distances and bytes in LDS)
     deep_parse_demand((const u32 *)(smem + e16), (const u16 *)smem, dprev, offg, smem + dbase, misc, wsum, pre, nb, n, lim, s0, depth, tid, ws, b,
                       stg);
     DSTAMP(4);

@@ -54,3 +54,9 @@ for use in (False, True):
     print("dict" if use else "no dict", "nseq mean", m[:, 0].mean(), "mean cycles/record", int(st[:, 4].mean()), "fix-up steps", fix)
     for k, nm in enumerate(names):
         print(f"  {nm:12s} {ph[:, k].mean():10.0f}  {ph[:, k].mean() / st[:, 4].mean() * 100:5.1f}%")
+    # demand-driven path (dbg[20..23] = m[24..28]): search rounds, positions searched, first walk, Jacobi
+    dm = m[:, 24:28].astype(np.float64)
+    if dm[:, 0].any():
+        print(f"  demand path: search rounds {dm[:, 0].mean():.1f}, positions searched {dm[:, 1].mean():.0f} of {REC}"
+              f" ({dm[:, 1].mean() / REC * 100:.1f}%), first walk {dm[:, 2].mean():.0f} cycles, Jacobi {dm[:, 3].mean():.0f}"
+              " (search+take+walk above = set-up; emit = walk + Jacobi + records)")
