@@ -55,15 +55,6 @@ extern "C" u32 zh_fixups_host() {
 #endif
 namespace {
 
-#ifndef ZH_PARSE_PRIO
-#define ZH_PARSE_PRIO 0
-#endif
-#ifndef ZH_FIRST_WALK_PLAIN
-#define ZH_FIRST_WALK_PLAIN 0
-#endif
-#ifndef ZH_WALK_V2
-#define ZH_WALK_V2 0
-#endif
 constexpr u32 K1_THREADS = 1024;
 constexpr u32 NROUND = ZH_WINDOW / 64;      // 64-position length rounds per window
 constexpr u32 SEGP = 32;                    // positions per walk segment (one lane of wave 0)
@@ -615,10 +606,11 @@ __device__ __forceinline__ void seg_walk(const u32 *ci, u32 tmk, u32 S, u32 SE, 
   u32 nl = 0, nm = 0;
   bool act = act0 && p < SE, merged = false;
   u32 mpos = 0;
-#if ZH_WALK_V2
   if constexpr (!REWALK) {
     // the first walk: the shortest dependent chain per step (shift, ctz, the length's LDS read,
-    // add); a lane's state stops changing once it leaves the segment
+    // add); a lane's state stops changing once it leaves the segment.  (Round 4: the first walk
+    // through the re-walk's step, with its merge test, cost wave 0 191 k cycles per block for
+    // walk + Jacobi, this one 161 k; K1 11.75 -> 11.50 ms.)
     while (__ballot(act)) {
       u32 const o = p - S;                          // (< 32 on active lanes)
       u32 const q = p + __builtin_ctzg(tmk >> o, 32);  // next take position (>= SE: none)
@@ -636,23 +628,22 @@ __device__ __forceinline__ void seg_walk(const u32 *ci, u32 tmk, u32 S, u32 SE, 
     }
     return;
   }
-#endif
   // branch-free steps (selects, no exec-mask branches): each is one literal run and the
   // position after it, or the point where the walk meets the old one
+  // (as the first walk's step; no take bit left: q >= SE, no old bit: x = p + 64 > q)
   while (__ballot(act)) {
-    u32 const o = min(p - S, SEGP - 1);
-    u32 const m = tmk >> o, ov = old >> o;
-    u32 const q = m ? p + (u32)__builtin_ctz(m) : SE;
-    u32 const x = ov ? p + (u32)__builtin_ctz(ov) : ~0u;
+    u32 const o = p - S;
+    u32 const q = p + __builtin_ctzg(tmk >> o, 32);
+    u32 const x = p + __builtin_ctzg(old >> o, 64);
     bool const mg = act && x <= q;
     bool const st = act && !mg && q < SE;
-    u32 const re = mg ? x : q;
+    u32 const re = mg ? x : min(q, SE);
     nl |= act ? bit_range32(o, re - S) : 0u;
-    u32 const len = ci[cidx(st ? q : 0u)] & 255u;
+    u32 const len = ci[cidx(q)] & 255u;
     nm |= st ? 1u << (q - S) : 0u;
     mpos = mg ? x - S : mpos;
     merged = merged || mg;
-    p = mg ? p : (st ? q + len : (act ? q : p));
+    p = (act && !mg) ? (st ? q + len : SE) : p;
     act = act && !mg && p < SE;
   }
   if (act0) {
@@ -1062,16 +1053,13 @@ __device__ __forceinline__ u32 lz_block(const ZhBlockDesc *__restrict__ blocks, 
     }
     if (wave == 0 && prev) {
       // ---- the parse of window k - 1, lanes = 32-position segments
-#if ZH_PARSE_PRIO
-      __builtin_amdgcn_s_setprio(ZH_PARSE_PRIO);  // the parse's dependent chain before the length waves' issue
-#endif
       u32 const wn = wep - wsp;
       u32 const S = SEGP * lane, SE = min(S + SEGP, wn);
       u32 const tmk = (u32)(tmP[lane >> 1] >> (32 * (lane & 1)));
       u32 const e0 = e_in - wsp;  // first parsed position (< 64 except in the window holding `pre`)
       u32 entry = lane == 0 ? e0 : max(S, e0), ex = entry;
       u32 LM = 0, MM = 0;
-      seg_walk<!ZH_FIRST_WALK_PLAIN>(ciP, tmk, S, SE, entry, true, LM, MM, ex);
+      seg_walk<false>(ciP, tmk, S, SE, entry, true, LM, MM, ex);
       // Jacobi rounds: a segment's entry is its predecessor's exit
       for (;;) {
         u32 const pe = wave_shr1(ex);
@@ -1118,9 +1106,6 @@ __device__ __forceinline__ u32 lz_block(const ZhBlockDesc *__restrict__ blocks, 
       }
       nwalk_tot += nwl;  // the window's walk literals (its last match may run past its end)
       if (lane == 0) { misc[MISC_WNM + (kb ^ 1u)] = nm; misc[MISC_NM + ((k - 1) & 3)] = nm; }
-#if ZH_PARSE_PRIO
-      __builtin_amdgcn_s_setprio(0);
-#endif
       ZH_STAMP(st_J);
     }
     if (wave == REC_WAVE && prev2) {

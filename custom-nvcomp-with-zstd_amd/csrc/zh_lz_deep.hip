@@ -52,6 +52,12 @@ constexpr u32 L_MM = L_LM + 8 * NSEG;      // u64 match-start bits per segment
 constexpr u32 L_EX = L_MM + 8 * NSEG;      // u32 walk exit per segment
 constexpr u32 L_LP = L_EX + 4 * NSEG;      // u32 literals before the segment
 constexpr u32 L_MP = L_LP + 4 * NSEG;      // u32 matches before the segment
+#ifndef ZH_DEEP_B64
+#define ZH_DEEP_B64 0
+#endif
+#ifndef ZH_DEEP_PIPE
+#define ZH_DEEP_PIPE 0
+#endif
 constexpr u32 DEEP_LDS = 160 * 1024;
 constexpr u32 L_WS = DEEP_LDS - 256;       // u32[32] per-wave sums
 constexpr u32 L_MISC = L_WS + 4 * 32;      // u32[8]: [0] block_any flag, [1] next block
@@ -251,6 +257,67 @@ __device__ __forceinline__ u32 deep_search_one(const u32 *D32, const u16 *P16, c
     for (u32 j = 0; j < 16; j++) O[j] = __builtin_amdgcn_alignbyte(R[j + 1], R[j], sh);
   }
   u32 ownb = 0;  // own byte at p + best (best >= 8)
+#if ZH_DEEP_PIPE
+  // Software-pipelined chain walk: the next candidate's link, first 8 bytes and filter byte are
+  // loaded while this one is compared.  The filter byte of a candidate is read at the best length
+  // when it was issued: a mismatch there still proves the candidate cannot beat the (only ever
+  // longer) current best.
+  u32 q = act ? c - 1u : 0u, nx = 0, clo = 0, chi = 0;
+  bool wv = true;
+  if (act) {
+    nx = link(q);
+    g64(D32, q, clo, chi);
+  }
+  while (__ballot(act)) {
+    if (act) {
+      bool const more = nx != 0 && dd + 1u < depth && p - (nx - 1u) <= ZH_DEEP_MAXOFF;
+      u32 const qn = more ? nx - 1u : q;
+      u32 const nxn = more ? link(qn) : 0u;
+      u32 clon, chin;
+      g64(D32, qn, clon, chin);
+      u32 const bi = best, oi = ownb;
+      u32 wbn = 0;
+      if (bi >= 8) {
+        u32 const bb = qn + bi;
+        wbn = (D32[bb >> 2] >> (8 * (bb & 3))) & 255u;
+      }
+      u32 l = 0;
+      if (wv) {
+        u32 const x = O[0] ^ clo, y = O[1] ^ chi;
+        l = x ? (u32)__builtin_ctz(x) >> 3 : y ? 4u + ((u32)__builtin_ctz(y) >> 3) : 8u;
+        if (l == 8 && p + 8 < n) {
+          u32 const sq = q & 3;
+          u32 e = 56;
+          u32 B[15];
+          u32 const wq = (q >> 2) + 2;
+#pragma unroll
+          for (u32 k = 0; k < 15; k++) B[k] = D32[wq + k];
+#pragma unroll
+          for (int j = 13; j >= 0; j--) {
+            u32 const xx = O[j + 2] ^ __builtin_amdgcn_alignbyte(B[j + 1], B[j], sq);
+            if (xx) e = 4 * (u32)j + ((u32)__builtin_ctz(xx) >> 3);
+          }
+          l = 8 + e;
+        }
+      }
+      l = min(l, p < n ? n - p : 0u);
+      if (l >= ZH_MIN_MATCH_SHORT && l > best) {
+        best = l;
+        bo = p - q;
+        u32 const a = p + l;
+        ownb = (D32[a >> 2] >> (8 * (a & 3))) & 255u;
+      }
+      dd++;
+      q = qn;
+      nx = nxn;
+      clo = clon;
+      chi = chin;
+      wv = bi < 8 || wbn == oi;
+      act = best < ZH_MAX_MATCH && more;
+    }
+  }
+  return bo << 8 | best;
+#endif
   while (__ballot(act)) {
     if (act) {
       u32 const q = c - 1u;
@@ -267,16 +334,52 @@ __device__ __forceinline__ u32 deep_search_one(const u32 *D32, const u16 *P16, c
         u32 const x = O[0] ^ clo, y = O[1] ^ chi;
         l = x ? (u32)__builtin_ctz(x) >> 3 : y ? 4u + ((u32)__builtin_ctz(y) >> 3) : 8u;
         if (l == 8 && p + 8 < n) {
-          u32 B[15];
-          u32 const wq = (q >> 2) + 2, sq = q & 3;
-#pragma unroll
-          for (u32 j = 0; j < 15; j++) B[j] = D32[wq + j];
+          u32 const sq = q & 3;
           u32 e = 56;
+#if ZH_DEEP_B64
+          // bytes [q + 8, q + 64) from aligned 8-byte loads (half the LDS instructions of dword
+          // loads), dword j of the candidate being W[odd + j]: dwords 0..6 first (five loads), the
+          // rest (five more) only when those all match
+          u32 const a8 = q + 8, wq8 = a8 >> 3, odd = (a8 >> 2) & 1u;
+          const u64 *const D64 = (const u64 *)D32 + wq8;
+          u32 W[10];
+#pragma unroll
+          for (u32 k = 0; k < 5; k++) {
+            u64 const v = D64[k];
+            W[2 * k] = (u32)v;
+            W[2 * k + 1] = (u32)(v >> 32);
+          }
+#pragma unroll
+          for (int j = 6; j >= 0; j--) {
+            u32 const lo = odd ? W[j + 1] : W[j], hi = odd ? W[j + 2] : W[j + 1];
+            u32 const xx = O[j + 2] ^ __builtin_amdgcn_alignbyte(hi, lo, sq);
+            if (xx) e = 4 * (u32)j + ((u32)__builtin_ctz(xx) >> 3);
+          }
+          if (e == 56) {
+#pragma unroll
+            for (u32 k = 0; k < 5; k++) {  // W[m] = dword 6 + m
+              u64 const v = D64[3 + k];
+              W[2 * k] = (u32)v;
+              W[2 * k + 1] = (u32)(v >> 32);
+            }
+#pragma unroll
+            for (int j = 13; j >= 7; j--) {
+              u32 const lo = odd ? W[j - 5] : W[j - 6], hi = odd ? W[j - 4] : W[j - 5];
+              u32 const xx = O[j + 2] ^ __builtin_amdgcn_alignbyte(hi, lo, sq);
+              if (xx) e = 4 * (u32)j + ((u32)__builtin_ctz(xx) >> 3);
+            }
+          }
+#else
+          u32 B[15];
+          u32 const wq = (q >> 2) + 2;
+#pragma unroll
+          for (u32 k = 0; k < 15; k++) B[k] = D32[wq + k];
 #pragma unroll
           for (int j = 13; j >= 0; j--) {
             u32 const xx = O[j + 2] ^ __builtin_amdgcn_alignbyte(B[j + 1], B[j], sq);
             if (xx) e = 4 * (u32)j + ((u32)__builtin_ctz(xx) >> 3);
           }
+#endif
           l = 8 + e;
         }
       }
