@@ -53,10 +53,7 @@ constexpr u32 L_EX = L_MM + 8 * NSEG;      // u32 walk exit per segment
 constexpr u32 L_LP = L_EX + 4 * NSEG;      // u32 literals before the segment
 constexpr u32 L_MP = L_LP + 4 * NSEG;      // u32 matches before the segment
 #ifndef ZH_DEEP_B64
-#define ZH_DEEP_B64 0
-#endif
-#ifndef ZH_DEEP_PIPE
-#define ZH_DEEP_PIPE 0
+#define ZH_DEEP_B64 1  // extension bytes by 8-byte loads (C5 12.1 -> 12.9 GB/s)
 #endif
 constexpr u32 DEEP_LDS = 160 * 1024;
 constexpr u32 L_WS = DEEP_LDS - 256;       // u32[32] per-wave sums
@@ -257,67 +254,6 @@ __device__ __forceinline__ u32 deep_search_one(const u32 *D32, const u16 *P16, c
     for (u32 j = 0; j < 16; j++) O[j] = __builtin_amdgcn_alignbyte(R[j + 1], R[j], sh);
   }
   u32 ownb = 0;  // own byte at p + best (best >= 8)
-#if ZH_DEEP_PIPE
-  // Software-pipelined chain walk: the next candidate's link, first 8 bytes and filter byte are
-  // loaded while this one is compared.  The filter byte of a candidate is read at the best length
-  // when it was issued: a mismatch there still proves the candidate cannot beat the (only ever
-  // longer) current best.
-  u32 q = act ? c - 1u : 0u, nx = 0, clo = 0, chi = 0;
-  bool wv = true;
-  if (act) {
-    nx = link(q);
-    g64(D32, q, clo, chi);
-  }
-  while (__ballot(act)) {
-    if (act) {
-      bool const more = nx != 0 && dd + 1u < depth && p - (nx - 1u) <= ZH_DEEP_MAXOFF;
-      u32 const qn = more ? nx - 1u : q;
-      u32 const nxn = more ? link(qn) : 0u;
-      u32 clon, chin;
-      g64(D32, qn, clon, chin);
-      u32 const bi = best, oi = ownb;
-      u32 wbn = 0;
-      if (bi >= 8) {
-        u32 const bb = qn + bi;
-        wbn = (D32[bb >> 2] >> (8 * (bb & 3))) & 255u;
-      }
-      u32 l = 0;
-      if (wv) {
-        u32 const x = O[0] ^ clo, y = O[1] ^ chi;
-        l = x ? (u32)__builtin_ctz(x) >> 3 : y ? 4u + ((u32)__builtin_ctz(y) >> 3) : 8u;
-        if (l == 8 && p + 8 < n) {
-          u32 const sq = q & 3;
-          u32 e = 56;
-          u32 B[15];
-          u32 const wq = (q >> 2) + 2;
-#pragma unroll
-          for (u32 k = 0; k < 15; k++) B[k] = D32[wq + k];
-#pragma unroll
-          for (int j = 13; j >= 0; j--) {
-            u32 const xx = O[j + 2] ^ __builtin_amdgcn_alignbyte(B[j + 1], B[j], sq);
-            if (xx) e = 4 * (u32)j + ((u32)__builtin_ctz(xx) >> 3);
-          }
-          l = 8 + e;
-        }
-      }
-      l = min(l, p < n ? n - p : 0u);
-      if (l >= ZH_MIN_MATCH_SHORT && l > best) {
-        best = l;
-        bo = p - q;
-        u32 const a = p + l;
-        ownb = (D32[a >> 2] >> (8 * (a & 3))) & 255u;
-      }
-      dd++;
-      q = qn;
-      nx = nxn;
-      clo = clon;
-      chi = chin;
-      wv = bi < 8 || wbn == oi;
-      act = best < ZH_MAX_MATCH && more;
-    }
-  }
-  return bo << 8 | best;
-#endif
   while (__ballot(act)) {
     if (act) {
       u32 const q = c - 1u;
@@ -449,6 +385,11 @@ __device__ void deep_parse_demand(const u32 *D32, const u16 *P16, const u32 *dpr
 #ifdef ZH_STAMPS
   u64 const dm0 = __builtin_amdgcn_s_memtime();
   u32 st_rounds = 0, st_searched = 0, st_walk = 0, st_jac = 0;
+  u32 st_adv = 0, st_sync1 = 0, st_srch = 0, st_sync2 = 0;  // (thread 0's wave)
+  u64 tq = 0;
+#define DMSTAMP(acc) do { u64 const _t = __builtin_amdgcn_s_memtime(); acc += (u32)(_t - tq); tq = _t; } while (0)
+#else
+#define DMSTAMP(acc) do { } while (0)
 #endif
   u64 LM = 0, MM = 0;
   u32 entry = S, ex = S;
@@ -461,6 +402,9 @@ __device__ void deep_parse_demand(const u32 *D32, const u16 *P16, const u32 *dpr
     u32 p = p0, mpos = 0;
     for (;;) {
       // advance as far as the memo allows
+#ifdef ZH_STAMPS
+      tq = __builtin_amdgcn_s_memtime();
+#endif
       u32 need = ~0u;
       bool adv = act;
       while (__ballot(adv)) {
@@ -506,8 +450,10 @@ __device__ void deep_parse_demand(const u32 *D32, const u16 *P16, const u32 *dpr
           if (x < nb && memo[x] == MEMO_UNK) q[atomicAdd(&misc[2], 1u)] = (u16)x;
         }
       }
+      DMSTAMP(st_adv);
       __syncthreads();
       u32 const nq = misc[2];
+      DMSTAMP(st_sync1);
       if (nq == 0) break;  // (every lane has finished: no lane needed anything)
 #ifdef ZH_STAMPS
       st_rounds++;
@@ -525,7 +471,9 @@ __device__ void deep_parse_demand(const u32 *D32, const u16 *P16, const u32 *dpr
           memo[x] = (u16)(l ? l | ((31u - (u32)__builtin_clz((r >> 8) + 1u)) << 8) : 0u);
         }
       }
+      DMSTAMP(st_srch);
       __syncthreads();
+      DMSTAMP(st_sync2);
       if (tid == 0) misc[2] = 0;
       __syncthreads();
     }
@@ -556,7 +504,8 @@ __device__ void deep_parse_demand(const u32 *D32, const u16 *P16, const u32 *dpr
   }
 #ifdef ZH_STAMPS
   st_jac = (u32)(__builtin_amdgcn_s_memtime() - dm0) - st_walk;
-  if (tid == 0) { u32 *dbg = ws.dbg(b); dbg[20] = st_rounds; dbg[21] = st_searched; dbg[22] = st_walk; dbg[23] = st_jac; }
+  if (tid == 0) { u32 *dbg = ws.dbg(b); dbg[20] = st_rounds; dbg[21] = st_searched; dbg[22] = st_walk; dbg[23] = st_jac;
+                  dbg[0] = st_adv; dbg[1] = st_sync1; dbg[2] = st_srch; dbg[3] = st_sync2; }
 #endif
   // ---- records and literals (step 5 of deep_block)
   u32 nm_tot, nl_tot;

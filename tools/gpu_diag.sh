@@ -6,6 +6,8 @@
 #   trace    rocprofv3 --kernel-trace --stats of the default bench workload
 #   tests    the -m gpu suite
 #   bench    default bench line (no CPU baseline)
+#   fullbench the default bench line (CPU baseline, legs, decode)
+#   dstamps  deep-matcher phase stamps (tools/deep_stamps.py)
 #   k1tests  the K1 / parity GPU tests only
 #   rstamps  K1/K2 phase stamps on random data
 #   c5       tools/c5_dict.py at level 9 (C5_LEVEL overrides)
@@ -28,6 +30,8 @@ for s in "$@"; do
       (cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/${TAG}_trace -o run --output-format csv -- python3 $R/bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-verify --no-legs --no-decompress > $R/gpurun_out/${TAG}_trace.log 2>&1) ;;
     tests) timeout -k 10 500 python3 -u -m pytest $R/tests -m gpu -x -q --timeout 120 --timeout-method thread > $R/gpurun_out/${TAG}_gpu_tests.log 2>&1 || { tail -30 $R/gpurun_out/${TAG}_gpu_tests.log; exit 1; } ;;
     bench) timeout -k 10 300 python3 $R/bench.py --no-cpu-baseline > $R/gpurun_out/${TAG}_bench.json 2> $R/gpurun_out/${TAG}_bench.err ;;
+    fullbench) timeout -k 10 400 python3 $R/bench.py > $R/gpurun_out/${TAG}_fullbench.json 2> $R/gpurun_out/${TAG}_fullbench.err ;;
+    dstamps) timeout -k 10 200 python3 $R/tools/deep_stamps.py > $R/gpurun_out/${TAG}_deep_stamps.log 2>&1 ;;
     k1tests) timeout -k 10 300 python3 -u -m pytest $R/tests/test_gpu_k1.py $R/tests/test_gpu_parity.py -x -q --timeout 120 --timeout-method thread > $R/gpurun_out/${TAG}_k1_tests.log 2>&1 || { tail -30 $R/gpurun_out/${TAG}_k1_tests.log; exit 1; }; tail -1 $R/gpurun_out/${TAG}_k1_tests.log ;;
     rstamps) timeout -k 10 200 python3 $R/tools/stamps.py random 4096 > $R/gpurun_out/${TAG}_rstamps.log 2>&1 ;;
     c5) C5_LEVEL=${C5_LEVEL:-9} timeout -k 10 300 python3 $R/tools/c5_dict.py > $R/gpurun_out/${TAG}_c5.json 2> $R/gpurun_out/${TAG}_c5.err; tail -c 400 $R/gpurun_out/${TAG}_c5.json ;;
