@@ -44,18 +44,25 @@ constexpr u32 U_HUF_END = OFF_NODES + 8 * 516;
 constexpr u32 OFF_ST_LL = OFF_U;                   // u16[512]
 constexpr u32 OFF_ST_OF = OFF_ST_LL + 1024;        // u16[256]
 constexpr u32 OFF_ST_ML = OFF_ST_OF + 512;         // u16[512]
-constexpr u32 OFF_SYM = OFF_ST_ML + 1024;          // 3 x 64 x (u32 dNb, s32 dFS)
-constexpr u32 OFF_TSYM = OFF_SYM + 3 * 64 * 8;     // u8[512] spread scratch
+constexpr u32 OFF_SYM = OFF_ST_ML + 1024;          // (u32 dNb, s32 dFS): LL [0, 36), OF [36, 68), ML [68, 121)
+constexpr u32 SYM_OF = 36, SYM_ML = 68;
+constexpr u32 OFF_TSYM = OFF_SYM + 976;            // u8[512] spread scratch
 constexpr u32 OFF_NORM = OFF_TSYM + 512;           // s16[64]
-constexpr u32 OFF_WTS = OFF_NORM + 128;            // u8[256] Huffman weights (used during Huffman header)
-constexpr u32 U_FSE_END = OFF_WTS + 256;
+constexpr u32 U_FSE_END = OFF_NORM + 128;
+// the Huffman weights' FSE table (tableLog <= 6, <= 13 symbols) and the weights, in the nodes'
+// region once the tree is built (wave 0 only)
+constexpr u32 OFF_W_ST = OFF_U, OFF_W_SYM = OFF_U + 128, OFF_W_TSYM = OFF_U + 256, OFF_W_NORM = OFF_U + 320;
+constexpr u32 OFF_WTS = OFF_U + 352;               // u8[256] Huffman weights
+static_assert(OFF_WTS + 256 <= U_HUF_END, "weights inside the nodes' region");
+// wave 0 (literals) uses [0, U_HUF_END), wave 1 (sequences) [OFF_MISC, U_FSE_END) of its copy:
+// wave 1's copy starts where wave 0's ends, less the literal-only head it never touches
 constexpr u32 K2_WAVE_LDS = (U_HUF_END > U_FSE_END ? U_HUF_END : U_FSE_END);  // one wave's layout
 static_assert(K2_WAVE_LDS < 16384, "K2 LDS budget");
-constexpr u32 K2_W1 = (K2_WAVE_LDS - OFF_MISC + 15) & ~15u;  // wave 1's layout base
+constexpr u32 K2_W1 = (U_HUF_END - OFF_MISC + 15) & ~15u;  // wave 1's layout base
 #ifndef ZH_K2_LDS_PAD
 #define ZH_K2_LDS_PAD 0  // (occupancy experiments: extra LDS per block)
 #endif
-constexpr u32 K2_LDS = K2_W1 + K2_WAVE_LDS + ZH_K2_LDS_PAD;
+constexpr u32 K2_LDS = K2_W1 + U_FSE_END + ZH_K2_LDS_PAD;  // 15,952 B: 10 blocks per CU (was 17,632: 9)
 
 __constant__ u8 c_LL_bits[36] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 1, 1, 1, 1, 2, 2, 3, 3, 4, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16};
 __constant__ u8 c_ML_bits[53] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0,
@@ -1192,7 +1199,7 @@ extern "C" __global__ __launch_bounds__(K2_THREADS) void zh_entropy_kernel(const
   u8 *hbuf = smem + OFF_HBUF;
   HufNode *nodes = (HufNode *)(smem + OFF_NODES);
   u16 *stLL = (u16 *)(smem + OFF_ST_LL), *stOF = (u16 *)(smem + OFF_ST_OF), *stML = (u16 *)(smem + OFF_ST_ML);
-  FseSym *symLL = (FseSym *)(smem + OFF_SYM), *symOF = symLL + 64, *symML = symLL + 128;
+  FseSym *symLL = (FseSym *)(smem + OFF_SYM), *symOF = symLL + SYM_OF, *symML = symLL + SYM_ML;
   u8 *tsym = smem + OFF_TSYM;
   s16 *norm = (s16 *)(smem + OFF_NORM);
   u8 *wts = smem + OFF_WTS;
@@ -1335,7 +1342,9 @@ extern "C" __global__ __launch_bounds__(K2_THREADS) void zh_entropy_kernel(const
           hl = huf_build_ctable_par(nodes, hval, hnb, hist, maxSV, hl, scr);
           ZH_STAMP(11);  // Huffman tree (parallel part)
           huffLog = hl;
-          hsz = hl ? huf_write_ctable_wave(hbuf, wts, hnb, maxSV, hl, stLL, symLL, tsym, norm, scr) : 0;
+          hsz = hl ? huf_write_ctable_wave(hbuf, wts, hnb, maxSV, hl, (u16 *)(smem + OFF_W_ST), (FseSym *)(smem + OFF_W_SYM), smem + OFF_W_TSYM,
+                                           (s16 *)(smem + OFF_W_NORM), scr)
+                   : 0;
           ZH_STAMP(1);  // Huffman tree + header (serial)
           if (hsz && hsz + 12 < nl) {
             // stream sizes: sum of code lengths per stream (+ end mark)
