@@ -328,14 +328,33 @@ __device__ __forceinline__ bool skip_window(const u32 *misc, u32 k, u32 kskip0) 
 // parses of the ZH_PROBE_WINDOWS probe windows from the one holding `pre` are done) a block
 // whose parse took no match in them stops -- it takes no sequences, every byte is a literal.
 // Wave-uniform; every wave (inserters too) evaluates it at the same step, before barrier P.
+// With ZH_PROBE_WINDOWS = 1 the decision is taken one step earlier, from the take masks
+// (probe_dead_tm below), and this check never fires.
 __device__ __forceinline__ bool probe_dead(const u32 *misc, u32 k, u32 kprobe) {
-  if (k != kprobe) return false;
+  if (ZH_PROBE_WINDOWS == 1 || k != kprobe) return false;
   u32 m = 0;
 #pragma unroll
   for (u32 j = 1; j <= ZH_PROBE_WINDOWS; j++) m |= __atomic_load_n(&misc[MISC_NM + ((k - 1 - j) & 3)], __ATOMIC_RELAXED);
   return (u32)__builtin_amdgcn_readfirstlane(m) == 0;
 }
 static_assert(ZH_PROBE_WINDOWS >= 1 && ZH_PROBE_WINDOWS <= 3, "probe windows fit the match-count ring");
+// The one-window probe from the take masks: before any match the parse visits every position,
+// so it takes a match in the probe window exactly when the window has a take bit at or after
+// its first parsed position e0.  Window k - 1's masks (and their span-top bits, set after
+// barrier X of step k - 1) are final at barrier P of step k = kprobe - 1, so every wave --
+// inserters too -- tests them right after that P and leaves the window loop together.
+__device__ __forceinline__ bool probe_dead_tm(u32 k, u32 kprobe, u32 e0) {
+  if (ZH_PROBE_WINDOWS != 1 || k + 1 != kprobe) return false;
+  extern __shared__ __attribute__((aligned(16))) u8 smem[];
+  u32 lane;
+  __asm__ volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(lane));
+  const u64 *const tmP = (const u64 *)(smem + OFF_HM) + ((k & 1u) ^ 1u) * NROUND;
+  u32 const r = lane & (NROUND - 1);
+  u64 const m = tmP[r];
+  u32 const lo = 64 * r;
+  u64 const keep = e0 <= lo ? ~0ull : e0 >= lo + 64 ? 0ull : ~0ull << (e0 - lo);
+  return __ballot(lane < NROUND && (m & keep) != 0) == 0;
+}
 
 // Dump an inserter's candidates into its half of the cinfo words (LONG: low half).
 template <bool LONG, u32 NT>
@@ -668,17 +687,18 @@ __device__ __forceinline__ void seg_walk(const u32 *ci, u32 tmk, u32 S, u32 SE, 
 constexpr u32 WIN_BARRIERS = 1;  // X
 // The long table's wave in modes 1, 2 (the short table only): no insertion, only the step's two
 // barriers (P, X) and the probe exit, so the workgroup's barrier sequence stays the same.
-__device__ __forceinline__ void idle_inserter_loop(u32 *misc_, u32 n, u32 wstart, u32 kprobe) {
+__device__ __forceinline__ void idle_inserter_loop(u32 *misc_, u32 n, u32 wstart, u32 kprobe, u32 e0p) {
   u32 const nwin = (n - wstart + ZH_WINDOW - 1) / ZH_WINDOW;
   for (u32 k = 0; k < nwin + 2; k++) {
     if (probe_dead(misc_, k, kprobe)) break;
     __syncthreads();  // P
+    if (probe_dead_tm(k, kprobe, e0p)) break;
     __syncthreads();  // X
   }
 }
 template <bool LONG>
 __device__ __forceinline__ void inserter_loop(const u32 *in32, u16 *T, u8 *ci8, u32 *misc_, u32 n, u32 lim, u32 lane, u32 *dbg, u32 wstart,
-                                              u32 pmin, u32 span_s, u32 span_e, u32 kskip0, u32 kprobe) {
+                                              u32 pmin, u32 span_s, u32 span_e, u32 kskip0, u32 kprobe, u32 e0p) {
   u32 creg[NCR];
   u32 cwe = 0;
   if (span_s < span_e) insert_span<LONG>(in32, T, span_s, span_e, lane);
@@ -697,6 +717,7 @@ __device__ __forceinline__ void inserter_loop(const u32 *in32, u16 *T, u8 *ci8, 
       else dump_window<LONG, TILES>(ci8 + (k & 1u) * 4 * CI_WORDS, lane, creg, cwe);
     }
     __syncthreads();  // P: candidates of window k in buffer k & 1
+    if (probe_dead_tm(k, kprobe, e0p)) break;
     u32 const done = passed + WIN_BARRIERS;
     // arr: the arrival counter as read with the last tile's read-back; a barrier taken
     // here means the counter is re-read for the next one
@@ -965,6 +986,7 @@ __device__ __forceinline__ u32 lz_block(const ZhBlockDesc *__restrict__ blocks, 
   // done, when the block has a window past them (windows counted up to lim, as the oracle does)
   u32 const a0 = pre / ZH_WINDOW, nwl = (lim + ZH_WINDOW - 1) / ZH_WINDOW;
   u32 const kprobe = a0 + ZH_PROBE_WINDOWS + 1 <= nwl ? a0 + ZH_PROBE_WINDOWS + 1 - wstart / ZH_WINDOW : ~0u;
+  u32 const e0p = pre - a0 * ZH_WINDOW;  // the probe window's first parsed position
   u32 nseq_tot = 0, nlit_tot = 0, e_in = pre;
   // ---- inserter waves: their own loop with the same barrier sequence as the workers'
   // (separate code, so their registers never add to the workers' pressure)
@@ -974,9 +996,9 @@ __device__ __forceinline__ u32 lz_block(const ZhBlockDesc *__restrict__ blocks, 
     // gate the workers' next window, so they take priority (MI355X_MICROARCH.md, "VALU issue
     // is arbitrated ... by priority, then age").
     __builtin_amdgcn_s_setprio(2);
-    if (tid >= INS_TID + 64) inserter_loop<false>(in32, TS, ci8, misc, n, lim, lane, ws.dbg(b), wstart, pmin, span_s, span_e, kskip0, kprobe);
-    else if (two_tables<MODE>()) inserter_loop<true>(in32, TL, ci8, misc, n, lim, lane, ws.dbg(b), wstart, pmin, span_s, span_e, kskip0, kprobe);
-    else idle_inserter_loop(misc, n, wstart, kprobe);
+    if (tid >= INS_TID + 64) inserter_loop<false>(in32, TS, ci8, misc, n, lim, lane, ws.dbg(b), wstart, pmin, span_s, span_e, kskip0, kprobe, e0p);
+    else if (two_tables<MODE>()) inserter_loop<true>(in32, TL, ci8, misc, n, lim, lane, ws.dbg(b), wstart, pmin, span_s, span_e, kskip0, kprobe, e0p);
+    else idle_inserter_loop(misc, n, wstart, kprobe, e0p);
     __builtin_amdgcn_s_setprio(0);
     return next_b;
   }
@@ -1023,6 +1045,10 @@ __device__ __forceinline__ u32 lz_block(const ZhBlockDesc *__restrict__ blocks, 
     u32 *const lmQ = sgm + segm(kb);        // window k - 2's (after its catch-up)
     u64 *const mlP = mlist + (kb ^ 1u) * ML_CAP, *const mlQ = mlist + kb * ML_CAP;
     __syncthreads();  // P: candidates of window k in buffer k & 1
+    if (probe_dead_tm(k, kprobe, e0p)) {
+      dead = true;
+      break;
+    }
     ZH_STAMP(st_A);
     // a miss-skip window has candidates in its first RS rounds only: waves 1..RS take one each
     // (the top one, wave RS, knows its next positions have none), the others clear the info and

@@ -52,9 +52,6 @@ constexpr u32 L_MM = L_LM + 8 * NSEG;      // u64 match-start bits per segment
 constexpr u32 L_EX = L_MM + 8 * NSEG;      // u32 walk exit per segment
 constexpr u32 L_LP = L_EX + 4 * NSEG;      // u32 literals before the segment
 constexpr u32 L_MP = L_LP + 4 * NSEG;      // u32 matches before the segment
-#ifndef ZH_DEEP_ONE_RT
-#define ZH_DEEP_ONE_RT 0
-#endif
 #ifndef ZH_DEEP_B64
 #define ZH_DEEP_B64 1  // extension bytes by 8-byte loads (C5 12.1 -> 12.9 GB/s)
 #endif
@@ -256,21 +253,6 @@ __device__ __forceinline__ u32 deep_search_one(const u32 *D32, const u16 *P16, c
 #pragma unroll
     for (u32 j = 0; j < 16; j++) O[j] = __builtin_amdgcn_alignbyte(R[j + 1], R[j], sh);
   }
-#if ZH_DEEP_ONE_RT
-  // One LDS round trip per candidate (plus the extension's): its link, first 8 bytes and the
-  // filter bytes at +best (its and the position's own) are loaded together, unconditionally.
-  while (__ballot(act)) {
-    if (act) {
-      u32 const q = c - 1u;
-      u32 const nx = link(q);
-      u32 clo, chi;
-      g64(D32, q, clo, chi);
-      u32 const bb = best >= 8 ? best : 0u, bq = q + bb, bp = p + bb;
-      u32 const cq = (D32[bq >> 2] >> (8 * (bq & 3))) & 255u, cp = (D32[bp >> 2] >> (8 * (bp & 3))) & 255u;
-      bool const w = best < 8 || cq == cp;  // (a candidate differing at best cannot beat it)
-      u32 l = 0;
-      if (w) {
-#else
   u32 ownb = 0;  // own byte at p + best (best >= 8)
   while (__ballot(act)) {
     if (act) {
@@ -285,7 +267,6 @@ __device__ __forceinline__ u32 deep_search_one(const u32 *D32, const u16 *P16, c
       if (w) {
         u32 clo, chi;
         g64(D32, q, clo, chi);
-#endif
         u32 const x = O[0] ^ clo, y = O[1] ^ chi;
         l = x ? (u32)__builtin_ctz(x) >> 3 : y ? 4u + ((u32)__builtin_ctz(y) >> 3) : 8u;
         if (l == 8 && p + 8 < n) {
@@ -342,10 +323,8 @@ __device__ __forceinline__ u32 deep_search_one(const u32 *D32, const u16 *P16, c
       if (l >= ZH_MIN_MATCH_SHORT && l > best) {
         best = l;
         bo = p - q;
-#if !ZH_DEEP_ONE_RT
         u32 const a = p + l;  // the own byte a candidate must match to beat the new best
         ownb = (D32[a >> 2] >> (8 * (a & 3))) & 255u;
-#endif
       }
       dd++;
       c = nx;
