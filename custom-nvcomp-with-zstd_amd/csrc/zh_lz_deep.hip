@@ -52,6 +52,9 @@ constexpr u32 L_MM = L_LM + 8 * NSEG;      // u64 match-start bits per segment
 constexpr u32 L_EX = L_MM + 8 * NSEG;      // u32 walk exit per segment
 constexpr u32 L_LP = L_EX + 4 * NSEG;      // u32 literals before the segment
 constexpr u32 L_MP = L_LP + 4 * NSEG;      // u32 matches before the segment
+#ifndef ZH_DEEP_WAVEQ
+#define ZH_DEEP_WAVEQ 0
+#endif
 #ifndef ZH_DEEP_B64
 #define ZH_DEEP_B64 1  // extension bytes by 8-byte loads (C5 12.1 -> 12.9 GB/s)
 #endif
@@ -361,7 +364,10 @@ __device__ __forceinline__ void deep_search(const u32 *gdata, const u16 *gP16, u
 // the memo fit in LDS (C5's 16 KiB records with or without the 64 KiB dictionary).
 //   memo[i] (u16): 0xFFFF unsearched; else len | (bit length of off + 1) << 8 (the LAZY2 gain)
 constexpr u32 MEMO_UNK = 0xFFFFu;
-constexpr u32 DQ_PER = 3;  // positions posted per blocked lane
+#ifndef ZH_DQ_PER
+#define ZH_DQ_PER 3
+#endif
+constexpr u32 DQ_PER = ZH_DQ_PER;  // positions posted per blocked lane (the needed one + lookahead)
 __device__ __forceinline__ int memo_gain(u32 m) { return (m & 255u) ? 4 * (int)(m & 255u) - (int)(m >> 8) : -1000; }
 __device__ __forceinline__ u32 demand_segl(u32 nb) { return nb <= 16384u ? 16u : nb <= 32768u ? 32u : 64u; }
 // LDS bytes the demand path needs above the staged bytes (memo, queue, exits), for nb positions
@@ -442,6 +448,46 @@ __device__ void deep_parse_demand(const u32 *D32, const u16 *P16, const u32 *dpr
           }
         }
       }
+#if ZH_DEEP_WAVEQ
+      // post the needed position and the two after it (the lazy check's lookahead) to this
+      // wave's own queue (ballot-compacted), then the wave searches it (lanes = entries): no
+      // workgroup barrier, every wave walks at its own pace.  A position another wave is
+      // searching at the same time may be searched twice (same result).
+      DMSTAMP(st_adv);
+      if (!__ballot(act)) break;  // every walk of this wave has left its segment or merged
+      u16 *const wq = q + (tid & ~63u) * DQ_PER;
+      u32 const lane = tid & 63u;
+      u32 nq = 0;
+#pragma unroll
+      for (u32 t = 0; t < DQ_PER; t++) {
+        u32 const x = need + t;
+        bool const post = need != ~0u && x < nb && memo[x] == MEMO_UNK;
+        u64 const bm = __ballot(post);
+        u32 const rank = __builtin_amdgcn_mbcnt_hi((u32)(bm >> 32), __builtin_amdgcn_mbcnt_lo((u32)bm, 0u));
+        if (post) wq[nq + rank] = (u16)x;
+        nq += (u32)__popcll(bm);
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+#ifdef ZH_STAMPS
+      st_rounds++;
+      st_searched += nq;
+#endif
+      for (u32 j0 = 0; j0 < nq; j0 += 64) {
+        u32 const j = j0 + lane;
+        bool const v = j < nq;
+        u32 const x = v ? wq[j] : 0u;
+        u32 const r = deep_search_one(D32, P16, dprev, x, v, pre, nb, n, lim, s0, depth);
+        if (v) {
+          offg[x] = r;
+          u32 const l = r & 255u;
+          memo[x] = (u16)(l ? l | ((31u - (u32)__builtin_clz((r >> 8) + 1u)) << 8) : 0u);
+        }
+      }
+      __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      DMSTAMP(st_srch);
+#else
       // post the needed position and the two after it (the lazy check's lookahead)
       if (need != ~0u) {
 #pragma unroll
@@ -476,6 +522,7 @@ __device__ void deep_parse_demand(const u32 *D32, const u16 *P16, const u32 *dpr
       DMSTAMP(st_sync2);
       if (tid == 0) misc[2] = 0;
       __syncthreads();
+#endif
     }
     if (act0) {
       if (merged) {
