@@ -55,6 +55,9 @@ extern "C" u32 zh_fixups_host() {
 #endif
 namespace {
 
+#ifndef ZH_K1_PMAX
+#define ZH_K1_PMAX 0
+#endif
 constexpr u32 K1_THREADS = 1024;
 constexpr u32 NROUND = ZH_WINDOW / 64;      // 64-position length rounds per window
 constexpr u32 SEGP = 32;                    // positions per walk segment (one lane of wave 0)
@@ -1088,7 +1091,13 @@ __device__ __forceinline__ u32 lz_block(const ZhBlockDesc *__restrict__ blocks, 
       seg_walk<false>(ciP, tmk, S, SE, entry, true, LM, MM, ex);
       // Jacobi rounds: a segment's entry is its predecessor's exit
       for (;;) {
+#if ZH_K1_PMAX
+        // the largest exit before the segment (its predecessor's once consistent): a match
+        // covering whole segments passes its end through them in one round
+        u32 const pe = wave_shr1(wave_scan_max_incl(ex));
+#else
         u32 const pe = wave_shr1(ex);
+#endif
         u32 const ne = lane == 0 ? e0 : max(pe, e0);
         bool const ch = ne != entry;
 #ifdef ZH_STAMPS
