@@ -55,9 +55,6 @@ constexpr u32 L_MP = L_LP + 4 * NSEG;      // u32 matches before the segment
 #ifndef ZH_DEEP_WAVEQ
 #define ZH_DEEP_WAVEQ 1  // per-wave demand queues (C5 no dictionary 12.9 -> 13.8 GB/s)
 #endif
-#ifndef ZH_DEEP_PMAX
-#define ZH_DEEP_PMAX 0
-#endif
 #ifndef ZH_DEEP_B64
 #define ZH_DEEP_B64 1  // extension bytes by 8-byte loads (C5 12.1 -> 12.9 GB/s)
 #endif
@@ -102,19 +99,6 @@ __device__ __forceinline__ u32 wg_excl_scan(u32 v, u32 *ws, u32 tid, u32 &total)
   __syncthreads();
   total = tot;
   return base + inc - v;
-}
-
-// Exclusive workgroup max scan (lane 0 of the workgroup: 0)
-__device__ __forceinline__ u32 wg_excl_max(u32 v, u32 *ws, u32 tid) {
-  u32 const inc = wave_scan_max_incl(v);
-  if ((tid & 63) == 63) ws[tid >> 6] = inc;
-  __syncthreads();
-  u32 base = 0;
-  u32 const w = tid >> 6;
-  for (u32 k = 0; k < w; k++) base = max(base, ws[k]);
-  __syncthreads();
-  u32 const ex = wave_shr1(inc);
-  return max(base, (tid & 63) ? ex : 0u);
 }
 
 __device__ __forceinline__ u64 bits_from(u32 a) { return a >= 64 ? 0ull : ~0ull << a; }
@@ -380,10 +364,7 @@ __device__ __forceinline__ void deep_search(const u32 *gdata, const u16 *gP16, u
 // the memo fit in LDS (C5's 16 KiB records with or without the 64 KiB dictionary).
 //   memo[i] (u16): 0xFFFF unsearched; else len | (bit length of off + 1) << 8 (the LAZY2 gain)
 constexpr u32 MEMO_UNK = 0xFFFFu;
-#ifndef ZH_DQ_PER
-#define ZH_DQ_PER 3
-#endif
-constexpr u32 DQ_PER = ZH_DQ_PER;  // positions posted per blocked lane (the needed one + lookahead)
+constexpr u32 DQ_PER = 3;  // positions posted per blocked lane (the needed one + lookahead)
 __device__ __forceinline__ int memo_gain(u32 m) { return (m & 255u) ? 4 * (int)(m & 255u) - (int)(m >> 8) : -1000; }
 __device__ __forceinline__ u32 demand_segl(u32 nb) { return nb <= 16384u ? 16u : nb <= 32768u ? 32u : 64u; }
 // LDS bytes the demand path needs above the staged bytes (memo, queue, exits), for nb positions
@@ -557,18 +538,9 @@ __device__ void deep_parse_demand(const u32 *D32, const u16 *P16, const u32 *dpr
   st_walk = (u32)(__builtin_amdgcn_s_memtime() - dm0);
 #endif
   for (;;) {
-#if ZH_DEEP_PMAX
-    // a segment's entry is the largest exit before it (equal to its predecessor's exit once
-    // the parse is consistent): a match covering whole segments passes its end through all of
-    // them in one round instead of one segment per round
-    u32 const pm = wg_excl_max(sv ? ex : 0u, wsum, tid);
-    u32 const ne = g == 0 ? 0u : (sv ? pm : entry);
-    (void)exL;
-#else
     if (sv) exL[g] = ex;
     __syncthreads();
     u32 const ne = g == 0 ? 0u : (sv ? exL[g - 1] : entry);
-#endif
     bool const ch = sv && ne != entry;
     if (!wg_any(ch, &misc[0], tid)) break;
     walk(ne, ch);
@@ -759,18 +731,9 @@ __device__ void deep_block(const ZhBlockDesc &d, ZhWorkspace ws, u32 b, u8 *slot
   u32 entry = S, ex = S;
   seg_walk64(lenL, tmk, S, SE, entry, sv, LM, MM, ex);
   for (;;) {
-#if ZH_DEEP_PMAX
-    // a segment's entry is the largest exit before it (equal to its predecessor's exit once
-    // the parse is consistent): a match covering whole segments passes its end through all of
-    // them in one round instead of one segment per round
-    u32 const pm = wg_excl_max(sv ? ex : 0u, wsum, tid);
-    u32 const ne = g == 0 ? 0u : (sv ? pm : entry);
-    (void)exL;
-#else
     if (sv) exL[g] = ex;
     __syncthreads();
     u32 const ne = g == 0 ? 0u : (sv ? exL[g - 1] : entry);
-#endif
     bool const ch = sv && ne != entry;
     if (!wg_any(ch, &misc[0], tid)) break;
     if (ch) {
