@@ -93,7 +93,7 @@ static_assert(ZH_K1_HIST_OFF + ZH_K1_HIST_WAVES * 1024u <= ZH_LIT_BYTES, "K1 sub
 
 struct ZhWorkspace {
   u8 *base;          // nblocks * ZH_WS_BLOCK_BYTES
-  u32 *ctr;          // block counters: [0] K1's (persistent workgroups take the next block from it), [1] K3's, [2] K4's
+  u32 *ctr;          // K1's block counter (persistent workgroups take the next block from it)
   // K1 hash tables of the batch dictionary's content, precomputed once per dictionary
   // (zh::lz_dict_tables; null: none): 2 x 2^14 u16 entries = tail position + 1 over the last
   // dtab_P content bytes, positions [0, dtab_P - ZH_DTAB_MARGIN) inserted

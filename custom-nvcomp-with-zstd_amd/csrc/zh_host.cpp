@@ -289,7 +289,7 @@ struct WsLayout {
     L.item_size = o; o = align256(o + nitems * 8);
     L.item_status = o; o = align256(o + nitems * 4);
     L.staging = o; o = align256(o + (staged ? nblocks * (size_t)ZH_STAGE_SLOT : 0));
-    L.counter = o; o = align256(o + 16);  // block counters (K1, K3, K4)
+    L.counter = o; o = align256(o + 4);
     L.blocks = o; o = align256(o + nblocks * (size_t)ZH_WS_BLOCK_BYTES);
     L.deep_slots = deep ? std::min(nblocks, (size_t)ZH_DEEP_SLOTS_MAX) : 0;
     L.deep = o; o = align256(o + L.deep_slots * ZH_DEEP_SLOT_BYTES);

@@ -211,7 +211,7 @@ hipError_t launch_compress(const ZhBlockDesc *d_descs, u32 nblocks, ZhWorkspace 
     if (prof().on) for (int k = 0; k < 4; k++) ev.push_back(prof_event());
   }
   if (!ev.empty()) (void)hipEventRecord(ev[0], stream);
-  (void)hipMemsetAsync(ws.ctr, 0, 16, stream);  // block counters: K1's, K3's, K4's
+  (void)hipMemsetAsync(ws.ctr, 0, 4, stream);  // K1's block counter
   // levels >= ZH_DEEP_LEVEL: the deep chain matcher; below: K1's dual-hash parse
   if (level >= ZH_DEEP_LEVEL) {
     hipError_t const e = lz_deep_launch(d_descs, nblocks, ws, level, stream);
