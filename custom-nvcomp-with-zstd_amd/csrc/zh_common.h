@@ -48,17 +48,24 @@ enum : u32 {
 // FSE chain segments (zh_entropy.hip K3): each of the three tables' chains is cut into
 // ZH_K3_SEGS segments of L steps (L a multiple of ZH_K3_RUN); lane t * ZH_K3_SEGS + g of the
 // chain wave runs segment g of table t.  Step e of table t is element
-//   ((r / RUN) * 64 + t * ZH_K3_SEGS + g) * RUN + r % RUN,   g = e / L, r = e % L
+//   ((r / RUN) * ZH_K3_SLOTS + t * ZH_K3_SEGS + g) * RUN + r % RUN,   g = e / L, r = e % L
 // of the state (u16) and code (u8) arrays, RUN = ZH_K3_RUN: RUN consecutive steps of a
 // segment are contiguous (the packing kernel's 64-step chunks are whole lines) and the 63
 // segments' runs are adjacent.
-#define ZH_K3_SEGS 21u
+// ZH_K3_W waves run one block's chains (21 segments per table and wave): the batch row of a
+// layout holds ZH_K3_SLOTS = 64 ZH_K3_W segment slots.
+#ifndef ZH_K3_W
+#define ZH_K3_W 1u
+#endif
+#define ZH_K3_SEGS (21u * ZH_K3_W)
+#define ZH_K3_SLOTS (64u * ZH_K3_W)
 #define ZH_K3_RUN 16u
 #define ZH_K3_TSTRIDE (ZH_K3_SEGS * ZH_K3_RUN)  // elements between a step's LL, OF and ML entries
 #define ZH_K3_SEGLEN(nbseq) ((((nbseq) + ZH_K3_SEGS - 1u) / ZH_K3_SEGS + ZH_K3_RUN - 1u) & ~(ZH_K3_RUN - 1u))
-#define ZH_K3_BYTES(nbseq) (192u * ZH_K3_SEGLEN(nbseq))
+#define ZH_K3_CODES(L) (2u * ZH_K3_SLOTS * (L))  // byte offset of the codes (after the u16 states)
+#define ZH_K3_BYTES(nbseq) (3u * ZH_K3_SLOTS * ZH_K3_SEGLEN(nbseq))
 #define ZH_LIT_BYTES (ZH_K3_BYTES(ZH_SEQ_CAP) > (u32)ZH_BLOCK_MAX ? ZH_K3_BYTES(ZH_SEQ_CAP) : (u32)ZH_BLOCK_MAX)
-static_assert(3u * ZH_K3_SEGS <= 64u, "one lane per (table, segment)");
+static_assert(3u * ZH_K3_SEGS <= ZH_K3_SLOTS, "one lane per (table, segment)");
 #define ZH_META_BYTES 256u  // u32[4] counters + u32[60] diagnostic stamps (-DZH_STAMPS builds)
 //   fse   : hand-off from the entropy kernel to the FSE chain and packing kernels:
 //           the block's three FSE tables (state tables + symbol transforms, ZH_FSE_TAB_BYTES)
@@ -124,7 +131,7 @@ struct ZhWorkspace {
 __host__ __device__ __forceinline__ u32 zh_k3_magic(u32 L) { return ((1u << 24) + L - 1u) / L; }
 __device__ __forceinline__ u32 zh_k3_index(u32 e, u32 t, u32 L, u32 m) {
   u32 const g = __umulhi(e << 8, m), r = e - g * L;
-  return ((r / ZH_K3_RUN) * 64u + t * ZH_K3_SEGS + g) * ZH_K3_RUN + (r & (ZH_K3_RUN - 1u));
+  return ((r / ZH_K3_RUN) * ZH_K3_SLOTS + t * ZH_K3_SEGS + g) * ZH_K3_RUN + (r & (ZH_K3_RUN - 1u));
 }
 
 // Status codes written per item (values of cuda_zstd::Status).

@@ -1735,7 +1735,7 @@ extern "C" __global__ __launch_bounds__(K2_THREADS) void zh_entropy_kernel(const
       // waves (wave 0 is otherwise idle here): a lane per 16-step run (contiguous in the
       // layout), its 16 records, three 16-byte stores
       u32 const k3L = ZH_K3_SEGLEN(ns), k3m = zh_k3_magic(k3L);
-      u8 *const cb = ws.lits(b) + 128u * k3L;
+      u8 *const cb = ws.lits(b) + ZH_K3_CODES(k3L);
       for (u32 k0 = 16u * (lane + 64u * wave); k0 < ns; k0 += 16u * K2_THREADS) {
         u64 r[16];
 #pragma unroll
@@ -1816,21 +1816,27 @@ extern "C" __global__ __launch_bounds__(K2_THREADS) void zh_entropy_kernel(const
 // neighbour's exit reruns from the right entry until its new trajectory meets the stored one
 // (from there on every state is already right).  The states written are exactly the serial
 // chain's.  The kernel's time is a block's longest segment, not its whole chain.
-constexpr u32 K3_SEGS = ZH_K3_SEGS;  // 3 x 21 = 63 lanes
+constexpr u32 K3_SEGS = ZH_K3_SEGS;  // 3 x 21 x ZH_K3_W lanes
+constexpr u32 K3_W = ZH_K3_W;        // waves per block
+#ifndef ZH_K3_OCC
+#define ZH_K3_OCC 8  // minimum waves per SIMD the chain kernel is compiled for (8: <= 64 VGPRs)
+#endif
 #ifndef ZH_K3_WARM
 #define ZH_K3_WARM 128
 #endif
 constexpr u32 K3_WARM = ZH_K3_WARM;  // warm-up steps before a segment's first step (64 -> 128: entropy
                                      // 3.05 -> 3.02 ms at 16,384 blocks, 0.775 -> 0.75 at 2,048)
-constexpr u32 K3_WAVES = 4;    // blocks (one per wave) per workgroup: the CU holds at most 16 workgroups
+constexpr u32 K3_WAVES = K3_W == 1 ? 4 : K3_W;  // waves per workgroup (the CU holds at most 16 workgroups)
+constexpr u32 K3_BPW = K3_WAVES / K3_W;          // blocks per workgroup
 constexpr u32 K3_TAB_STRIDE = (ZH_FSE_TAB_BYTES + 15) & ~15u;
-constexpr u32 K3_LDS = K3_WAVES * K3_TAB_STRIDE;
+constexpr u32 K3_LDS = K3_BPW * K3_TAB_STRIDE + 64;  // + the workgroup's exchange words (K3_W > 1)
 constexpr u32 K3_BATCH = 16;   // steps per code load / state store
 constexpr u32 K3_TABW = ZH_FSE_TAB_BYTES / 4;
 
-// K3 of block bb (one wave; the caller checked that the block needs it); smem = the wave's
-// K3_TAB_STRIDE bytes of LDS
-__device__ __forceinline__ void k3_chain(ZhWorkspace ws, u32 bb, u8 *smem, u32 lane) {
+// K3 of block bb (K3_W waves; the caller checked that the block needs it); smem = the block's
+// K3_TAB_STRIDE bytes of LDS, xw = the workgroup's exchange words (K3_W > 1); lane = the
+// thread's index among the block's K3_W * 64 (lane t * K3_SEGS + g runs segment g of table t)
+__device__ __forceinline__ void k3_chain(ZhWorkspace ws, u32 bb, u8 *smem, u32 lane, u32 *xw) {
 #ifdef ZH_STAMPS
   u64 const k3pre = __builtin_amdgcn_s_memtime();
   u64 const k3rt0 = __builtin_amdgcn_s_memrealtime();
@@ -1838,27 +1844,32 @@ __device__ __forceinline__ void k3_chain(ZhWorkspace ws, u32 bb, u8 *smem, u32 l
   u32 *ff = ws.fsef(bb);
   {
     const u32 *src = (const u32 *)ws.fse(bb);
-    u32 v[(K3_TABW + 63) / 64];
+    constexpr u32 NT = 64 * K3_W;
+    u32 v[(K3_TABW + NT - 1) / NT];
 #pragma unroll
-    for (u32 q = 0; q < (K3_TABW + 63) / 64; q++) v[q] = 64 * q + lane < K3_TABW ? src[64 * q + lane] : 0u;
+    for (u32 q = 0; q < (K3_TABW + NT - 1) / NT; q++) v[q] = NT * q + lane < K3_TABW ? src[NT * q + lane] : 0u;
 #pragma unroll
-    for (u32 q = 0; q < (K3_TABW + 63) / 64; q++)
-      if (64 * q + lane < K3_TABW) ((u32 *)smem)[64 * q + lane] = v[q];
+    for (u32 q = 0; q < (K3_TABW + NT - 1) / NT; q++)
+      if (NT * q + lane < K3_TABW) ((u32 *)smem)[NT * q + lane] = v[q];
   }
-  // the tables are this wave's own: LDS executes one wave's operations in order
-  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  u32 const t = min(lane / K3_SEGS, 2u), g = lane - K3_SEGS * t;  // lane 63: an empty segment
+  if constexpr (K3_W == 1) {
+    // the tables are this wave's own: LDS executes one wave's operations in order
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+  } else {
+    __syncthreads();
+  }
+  u32 const t = min(lane / K3_SEGS, 2u), g = lane - K3_SEGS * t;  // lanes >= 3 K3_SEGS: an empty segment
   u32 const nbSeq = ff[ZH_FF_NBSEQ];
   const u16 *stT = (const u16 *)(smem + (t == 0 ? ZH_FT_STLL : t == 1 ? ZH_FT_STOF : ZH_FT_STML));
   const FseSym *syT = (const FseSym *)(smem + (t == 0 ? ZH_FT_SYLL : t == 1 ? ZH_FT_SYOF : ZH_FT_SYML));
-  // chain layout (zh_common.h): batch k of this lane's segment at element (64 k + lane) * 16
+  // chain layout (zh_common.h): batch k of this lane's segment at element (SLOTS k + lane) * 16
   u32 const seglen = ZH_K3_SEGLEN(nbSeq), nk = seglen / K3_BATCH;
-  u16 *const gst = (u16 *)ws.lits(bb);                 // states
-  const u8 *const cbase = ws.lits(bb) + 128u * seglen;  // codes
-  u32 const ln = lane;  // (slot 63 exists in the layout and is never read by the packing kernel)
+  u16 *const gst = (u16 *)ws.lits(bb);                          // states
+  const u8 *const cbase = ws.lits(bb) + ZH_K3_CODES(seglen);    // codes
+  u32 const ln = lane;  // (slots past 3 K3_SEGS exist in the layout and are never read by the packing kernel)
   // element of batch k (16 steps) of a slot's segment
-  auto at = [&](u32 k, u32 slot) { return ((k * K3_BATCH / ZH_K3_RUN) * 64u + slot) * ZH_K3_RUN + (k * K3_BATCH) % ZH_K3_RUN; };
+  auto at = [&](u32 k, u32 slot) { return ((k * K3_BATCH / ZH_K3_RUN) * ZH_K3_SLOTS + slot) * ZH_K3_RUN + (k * K3_BATCH) % ZH_K3_RUN; };
   auto codes_at = [&](u32 k, u32 slot) { return *(const uint4 *)(cbase + at(k, slot)); };  // batch k's 16 codes
   u32 const a = lane < 3 * K3_SEGS ? g * seglen : 3u * K3_SEGS * seglen;  // first step (lane 63: none)
   auto init_state = [&](u32 code) {  // FSE_initCState2
@@ -1880,18 +1891,23 @@ __device__ __forceinline__ void k3_chain(ZhWorkspace ws, u32 bb, u8 *smem, u32 l
     entry = init_state(codes_at(0, ln).x & 63u);
   } else {
     constexpr u32 NW = K3_WARM / K3_BATCH;
+    constexpr u32 CH = NW < 8u ? NW : 8u;  // batches per group of loads (8 x 16 B in flight)
+    static_assert(NW % CH == 0, "warm-up groups");
     u32 const kw = nk > NW ? nk - NW : 0u, ep = a - seglen;  // first warm-up batch, first step of segment g-1
-    uint4 cw[NW];
-#pragma unroll
-    for (u32 j = 0; j < NW; j++) cw[j] = kw + j < nk ? codes_at(kw + j, ln - 1) : make_uint4(0, 0, 0, 0);
     u32 s = stT[0];
 #pragma unroll
-    for (u32 j = 0; j < NW; j++) {
-      u32 const w[4] = {cw[j].x, cw[j].y, cw[j].z, cw[j].w};
+    for (u32 j0 = 0; j0 < NW; j0 += CH) {
+      uint4 cw[CH];
 #pragma unroll
-      for (u32 q = 0; q < K3_BATCH; q++) {
-        u32 const e = ep + K3_BATCH * (kw + j) + q;
-        s = step(s, (w[q >> 2] >> (8 * (q & 3))) & 63u, kw + j < nk && e >= 1 && e < nbSeq);
+      for (u32 j = 0; j < CH; j++) cw[j] = kw + j0 + j < nk ? codes_at(kw + j0 + j, ln - 1) : make_uint4(0, 0, 0, 0);
+#pragma unroll
+      for (u32 j = 0; j < CH; j++) {
+        u32 const w[4] = {cw[j].x, cw[j].y, cw[j].z, cw[j].w};
+#pragma unroll
+        for (u32 q = 0; q < K3_BATCH; q++) {
+          u32 const e = ep + K3_BATCH * (kw + j0 + j) + q;
+          s = step(s, (w[q >> 2] >> (8 * (q & 3))) & 63u, kw + j0 + j < nk && e >= 1 && e < nbSeq);
+        }
       }
     }
     entry = s;
@@ -1936,10 +1952,26 @@ __device__ __forceinline__ void k3_chain(ZhWorkspace ws, u32 bb, u8 *smem, u32 l
   // Jacobi rounds: entry(g) = exit(g - 1); a changed entry reruns its segment until the new
   // trajectory merges with the stored one (exit then unchanged) or the segment ends
   for (;;) {
-    u32 const pe = wave_shr1(x);
+    u32 pe = wave_shr1(x);
+    if constexpr (K3_W > 1) {
+      // the first lane of a wave takes the last lane of the wave before (LDS, one barrier)
+      if ((lane & 63u) == 63u) xw[lane >> 6] = x;
+      __syncthreads();
+      if ((lane & 63u) == 0u && lane) pe = xw[(lane >> 6) - 1u];
+    }
     u32 const ne = (g == 0 || lane >= 3 * K3_SEGS) ? entry : pe;
     bool const active = ne != entry;
-    if (!__ballot(active)) break;
+    if constexpr (K3_W > 1) {
+      // any segment of the block to rerun: flag word xw[K3_W], cleared for the next round
+      if (__ballot(active) && (lane & 63u) == 0u) atomicOr(&xw[K3_W], 1u);
+      __syncthreads();
+      bool const any = xw[K3_W] != 0u;
+      __syncthreads();
+      if (lane == 0) xw[K3_W] = 0u;
+      if (!any) break;
+    } else {
+      if (!__ballot(active)) break;
+    }
 #ifdef ZH_STAMPS
     k3rounds++;
     k3rerun += __builtin_popcountll(__ballot(active));
@@ -1957,13 +1989,13 @@ __device__ __forceinline__ void k3_chain(ZhWorkspace ws, u32 bb, u8 *smem, u32 l
 #endif
 }
 
-extern "C" __global__ __launch_bounds__(64 * K3_WAVES) __attribute__((amdgpu_waves_per_eu(8, 8))) void zh_fse_chain_kernel(const ZhBlockDesc *__restrict__ blocks, u32 nblocks, ZhWorkspace ws) {
+extern "C" __global__ __launch_bounds__(64 * K3_WAVES) __attribute__((amdgpu_waves_per_eu(ZH_K3_OCC, 8))) void zh_fse_chain_kernel(const ZhBlockDesc *__restrict__ blocks, u32 nblocks, ZhWorkspace ws) {
   extern __shared__ __attribute__((aligned(16))) u8 smem_all[];
-  u32 const lane = lane_id(), wv = threadIdx.x >> 6;
-  u32 const bb = blockIdx.x * K3_WAVES + wv;
-  if (bb >= nblocks || blocks[bb].n == 0) return;
+  u32 const bw = threadIdx.x / (64 * K3_W), lane = threadIdx.x % (64 * K3_W);  // block of the workgroup, lane in it
+  u32 const bb = blockIdx.x * K3_BPW + bw;
+  if (bb >= nblocks || blocks[bb].n == 0) return;  // (block-uniform: all K3_W waves return)
   if (ws.fsef(bb)[ZH_FF_NEED] == 0) return;
-  k3_chain(ws, bb, smem_all + wv * K3_TAB_STRIDE, lane);  // this wave's block tables
+  k3_chain(ws, bb, smem_all + bw * K3_TAB_STRIDE, lane, (u32 *)(smem_all + K3_BPW * K3_TAB_STRIDE));  // this block's tables
 }
 
 // ======================= sequence bitstream packing (K2b) =======================
@@ -2083,7 +2115,7 @@ void entropy_launch(const ZhBlockDesc *d_descs, u32 nblocks, ZhWorkspace ws, u32
                      d_item_status, d_blk_size);
   // (persistent K3 / K4 waves taking blocks from a counter measured slower: entropy stage
   // 3.04 -> 3.22 ms at 16,384 blocks, 0.75 -> 0.80 ms at 2,048)
-  u32 const g3 = (nblocks + K3_WAVES - 1) / K3_WAVES, g4 = (nblocks + K4_WAVES - 1) / K4_WAVES;
+  u32 const g3 = (nblocks + K3_BPW - 1) / K3_BPW, g4 = (nblocks + K4_WAVES - 1) / K4_WAVES;
   hipLaunchKernelGGL(zh_fse_chain_kernel, dim3(g3), dim3(64 * K3_WAVES), K3_LDS, stream, d_descs, nblocks, ws);
   hipLaunchKernelGGL(zh_seq_pack_kernel, dim3(g4), dim3(64 * K4_WAVES), K4_WAVES * KP_LDS, stream, d_descs, nblocks, ws, d_item_size,
                      d_item_status, d_blk_size);

@@ -31,7 +31,7 @@ done
 for k in $(seq 1 ${ROUNDS:-3}); do
   for v in $VS; do
     if [ $v = A ]; then L=$P/libcuda_zstd_hip.so; elif [ $v = B ]; then L=$R/tools/libB.so; else L=$R/tools/libV_$v.so; fi
-    CUDA_ZSTD_HIP_LIB=$L timeout -k 10 200 python3 $R/bench.py --dataset ${DATASET:-mix} --steps 8 --warmup 2 --no-cpu-baseline --no-verify --no-decompress --no-legs > $R/gpurun_out/${TAG}_${v}${k}.json 2>/dev/null
+    CUDA_ZSTD_HIP_LIB=$L timeout -k 10 200 python3 $R/bench.py --dataset ${DATASET:-mix} --chunks ${CHUNKS:-16384} --steps 8 --warmup 2 --no-cpu-baseline --no-verify --no-decompress --no-legs > $R/gpurun_out/${TAG}_${v}${k}.json 2>/dev/null
     python3 -c "import json; d=json.loads(open('$R/gpurun_out/${TAG}_${v}${k}.json').read().strip().splitlines()[-1]); print('$v', d['value'], d['ms_per_step'], d['config']['kernel_ms'], d['config']['ratio'])"
   done
 done
