@@ -144,9 +144,6 @@ struct Out {
 
 // ---------------- bit sink: LSB-first fields, little-endian bytes (BIT_CStream) ----------------
 // Wave-uniform state; sw[] holds the pending partial byte in sw[0] bits [0, pend).
-#ifndef ZH_SINK_PACK
-#define ZH_SINK_PACK 0
-#endif
 struct BitSink {
   u32 pos;   // next byte to write in Out
   u32 pend;  // pending bits in sw[0] (0..7)
@@ -164,29 +161,6 @@ __device__ __forceinline__ void sink_append(BitSink &bs, const Out &o, u32 *sw, 
   u32 const nwords = (end + 31) >> 5;
   for (u32 w = 1 + lane; w < nwords + 1; w += 64) sw[w] = 0;
   wave_sync();
-#if ZH_SINK_PACK
-  {
-    // the lane's fields concatenated LSB-first into 128 bits (every caller appends <= 128 bits
-    // per lane), shifted to the lane's bit offset and ORed into the <= 5 sink words it touches:
-    // one ds_or per word instead of one or two per field
-    u64 lo = 0, hi = 0;
-    u32 off = 0;
-#pragma unroll
-    for (int k = 0; k < K; k++) {
-      u64 const v = (u64)(val[k] & ((nb[k] >= 32) ? 0xFFFFFFFFu : ((1u << nb[k]) - 1u)));
-      lo |= off < 64 ? v << off : 0ull;
-      hi |= off >= 64 ? v << (off - 64) : (off ? v >> (64 - off) : 0ull);
-      off += nb[k];
-    }
-    u32 const w = bit >> 5, sh = bit & 31, nwl = (sh + tot + 31) >> 5;
-    u32 const x0 = (u32)lo, x1 = (u32)(lo >> 32), x2 = (u32)hi, x3 = (u32)(hi >> 32);
-    u32 const y[5] = {x0 << sh, (x1 << sh) | (sh ? x0 >> (32 - sh) : 0u), (x2 << sh) | (sh ? x1 >> (32 - sh) : 0u),
-                      (x3 << sh) | (sh ? x2 >> (32 - sh) : 0u), sh ? x3 >> (32 - sh) : 0u};
-#pragma unroll
-    for (u32 i = 0; i < 5; i++)
-      if (i < nwl) atomicOr(&sw[w + i], y[i]);
-  }
-#else
 #pragma unroll
   for (int k = 0; k < K; k++) {
     if (nb[k]) {
@@ -197,7 +171,6 @@ __device__ __forceinline__ void sink_append(BitSink &bs, const Out &o, u32 *sw, 
       bit += nb[k];
     }
   }
-#endif
   wave_sync();
   u32 const full = end >> 3;
   const u8 *sb = (const u8 *)sw;

@@ -366,7 +366,13 @@ __device__ __forceinline__ void deep_search(const u32 *gdata, const u16 *gP16, u
 constexpr u32 MEMO_UNK = 0xFFFFu;
 constexpr u32 DQ_PER = 3;  // positions posted per blocked lane (the needed one + lookahead)
 __device__ __forceinline__ int memo_gain(u32 m) { return (m & 255u) ? 4 * (int)(m & 255u) - (int)(m >> 8) : -1000; }
-__device__ __forceinline__ u32 demand_segl(u32 nb) { return nb <= 16384u ? 16u : nb <= 32768u ? 32u : 64u; }
+#ifndef ZH_DEMAND_SEGL_MIN
+#define ZH_DEMAND_SEGL_MIN 16u  // segment length for blocks of <= 16 KiB (doubled per doubling of nb, <= 64)
+#endif
+__device__ __forceinline__ u32 demand_segl(u32 nb) {
+  u32 const s = nb <= 16384u ? ZH_DEMAND_SEGL_MIN : nb <= 32768u ? 2u * ZH_DEMAND_SEGL_MIN : 4u * ZH_DEMAND_SEGL_MIN;
+  return s < 64u ? s : 64u;
+}
 // LDS bytes the demand path needs above the staged bytes (memo, queue, exits), for nb positions
 __device__ __forceinline__ u32 demand_lds(u32 nb) { return ((2u * nb + 15u) & ~15u) + 2u * DQ_PER * DT + 4u * DT; }
 
