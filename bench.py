@@ -27,9 +27,9 @@ the measured thread count, one thread and all cores (the north star's ">= 10x al
 also the line's `vs_cpu_all_core`): all-core is measured when the process may use every core,
 otherwise the larger of the measured rate and the 1-thread rate x physical cores x the measured
 parallel efficiency (the conservative denominator).
-Extra legs at N=1 (not `value`): C3 on uniform random bytes and C2 (one 64 MiB frame through
-ZstdManager::compress), each with its roofline and libzstd beside it, and GPU decompression of
-the C3 frames.
+Extra legs at N=1 (not `value`): C3 on uniform random bytes, C2 (one 64 MiB frame through
+ZstdManager::compress) and C5 (level 9 with a COVER dictionary on 4,096 x 16 KiB JSON records),
+each with its roofline and libzstd beside it, and GPU decompression of the C3 frames.
 """
 import argparse
 import ctypes
@@ -321,6 +321,48 @@ def c2_leg(dev, steps, threads):
     return res
 
 
+def c5_leg(dev, threads):
+    """C5 (BASELINE.json configs[4]): 4,096 x 16 KiB JSON-like records at level 9 (the deep chain
+    matcher, LAZY2 parse) through the stream-ordered batch path, without a dictionary and with a
+    64 KiB COVER dictionary trained on every fourth record (tools/c5_dict.py's workload and
+    timing: device-resident records, HIP events, median of 5 after a warm-up).  CPU baseline:
+    libzstd ZSTD_compress_usingCDict level 9 with the same dictionary, one thread, every record.
+    libzstd decodes every GPU frame with the dictionary."""
+    import cuda_zstd
+    import zh_testlib as T
+
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import c5_dict as C
+
+    host = T.gen(T.DG_JSON, C.N, C.SEED, C.REC)
+    recs = [host[i * C.REC:(i + 1) * C.REC] for i in range(C.N)]
+    cover = cuda_zstd.Dictionary.train(recs[::4], C.DICT).content()
+    d_recs = torch.from_numpy(host).to(dev)
+    total = C.N * C.REC
+    runs = {}
+    for name, d in (("none", None), ("cover", cover)):
+        cuda_zstd.profile_enable(True)
+        frames, t = C.gpu_run(d_recs, d)
+        cuda_zstd.profile_enable(False)
+        launches, kms = cuda_zstd.profile_collect()
+        comp = sum(len(f) for f in frames)
+        ok = all(T.zstd_decompress(f, C.REC, dictionary=d) == r.tobytes() for r, f in zip(recs, frames)) if T.zstd() else None
+        runs[name] = {"value": round(total / t / 1e9, 3), "ratio": round(total / comp, 4), "libzstd_verified": ok,
+                      "roofline": leg_roofline(total + comp, kms, launches)}
+    res = dict(runs["cover"])
+    res.update({"unit": "GB/s", "level": C.LEVEL, "dict_bytes": len(cover),
+                "workload": "C5: 4096 x 16 KiB JSON-like records, level 9 (LAZY2 deep chain matcher), 64 KiB COVER dictionary "
+                            "trained on every 4th record; BatchedCompressor with the dictionary on the handle",
+                "no_dict": runs["none"]})
+    if threads and T.zstd():
+        lz, el = C.libzstd_cdict(recs, cover, C.LEVEL)
+        res["cpu_baseline"] = {"value": round(total / el / 1e9, 4), "unit": "GB/s", "cores": 1, "kind": "reference",
+                               "sample": "libzstd ZSTD_compress_usingCDict level 9 with the same COVER dictionary, one thread, all 4096 records",
+                               "ratio": round(total / lz, 4)}
+    del d_recs
+    return res
+
+
 def decompress_leg(b, steps, world):
     """GPU decompression of the frames just produced, device-resident:
     zh_decode_kernel through nvcomp_zstd_batched_decompress_async_v5, timed with events on
@@ -421,7 +463,7 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-verify", action="store_true", help="skip the libzstd decode of every rank-0 frame after timing")
     ap.add_argument("--no-decompress", action="store_true", help="skip the GPU decompression leg")
-    ap.add_argument("--no-legs", action="store_true", help="skip the C3-random and C2 legs (N=1)")
+    ap.add_argument("--no-legs", action="store_true", help="skip the C3-random, C2 and C5 legs (N=1)")
     ap.add_argument("--cpu-threads", default=None,
                     help="libzstd baseline threads: a number, or 'all' (the process affinity); default: every thread the "
                          "process may keep busy (affinity, capped by the cgroup quota and the pool share OMP_NUM_THREADS)")
@@ -525,6 +567,7 @@ def main():
         leg_threads = None if args.no_cpu_baseline else threads
         legs["c3_random"] = random_leg(dev, 5, leg_threads)
         legs["c2_64mib"] = c2_leg(dev, 5, leg_threads)
+        legs["c5_level9_dict"] = c5_leg(dev, leg_threads)
 
     if rank == 0:
         total_in = float(n_total * CHUNK)
