@@ -237,7 +237,8 @@ __device__ void deep_chains(const u32 *s32, u32 *prev, u32 *head, u16 *hb, u32 s
 // lane, both loading the whole 112 bytes per extension: C5 8.5 / 6.7 GB/s vs 9.1 / 7.3 this way).
 __device__ __forceinline__ u32 deep_search_one(const u32 *D32, const u16 *P16, const u32 *dprev, u32 i, bool valid, u32 pre, u32 nb, u32 n,
                                                u32 lim, u32 s0, u32 depth) {
-  // the next candidate after q (+ 1, 0 = none)
+  // the next candidate after q (+ 1, 0 = none).  (A four-hop table of the dictionary's links, one
+  // 8-byte L2 load per four candidates, measured slower: C5 with the COVER dictionary 13.5 -> 12.1 GB/s.)
   auto link = [&](u32 q) -> u32 {
     if (q < s0) return dprev[q];
     u32 const dl = P16[q - s0];
@@ -364,7 +365,25 @@ __device__ __forceinline__ void deep_search(const u32 *gdata, const u16 *gP16, u
 // the memo fit in LDS (C5's 16 KiB records with or without the 64 KiB dictionary).
 //   memo[i] (u16): 0xFFFF unsearched; else len | (bit length of off + 1) << 8 (the LAZY2 gain)
 constexpr u32 MEMO_UNK = 0xFFFFu;
-constexpr u32 DQ_PER = 3;  // positions posted per blocked lane (the needed one + lookahead)
+#ifndef ZH_DEEP_DEDUP
+#define ZH_DEEP_DEDUP 1  // (with the warm-up below: C5 13.8 / 12.3 -> 15.5 / 13.5 GB/s; alone no change)
+#endif
+// A position being searched (ZH_DEEP_DEDUP): a lane claims an unsearched position by clearing bit
+// 15 of its memo entry with an LDS atomic (known entries never have bit 15 set, so the clear cannot
+// touch them), and only the lane that saw MEMO_UNK come back searches it -- lanes and waves that
+// need the same position in the same round wait for that one search instead of repeating it.
+constexpr u32 MEMO_PEND = 0x7FFFu;
+__device__ __forceinline__ bool memo_unknown(u32 m) { return ZH_DEEP_DEDUP ? m >= MEMO_PEND : m == MEMO_UNK; }
+#ifndef ZH_DEEP_DQ
+#define ZH_DEEP_DQ 3
+#endif
+constexpr u32 DQ_PER = ZH_DEEP_DQ;  // positions posted per blocked lane (the needed one + lookahead)
+#ifndef ZH_DEEP_WARM
+#define ZH_DEEP_WARM (-2)  // first-walk warm-up: >= 0 positions, < 0 that many segment lengths
+#endif
+#ifndef ZH_DEEP_SEG0
+#define ZH_DEEP_SEG0 16u
+#endif
 __device__ __forceinline__ int memo_gain(u32 m) { return (m & 255u) ? 4 * (int)(m & 255u) - (int)(m >> 8) : -1000; }
 // Segment length: 16 positions for blocks of <= 16 KiB, doubled per doubling of nb (<= 64), and
 // doubled again for a dictionary's first block, whose searches (chains through the dictionary's
@@ -372,9 +391,18 @@ __device__ __forceinline__ int memo_gain(u32 m) { return (m & 255u) ? 4 * (int)(
 // entries (C5 level 9 with the 64 KiB dictionary 11.2 / 11.5 -> 11.7 / 12.2 GB/s; without a
 // dictionary 16 stays faster, 13.8 vs 13.0, as every wave keeps a segment).
 __device__ __forceinline__ u32 demand_segl(u32 nb, bool dict) {
-  u32 const s = (nb <= 16384u ? 16u : nb <= 32768u ? 32u : 64u) << (dict ? 1 : 0);
+  u32 const s = (nb <= 16384u ? ZH_DEEP_SEG0 : nb <= 32768u ? 2u * ZH_DEEP_SEG0 : 4u * ZH_DEEP_SEG0) << (dict ? 1 : 0);
   return s < 64u ? s : 64u;
 }
+// First-walk warm-up: a segment's first walk starts this many positions before the segment (a
+// walk from a wrong position meets the serial parse within a few steps, as K3's FSE chains do),
+// so its entry guess is usually the true one and fewer Jacobi iterations follow; positions before
+// the segment are walked but not recorded (tools/deep_jacobi_model.c).  The warm-up walks need the
+// positions the segment before also needs at the same time, hence ZH_DEEP_DEDUP.  Measured (C5
+// level 9, none / COVER dictionary GB/s, tools/gpu_diag.sh c5var): no warm-up 13.8 / 12.3; 16
+// positions 15.0 / 12.9; one segment 14.9 / 13.2; two 15.5 / 13.5 (Jacobi iterations 4.3 -> 2.3
+// and 3.5 -> 1.5); three 15.5 / 12.9; four 15.2 / 12.1.  Without the claims: 13.1-13.3 / 12.4-12.6.
+__device__ __forceinline__ u32 demand_warm(u32 segl) { return ZH_DEEP_WARM < 0 ? (u32)(-(ZH_DEEP_WARM)) * segl : (u32)ZH_DEEP_WARM; }
 // LDS bytes the demand path needs above the staged bytes (memo, queue, exits), for nb positions
 __device__ __forceinline__ u32 demand_lds(u32 nb) { return ((2u * nb + 15u) & ~15u) + 2u * DQ_PER * DT + 4u * DT; }
 
@@ -390,6 +418,9 @@ __device__ void deep_parse_demand(const u32 *D32, const u16 *P16, const u32 *dpr
   // unsearched below lim, no match at or past it (the oracle's len[] is 0 there)
   for (u32 i = tid; i < nb; i += DT) memo[i] = pre + i < lim ? (u16)MEMO_UNK : (u16)0;
   if (tid == 0) misc[2] = 0;
+#ifdef ZH_STAMPS
+  if (tid == 0) misc[4] = 0;
+#endif
   __syncthreads();
   u32 const g = tid, S = SEGL * g, SE = min(S + SEGL, nb);
   bool const sv = g < nseg;
@@ -406,11 +437,11 @@ __device__ void deep_parse_demand(const u32 *D32, const u16 *P16, const u32 *dpr
   u32 entry = S, ex = S;
   // one walk (first or Jacobi re-walk) of every lane with act0 set; all threads take part in the
   // search rounds.  old: the visited bits of the previous walk (re-walks).
-  auto walk = [&](u32 p0, bool act0) {
+  auto walk = [&](u32 p0, bool act0, u32 warm) {
     u64 const old = act0 ? (LM | MM) : 0ull;
     u64 nl = 0, nm = 0;
     bool act = act0 && p0 < SE, merged = false;
-    u32 p = p0, mpos = 0;
+    u32 p = p0 > warm ? p0 - warm : 0u, mpos = 0, ent = p;  // ent: the first position >= S reached
     for (;;) {
       // advance as far as the memo allows
 #ifdef ZH_STAMPS
@@ -420,32 +451,33 @@ __device__ void deep_parse_demand(const u32 *D32, const u16 *P16, const u32 *dpr
       bool adv = act;
       while (__ballot(adv)) {
         if (adv) {
+          if (ent < S && p >= S) ent = p;  // (warm-up: below S nothing is recorded)
           if (p >= SE) {
             act = adv = false;
-          } else if ((old >> (p - S)) & 1ull) {  // met the old trajectory: the rest is the old walk's
+          } else if (p >= S && ((old >> (p - S)) & 1ull)) {  // met the old trajectory: the rest is the old walk's
             merged = true;
             mpos = p - S;
             act = adv = false;
           } else {
             u32 const m0 = memo[p];
-            if (m0 == MEMO_UNK) {
+            if (memo_unknown(m0)) {
               need = p;
               adv = false;
             } else if ((m0 & 255u) == 0) {
-              nl |= 1ull << (p - S);
+              if (p >= S) nl |= 1ull << (p - S);
               p++;
             } else {
               u32 const m1 = p + 1 < nb ? (u32)memo[p + 1] : 0u, m2 = p + 2 < nb ? (u32)memo[p + 2] : 0u;
-              if (m1 == MEMO_UNK || m2 == MEMO_UNK) {
-                need = m1 == MEMO_UNK ? p + 1 : p + 2;
+              if (memo_unknown(m1) || memo_unknown(m2)) {
+                need = memo_unknown(m1) ? p + 1 : p + 2;
                 adv = false;
               } else {
                 int const g0 = memo_gain(m0);
                 if (memo_gain(m1) > g0 + 4 || memo_gain(m2) > g0 + 7) {  // deferred: p is a literal
-                  nl |= 1ull << (p - S);
+                  if (p >= S) nl |= 1ull << (p - S);
                   p++;
                 } else {
-                  nm |= 1ull << (p - S);
+                  if (p >= S) nm |= 1ull << (p - S);
                   p += m0 & 255u;
                 }
               }
@@ -466,7 +498,14 @@ __device__ void deep_parse_demand(const u32 *D32, const u16 *P16, const u32 *dpr
 #pragma unroll
       for (u32 t = 0; t < DQ_PER; t++) {
         u32 const x = need + t;
-        bool const post = need != ~0u && x < nb && memo[x] == MEMO_UNK;
+        bool post = need != ~0u && x < nb && memo[x] == MEMO_UNK;
+#if ZH_DEEP_DEDUP
+        if (post) {  // claim it: UNK -> PEND; a lane that finds it claimed leaves it to its claimant
+          u32 const sh = 16u * (x & 1u);
+          u32 const o = atomicAnd((u32 *)memo + (x >> 1), ~(0x8000u << sh));
+          post = ((o >> sh) & 0xFFFFu) == MEMO_UNK;
+        }
+#endif
         u64 const bm = __ballot(post);
         u32 const rank = __builtin_amdgcn_mbcnt_hi((u32)(bm >> 32), __builtin_amdgcn_mbcnt_lo((u32)bm, 0u));
         if (post) wq[nq + rank] = (u16)x;
@@ -489,7 +528,13 @@ __device__ void deep_parse_demand(const u32 *D32, const u16 *P16, const u32 *dpr
           memo[x] = (u16)(l ? l | ((31u - (u32)__builtin_clz((r >> 8) + 1u)) << 8) : 0u);
         }
       }
+#if ZH_DEEP_DEDUP
+      // (positions this wave waits for may be another wave's: re-read the memo from LDS)
+      if (nq == 0) __builtin_amdgcn_s_sleep(2);
+      __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
+#else
       __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+#endif
       __builtin_amdgcn_wave_barrier();
       DMSTAMP(st_srch);
 #else
@@ -539,11 +584,14 @@ __device__ void deep_parse_demand(const u32 *D32, const u16 *P16, const u32 *dpr
         MM = nm;
         ex = p;
       }
+      if (warm) entry = ent;  // (every walk ends at or past SE or merged at or past S)
     }
   };
-  walk(entry, sv);
+  walk(entry, sv, g == 0 ? 0u : demand_warm(SEGL));
 #ifdef ZH_STAMPS
   st_walk = (u32)(__builtin_amdgcn_s_memtime() - dm0);
+  u32 st_iter = 0;
+  if ((tid & 63u) == 0) atomicMax(&misc[4], st_walk);  // the slowest wave's first walk
 #endif
   for (;;) {
     if (sv) exL[g] = ex;
@@ -551,12 +599,16 @@ __device__ void deep_parse_demand(const u32 *D32, const u16 *P16, const u32 *dpr
     u32 const ne = g == 0 ? 0u : (sv ? exL[g - 1] : entry);
     bool const ch = sv && ne != entry;
     if (!wg_any(ch, &misc[0], tid)) break;
-    walk(ne, ch);
+    walk(ne, ch, 0u);
     if (ch) entry = ne;
+#ifdef ZH_STAMPS
+    st_iter++;
+#endif
   }
 #ifdef ZH_STAMPS
   st_jac = (u32)(__builtin_amdgcn_s_memtime() - dm0) - st_walk;
   if (tid == 0) { u32 *dbg = ws.dbg(b); dbg[20] = st_rounds; dbg[21] = st_searched; dbg[22] = st_walk; dbg[23] = st_jac;
+                  dbg[24] = st_iter; dbg[25] = misc[4];
                   dbg[0] = st_adv; dbg[1] = st_sync1; dbg[2] = st_srch; dbg[3] = st_sync2; }
 #endif
   // ---- records and literals (step 5 of deep_block)

@@ -60,6 +60,7 @@ for use in (False, True):
         print(f"  demand path: search rounds {dm[:, 0].mean():.1f}, positions searched {dm[:, 1].mean():.0f} of {REC}"
               f" ({dm[:, 1].mean() / REC * 100:.1f}%), first walk {dm[:, 2].mean():.0f} cycles, Jacobi {dm[:, 3].mean():.0f}"
               " (search+take+walk above = set-up; emit = walk + Jacobi + records)")
+        print(f"  Jacobi iterations {m[:, 28].astype(np.float64).mean():.2f}, slowest wave's first walk {m[:, 29].astype(np.float64).mean():.0f} cycles")
         ph4 = m[:, 4:8].astype(np.float64).mean(0)
         print(f"  wave 0 of the workgroup, summed over rounds: advance {ph4[0]:.0f}, post + barrier {ph4[1]:.0f}, search {ph4[2]:.0f},"
               f" barrier after search {ph4[3]:.0f} cycles")
