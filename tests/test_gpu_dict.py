@@ -4,6 +4,8 @@ reads them and libzstd's own dictionary frames at levels 1-19 (the dictionary's 
 repcodes and content).  Mirrors the reference's tests/test_dictionary.cu (train, compress with and
 without, round trip) and tests/test_dictionary_compression.cu (set_dictionary, compress,
 decompress)."""
+import os
+
 import numpy as np
 import pytest
 
@@ -148,6 +150,37 @@ def test_c5_level9_cover_64k(torch_cuda, libzstd):
     print(f"C5 (256 x 16 KiB, level 9): ratio {ratio0:.3f} without -> {ratio:.3f} with the 64 KiB COVER dictionary")
     assert ratio > 1.15 * ratio0
     assert ratio0 >= 6.6 and ratio >= 8.5, (ratio0, ratio)
+
+
+def test_c5_full_workload_vs_oracle(torch_cuda, libzstd):
+    """Config C5 at its full size (BASELINE.json configs[4], the bench's C5 leg): all 4,096 JSON-like
+    records of 16 KiB at level 9, without a dictionary and with the 64 KiB COVER dictionary trained
+    on every fourth record, through the stream-ordered batch path the bench times
+    (tools/c5_dict.py gpu_run).  Every GPU frame equals the oracle's and libzstd decodes it (the
+    oracle calls run on a thread pool: ctypes releases the GIL)."""
+    import sys
+    from concurrent.futures import ThreadPoolExecutor
+    import cuda_zstd
+
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools"))
+    import c5_dict as C
+
+    host = T.gen(T.DG_JSON, C.N, C.SEED, C.REC)
+    recs = [host[i * C.REC:(i + 1) * C.REC] for i in range(C.N)]
+    cover = cuda_zstd.Dictionary.train(recs[::4], C.DICT).content()
+    d_recs = torch_cuda.from_numpy(host).cuda()
+    workers = min(16, os.cpu_count() or 1)
+    for d in (None, cover):
+        frames, _ = C.gpu_run(d_recs, d)
+        assert len(frames) == C.N
+
+        def check(k):
+            f = frames[k]
+            return f == T.oracle_frame(recs[k], dictionary=d, level=9) and T.zstd_decompress(f, C.REC, dictionary=d) == recs[k].tobytes()
+
+        with ThreadPoolExecutor(workers) as ex:
+            bad = [k for k, ok in enumerate(ex.map(check, range(C.N))) if not ok]
+        assert not bad, (d is not None, bad[:8], len(bad))
 
 
 def test_dictionary_tables_ragged_sizes(torch_cuda):
