@@ -1488,7 +1488,13 @@ hipError_t launch_decompress(const ZhDecArgs &a0, u32 nitems, hipStream_t stream
   // every group + one chain + the last group's execution, so the first group is the larger
   // (2 : 1).  Measured (profiles/r02m_dec_seq.json): G = 1 / 2 / 3 / 4 / 8 -> 56.8 / 59.1 /
   // 56.0 / 56.2 / 36.6 GB/s, 2 : 1 and 3 : 1 splits 59.3 / 59.7.
-  constexpr u32 G = 2, W0 = 2, MIN_GROUP = 1024;
+#ifndef ZH_DEC_G
+#define ZH_DEC_G 2
+#endif
+#ifndef ZH_DEC_W0
+#define ZH_DEC_W0 2
+#endif
+  constexpr u32 G = ZH_DEC_G, W0 = ZH_DEC_W0, MIN_GROUP = 1024;
   StreamPipe<G> *p = (!dbg && nitems >= G * MIN_GROUP) ? stream_pipe<DecPipeTag, G>(stream) : nullptr;
   if (!p) {
     group(0, nitems, stream, nullptr);

@@ -71,7 +71,7 @@ def _worker(rank, world, port, outdir, n_total):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,n_total", [(2, 24), (3, 10)])
+@pytest.mark.parametrize("world,n_total", [(2, 24), (3, 10), (8, 67)])  # (8: the driver's scaling node, ragged 9 x 7 + 4)
 def test_sharded_batch_on_gpu(tmp_path, libzstd, world, n_total):
     mp.spawn(_worker, args=(world, _free_port(), str(tmp_path), n_total), nprocs=world, join=True)
     img = np.load(tmp_path / "img.npy")

@@ -9,13 +9,13 @@ if [ "$1" = build ]; then
   while [ $# -ge 2 ]; do
     N=$1; F=$2; shift 2
     mkdir -p /tmp/vb_$N
-    # (zh_lz.hip, zh_lz_deep.hip and zh_entropy.hip get the flags; the other objects are the in-tree build's)
-    for f in zh_lz zh_lz_deep zh_entropy; do
+    # (zh_lz.hip, zh_lz_deep.hip, zh_entropy.hip and zh_decode.hip get the flags; the other objects are the in-tree build's)
+    for f in zh_lz zh_lz_deep zh_entropy zh_decode; do
       /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -Wall -I$R/include -I$P/csrc $F -c $P/csrc/$f.hip -o /tmp/vb_$N/$f.o
       /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -Wall -I$R/include -I$P/csrc $F -DZH_STAMPS -c $P/csrc/$f.hip -o /tmp/vb_$N/${f}_s.o
     done
-    /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o $R/tools/libV_$N.so /tmp/vb_$N/zh_lz.o /tmp/vb_$N/zh_entropy.o /tmp/vb_$N/zh_lz_deep.o $P/build/zh_plan.o $P/build/zh_decode.o $P/build/zh_host.o $P/build/zh_dict.o -ldl
-    /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o $R/tools/libVS_$N.so /tmp/vb_$N/zh_lz_s.o /tmp/vb_$N/zh_entropy_s.o /tmp/vb_$N/zh_lz_deep_s.o $P/build_stamps/zh_plan.o $P/build_stamps/zh_decode.o $P/build_stamps/zh_host.o $P/build_stamps/zh_dict.o -ldl
+    /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o $R/tools/libV_$N.so /tmp/vb_$N/zh_lz.o /tmp/vb_$N/zh_entropy.o /tmp/vb_$N/zh_lz_deep.o /tmp/vb_$N/zh_decode.o $P/build/zh_plan.o $P/build/zh_host.o $P/build/zh_dict.o -ldl
+    /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o $R/tools/libVS_$N.so /tmp/vb_$N/zh_lz_s.o /tmp/vb_$N/zh_entropy_s.o /tmp/vb_$N/zh_lz_deep_s.o /tmp/vb_$N/zh_decode_s.o $P/build_stamps/zh_plan.o $P/build_stamps/zh_host.o $P/build_stamps/zh_dict.o -ldl
   done
   exit 0
 fi
