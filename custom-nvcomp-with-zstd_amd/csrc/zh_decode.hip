@@ -1487,7 +1487,9 @@ hipError_t launch_decompress(const ZhDecArgs &a0, u32 nitems, hipStream_t stream
   // of the later group and the execution of the earlier one.  The end is about phase 1 of
   // every group + one chain + the last group's execution, so the first group is the larger
   // (2 : 1).  Measured (profiles/r02m_dec_seq.json): G = 1 / 2 / 3 / 4 / 8 -> 56.8 / 59.1 /
-  // 56.0 / 56.2 / 36.6 GB/s, 2 : 1 and 3 : 1 splits 59.3 / 59.7.
+  // 56.0 / 56.2 / 36.6 GB/s, 2 : 1 and 3 : 1 splits 59.3 / 59.7.  Re-measured in round 4 with
+  // the current kernels (tools/dec_ab.sh, profiles/r04zd_decode_groups_ab.json): G = 1 / 2 / 3
+  // -> 57.6 / 60.6 / 59.1 GB/s; two groups 1 : 1 / 2 : 1 / 3 : 1 -> 60.6 / 60.6 / 60.5.
 #ifndef ZH_DEC_G
 #define ZH_DEC_G 2
 #endif
