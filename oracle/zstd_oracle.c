@@ -819,7 +819,7 @@ static u32 g_TL[1 << ZH_HASH_LOG_LONG], g_TS[1 << ZH_HASH_LOG_SHORT];
 /* K1's parse mode of the level (ZH_K1_MODE): 0 = both tables, lazy-1 check (levels 3-4);
  * 1 = the short (5-byte) table only, lazy-1 (level 2); 2 = the short table only, greedy (level 1).
  * Set by orc_compress_frame_lv. */
-static int orc_lz_mode = 0;
+static _Thread_local int orc_lz_mode = 0; /* per thread: callers may run frames on a thread pool */
 static void match_info_tiles(const u8 *src, u32 n, u32 t0, u32 t1, u32 skip_from, u8 *len, u16 *off) {
   const u32 EMPTY = 0xFFFFFFFFu;
   u32 const lim = n - ZH_HASH_READ;
@@ -861,8 +861,8 @@ void orc_lz_match_info(const u8 *src, u32 n, u8 *len, u16 *off) {
  * libzstd ZSTD_compressBlock_lazy_generic's depth-2 rule on this matcher's candidates -- the
  * match at p is deferred when the match at p+1 gains more than 4, or the one at p+2 more than 7,
  * with gain = 4 x length - bit length of (offset + 1).  Set by orc_compress_frame_lv. */
-static int orc_parse_lazy2 = 0;
-static int orc_parse_level = 3; /* levels >= ZH_DEEP_LEVEL: the deep matcher (orc_lz_parse_deep) */
+static _Thread_local int orc_parse_lazy2 = 0;
+static _Thread_local int orc_parse_level = 3; /* levels >= ZH_DEEP_LEVEL: the deep matcher (orc_lz_parse_deep) */
 static int match_gain(const u8 *len, const u16 *off, u32 p) {
   return len[p] ? 4 * (int)len[p] - (31 - __builtin_clz((u32)off[p] + 1u)) : -1000;
 }
