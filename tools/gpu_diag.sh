@@ -14,6 +14,7 @@
 #   c5var    for B (the in-tree build) and each tools/libV_<X>.so in $VARIANTS: the deep-matcher
 #            GPU tests, C5 at level 9 and the deep-matcher stamps
 #   c5lds    LDS / wave-state counters of the deep matcher on the C5 workload (one --pmc pass)
+#   c5sq     instruction mix / issue counters of the deep matcher on the C5 workload (one --pmc pass)
 # usage: bash tools/gpu_diag.sh TAG step...
 set -e
 R=${GRAFT_REPO_ROOT:-$(pwd)}
@@ -38,6 +39,9 @@ for s in "$@"; do
     c5lds)
       (cd /tmp && export TMPDIR=/tmp && C5_GPU_ONLY=1 C5_LEVEL=9 timeout -s KILL 200 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_INST_LDS SQ_ACTIVE_INST_LDS SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAIT_ANY SQ_INSTS_VALU GRBM_GUI_ACTIVE \
         --kernel-trace -d $R/gpurun_out/${TAG}_c5lds -o run --output-format csv -- python3 $R/tools/c5_dict.py > $R/gpurun_out/${TAG}_c5lds.log 2>&1) || { echo "c5lds failed"; exit 3; } ;;
+    c5sq)
+      (cd /tmp && export TMPDIR=/tmp && C5_GPU_ONLY=1 C5_LEVEL=9 timeout -s KILL 200 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_ANY SQ_WAIT_INST_ANY GRBM_GUI_ACTIVE \
+        --kernel-trace -d $R/gpurun_out/${TAG}_c5sq -o run --output-format csv -- python3 $R/tools/c5_dict.py > $R/gpurun_out/${TAG}_c5sq.log 2>&1) || { echo "c5sq failed"; exit 3; } ;;
     c5var)
       for v in B $VARIANTS; do
         L=$R/custom-nvcomp-with-zstd_amd/libcuda_zstd_hip.so; LS=$R/tools/libcuda_zstd_hip_stamps.so
