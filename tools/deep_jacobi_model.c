@@ -8,7 +8,9 @@
  * On 64 C5 records (no dictionary, 16-position segments) it reproduces the GPU's 10.9 search rounds
  * and 37.6 % of positions searched; a prefix-max entry rule and speculative posting at p + len
  * change nothing, a warm-up walk before each segment cuts the Jacobi iterations (4.2 -> 2.2 at 32
- * positions), which the GPU confirmed once duplicate searches were claimed away.
+ * positions), which the GPU confirmed once duplicate searches were claimed away;
+ * dealing segments to waves round-robin instead of in 64-segment runs needs more passes (the
+ * slowest wave's first walk 13.7 -> 18.7 at 16 positions + 32 warm-up).
  */
 #include "../oracle/zstd_oracle.c"
 #include <stdio.h>
@@ -47,14 +49,15 @@ static void matches(const u8 *buf, u32 pre, u32 n) {
 /* one lane's walk state */
 typedef struct { u32 S, SE, p, need, spec, ent; int act, adv, merged; u32 mpos; u64 nl, nm, old; } Lane;
 
-static int DQ = 3, SEGL = 16, RULE = 0, SPEC = 0, WARM = 0; /* RULE 0: predecessor's exit, 1: prefix max of exits */
+static int DQ = 3, SEGL = 16, RULE = 0, SPEC = 0, WARM = 0, INTER = 0; /* INTER: wave w takes segments w, w + nw, ... */
+static u32 NW = 16; /* RULE 0: predecessor's exit, 1: prefix max of exits */
 static long searched;
 
 /* walk of the lanes [w*64, w*64+64) with act0 set, from p0[]; returns the wave's search passes */
 static int walk_wave(u32 w, u32 nseg, const u32 *p0, const int *act0, u64 *LM, u64 *MM, u32 *ex, u32 *entry_out, u32 warm) {
   Lane L[64];
   for (int l = 0; l < 64; l++) {
-    u32 g = w * 64 + l;
+    u32 g = INTER ? w + NW * l : w * 64 + l;
     Lane *x = &L[l];
     memset(x, 0, sizeof *x);
     if (g >= nseg) continue;
@@ -109,7 +112,7 @@ static int walk_wave(u32 w, u32 nseg, const u32 *p0, const int *act0, u64 *LM, u
     rounds += (nq + 63) / 64; /* search passes: lanes = queue entries, 64 at a time */
   }
   for (int l = 0; l < 64; l++) {
-    u32 g = w * 64 + l;
+    u32 g = INTER ? w + NW * l : w * 64 + l;
     if (g >= nseg || !act0[g]) continue;
     Lane *x = &L[l];
     if (x->merged) {
@@ -130,6 +133,7 @@ static void model(const u8 *buf, u32 pre, u32 n, long *acc) {
   matches(buf, pre, n);
   for (u32 i = 0; i < NB; i++) MEMO[i] = pre + i < LIM ? 0 : 1;
   u32 const nseg = (NB + SEGL - 1) / SEGL, nw = (nseg + 63) / 64;
+  NW = nw;
   u32 *entry = calloc(nseg, 4), *ex = calloc(nseg, 4), *ne = calloc(nseg, 4);
   u64 *LM = calloc(nseg, 8), *MM = calloc(nseg, 8);
   int *act = calloc(nseg, sizeof(int));
@@ -194,10 +198,9 @@ int main(int argc, char **argv) {
   LEN = malloc(rec + 64);
   OFF = malloc(4 * (rec + 64));
   MEMO = malloc(2 * (rec + 64));
-  static const int cfg[][5] = {{3, 16, 0, 0, 0}, {3, 16, 1, 0, 0}, {4, 16, 0, 0, 0}, {3, 16, 0, 3, 0}, {3, 16, 0, 0, 16}, {3, 16, 0, 0, 32},
-                               {3, 32, 0, 0, 0}, {3, 32, 0, 0, 32}, {3, 32, 0, 0, 64}};  /* DQ, SEGL, rule, spec, warm-up */
+  static const int cfg[][6] = {{3, 16, 0, 0, 32, 0}, {3, 16, 0, 0, 32, 1}, {3, 32, 0, 0, 64, 0}, {3, 32, 0, 0, 64, 1}};  /* DQ, SEGL, rule, spec, warm-up, interleave */  /* DQ, SEGL, rule, spec, warm-up */
   for (u32 c = 0; c < sizeof cfg / sizeof cfg[0]; c++) {
-    DQ = cfg[c][0]; SEGL = cfg[c][1]; RULE = cfg[c][2]; SPEC = cfg[c][3]; WARM = cfg[c][4];
+    DQ = cfg[c][0]; SEGL = cfg[c][1]; RULE = cfg[c][2]; SPEC = cfg[c][3]; WARM = cfg[c][4]; INTER = cfg[c][5];
     long acc[7] = {0};
     for (u32 r = 0; r < nrec; r++) {
       if (dn) memcpy(buf, dict, dn);
@@ -205,9 +208,9 @@ int main(int argc, char **argv) {
       memset(buf + dn + rec, 0, 64);
       model(buf, dn, dn + rec, acc);
     }
-    printf("DQ %d spec %d warm %d SEGL %d rule %s: first-walk passes %.2f, Jacobi iterations %.2f, Jacobi passes %.2f, total passes %.2f, "
+    printf("DQ %d spec %d warm %d inter %d SEGL %d rule %s: first-walk passes %.2f, Jacobi iterations %.2f, Jacobi passes %.2f, total passes %.2f, "
            "searched %.1f%%, parse ok %ld/%u\n",
-           DQ, SPEC, WARM, SEGL, RULE ? "prefix-max" : "predecessor", (double)acc[0] / nrec, (double)acc[1] / nrec, (double)acc[2] / nrec,
+           DQ, SPEC, WARM, INTER, SEGL, RULE ? "prefix-max" : "predecessor", (double)acc[0] / nrec, (double)acc[1] / nrec, (double)acc[2] / nrec,
            (double)(acc[0] + acc[2]) / nrec, 100.0 * acc[3] / acc[6], acc[4], nrec);
   }
   return 0;
