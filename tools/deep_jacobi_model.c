@@ -10,7 +10,10 @@
  * change nothing, a warm-up walk before each segment cuts the Jacobi iterations (4.2 -> 2.2 at 32
  * positions), which the GPU confirmed once duplicate searches were claimed away;
  * dealing segments to waves round-robin instead of in 64-segment runs needs more passes (the
- * slowest wave's first walk 13.7 -> 18.7 at 16 positions + 32 warm-up).
+ * slowest wave's first walk 13.7 -> 18.7 at 16 positions + 32 warm-up; runs of 32: 12.9), and so
+ * does posting 4-8 positions after a literal step (13.4-13.8).  The slowest wave is the one over
+ * the record's first KiB (few matches yet: almost every position searched, PERWAVE=1 prints the
+ * per-wave passes), about 1.65 x the mean wave.
  */
 #include "../oracle/zstd_oracle.c"
 #include <stdio.h>
@@ -47,9 +50,9 @@ static void matches(const u8 *buf, u32 pre, u32 n) {
 }
 
 /* one lane's walk state */
-typedef struct { u32 S, SE, p, need, spec, ent; int act, adv, merged; u32 mpos; u64 nl, nm, old; } Lane;
+typedef struct { u32 S, SE, p, need, spec, ent; int lit; int act, adv, merged; u32 mpos; u64 nl, nm, old; } Lane;
 
-static int DQ = 3, SEGL = 16, RULE = 0, SPEC = 0, WARM = 0, INTER = 0; /* INTER: wave w takes segments w, w + nw, ... */
+static int DQ = 3, SEGL = 16, RULE = 0, SPEC = 0, WARM = 0, INTER = 0, DQL = 0; /* INTER: segments dealt to waves in runs of INTER (0: 64); DQL: posts after a literal step */ /* INTER: wave w takes segments w, w + nw, ... */
 static u32 NW = 16; /* RULE 0: predecessor's exit, 1: prefix max of exits */
 static long searched;
 
@@ -57,7 +60,7 @@ static long searched;
 static int walk_wave(u32 w, u32 nseg, const u32 *p0, const int *act0, u64 *LM, u64 *MM, u32 *ex, u32 *entry_out, u32 warm) {
   Lane L[64];
   for (int l = 0; l < 64; l++) {
-    u32 g = INTER ? w + NW * l : w * 64 + l;
+    u32 g = INTER ? ((l / INTER) * NW + w) * INTER + l % INTER : w * 64 + l;
     Lane *x = &L[l];
     memset(x, 0, sizeof *x);
     if (g >= nseg) continue;
@@ -81,7 +84,7 @@ static int walk_wave(u32 w, u32 nseg, const u32 *p0, const int *act0, u64 *LM, u
         if (p >= x->S && x->ent == ~0u) x->ent = p;
         if (p >= x->S && ((x->old >> (p - x->S)) & 1)) { x->merged = 1; x->mpos = p - x->S; x->act = x->adv = 0; break; }
         if (!MEMO[p]) { x->need = p; x->adv = 0; break; }
-        if (!LEN[p]) { if (p >= x->S) x->nl |= 1ull << (p - x->S); x->p++; continue; }
+        if (!LEN[p]) { if (p >= x->S) x->nl |= 1ull << (p - x->S); x->p++; x->lit = 1; continue; }
         int k1 = p + 1 < NB && !MEMO[p + 1], k2 = p + 2 < NB && !MEMO[p + 2];
         if (k1 || k2) {
           x->need = k1 ? p + 1 : p + 2;
@@ -90,8 +93,8 @@ static int walk_wave(u32 w, u32 nseg, const u32 *p0, const int *act0, u64 *LM, u
           break;
         }
         int g0 = gain(p);
-        if (gain(p + 1) > g0 + 4 || gain(p + 2) > g0 + 7) { if (p >= x->S) x->nl |= 1ull << (p - x->S); x->p++; }
-        else { if (p >= x->S) x->nm |= 1ull << (p - x->S); x->p += LEN[p]; }
+        if (gain(p + 1) > g0 + 4 || gain(p + 2) > g0 + 7) { if (p >= x->S) x->nl |= 1ull << (p - x->S); x->p++; x->lit = 1; }
+        else { if (p >= x->S) x->nm |= 1ull << (p - x->S); x->p += LEN[p]; x->lit = 0; }
       }
       any |= x->act;
     }
@@ -99,7 +102,7 @@ static int walk_wave(u32 w, u32 nseg, const u32 *p0, const int *act0, u64 *LM, u
     int nq = 0;
     for (int l = 0; l < 64; l++) {
       if (L[l].need == ~0u) continue;
-      for (int t = 0; t < DQ; t++) {
+      for (int t = 0; t < ((DQL && L[l].lit) ? DQL : DQ); t++) {
         u32 xx = L[l].need + t;
         if (xx < NB && !MEMO[xx]) { MEMO[xx] = 1; searched++; nq++; }
       }
@@ -112,7 +115,7 @@ static int walk_wave(u32 w, u32 nseg, const u32 *p0, const int *act0, u64 *LM, u
     rounds += (nq + 63) / 64; /* search passes: lanes = queue entries, 64 at a time */
   }
   for (int l = 0; l < 64; l++) {
-    u32 g = INTER ? w + NW * l : w * 64 + l;
+    u32 g = INTER ? ((l / INTER) * NW + w) * INTER + l % INTER : w * 64 + l;
     if (g >= nseg || !act0[g]) continue;
     Lane *x = &L[l];
     if (x->merged) {
@@ -139,8 +142,19 @@ static void model(const u8 *buf, u32 pre, u32 n, long *acc) {
   int *act = calloc(nseg, sizeof(int));
   searched = 0;
   for (u32 g = 0; g < nseg; g++) { entry[g] = SEGL * g; ex[g] = entry[g]; act[g] = 1; }
-  int r0 = 0;
-  for (u32 w = 0; w < nw; w++) { int r = walk_wave(w, nseg, entry, act, LM, MM, ex, WARM ? entry : NULL, WARM); if (r > r0) r0 = r; }
+  int r0 = 0, rsum = 0;
+  for (u32 w = 0; w < nw; w++) { int r = walk_wave(w, nseg, entry, act, LM, MM, ex, WARM ? entry : NULL, WARM); if (r > r0) r0 = r; rsum += r; }
+  acc[7] += rsum; acc[8] += nw;
+  if (getenv("PERWAVE") && WARM == 32 && !INTER) {  /* per-wave first-walk passes (fresh memo) */
+    static int once = 0;
+    if (once++ < 3) {
+      for (u32 i = 0; i < NB; i++) MEMO[i] = pre + i < LIM ? 0 : 1;
+      for (u32 g = 0; g < nseg; g++) { entry[g] = SEGL * g; ex[g] = entry[g]; act[g] = 1; LM[g] = MM[g] = 0; }
+      fprintf(stderr, "per-wave:");
+      for (u32 w = nw; w-- > 0;) fprintf(stderr, " %d", walk_wave(w, nseg, entry, act, LM, MM, ex, entry, WARM));
+      fprintf(stderr, "  (waves %u..0, walked last to first)\n", nw - 1);
+    }
+  }
   entry[0] = 0;
   int iters = 0, rj = 0;
   for (;;) {
@@ -198,19 +212,21 @@ int main(int argc, char **argv) {
   LEN = malloc(rec + 64);
   OFF = malloc(4 * (rec + 64));
   MEMO = malloc(2 * (rec + 64));
-  static const int cfg[][6] = {{3, 16, 0, 0, 32, 0}, {3, 16, 0, 0, 32, 1}, {3, 32, 0, 0, 64, 0}, {3, 32, 0, 0, 64, 1}};  /* DQ, SEGL, rule, spec, warm-up, interleave */  /* DQ, SEGL, rule, spec, warm-up */
+  static const int cfg[][7] = {{3, 16, 0, 0, 0, 0, 0}, {3, 16, 1, 0, 0, 0, 0}, {3, 16, 0, 3, 0, 0, 0}, {3, 16, 0, 0, 32, 0, 0}, {3, 16, 0, 0, 32, 1, 0},
+                               {3, 16, 0, 0, 32, 32, 0}, {3, 16, 0, 0, 32, 0, 6}, {3, 32, 0, 0, 0, 0, 0}, {3, 32, 0, 0, 64, 0, 0}};
+  /* DQ, SEGL, rule, spec, warm-up, run of segments per wave (0: 64), posts after a literal */  /* DQ, SEGL, rule, spec, warm-up, run of segments per wave (0: 64), posts after a literal */  /* DQ, SEGL, rule, spec, warm-up, interleave, posts after a literal */  /* DQ, SEGL, rule, spec, warm-up, interleave */  /* DQ, SEGL, rule, spec, warm-up */
   for (u32 c = 0; c < sizeof cfg / sizeof cfg[0]; c++) {
-    DQ = cfg[c][0]; SEGL = cfg[c][1]; RULE = cfg[c][2]; SPEC = cfg[c][3]; WARM = cfg[c][4]; INTER = cfg[c][5];
-    long acc[7] = {0};
+    DQ = cfg[c][0]; SEGL = cfg[c][1]; RULE = cfg[c][2]; SPEC = cfg[c][3]; WARM = cfg[c][4]; INTER = cfg[c][5]; DQL = cfg[c][6];
+    long acc[9] = {0};
     for (u32 r = 0; r < nrec; r++) {
       if (dn) memcpy(buf, dict, dn);
       memcpy(buf + dn, data + (size_t)r * rec, rec);
       memset(buf + dn + rec, 0, 64);
       model(buf, dn, dn + rec, acc);
     }
-    printf("DQ %d spec %d warm %d inter %d SEGL %d rule %s: first-walk passes %.2f, Jacobi iterations %.2f, Jacobi passes %.2f, total passes %.2f, "
+    printf("DQ %d/%d spec %d warm %d inter %d SEGL %d rule %s: first-walk passes %.2f (wave mean %.2f), Jacobi iterations %.2f, Jacobi passes %.2f, total passes %.2f, "
            "searched %.1f%%, parse ok %ld/%u\n",
-           DQ, SPEC, WARM, INTER, SEGL, RULE ? "prefix-max" : "predecessor", (double)acc[0] / nrec, (double)acc[1] / nrec, (double)acc[2] / nrec,
+           DQ, DQL, SPEC, WARM, INTER, SEGL, RULE ? "prefix-max" : "predecessor", (double)acc[0] / nrec, (double)acc[7] / acc[8], (double)acc[1] / nrec, (double)acc[2] / nrec,
            (double)(acc[0] + acc[2]) / nrec, 100.0 * acc[3] / acc[6], acc[4], nrec);
   }
   return 0;
