@@ -55,6 +55,9 @@ constexpr u32 L_MP = L_LP + 4 * NSEG;      // u32 matches before the segment
 #ifndef ZH_DEEP_WAVEQ
 #define ZH_DEEP_WAVEQ 1  // per-wave demand queues (C5 no dictionary 12.9 -> 13.8 GB/s)
 #endif
+#ifndef ZH_DEEP_G64EARLY
+#define ZH_DEEP_G64EARLY 1  // (C5 15.5 / 13.5 -> 15.8 / 14.0 GB/s without / with the COVER dictionary)
+#endif
 #ifndef ZH_DEEP_B64
 #define ZH_DEEP_B64 1  // extension bytes by 8-byte loads (C5 12.1 -> 12.9 GB/s)
 #endif
@@ -261,6 +264,12 @@ __device__ __forceinline__ u32 deep_search_one(const u32 *D32, const u16 *P16, c
   while (__ballot(act)) {
     if (act) {
       u32 const q = c - 1u;
+#if ZH_DEEP_G64EARLY
+      // the first 8 candidate bytes loaded with the reject byte, not after it: one dependent LDS
+      // round trip per candidate instead of two once best >= 8 (the bytes are dropped on a reject)
+      u32 clo, chi;
+      g64(D32, q, clo, chi);
+#endif
       bool w = true;
       if (best >= 8) {
         u32 const b = q + best;
@@ -269,8 +278,10 @@ __device__ __forceinline__ u32 deep_search_one(const u32 *D32, const u16 *P16, c
       u32 const nx = link(q);
       u32 l = 0;
       if (w) {
+#if !ZH_DEEP_G64EARLY
         u32 clo, chi;
         g64(D32, q, clo, chi);
+#endif
         u32 const x = O[0] ^ clo, y = O[1] ^ chi;
         l = x ? (u32)__builtin_ctz(x) >> 3 : y ? 4u + ((u32)__builtin_ctz(y) >> 3) : 8u;
         if (l == 8 && p + 8 < n) {
