@@ -27,7 +27,7 @@ the measured thread count, one thread and all cores (the north star's ">= 10x al
 also the line's `vs_cpu_all_core`): all-core is measured when the process may use every core,
 otherwise the larger of the measured rate and the 1-thread rate x physical cores x the measured
 parallel efficiency (the conservative denominator).
-Extra legs at N=1 (not `value`): C3 on uniform random bytes, C2 (one 64 MiB frame through
+Extra legs at N=1 (not `value`): C3 on uniform random bytes, C3 at levels 1 and 2, C2 (one 64 MiB frame through
 ZstdManager::compress) and C5 (level 9 with a COVER dictionary on 4,096 x 16 KiB JSON records),
 each with its roofline and libzstd beside it, and GPU decompression of the C3 frames.
 """
@@ -117,23 +117,55 @@ def _cpubench():
     L.cpub_run.restype = ctypes.c_int
     L.cpub_run.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_size_t, ctypes.c_size_t, ctypes.c_int,
                            ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_size_t)]
+    L.cpub_run_pinned.restype = ctypes.c_int
+    L.cpub_run_pinned.argtypes = L.cpub_run.argtypes + [ctypes.POINTER(ctypes.c_int)]
     L.cpub_zstd_version.restype = ctypes.c_uint
     return L
 
 
-def cpu_run(mode, data, nchunks, threads, passes=5, sizes=None, slot=0, chunk=CHUNK):
-    """Median wall time of `passes` sweeps over nchunks chunks (after one warm-up sweep)."""
+def cpu_run(mode, data, nchunks, threads, passes=5, sizes=None, slot=0, chunk=CHUNK, level=3, cpus=None):
+    """Median wall time of `passes` sweeps over nchunks chunks (after one warm-up sweep); cpus:
+    pin thread t to CPU cpus[t]."""
     L = _cpubench()
     if L is None:
         return None
     secs = (ctypes.c_double * (passes + 1))()
     outb = ctypes.c_size_t()
     sz = sizes.ctypes.data if sizes is not None else None
-    rc = L.cpub_run(mode, data.ctypes.data, sz, nchunks, chunk, slot, 3, threads, passes + 1, secs, ctypes.byref(outb))
+    pin = (ctypes.c_int * threads)(*cpus) if cpus else None
+    rc = L.cpub_run_pinned(mode, data.ctypes.data, sz, nchunks, chunk, slot, level, threads, passes + 1, secs, ctypes.byref(outb), pin)
     if rc:
         return None
     t = statistics.median(list(secs)[1:])
     return {"seconds": t, "out_bytes": outb.value, "version": L.cpub_zstd_version()}
+
+
+def smt_yield(host):
+    """libzstd level-3 throughput of one core's two hardware threads over one thread alone, both
+    pinned (the hardware threads the affinity holds beyond the physical cores are worth this
+    much each, not a whole core).  None when the affinity holds no sibling pair."""
+    aff = sorted(os.sched_getaffinity(0))
+    for a in aff:
+        try:
+            sib = open(f"/sys/devices/system/cpu/cpu{a}/topology/thread_siblings_list").read().strip()
+        except OSError:
+            return None
+        ids = set()
+        for part in sib.split(","):
+            lo, _, hi = part.partition("-")
+            ids.update(range(int(lo), int(hi or lo) + 1))
+        b = next((x for x in sorted(ids) if x != a and x in aff), None)
+        if b is None:
+            continue
+        n = min(len(host) // CHUNK, 512)
+        r1 = cpu_run(0, host, n, 1, passes=3, cpus=[a])
+        r2 = cpu_run(0, host, 2 * n if len(host) // CHUNK >= 2 * n else n, 2, passes=3, cpus=[a, b])
+        if not r1 or not r2:
+            return None
+        g1 = n * CHUNK / r1["seconds"]
+        g2 = (2 * n if len(host) // CHUNK >= 2 * n else n) * CHUNK / r2["seconds"]
+        return {"value": round(g2 / g1, 3), "cpus": [a, b], "one_thread_GBps": round(g1 / 1e9, 4), "two_siblings_GBps": round(g2 / 1e9, 4)}
+    return None
 
 
 def cpu_baseline(host, threads, gpu_gbs):
@@ -163,6 +195,14 @@ def cpu_baseline(host, threads, gpu_gbs):
     for c in curve:
         c.pop("_r", None)
     measured_all = threads >= (info["physical_cores"] or info["affinity_threads"] or threads)
+    # every hardware thread: the physical-core figure times the measured SMT yield of a core's two
+    # threads (the affinity holds 2 threads per core); the denominator of
+    # gpu_speedup.vs_all_core
+    hw = info["affinity_threads"] or threads
+    smt = smt_yield(host) if (hw > cores and not measured_all) else None
+    smt_f = min(smt["value"], 2.0) if smt else (hw / cores if hw > cores else 1.0)
+    base_all = gm if measured_all else max(gm, all_core)
+    all_hw = base_all * (smt_f if hw > cores and not measured_all else 1.0)
     return {"value": round(gm, 3), "unit": "GB/s", "cores": threads, "kind": "reference",
             "sample": f"libzstd {r['version']} ZSTD_compressCCtx level 3 (one CCtx per POSIX thread, tools/cpubench.c) over the same 64 KiB "
                       f"chunks: {threads} threads x {n} chunks ({n * CHUNK >> 20} MiB), median of 5 sweeps; ratio {n * CHUNK / r['out_bytes']:.4f}",
@@ -170,15 +210,17 @@ def cpu_baseline(host, threads, gpu_gbs):
             "single_thread": {"value": g1, "unit": "GB/s", "sample": f"{curve[0]['chunks']} chunks, median of 5 sweeps"},
             "thread_curve": curve,
             "host": info,
-            "all_core": {"value": round(gm if measured_all else max(gm, all_core), 2), "unit": "GB/s", "measured": measured_all,
+            "all_core": {"value": round(all_hw, 2), "unit": "GB/s", "measured": measured_all,
+                         "physical_cores_value": round(base_all, 2), "hw_threads": hw, "smt_yield": smt,
                          "how": ("measured: one thread per physical core or more" if measured_all else
                                  f"1-thread rate x {cores} physical cores x the parallel efficiency {eff:.3f} measured at {threads} threads "
-                                 f"(the process may keep {threads} host threads busy: affinity {info['affinity_threads']}, cgroup quota "
-                                 f"{info['cgroup_cpu_quota']}, pool share OMP_NUM_THREADS={os.environ.get('OMP_NUM_THREADS')}; "
-                                 f"bench.py --cpu-threads all measures it on a whole machine)")},
+                                 f"= {base_all:.2f} GB/s, x {smt_f:.3f} for the second hardware thread of each core "
+                                 f"({'measured: two pinned sibling threads over one' if smt else 'not measurable here: counted as a whole core'}; "
+                                 f"affinity {info['affinity_threads']} threads, cgroup quota {info['cgroup_cpu_quota']}, pool share "
+                                 f"OMP_NUM_THREADS={os.environ.get('OMP_NUM_THREADS')}; bench.py --cpu-threads all measures it on a whole machine)")},
             "gpu_speedup": {"vs_measured_threads": round(gpu_gbs / gm, 2), "vs_single_thread": round(gpu_gbs / g1, 1),
-                            "vs_all_core": round(gpu_gbs / (gm if measured_all else max(gm, all_core)), 2),
-                            "north_star_10x_all_core": gpu_gbs >= 10 * (gm if measured_all else max(gm, all_core))}}
+                            "vs_all_core": round(gpu_gbs / all_hw, 2), "vs_all_physical_cores": round(gpu_gbs / base_all, 2),
+                            "north_star_10x_all_core": gpu_gbs >= 10 * all_hw}}
 
 
 def libzstd_roundtrip(frames, sizes, slot, host):
@@ -282,6 +324,38 @@ def random_leg(dev, steps, threads):
     torch.cuda.empty_cache()
     if threads:
         res["cpu_baseline"] = cpu_baseline(host, threads, gbs)
+    return res
+
+
+def level_leg(host, dev, level, steps, threads):
+    """C3 (the main line's 16,384 mix chunks) at another level: level 1 is
+    K1's short-table greedy parse (ZH_K1_MODE 2), level 2 the short-table lazy-1 (mode 1).  GB/s,
+    ratio, libzstd decode of every frame, and libzstd at the same level on one thread over the
+    first 1,024 chunks (64 MiB) beside it."""
+    import cuda_zstd
+
+    b = Batch(host, dev, level)
+    b.compress()
+    torch.cuda.synchronize()
+    cuda_zstd.profile_enable(True)
+    ms = timed_events(b.compress, steps)
+    cuda_zstd.profile_enable(False)
+    launches, kms = cuda_zstd.profile_collect()
+    ok = int((b.status != 0).sum().item()) == 0
+    comp = int(b.out_sizes.sum().item())
+    gbs = b.n * CHUNK / (ms / 1e3) / 1e9
+    res = {"value": round(gbs, 3), "unit": "GB/s", "ms_per_step": round(ms, 3), "ratio": round(b.n * CHUNK / comp, 4), "status_ok": ok,
+           "workload": f"C3 mix: {b.n} x 64 KiB chunks, level {level}", "roofline": leg_roofline(b.n * CHUNK + comp, kms, launches)}
+    res["libzstd_verified"] = libzstd_roundtrip(b.d_out.cpu().numpy(), b.out_sizes.cpu().numpy(), b.slot, host)
+    del b
+    torch.cuda.empty_cache()
+    if threads:
+        n = min(len(host) // CHUNK, 1024)
+        r = cpu_run(0, host, n, 1, passes=3, level=level)
+        if r:
+            res["cpu_baseline"] = {"value": round(n * CHUNK / r["seconds"] / 1e9, 4), "unit": "GB/s", "cores": 1, "kind": "reference",
+                                   "sample": f"libzstd {r['version']} ZSTD_compressCCtx level {level}, one thread, the first {n} chunks, "
+                                             "median of 3 after a warm-up", "ratio": round(n * CHUNK / r["out_bytes"], 4)}
     return res
 
 
@@ -566,6 +640,8 @@ def main():
     if world == 1 and not args.no_legs and args.dataset == "mix" and args.chunks == CHUNKS:
         leg_threads = None if args.no_cpu_baseline else threads
         legs["c3_random"] = random_leg(dev, 5, leg_threads)
+        for lv in (1, 2):
+            legs[f"c3_level{lv}"] = level_leg(host, dev, lv, 5, leg_threads)
         legs["c2_64mib"] = c2_leg(dev, 5, leg_threads)
         legs["c5_level9_dict"] = c5_leg(dev, leg_threads)
 
@@ -587,7 +663,7 @@ def main():
             # the SQ summary prices a VALU at the 1-wave rate (4 cycles); the pipe's own rate is 2
             issue["valu_pipe_frac"] = round(iss * VALU_CYCLES_PIPE / VALU_CYCLES_1W, 4)
         if iss is None:
-            bound, limiter = "hbm", "unknown (no SQ summary for this workload)"
+            bound, limiter = "unknown", f"unknown: no SQ summary for this workload (HBM {hbm_frac:.4f} of peak)"
         elif hbm_frac >= iss:
             bound, limiter = "hbm", f"hbm ({hbm_frac:.3f} of peak >= VALU issue {iss:.3f})"
         else:

@@ -257,86 +257,10 @@ __device__ bool fse_normalize_m2(s16 *norm, u32 tableLog, const u32 *count, u32 
   return true;
 }
 
-__device__ bool fse_normalize(s16 *norm, u32 tableLog, const u32 *count, u32 total, u32 maxSV, bool useLowProbCount) {
-  const u32 *rtbTable = c_rtb;
-  if (tableLog < fse_min_table_log(total, maxSV)) return false;
-  s16 const lowProbCount = useLowProbCount ? -1 : 1;
-  u64 const scale = 62 - tableLog;
-  u64 const step = (1ull << 62) / total;
-  u64 const vStep = 1ull << (scale - 20);
-  int stillToDistribute = 1 << tableLog;
-  u32 largest = 0;
-  s16 largestP = 0;
-  u32 const lowThreshold = total >> tableLog;
-  for (u32 s = 0; s <= maxSV; s++) {
-    if (count[s] == total) return true;  // never reached: RLE handled by the caller
-    if (count[s] == 0) { norm[s] = 0; continue; }
-    if (count[s] <= lowThreshold) { norm[s] = lowProbCount; stillToDistribute--; }
-    else {
-      s16 proba = (s16)((count[s] * step) >> scale);
-      if (proba < 8) {
-        u64 const restToBeat = vStep * rtbTable[proba];
-        proba += (count[s] * step) - ((u64)proba << scale) > restToBeat;
-      }
-      if (proba > largestP) { largestP = proba; largest = s; }
-      norm[s] = proba;
-      stillToDistribute -= proba;
-    }
-  }
-  if (-stillToDistribute >= (norm[largest] >> 1)) return fse_normalize_m2(norm, tableLog, count, total, maxSV, lowProbCount);
-  norm[largest] += (s16)stillToDistribute;
-  return true;
-}
-
-// FSE_writeNCount into out[] (LDS); returns size (0 on error)
-__device__ u32 fse_write_ncount(u8 *out, const s16 *norm, u32 maxSV, u32 tableLog) {
-  u8 *const ostart = out;
-  int const tableSize = 1 << tableLog;
-  int remaining = tableSize + 1, threshold = tableSize, nbBits = (int)tableLog + 1;
-  u32 bitStream = (tableLog - 5);
-  int bitCount = 4;
-  u32 symbol = 0;
-  u32 const alphabetSize = maxSV + 1;
-  bool previousIs0 = false;
-  while (symbol < alphabetSize && remaining > 1) {
-    if (previousIs0) {
-      u32 start = symbol;
-      while (symbol < alphabetSize && !norm[symbol]) symbol++;
-      if (symbol == alphabetSize) break;
-      while (symbol >= start + 24) {
-        start += 24;
-        bitStream += 0xFFFFu << bitCount;
-        out[0] = (u8)bitStream; out[1] = (u8)(bitStream >> 8); out += 2; bitStream >>= 16;
-      }
-      while (symbol >= start + 3) { start += 3; bitStream += 3u << bitCount; bitCount += 2; }
-      bitStream += (symbol - start) << bitCount;
-      bitCount += 2;
-      if (bitCount > 16) { out[0] = (u8)bitStream; out[1] = (u8)(bitStream >> 8); out += 2; bitStream >>= 16; bitCount -= 16; }
-    }
-    int count = norm[symbol++];
-    int const max = (2 * threshold - 1) - remaining;
-    remaining -= count < 0 ? -count : count;
-    count++;
-    if (count >= threshold) count += max;
-    bitStream += (u32)count << bitCount;
-    bitCount += nbBits;
-    bitCount -= (count < max);
-    previousIs0 = (count == 1);
-    if (remaining < 1) return 0;
-    while (remaining < threshold) { nbBits--; threshold >>= 1; }
-    if (bitCount > 16) { out[0] = (u8)bitStream; out[1] = (u8)(bitStream >> 8); out += 2; bitStream >>= 16; bitCount -= 16; }
-  }
-  if (remaining != 1) return 0;
-  out[0] = (u8)bitStream;
-  out[1] = (u8)(bitStream >> 8);
-  out += (bitCount + 7) / 8;
-  return (u32)(out - ostart);
-}
-
 // ---------------- FSE normalisation + NCount, wave-parallel (lane = symbol, maxSV < 64) ----------------
 // FSE_normalizeCount (libzstd v1.4.9) with the per-symbol probabilities on the lanes and the
 // two reductions (sum, first-maximum) on DPP; the rare "m2" redistribution falls back to the
-// serial code above on lane 0.  c = this lane's count (0 past maxSV).  The result is
+// serial fse_normalize_m2 on lane 0.  c = this lane's count (0 past maxSV).  The result is
 // returned per lane (lane s: norm[s]) and stored to norm[] in LDS.
 __device__ int fse_normalize_wave(s16 *norm, u32 tableLog, u32 c, u32 total, u32 maxSV, bool useLowProbCount, u32 lane, u32 *cnt_scratch) {
   s16 const lowProbCount = useLowProbCount ? -1 : 1;
@@ -426,41 +350,7 @@ __device__ u32 fse_write_ncount_wave(u8 *out, int normv, u32 maxSV, u32 tableLog
 
 struct FseSym { u32 dNb; s32 dFS; };
 
-// FSE_buildCTable_wksp into LDS (stateTable + symbol transforms)
-__device__ void fse_build_ctable(u16 *st, FseSym *sym, u8 *tableSymbol, const s16 *norm, u32 maxSV, u32 tableLog, SerialScratch *scr) {
-  u32 const tableSize = 1u << tableLog, tableMask = tableSize - 1;
-  u32 const step = (tableSize >> 1) + (tableSize >> 3) + 3;
-  u32 *cumul = scr->cumul;
-  u32 highThreshold = tableSize - 1;
-  cumul[0] = 0;
-  for (u32 u = 1; u <= maxSV + 1; u++) {
-    if (norm[u - 1] == -1) { cumul[u] = cumul[u - 1] + 1; tableSymbol[highThreshold--] = (u8)(u - 1); }
-    else cumul[u] = cumul[u - 1] + (u32)norm[u - 1];
-  }
-  u32 position = 0;
-  for (u32 s = 0; s <= maxSV; s++)
-    for (int k = 0; k < norm[s]; k++) {
-      tableSymbol[position] = (u8)s;
-      position = (position + step) & tableMask;
-      while (position > highThreshold) position = (position + step) & tableMask;
-    }
-  for (u32 u = 0; u < tableSize; u++) { u8 s = tableSymbol[u]; st[cumul[s]++] = (u16)(tableSize + u); }
-  u32 total = 0;
-  for (u32 s = 0; s <= maxSV; s++) {
-    int const nv = norm[s];
-    if (nv == 0) { sym[s].dNb = ((tableLog + 1) << 16) - (1u << tableLog); sym[s].dFS = 0; }
-    else if (nv == -1 || nv == 1) { sym[s].dNb = (tableLog << 16) - (1u << tableLog); sym[s].dFS = (s32)total - 1; total++; }
-    else {
-      u32 const maxBitsOut = tableLog - highbit32((u32)nv - 1);
-      u32 const minStatePlus = (u32)nv << maxBitsOut;
-      sym[s].dNb = (maxBitsOut << 16) - minStatePlus;
-      sym[s].dFS = (s32)total - nv;
-      total += (u32)nv;
-    }
-  }
-}
-
-// Wave-parallel FSE_buildCTable (same tables as fse_build_ctable).  Symbols <= 63.
+// Wave-parallel FSE_buildCTable (libzstd 1.4.9's FSE_buildCTable_wksp tables).  Symbols <= 63.
 // Spread: the i-th positive-count cell in symbol order goes to the i-th position of
 // (k * step) & mask, k = 0, 1, ... skipping positions above highThreshold; with
 // step odd, position u is reached at k(u) = u * step^-1 mod tableSize, so its rank is
@@ -538,21 +428,6 @@ __device__ void fse_build_ctable_par(u16 *st, FseSym *sym, u8 *tableSymbol, cons
     }
   }
   wave_sync();
-}
-
-__device__ __forceinline__ u32 fse_init_state(const u16 *st, const FseSym *sym, u32 s) {
-  FseSym const tt = sym[s];
-  u32 const nbBitsOut = (tt.dNb + (1u << 15)) >> 16;
-  u32 const v = (nbBitsOut << 16) - tt.dNb;
-  return st[(v >> nbBitsOut) + tt.dFS];
-}
-__device__ __forceinline__ u32 fse_step(const u16 *st, const FseSym *sym, u32 &state, u32 s, u32 &nbOut) {
-  FseSym const tt = sym[s];
-  u32 const nb = (state + tt.dNb) >> 16;
-  u32 const v = state & ((1u << nb) - 1u);
-  state = st[(state >> nb) + tt.dFS];
-  nbOut = nb;
-  return v;
 }
 
 // ---------------- Huffman (libzstd v1.4.9 HUF_buildCTable) ----------------
@@ -834,82 +709,11 @@ __device__ u32 huf_build_ctable_par(HufNode *huffNode0, u16 *hval, u8 *hnb, cons
   return maxNbBits;
 }
 
-// serial FSE_compress_usingCTable of Huffman weights into out[] (LDS), two states
-__device__ u32 fse_compress_weights_stream(u8 *out, const u8 *src, u32 n, const u16 *st, const FseSym *sym, u32 tableLog) {
-  u64 acc = 0;
-  u32 nbits = 0, o = 0;
-#define ZH_ADD(v, nb)                                           \
-  do {                                                          \
-    acc |= ((u64)(v) & ((1ull << (nb)) - 1)) << nbits;          \
-    nbits += (nb);                                              \
-    while (nbits >= 8) { out[o++] = (u8)acc; acc >>= 8; nbits -= 8; } \
-  } while (0)
-  u32 s1, s2, nb;
-  int ip = (int)n;
-  if (n & 1) {
-    s1 = fse_init_state(st, sym, src[--ip]);
-    s2 = fse_init_state(st, sym, src[--ip]);
-    u32 v = fse_step(st, sym, s1, src[--ip], nb);
-    ZH_ADD(v, nb);
-  } else {
-    s2 = fse_init_state(st, sym, src[--ip]);
-    s1 = fse_init_state(st, sym, src[--ip]);
-  }
-  while (ip > 0) {
-    u32 v = fse_step(st, sym, s2, src[--ip], nb);
-    ZH_ADD(v, nb);
-    v = fse_step(st, sym, s1, src[--ip], nb);
-    ZH_ADD(v, nb);
-  }
-  ZH_ADD(s2, tableLog);
-  ZH_ADD(s1, tableLog);
-  ZH_ADD(1, 1);
-  if (nbits) out[o++] = (u8)acc;
-#undef ZH_ADD
-  return o;
-}
-
-// HUF_writeCTable into hbuf; returns size (0 = error -> raw literals)
-__device__ u32 huf_write_ctable(u8 *hbuf, u8 *w, const u8 *hnb, u32 maxSV, u32 huffLog, u16 *st, FseSym *sym, u8 *tsym, s16 *norm,
-                                SerialScratch *scr) {
-  for (u32 n = 0; n < maxSV; n++) w[n] = hnb[n] ? (u8)(huffLog + 1 - hnb[n]) : 0;
-  // HUF_compressWeights
-  u32 h = 0;
-  if (maxSV > 1) {
-    u32 *count = scr->wcount;
-    for (int i = 0; i < 13; i++) count[i] = 0;
-    for (u32 i = 0; i < maxSV; i++) count[w[i]]++;
-    u32 mx = 12;
-    while (!count[mx]) mx--;
-    u32 maxCount = 0;
-    for (u32 s = 0; s <= mx; s++) if (count[s] > maxCount) maxCount = count[s];
-    if (maxCount == maxSV) h = 1;
-    else if (maxCount == 1) h = 0;
-    else {
-      u32 tableLog = fse_optimal_table_log(6, maxSV, mx, 2);
-      if (fse_normalize(norm, tableLog, count, maxSV, mx, false)) {
-        u32 hs = fse_write_ncount(hbuf + 1, norm, mx, tableLog);
-        if (hs) {
-          fse_build_ctable(st, sym, tsym, norm, mx, tableLog, scr);
-          u32 cs = maxSV > 2 ? fse_compress_weights_stream(hbuf + 1 + hs, w, maxSV, st, sym, tableLog) : 0;
-          h = cs ? hs + cs : 0;
-        }
-      }
-    }
-  }
-  if ((h > 1) & (h < maxSV / 2)) { hbuf[0] = (u8)h; return h + 1; }
-  if (maxSV > 128) return 0;
-  hbuf[0] = (u8)(128 + (maxSV - 1));
-  w[maxSV] = 0;
-  for (u32 n = 0; n < maxSV; n += 2) hbuf[(n / 2) + 1] = (u8)((w[n] << 4) + w[n + 1]);
-  return ((maxSV + 1) / 2) + 1;
-}
-
 // HUF_writeCTable with the whole wave: weights and their histogram lane-parallel, the weights'
 // FSE table by the wave-parallel normalisation / NCount / table build, and the two-state
 // FSE_compress_usingCTable of the weights as a wave-uniform loop whose table lookups are
 // v_readlane from lane-held copies (weights <= 12, table <= 64 cells).  Same bytes as
-// huf_write_ctable; returns the size (0 = raw literals), uniform.
+// libzstd 1.4.9's HUF_writeCTable; returns the size (0 = raw literals), uniform.
 __device__ u32 huf_write_ctable_wave(u8 *hbuf, u8 *w, const u8 *hnb, u32 maxSV, u32 huffLog, u16 *st, FseSym *sym, u8 *tsym, s16 *norm,
                                     SerialScratch *scr) {
   u32 const lane = lane_id();

@@ -197,7 +197,9 @@ struct LibZstd {
   LibZstd() {
     const char *names[] = {"libzstd.so.1", "libzstd.so", "/opt/conda/lib/libzstd.so.1", "/usr/lib/x86_64-linux-gnu/libzstd.so.1"};
     for (const char *nm : names) {
-      void *h = dlopen(nm, RTLD_NOW | RTLD_LOCAL);
+      // RTLD_DEEPBIND: a libzstd opened here binds its own calls inside itself even when another
+      // libzstd image sits in the global scope (a preloaded tool's), never mixing two versions
+      void *h = dlopen(nm, RTLD_NOW | RTLD_LOCAL | RTLD_DEEPBIND);
       if (!h) continue;
       compress = (decltype(compress))dlsym(h, "ZSTD_compress");
       decompress = (decltype(decompress))dlsym(h, "ZSTD_decompress");
@@ -528,7 +530,8 @@ class ZstdBatchManager::Impl {
  public:
   CompressionConfig config;
   CompressionStats stats;
-  dictionary::Dictionary dict;
+  dictionary::DictionaryHeader dict_hdr{};  // set_dictionary's header (dictionary_id: the frames' RFC ID)
+  bool has_dict = false;
   std::mutex api_mutex;  // one manager serialises calls (reference src/cuda_zstd_manager.cu:1542)
   void *pinned = nullptr;
   size_t pinned_bytes = 0;
@@ -815,19 +818,35 @@ Status ZstdBatchManager::decompress_with_history(const void *in, size_t n, void 
 // Dictionary compression and decompression: raw content or a formatted RFC 8878
 // dictionary; copied to the device once (the reference keeps a shallow pointer and copies it
 // into the workspace per call, src/cuda_zstd_manager.cu:1699-1775, 3711-3764)
+// The reference's checks (src/cuda_zstd_manager.cu:3711-3736): content present, MIN_DICT_SIZE ..
+// MAX_DICT_SIZE bytes.  raw_content may be host or device memory (copied once, DevDict::load).
 Status ZstdBatchManager::set_dictionary(const dictionary::Dictionary &d) {
   std::lock_guard<std::mutex> lock(pimpl_->api_mutex);
-  if (d.raw_content.empty()) return Status::ERROR_INVALID_PARAMETER;
-  Status s = pimpl_->mgr_dict.load(d.raw_content.data(), d.raw_content.size(), 0);
+  if (!d.raw_content || d.raw_size == 0) return Status::ERROR_INVALID_PARAMETER;
+  if (d.raw_size < dictionary::MIN_DICT_SIZE || d.raw_size > dictionary::MAX_DICT_SIZE) return Status::ERROR_INVALID_PARAMETER;
+  Status s = pimpl_->mgr_dict.load(d.raw_content, d.raw_size, 0);
   if (s != Status::SUCCESS) return s;
-  pimpl_->dict = d;
-  pimpl_->dict.dict_id = pimpl_->mgr_dict.id;
+  pimpl_->dict_hdr = d.header;
+  pimpl_->dict_hdr.dictionary_id = pimpl_->mgr_dict.id;
+  pimpl_->dict_hdr.raw_content_size = d.raw_size;
+  pimpl_->has_dict = true;
   return Status::SUCCESS;
 }
-Status ZstdBatchManager::get_dictionary(dictionary::Dictionary &d) const { d = pimpl_->dict; return Status::SUCCESS; }
+// reference :3858-3863: no dictionary -> ERROR_INVALID_PARAMETER; else a deep copy (the caller
+// frees dict.raw_content with free(), Dictionary's copy semantics)
+Status ZstdBatchManager::get_dictionary(dictionary::Dictionary &d) const {
+  if (!pimpl_->has_dict) return Status::ERROR_INVALID_PARAMETER;
+  dictionary::Dictionary view;
+  view.header = pimpl_->dict_hdr;
+  view.raw_content = pimpl_->mgr_dict.host.data();
+  view.raw_size = (u32)pimpl_->mgr_dict.host.size();
+  d = view;
+  return d.raw_content ? Status::SUCCESS : Status::ERROR_OUT_OF_MEMORY;
+}
 Status ZstdBatchManager::clear_dictionary() {
   std::lock_guard<std::mutex> lock(pimpl_->api_mutex);
-  pimpl_->dict = dictionary::Dictionary{};
+  pimpl_->has_dict = false;
+  pimpl_->dict_hdr = dictionary::DictionaryHeader{};
   pimpl_->mgr_dict.n = 0;
   return Status::SUCCESS;
 }
@@ -975,6 +994,8 @@ Status ZstdBatchManager::free_inference_workspace(void *ptr) { return hipFree(pt
 
 // (static: no dictionary, levels below ZH_DEEP_LEVEL; get_batch_device_temp_size_for covers the
 // manager's level and dictionary)
+// levels below ZH_DEEP_LEVEL without a dictionary (the deep matcher's scratch slots of levels >=
+// ZH_DEEP_LEVEL, up to ZH_DEEP_SLOTS_MAX x ZH_DEEP_SLOT_BYTES, are in get_batch_device_temp_size_for)
 size_t ZstdBatchManager::get_batch_device_temp_size(size_t count, size_t max_chunk) {
   size_t const bpi = std::max<size_t>(1, blocks_of(max_chunk));
   return WsLayout::make(count * bpi, count, bpi > 1).total;
@@ -987,6 +1008,8 @@ size_t ZstdBatchManager::get_batch_device_temp_size_for(size_t count, size_t max
 Status ZstdBatchManager::compress_batch_device(const void *const *d_in_ptrs, const size_t *d_in_sizes, size_t max_chunk, size_t count,
                                                void *const *d_out_ptrs, size_t *d_out_sizes, int *d_statuses, void *temp, size_t temp_size,
                                                hipStream_t stream) {
+  // one manager serialises calls (the dictionary's use events: set_dictionary waits on them)
+  std::lock_guard<std::mutex> lock(pimpl_->api_mutex);
   Status s = ensure_kernels();
   if (s != Status::SUCCESS) return s;
   if (!count) return Status::SUCCESS;
@@ -1026,6 +1049,8 @@ size_t ZstdBatchManager::get_batch_device_decompress_temp_size(size_t count, siz
 Status ZstdBatchManager::decompress_batch_device(const void *const *d_in_ptrs, const size_t *d_in_sizes, const size_t *d_out_caps, size_t max_out,
                                                  size_t count, void *const *d_out_ptrs, size_t *d_out_sizes, int *d_statuses, void *temp,
                                                  size_t temp_size, hipStream_t stream) {
+  // one manager serialises calls (the dictionary's use events: set_dictionary waits on them)
+  std::lock_guard<std::mutex> lock(pimpl_->api_mutex);
   Status s = ensure_kernels();
   if (s != Status::SUCCESS) return s;
   if (!count) return Status::SUCCESS;
@@ -1123,6 +1148,7 @@ class ZstdStreamingManager::Impl {
   // compress_chunk_with_history): decompress_chunk then decodes against the decoded window;
   // otherwise chunks are frames of their own and decode with the manager's dictionary, if any
   bool hist_mode = false;
+  bool has_dict = false;  // set_dictionary succeeded (frames with its Dictionary_ID decode with it)
   explicit Impl(const CompressionConfig &c) : config(c), mgr(c) {}
   ~Impl() { if (ws) (void)hipFree(ws); }
   Status ensure_ws(size_t need) {
@@ -1205,21 +1231,16 @@ Status ZstdStreamingManager::decompress_chunk(const void *in, size_t n, void *ou
   Status s = pimpl_->ensure_ws(pimpl_->mgr.get_decompress_temp_size(n));
   if (s != Status::SUCCESS) return s;
   // Per frame: the decoded window is the frame's history unless the frame was compressed with
-  // the manager's dictionary.  A formatted dictionary names itself in the frame header, so a
-  // frame without its ID is a history frame; a raw-content dictionary has ID 0 like a history
-  // frame, so there the session decides (compression with history in this manager, or
-  // init_decompression_with_history).  Without a dictionary the window is harmless (a frame of
-  // its own never reaches before its start).
-  dictionary::Dictionary dct;
-  (void)pimpl_->mgr.get_dictionary(dct);
+  // the manager's dictionary.  Without a dictionary the window is harmless (a frame of its own
+  // never reaches before its start).  With one, only a history session (compression with history
+  // in this manager, or init_decompression_with_history) has history frames, and those carry no
+  // Dictionary_ID: a frame naming the dictionary, or any frame outside a history session -- a
+  // formatted dictionary's frame written without its ID (libzstd dictIDFlag 0) included -- decodes
+  // with the dictionary.
   bool hist_frame = true;
-  if (!dct.raw_content.empty()) {
-    if (dct.dict_id) {
-      FrameProbe fp;
-      hist_frame = probe_frame(in, n, fp) == Status::SUCCESS && fp.dict_id == 0;
-    } else {
-      hist_frame = pimpl_->hist_mode;
-    }
+  if (pimpl_->has_dict) {
+    FrameProbe fp;
+    hist_frame = pimpl_->hist_mode && probe_frame(in, n, fp) == Status::SUCCESS && fp.dict_id == 0;
   }
   bool const use_hist = pimpl_->dhist.n && hist_frame;
   s = pimpl_->mgr.decompress_with_history(in, n, out, out_size, pimpl_->ws, pimpl_->ws_size, use_hist ? pimpl_->dhist.data() : nullptr,
@@ -1242,11 +1263,72 @@ Status ZstdStreamingManager::reset_streaming() {
 Status ZstdStreamingManager::flush(hipStream_t s) { return hipStreamSynchronize(s) == hipSuccess ? Status::SUCCESS : Status::ERROR_CUDA_ERROR; }
 Status ZstdStreamingManager::flush_streaming(hipStream_t s) { return flush(s); }
 Status ZstdStreamingManager::set_config(const CompressionConfig &c) { pimpl_->config = c; return pimpl_->mgr.configure(c); }
-Status ZstdStreamingManager::set_dictionary(const dictionary::Dictionary &d) { return pimpl_->mgr.set_dictionary(d); }
+Status ZstdStreamingManager::set_dictionary(const dictionary::Dictionary &d) {
+  Status const s = pimpl_->mgr.set_dictionary(d);
+  if (s == Status::SUCCESS) pimpl_->has_dict = true;
+  return s;
+}
 CompressionConfig ZstdStreamingManager::get_config() const { return pimpl_->config; }
 size_t ZstdStreamingManager::get_temp_size() const { return pimpl_->ws_size; }
 bool ZstdStreamingManager::is_compression_initialized() const { return pimpl_->comp; }
 bool ZstdStreamingManager::is_decompression_initialized() const { return pimpl_->decomp; }
+
+// ============================================================================
+// dictionary training API (reference include/cuda_zstd_dictionary.h:176-210,
+// src/cuda_zstd_dictionary.cu:421-520): COVER (zh_dict.cpp) instead of the reference's
+// byte-frequency / 4-gram fill, same validation and buffer contract
+// ============================================================================
+namespace dictionary {
+Status train_dictionary(const std::vector<const void *> &samples, const std::vector<size_t> &sample_sizes, void *dict_buffer,
+                        size_t dict_size, const DictionaryTrainingParams *params, hipStream_t stream) {
+  (void)params;
+  (void)stream;
+  if (samples.empty() || sample_sizes.empty() || !dict_buffer || samples.size() != sample_sizes.size()) return Status::ERROR_INVALID_PARAMETER;
+  if (!is_valid_dictionary_size(dict_size)) return Status::ERROR_INVALID_PARAMETER;
+  std::vector<std::pair<const u8 *, size_t>> s;
+  size_t total = 0;
+  for (size_t i = 0; i < samples.size(); i++) {
+    if (!samples[i] && sample_sizes[i]) return Status::ERROR_INVALID_PARAMETER;
+    s.emplace_back((const u8 *)samples[i], sample_sizes[i]);
+    total += sample_sizes[i];
+  }
+  if (total == 0) return Status::ERROR_INVALID_PARAMETER;
+  std::vector<u8> c;
+  try {
+    c = zh::cover_train(s, dict_size);
+  } catch (...) {
+    return Status::ERROR_OUT_OF_MEMORY;
+  }
+  if (c.empty() || c.size() > dict_size) return Status::ERROR_DICTIONARY_FAILED;
+  // the buffer holds dict_size bytes: the trained content at its end (the most useful segments
+  // nearest the data, as ZDICT lays them out), zeros before it when the samples gave less
+  u8 *const out = (u8 *)dict_buffer;
+  memset(out, 0, dict_size - c.size());
+  memcpy(out + dict_size - c.size(), c.data(), c.size());
+  return Status::SUCCESS;
+}
+Status create_dictionary_from_samples(const void *samples_buffer, const size_t *sample_offsets, size_t num_samples, void *dict_buffer,
+                                      size_t dict_size, const DictionaryTrainingParams *params, hipStream_t stream) {
+  if (!samples_buffer || !sample_offsets || !dict_buffer || num_samples == 0) return Status::ERROR_INVALID_PARAMETER;
+  std::vector<const void *> samples;
+  std::vector<size_t> sizes;
+  const u8 *const base = (const u8 *)samples_buffer;
+  for (size_t i = 0; i < num_samples; i++) {
+    size_t const a = sample_offsets[i], e = i + 1 < num_samples ? sample_offsets[i + 1] : a + 8 * 1024;
+    if (e < a) return Status::ERROR_INVALID_PARAMETER;
+    samples.push_back(base + a);
+    sizes.push_back(e - a);
+  }
+  return train_dictionary(samples, sizes, dict_buffer, dict_size, params, stream);
+}
+u32 get_optimal_dict_size(size_t total) {
+  size_t const s = total / 100;
+  if (s < MIN_DICT_SIZE) return MIN_DICT_SIZE;
+  if (s > MAX_DICT_SIZE) return MAX_DICT_SIZE;
+  return (u32)((s + 1023) / 1024 * 1024);
+}
+bool is_valid_dictionary_size(size_t size) { return size >= MIN_DICT_SIZE && size <= MAX_DICT_SIZE; }
+}  // namespace dictionary
 
 // ============================================================================
 // factories / convenience (reference include/cuda_zstd_manager.h:358-386)
@@ -1797,34 +1879,52 @@ Status HybridEngine::decompress(const void *in, size_t n, void *out, size_t *out
     res->input_location = il;
     res->output_location = ol;
     res->total_time_ms = ms;
+    res->compute_time_ms = ms;
     res->input_bytes = n;
     res->output_bytes = s == Status::SUCCESS ? *out_size : 0;
   }
   return ZH_NOTED(s);
 }
 
+// reference src/cuda_zstd_hybrid.cu:912-992: items one by one through the routing; per-item
+// BatchRoutingResult; ERROR_COMPRESSION / ERROR_DECOMPRESSION when any item failed
 Status HybridEngine::compress_batch(const void *const *inputs, const size_t *sizes, void **outputs, size_t *out_sizes, size_t count,
                                     DataLocation il, DataLocation ol, BatchRoutingResult *results, hipStream_t stream) {
+  if (!inputs || !sizes || !outputs || !out_sizes || count == 0) return ZH_NOTED(Status::ERROR_INVALID_PARAMETER);
   bool ok = true;
   for (size_t i = 0; i < count; i++) {
     HybridResult r;
     Status s = compress(inputs[i], sizes[i], outputs[i], &out_sizes[i], il, ol, &r, stream);
-    if (results) { results[i].backend_used = r.backend_used; results[i].status = s; results[i].output_size = out_sizes[i]; }
+    if (results) {
+      results[i].item_index = i;
+      results[i].backend_used = r.backend_used;
+      results[i].status = s;
+      results[i].input_bytes = sizes[i];
+      results[i].output_bytes = out_sizes[i];
+      results[i].compute_time_ms = r.compute_time_ms;
+    }
     ok &= s == Status::SUCCESS;
   }
-  return ok ? Status::SUCCESS : Status::ERROR_GENERIC;
+  return ok ? Status::SUCCESS : ZH_NOTED(Status::ERROR_COMPRESSION);
 }
 Status HybridEngine::decompress_batch(const void *const *inputs, const size_t *sizes, void **outputs, size_t *out_sizes, size_t count,
                                       DataLocation il, DataLocation ol, BatchRoutingResult *results, hipStream_t stream) {
-  if (count && (!inputs || !sizes || !outputs || !out_sizes)) return ZH_NOTED(Status::ERROR_INVALID_PARAMETER);
+  if (!inputs || !sizes || !outputs || !out_sizes || count == 0) return ZH_NOTED(Status::ERROR_INVALID_PARAMETER);
   bool ok = true;
   for (size_t i = 0; i < count; i++) {
     HybridResult r;
     Status s = decompress(inputs[i], sizes[i], outputs[i], &out_sizes[i], il, ol, &r, stream);
-    if (results) { results[i].backend_used = r.backend_used; results[i].status = s; results[i].output_size = s == Status::SUCCESS ? out_sizes[i] : 0; }
+    if (results) {
+      results[i].item_index = i;
+      results[i].backend_used = r.backend_used;
+      results[i].status = s;
+      results[i].input_bytes = sizes[i];
+      results[i].output_bytes = out_sizes[i];
+      results[i].compute_time_ms = r.compute_time_ms;
+    }
     ok &= s == Status::SUCCESS;
   }
-  return ok ? Status::SUCCESS : Status::ERROR_GENERIC;
+  return ok ? Status::SUCCESS : ZH_NOTED(Status::ERROR_DECOMPRESSION);
 }
 
 Status hybrid_decompress(const void *in, size_t n, void *out, size_t *out_size, DataLocation il, DataLocation ol, HybridResult *res, hipStream_t stream) {
@@ -1854,7 +1954,20 @@ using namespace cuda_zstd;
 using nvcomp_v5::status_to_nvcomp_error;
 
 struct cuda_zstd_manager_t { std::unique_ptr<ZstdBatchManager> manager; };
-struct cuda_zstd_dict_t { std::unique_ptr<dictionary::Dictionary> dict; };
+// the handle owns the bytes; `dict` is the reference-shaped view of them (its copy operations
+// would malloc, so it is never copied here)
+struct cuda_zstd_dict_t {
+  std::vector<u8> bytes;
+  std::unique_ptr<dictionary::Dictionary> dict;
+  void set(std::vector<u8> &&b, u32 id) {
+    bytes = std::move(b);
+    dict.reset(new dictionary::Dictionary);
+    dict->raw_content = bytes.data();
+    dict->raw_size = (u32)bytes.size();
+    dict->header.dictionary_id = id;
+    dict->header.raw_content_size = (u32)bytes.size();
+  }
+};
 struct nvcomp_zstd_batch_manager_t { std::unique_ptr<nvcomp_v5::NvcompV5BatchManager> mgr; };
 struct cuda_zstd_hybrid_engine_t { std::unique_ptr<HybridEngine> engine; };
 
@@ -1894,14 +2007,13 @@ cuda_zstd_dict_t *cuda_zstd_train_dictionary(const void **samples, const size_t 
     // (src/cuda_zstd_dictionary.cu:179-415); samples are host buffers
     std::vector<std::pair<const u8 *, size_t>> s;
     for (size_t i = 0; i < num; i++) {
-      if (!samples[i] && sizes[i]) return nullptr;
+      if (!samples[i] || sizes[i] == 0) return nullptr;  // (reference src/cuda_zstd_c_api.cpp:142-145)
       s.emplace_back((const u8 *)samples[i], sizes[i]);
     }
     std::vector<u8> c = zh::cover_train(s, std::min(dict_size, zh::kDictMaxBytes));
     if (c.empty()) return nullptr;
     auto *d = new cuda_zstd_dict_t;
-    d->dict.reset(new dictionary::Dictionary);
-    d->dict->raw_content = std::move(c);
+    d->set(std::move(c), 0);
     return d;
   } catch (...) {
     return nullptr;
@@ -1917,9 +2029,7 @@ cuda_zstd_dict_t *cuda_zstd_load_dictionary(const void *buffer, size_t size) {
   if (!zh::dict_layout((const u8 *)buffer, size, id, off)) return nullptr;
   try {
     auto *d = new cuda_zstd_dict_t;
-    d->dict.reset(new dictionary::Dictionary);
-    d->dict->raw_content.assign((const u8 *)buffer, (const u8 *)buffer + size);
-    d->dict->dict_id = id;
+    d->set(std::vector<u8>((const u8 *)buffer, (const u8 *)buffer + size), id);
     return d;
   } catch (...) {
     return nullptr;
@@ -1927,15 +2037,15 @@ cuda_zstd_dict_t *cuda_zstd_load_dictionary(const void *buffer, size_t size) {
 }
 size_t cuda_zstd_get_dictionary_content(const cuda_zstd_dict_t *d, void *out, size_t capacity) {
   if (!d || !d->dict) return 0;
-  size_t const n = d->dict->raw_content.size();
-  if (out && capacity >= n) memcpy(out, d->dict->raw_content.data(), n);
+  size_t const n = d->bytes.size();
+  if (out && capacity >= n) memcpy(out, d->bytes.data(), n);
   return n;
 }
 int cuda_zstd_get_dictionary_layout(const cuda_zstd_dict_t *d, unsigned int *dict_id, size_t *content_offset) {
   if (!d || !d->dict) return c_err(Status::ERROR_INVALID_PARAMETER);
   u32 id = 0;
   size_t off = 0;
-  if (!zh::dict_layout(d->dict->raw_content.data(), d->dict->raw_content.size(), id, off)) return c_err(Status::ERROR_DICTIONARY_FAILED);
+  if (!zh::dict_layout(d->bytes.data(), d->bytes.size(), id, off)) return c_err(Status::ERROR_DICTIONARY_FAILED);
   if (dict_id) *dict_id = id;
   if (content_offset) *content_offset = off;
   return 0;

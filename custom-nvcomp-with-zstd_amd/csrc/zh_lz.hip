@@ -59,6 +59,7 @@ namespace {
 #define ZH_K1_PMAX 1  // Jacobi entries from the prefix max of exits (K1 11.53 -> 11.50 ms)
 #endif
 constexpr u32 K1_THREADS = 1024;
+constexpr u32 K1_REDO = ~0u;      // lz_block: parse this block again without the probe
 constexpr u32 NROUND = ZH_WINDOW / 64;      // 64-position length rounds per window
 constexpr u32 SEGP = 32;                    // positions per walk segment (one lane of wave 0)
 constexpr u32 NSEG = ZH_WINDOW / SEGP;      // walk segments per window
@@ -99,6 +100,10 @@ constexpr u32 MISC_WNM = 0;   // misc[par]: matches of the window of that parity
 constexpr u32 MISC_ARR = 12;  // misc[12]: worker-wave barrier arrivals (cumulative)
 constexpr u32 MISC_NM = 4;    // misc[4 + (j & 3)]: matches the parse took in window j (miss skip)
 constexpr u32 MISC_ANY = 13;  // misc[13]: block_any's flag (0 between calls)
+constexpr u32 MISC_SCAN = 2;  // misc[2]: the repeat scan's count
+constexpr u32 MISC_XCH = 8;   // misc[8 + 2 (j & 1) + LONG]: inserter's resume check of miss-skip window j
+                              // ((j + 1) << 1 | hit; 0 at the block's start)
+constexpr u32 MISC_RESF = 14; // misc[14 + (j & 1)]: miss-skip window j resumed (its search is whole)
 static_assert(K1_LDS <= 163840 - 256, "K1 LDS budget");
 static_assert(OFF_TL % 16 == 0 && OFF_CI % 16 == 0 && OFF_HM % 16 == 0 && OFF_MISC % 4 == 0, "alignment");
 
@@ -214,15 +219,22 @@ __device__ __forceinline__ void insert_repair(u16 *T, u32 tb0, u32 lane, const u
 // slot verifies (insert_repair otherwise).  BT tiles are issued per LDS round trip together
 // with the next batch's input dwords and the workers' arrival counter.  Candidates
 // (position + 1, 0 = none) go to creg as u16 pairs.
-template <bool LONG, u32 NT, typename Hook>
-__device__ __forceinline__ void insert_window(const u32 *in32, u16 *T, u32 wsb, u32 we, u32 lim, u32 lane, u32 (&creg)[NCR], u32 &cwe,
-                                              const u32 *arrivals, Hook &&between_tiles, u32 pmin = 0) {
+// Tiles [T0, NT) of the window (a window is inserted as tiles [0, NT) in one call, or -- a
+// miss-skip window whose first tiles found a match -- as [0, ZH_SKIP_TILES) and then the rest).
+// CHECK (a miss-skip window's single first batch): before the batch's between_tiles hook, on_check
+// gets whether any position of the batch has a candidate matching its first ZH_MIN_MATCH_LONG
+// (long table) / ZH_MIN_MATCH_SHORT (short) bytes -- the oracle's "a match among the searched
+// tiles" (orc_lz_parse_pre), which resumes the search of the whole window.
+template <bool LONG, u32 T0, u32 NT, bool CHECK, typename Hook, typename Check>
+__device__ __forceinline__ void insert_window(const u32 *in32, u16 *T, u32 wsb, u32 lim, u32 lane, u32 (&creg)[NCR], const u32 *arrivals,
+                                              Hook &&between_tiles, Check &&on_check, u32 pmin = 0) {
   // positions below pmin are already in T (a dictionary's precomputed tables): treated like
   // positions past lim (the junk slot, no candidate); tiles from NT on (a miss-skip window,
   // orc_lz_parse_pre) are neither looked up nor inserted and their candidates never dumped
   constexpr u32 JUNK = LONG ? HL_SIZE : HS_SIZE;
   constexpr u32 BT = 2;  // tiles per LDS round trip
-  static_assert(TILES % BT == 0 && ZH_SKIP_TILES % BT == 0, "batches tile windows");
+  static_assert(TILES % BT == 0 && ZH_SKIP_TILES % BT == 0 && T0 % BT == 0, "batches tile windows");
+  static_assert(!CHECK || (T0 == 0 && NT == BT), "the resume check covers the first batch only");
   u32 wv[BT][TPL][3];
   auto load_in = [&](u32 tb0, u32 lim_t) {
 #pragma unroll
@@ -235,9 +247,9 @@ __device__ __forceinline__ void insert_window(const u32 *in32, u16 *T, u32 wsb, 
         wv[b][k][2] = in32[q + 2];
       }
   };
-  load_in(wsb, lim);
+  load_in(wsb + T0 * ZH_TILE, lim);
 #pragma unroll
-  for (u32 t0 = 0; t0 < NT; t0 += BT) {
+  for (u32 t0 = T0; t0 < NT; t0 += BT) {
     // opaque per-batch copy of lim: keeps the compiler from hoisting every tile's
     // bounds checks (64 masks) to the top of the unrolled loop
     u32 lim_t;
@@ -284,18 +296,42 @@ __device__ __forceinline__ void insert_window(const u32 *in32, u16 *T, u32 wsb, 
         // computation to the dump and keeps every tile's temporaries alive)
         __asm__ volatile("" : "+v"(creg[ri]) :: "memory");
       }
+    if constexpr (CHECK) {
+      bool v = false;
+#pragma unroll
+      for (u32 b = 0; b < BT; b++)
+#pragma unroll
+        for (u32 k = 0; k < TPL; k++) {
+          u32 const p = tb0 + b * ZH_TILE + 64 * k + lane, sh = min(p, lim_t) & 3u;
+          u32 const lo = __builtin_amdgcn_alignbyte(wv[b][k][1], wv[b][k][0], sh), hi = __builtin_amdgcn_alignbyte(wv[b][k][2], wv[b][k][1], sh);
+          u32 const c = h[b][k] != JUNK ? e[b][k] : 0u;
+          u32 clo, chi;
+          ld64u(in32, c ? c - 1u : 0u, clo, chi);
+          u32 const dx = (lo ^ clo) | ((hi ^ chi) & (LONG ? ~0u : 0xFFu));
+          v |= c != 0 && dx == 0;
+        }
+      on_check(__ballot(v) != 0);
+    }
     between_tiles(arr);
   }
-  // the next window's first position (lazy rule at this window's end): looked up
-  // after all of this window's tiles, before any of the next window's
-  cwe = 0;
+  __asm__ volatile("" ::: "memory");
+}
+// The next window's first position (lazy rule at this window's end): looked up after all of this
+// window's tiles, before any of the next window's.
+template <bool LONG>
+__device__ __forceinline__ u32 lookahead(const u32 *in32, const u16 *T, u32 we, u32 lim, u32 lane) {
+  u32 cwe = 0;
   if (lane < 2 && we + lane < lim) {  // (lane 1: we + 1, kept for the span-top rule)
     u32 lo, hi;
     ld64u(in32, we + lane, lo, hi);
     cwe = T[hash_of<LONG>(lo, hi)];
   }
   __asm__ volatile("" ::: "memory");
+  return cwe;
 }
+struct NoCheck {
+  __device__ void operator()(bool) const {}
+};
 
 // Positions [s, e) into T in order (the latest position wins every slot), lookups discarded:
 // the few dictionary positions between a precomputed table's end and the first tile a block
@@ -325,6 +361,34 @@ __device__ __forceinline__ void insert_span(const u32 *in32, u16 *T, u32 s, u32 
 // three past the one holding `pre`) never skip.  Wave-uniform.
 __device__ __forceinline__ bool skip_window(const u32 *misc, u32 k, u32 kskip0) {
   return k >= kskip0 && (u32)__builtin_amdgcn_readfirstlane(__atomic_load_n(&misc[MISC_NM + ((k - 3) & 3)], __ATOMIC_RELAXED)) == 0;
+}
+// ... unless its first tiles found a match and the inserters resumed the whole window's search
+// (decided while window k was inserted, in step k - 1; read by the workers after barrier P of
+// step k -- the next write to that parity is window k + 2's, in step k + 1).
+__device__ __forceinline__ bool skip_window_eff(const u32 *misc, u32 k, u32 kskip0) {
+#ifdef ZH_NO_RESUME
+  return skip_window(misc, k, kskip0);  // (A/B variant without the resume; not the oracle's rule)
+#endif
+  return skip_window(misc, k, kskip0) && (u32)__builtin_amdgcn_readfirstlane(__atomic_load_n(&misc[MISC_RESF + (k & 1)], __ATOMIC_RELAXED)) == 0;
+}
+// The two inserter waves' resume checks of miss-skip window j combined (mode 0: each table's wave
+// sees only its own candidates).  Both reach this after their first batch of the window and
+// before any barrier of the step, so neither waits on a wave held at a barrier.
+template <bool LONG, bool TWO>
+__device__ __forceinline__ bool resume_exchange(u32 *misc, u32 j, bool hit, u32 lane) {
+  if constexpr (TWO) {
+    u32 *const x = &misc[MISC_XCH + 2 * (j & 1)];
+    if (lane == 0) __atomic_store_n(&x[LONG ? 1 : 0], ((j + 1) << 1) | (hit ? 1u : 0u), __ATOMIC_RELAXED);
+    u32 v;
+    for (;;) {
+      v = (u32)__builtin_amdgcn_readfirstlane(__atomic_load_n(&x[LONG ? 0 : 1], __ATOMIC_RELAXED));
+      if ((v >> 1) == j + 1) break;
+      __builtin_amdgcn_s_sleep(1);
+    }
+    hit = hit || (v & 1u);
+  }
+  if (lane == 0) __atomic_store_n(&misc[MISC_RESF + (j & 1)], hit ? 1u : 0u, __ATOMIC_RELAXED);
+  return hit;
 }
 
 // Incompressibility probe (oracle orc_lz_parse_pre): at the top of loop step kprobe (the
@@ -690,37 +754,40 @@ __device__ __forceinline__ void seg_walk(const u32 *ci, u32 tmk, u32 S, u32 SE, 
 constexpr u32 WIN_BARRIERS = 1;  // X
 // The long table's wave in modes 1, 2 (the short table only): no insertion, only the step's two
 // barriers (P, X) and the probe exit, so the workgroup's barrier sequence stays the same.
-__device__ __forceinline__ void idle_inserter_loop(u32 *misc_, u32 n, u32 wstart, u32 kprobe, u32 e0p) {
+// Returns whether the loop ended at the incompressibility probe.
+__device__ __forceinline__ bool idle_inserter_loop(u32 *misc_, u32 n, u32 wstart, u32 kprobe, u32 e0p) {
   u32 const nwin = (n - wstart + ZH_WINDOW - 1) / ZH_WINDOW;
   for (u32 k = 0; k < nwin + 2; k++) {
-    if (probe_dead(misc_, k, kprobe)) break;
+    if (probe_dead(misc_, k, kprobe)) return true;
     __syncthreads();  // P
-    if (probe_dead_tm(k, kprobe, e0p)) break;
+    if (probe_dead_tm(k, kprobe, e0p)) return true;
     __syncthreads();  // X
   }
+  return false;
 }
-template <bool LONG>
-__device__ __forceinline__ void inserter_loop(const u32 *in32, u16 *T, u8 *ci8, u32 *misc_, u32 n, u32 lim, u32 lane, u32 *dbg, u32 wstart,
+template <bool LONG, bool TWO>
+__device__ __forceinline__ bool inserter_loop(const u32 *in32, u16 *T, u8 *ci8, u32 *misc_, u32 n, u32 lim, u32 lane, u32 *dbg, u32 wstart,
                                               u32 pmin, u32 span_s, u32 span_e, u32 kskip0, u32 kprobe, u32 e0p) {
   u32 creg[NCR];
-  u32 cwe = 0;
   if (span_s < span_e) insert_span<LONG>(in32, T, span_s, span_e, lane);
-  insert_window<LONG, TILES>(in32, T, wstart, min(wstart + (u32)ZH_WINDOW, n), lim, lane, creg, cwe, &misc_[MISC_ARR], [](u32) {}, pmin);
-  bool skipc = false;  // the window whose candidates creg holds is a miss-skip window
+  u32 const we0 = min(wstart + (u32)ZH_WINDOW, n);
+  insert_window<LONG, 0, TILES, false>(in32, T, wstart, lim, lane, creg, &misc_[MISC_ARR], [](u32) {}, NoCheck{}, pmin);
+  u32 cwe = lookahead<LONG>(in32, T, we0, lim, lane);
+  bool skipc = false;  // the window whose candidates creg holds is a miss-skip window (not resumed)
 #ifdef ZH_STAMPS
   u32 st_ins = 0;
 #endif
   u32 const nwin = (n - wstart + ZH_WINDOW - 1) / ZH_WINDOW;
   u32 passed = 0;  // X barriers taken so far
   for (u32 k = 0; k < nwin + 2; k++) {
-    if (probe_dead(misc_, k, kprobe)) break;
+    if (probe_dead(misc_, k, kprobe)) return true;
     u32 const wsb = wstart + k * ZH_WINDOW;
     if (k < nwin) {
       if (skipc) dump_window<LONG, ZH_SKIP_TILES>(ci8 + (k & 1u) * 4 * CI_WORDS, lane, creg, cwe);
       else dump_window<LONG, TILES>(ci8 + (k & 1u) * 4 * CI_WORDS, lane, creg, cwe);
     }
     __syncthreads();  // P: candidates of window k in buffer k & 1
-    if (probe_dead_tm(k, kprobe, e0p)) break;
+    if (probe_dead_tm(k, kprobe, e0p)) return true;
     u32 const done = passed + WIN_BARRIERS;
     // arr: the arrival counter as read with the last tile's read-back; a barrier taken
     // here means the counter is re-read for the next one
@@ -740,8 +807,25 @@ __device__ __forceinline__ void inserter_loop(const u32 *in32, u16 *T, u8 *ci8, 
     // (a second, short instantiation for miss-skip windows: a runtime tile bound in the full one
     // costs its unrolled batches more than the extra code does)
     if (k + 1 < nwin) {
-      if (skipc) insert_window<LONG, ZH_SKIP_TILES>(in32, T, nx, min(nx + ZH_WINDOW, n), lim, lane, creg, cwe, &misc_[MISC_ARR], take_ready);
-      else insert_window<LONG, TILES>(in32, T, nx, min(nx + ZH_WINDOW, n), lim, lane, creg, cwe, &misc_[MISC_ARR], take_ready);
+#ifdef ZH_NO_RESUME
+      if (skipc) {
+        insert_window<LONG, 0, ZH_SKIP_TILES, false>(in32, T, nx, lim, lane, creg, &misc_[MISC_ARR], take_ready, NoCheck{});
+      } else
+#endif
+      if (skipc) {
+        // the first tiles, then the rest of the window if any of them found a match (both
+        // inserters' checks combined before either takes a barrier)
+        bool hit = false;
+        insert_window<LONG, 0, ZH_SKIP_TILES, true>(in32, T, nx, lim, lane, creg, &misc_[MISC_ARR], take_ready,
+                                                    [&](bool h) { hit = resume_exchange<LONG, TWO>(misc_, k + 1, h, lane); });
+        if (hit) {
+          insert_window<LONG, ZH_SKIP_TILES, TILES, false>(in32, T, nx, lim, lane, creg, &misc_[MISC_ARR], take_ready, NoCheck{});
+          skipc = false;
+        }
+      } else {
+        insert_window<LONG, 0, TILES, false>(in32, T, nx, lim, lane, creg, &misc_[MISC_ARR], take_ready, NoCheck{});
+      }
+      cwe = lookahead<LONG>(in32, T, min(nx + ZH_WINDOW, n), lim, lane);
     }
 #ifdef ZH_STAMPS
     st_ins += (u32)(__builtin_amdgcn_s_memtime() - ti0);
@@ -752,6 +836,7 @@ __device__ __forceinline__ void inserter_loop(const u32 *in32, u16 *T, u8 *ci8, 
   if (LONG && lane == 0) dbg[16] = st_ins;
 #endif
   (void)dbg;
+  return false;
 }
 
 }  // namespace
@@ -831,8 +916,83 @@ __device__ __forceinline__ u32 k1_tid(u32 w) {
   return (u32)((K1_WAVE_MAP >> (4 * w)) & 15u) << 6 | lane;
 }
 
+// Repeat scan (ZH_SCAN_*, oracle orc_repeat_scan), all 1024 threads, after the probe found no
+// match: the hash tables' 64 KiB hold 2^ZH_SCAN_LOG u32 slots; positions q = 0 mod 4 below lim
+// enter min(sig16 << 16 | q) into the slot of their long hash (ds_min), then every block position
+// p counts when its slot holds its own sig16 with a position below p.  True: the block has enough
+// repeated 8-byte strings to be parsed after all.
+__device__ __forceinline__ bool repeat_scan(const u32 *in32, u32 *E, u32 *misc, u32 pre, u32 n, u32 tid) {
+  static_assert(ZH_SCAN_STRIDE == 4 && (4u << ZH_SCAN_LOG) <= 2 * (HL_SIZE + HS_SIZE + 2 * T_PAD), "scan table in the hash tables' space");
+  constexpr u32 NS = 1u << ZH_SCAN_LOG;
+  u32 const lim = n > ZH_HASH_READ ? n - ZH_HASH_READ : 0u;
+  // slot and signature of a position's long-hash sum t: E[t >> 18], entry (t << 14) & ~0xFFFF | q
+  auto slot = [&](u32 t) -> u32 * { return E + (t >> (32 - ZH_SCAN_LOG)); };
+  auto key = [](u32 t) { return (t << ZH_SCAN_LOG) & 0xFFFF0000u; };
+  for (u32 i = tid; i < NS / 4; i += K1_THREADS) ((uint4 *)E)[i] = make_uint4(~0u, ~0u, ~0u, ~0u);
+  if (tid == 0) misc[MISC_SCAN] = 0;
+  __syncthreads();
+  // positions q = 4j < lim: the 8 bytes at q are dwords j, j + 1; four per lane in flight
+  u32 const nq = (lim + 3) >> 2;
+  for (u32 j0 = tid; j0 < nq; j0 += 4 * K1_THREADS) {
+    u32 w[4][2];
+#pragma unroll
+    for (u32 u = 0; u < 4; u++) {
+      u32 const j = min(j0 + u * K1_THREADS, nq - 1u);
+      w[u][0] = in32[j];
+      w[u][1] = in32[j + 1];
+    }
+#pragma unroll
+    for (u32 u = 0; u < 4; u++) {
+      u32 const j = j0 + u * K1_THREADS;
+      u32 const t = hash_long_sum(w[u][0], w[u][1]);
+      if (j < nq) atomicMin(slot(t), key(t) | (4 * j));
+    }
+  }
+  __syncthreads();
+  // every block position p in [pre, lim) counts when E[slot] - key < p.  Groups of four
+  // positions (dwords j .. j + 2), two groups per lane in flight; only the first and last group
+  // of the range need the bounds (the others are checked by the unsigned range test alone)
+  u32 c = 0;
+  u32 const g0 = pre >> 2, g1 = (lim + 3) >> 2, span = lim > pre ? lim - pre : 0u;
+  for (u32 j0 = g0 + tid; j0 < g1; j0 += 2 * K1_THREADS) {
+    u32 w[2][3];
+#pragma unroll
+    for (u32 u = 0; u < 2; u++) {
+      u32 const j = min(j0 + u * K1_THREADS, g1 - 1u);
+      w[u][0] = in32[j];
+      w[u][1] = in32[j + 1];
+      w[u][2] = in32[j + 2];
+    }
+    u32 t[2][4], e[2][4];
+#pragma unroll
+    for (u32 u = 0; u < 2; u++)
+#pragma unroll
+      for (u32 r = 0; r < 4; r++) {
+        u32 const lo = r ? __builtin_amdgcn_alignbyte(w[u][1], w[u][0], r) : w[u][0];
+        u32 const hi = r ? __builtin_amdgcn_alignbyte(w[u][2], w[u][1], r) : w[u][1];
+        t[u][r] = hash_long_sum(lo, hi);
+        e[u][r] = *slot(t[u][r]);
+      }
+#pragma unroll
+    for (u32 u = 0; u < 2; u++) {
+      u32 const j = j0 + u * K1_THREADS;
+#pragma unroll
+      for (u32 r = 0; r < 4; r++) {
+        u32 const p = 4 * j + r;
+        c += (e[u][r] - key(t[u][r]) < p && p - pre < span) ? 1u : 0u;
+      }
+    }
+  }
+  u32 const wsum = lane_value(wave_scan_incl(c), 63);
+  if ((tid & 63) == 0 && wsum) atomicAdd(&misc[MISC_SCAN], wsum);
+  __syncthreads();
+  u32 const total = (u32)__builtin_amdgcn_readfirstlane(__atomic_load_n(&misc[MISC_SCAN], __ATOMIC_RELAXED));
+  u32 const need = span >> ZH_SCAN_SHIFT;
+  return total >= max(need, (u32)ZH_SCAN_MIN);
+}
+
 template <u32 MODE>
-__device__ __forceinline__ u32 lz_block(const ZhBlockDesc *__restrict__ blocks, ZhWorkspace ws, u32 b, u32 nblocks, u32 *s_take, Prefetch &pf, u32 wv) {
+__device__ __forceinline__ u32 lz_block(const ZhBlockDesc *__restrict__ blocks, ZhWorkspace ws, u32 b, u32 nblocks, u32 *s_take, Prefetch &pf, u32 wv, bool redo) {
   extern __shared__ __attribute__((aligned(16))) u8 smem[];
   u8 *in = smem + OFF_IN;
   u32 *in32 = (u32 *)in;
@@ -848,8 +1008,9 @@ __device__ __forceinline__ u32 lz_block(const ZhBlockDesc *__restrict__ blocks, 
   __asm__ volatile("v_mov_b32 %0, %1" : "=v"(tid) : "v"(k1_tid(wv)));
   u32 const lane = tid & 63;
   ZhBlockDesc const d = blocks[b];
-  // the next block for this workgroup (dynamic: a slow block does not hold up a fixed share)
-  if (tid == 0) *s_take = atomicAdd(ws.ctr, 1u);
+  // the next block for this workgroup (dynamic: a slow block does not hold up a fixed share;
+  // taken once per block, not again when the block is redone without the probe)
+  if (tid == 0 && !redo) *s_take = atomicAdd(ws.ctr, 1u);
   if (d.n == 0) {
     __syncthreads();
     u32 const next_b = *s_take;
@@ -874,7 +1035,7 @@ __device__ __forceinline__ u32 lz_block(const ZhBlockDesc *__restrict__ blocks, 
   const u8 *src = d.src;
   bool same = true;
   u32 nst;
-  if (pf.ok && staged_region(d, nst)) {  // prefetched during the previous block
+  if (!redo && pf.ok && staged_region(d, nst)) {  // prefetched during the previous block (a redo: pf holds the next)
     u32 const nv = n >> 4, pv = pre >> 4;
     u32 const f4 = src[0] * 0x01010101u;
 #pragma unroll
@@ -918,20 +1079,6 @@ __device__ __forceinline__ u32 lz_block(const ZhBlockDesc *__restrict__ blocks, 
   // inserting every history position (the oracle's order), without the history windows.
   bool const use_dt = ws.dtab && (d.flags & ZH_F_DICT) && (d.flags & ZH_F_FIRST) && pre >= 2 * ZH_DTAB_MARGIN && d.n >= 16 &&
                       ws.dtab_P >= pre;
-  if (use_dt) {
-    u32 const delta = ws.dtab_P - pre;
-    const u32 *dt32 = (const u32 *)ws.dtab;
-    auto clip = [&](u32 e) { return e > delta ? e - delta : 0u; };
-    for (u32 i = tid; i < (HL_SIZE + HS_SIZE) / 2; i += K1_THREADS) {
-      u32 const w = dt32[i];
-      u32 const v = clip(w & 0xFFFFu) | (clip(w >> 16) << 16);
-      u32 const j = i < HL_SIZE / 2 ? i : i + T_PAD / 2;  // TS follows TL's pad
-      ((u32 *)TL)[j] = v;
-    }
-    if (tid < T_PAD) ((u16 *)TL)[tid < T_PAD / 2 ? HL_SIZE + tid : HL_SIZE + T_PAD + HS_SIZE + (tid - T_PAD / 2)] = 0;
-  } else {
-    for (u32 i = tid; i < (HL_SIZE + HS_SIZE + 2 * T_PAD) / 2; i += K1_THREADS) ((u32 *)TL)[i] = 0;  // both tables (adjacent)
-  }
   // History without precomputed tables (a frame's later blocks, stream history, dictionary
   // views): only the final table over positions [0, pmin) -- the latest position per slot --
   // matters, so every wave inserts them at once (below) instead of the inserter waves walking
@@ -946,17 +1093,48 @@ __device__ __forceinline__ u32 lz_block(const ZhBlockDesc *__restrict__ blocks, 
 #else
   u32 const kskip0 = pre / ZH_WINDOW + 3 - wstart / ZH_WINDOW;  // first loop window that may skip
 #endif
-  if (tid == 0) misc[MISC_ARR] = 0;
-  bool const rle = !block_any(!same, &misc[MISC_ANY], tid) && d.n >= 2;
-  u32 const next_b = *s_take;  // (written before the barrier above)
-  prefetch_block(blocks, next_b, nblocks, tid, pf);  // the next block's input, in flight from here
-  if (rle) {
-    if (tid == 0) {
-      u32 one;  // (opaque: a constant {0, 0, 1} vector would be hoisted out of the block loop and spilled)
-      __asm__ volatile("v_mov_b32 %0, 1" : "=v"(one));
-      meta[0] = one - 1u; meta[1] = one - 1u; meta[2] = one;
+  u32 const lim = n > ZH_HASH_READ ? n - ZH_HASH_READ : 0;
+  // the probe's step: the oracle checks once the parse of windows [a0, a0 + ZH_PROBE_WINDOWS) is
+  // done, when the block has a window past them (windows counted up to lim, as the oracle does)
+  // and the probe window holds enough block positions (ZH_PROBE_MAX_E0)
+  u32 const a0 = pre / ZH_WINDOW, nwl = (lim + ZH_WINDOW - 1) / ZH_WINDOW;
+  u32 const e0p = pre - a0 * ZH_WINDOW;  // the probe window's first parsed position
+  u32 const kprobe0 = a0 + ZH_PROBE_WINDOWS + 1 <= nwl && e0p <= ZH_PROBE_MAX_E0 ? a0 + ZH_PROBE_WINDOWS + 1 - wstart / ZH_WINDOW : ~0u;
+  u32 next_b = 0;
+  if (use_dt) {
+    u32 const delta = ws.dtab_P - pre;
+    const u32 *dt32 = (const u32 *)ws.dtab;
+    auto clip = [&](u32 e) { return e > delta ? e - delta : 0u; };
+    for (u32 i = tid; i < (HL_SIZE + HS_SIZE) / 2; i += K1_THREADS) {
+      u32 const w = dt32[i];
+      u32 const v = clip(w & 0xFFFFu) | (clip(w >> 16) << 16);
+      u32 const j = i < HL_SIZE / 2 ? i : i + T_PAD / 2;  // TS follows TL's pad
+      ((u32 *)TL)[j] = v;
     }
-    return next_b;
+    if (tid < T_PAD) ((u16 *)TL)[tid < T_PAD / 2 ? HL_SIZE + tid : HL_SIZE + T_PAD + HS_SIZE + (tid - T_PAD / 2)] = 0;
+  } else {
+    for (u32 i = tid; i < (HL_SIZE + HS_SIZE + 2 * T_PAD) / 2; i += K1_THREADS) ((u32 *)TL)[i] = 0;  // both tables (adjacent)
+  }
+  if (tid == 0) {
+    misc[MISC_ARR] = 0;
+#pragma unroll
+    for (u32 i = 0; i < 4; i++) misc[MISC_XCH + i] = 0;
+  }
+  if (!redo) {
+    bool const rle = !block_any(!same, &misc[MISC_ANY], tid) && d.n >= 2;
+    next_b = *s_take;  // (written before the barrier above)
+    prefetch_block(blocks, next_b, nblocks, tid, pf);  // the next block's input, in flight from here
+    if (rle) {
+      if (tid == 0) {
+        u32 one;  // (opaque: a constant {0, 0, 1} vector would be hoisted out of the block loop and spilled)
+        __asm__ volatile("v_mov_b32 %0, 1" : "=v"(one));
+        meta[0] = one - 1u; meta[1] = one - 1u; meta[2] = one;
+      }
+      return next_b;
+    }
+  } else {
+    next_b = *s_take;
+    __syncthreads();  // the tables and counters
   }
   if (par_hist) {
     // store every position, then rounds of read-back: a slot holding an older position than
@@ -982,15 +1160,8 @@ __device__ __forceinline__ u32 lz_block(const ZhBlockDesc *__restrict__ blocks, 
   }
 
   ZH_STAMP(st_stage);
-  u64 *seq_out = ws.seq(b);
-  u8 *lit_out = ws.lits(b);
-  u32 const lim = n > ZH_HASH_READ ? n - ZH_HASH_READ : 0;
-  // the probe's step: the oracle checks once the parse of windows [a0, a0 + ZH_PROBE_WINDOWS) is
-  // done, when the block has a window past them (windows counted up to lim, as the oracle does)
-  u32 const a0 = pre / ZH_WINDOW, nwl = (lim + ZH_WINDOW - 1) / ZH_WINDOW;
-  u32 const kprobe = a0 + ZH_PROBE_WINDOWS + 1 <= nwl ? a0 + ZH_PROBE_WINDOWS + 1 - wstart / ZH_WINDOW : ~0u;
-  u32 const e0p = pre - a0 * ZH_WINDOW;  // the probe window's first parsed position
-  u32 nseq_tot = 0, nlit_tot = 0, e_in = pre;
+  u32 const kprobe = redo ? ~0u : kprobe0;
+  bool dead = false;
   // ---- inserter waves: their own loop with the same barrier sequence as the workers'
   // (separate code, so their registers never add to the workers' pressure)
   if (tid >= INS_TID) {
@@ -999,13 +1170,18 @@ __device__ __forceinline__ u32 lz_block(const ZhBlockDesc *__restrict__ blocks, 
     // gate the workers' next window, so they take priority (MI355X_MICROARCH.md, "VALU issue
     // is arbitrated ... by priority, then age").
     __builtin_amdgcn_s_setprio(2);
-    if (tid >= INS_TID + 64) inserter_loop<false>(in32, TS, ci8, misc, n, lim, lane, ws.dbg(b), wstart, pmin, span_s, span_e, kskip0, kprobe, e0p);
-    else if (two_tables<MODE>()) inserter_loop<true>(in32, TL, ci8, misc, n, lim, lane, ws.dbg(b), wstart, pmin, span_s, span_e, kskip0, kprobe, e0p);
-    else idle_inserter_loop(misc, n, wstart, kprobe, e0p);
+    if (tid >= INS_TID + 64)
+      dead = inserter_loop<false, two_tables<MODE>()>(in32, TS, ci8, misc, n, lim, lane, ws.dbg(b), wstart, pmin, span_s, span_e, kskip0, kprobe, e0p);
+    else if (two_tables<MODE>())
+      dead = inserter_loop<true, true>(in32, TL, ci8, misc, n, lim, lane, ws.dbg(b), wstart, pmin, span_s, span_e, kskip0, kprobe, e0p);
+    else
+      dead = idle_inserter_loop(misc, n, wstart, kprobe, e0p);
     __builtin_amdgcn_s_setprio(0);
-    return next_b;
-  }
-
+    if (!dead) return next_b;
+  } else {
+  u64 *const seq_out = ws.seq(b);
+  u8 *const lit_out = ws.lits(b);
+  u32 nseq_tot = 0, nlit_tot = 0, e_in = pre;
   u32 const tid_ = tid;
   u32 const wave = tid >> 6;
   u32 r_lo = 0;
@@ -1023,7 +1199,6 @@ __device__ __forceinline__ u32 lz_block(const ZhBlockDesc *__restrict__ blocks, 
   //   X
   //   phase B  take decisions at window k's span tops (each wave its own), the literals of
   //            window k - 1 (lanes = positions, all worker waves)
-  bool dead = false;
   for (u32 k = 0; k < nwin + 2; k++) {
     if (probe_dead(misc, k, kprobe)) {
       dead = true;
@@ -1058,7 +1233,7 @@ __device__ __forceinline__ u32 lz_block(const ZhBlockDesc *__restrict__ blocks, 
     // take masks of the rounds above
     constexpr u32 RS = 2 * ZH_SKIP_TILES;
     static_assert(RS < NWW && (RS & 1) == 0, "miss-skip rounds");
-    bool const skipk = have && skip_window(misc, k, kskip0);
+    bool const skipk = have && skip_window_eff(misc, k, kskip0);
     if (skipk && wave != 0) {
       if (wave <= RS) span_lengths<MODE>(in32, ciK, tmK, xq, wave - 1, wave, wsb, we, n, lim, lane, wave == RS, 0u);
       for (u32 r = RS + wave - 1; r < NROUND; r += NWW - 1) {
@@ -1198,11 +1373,49 @@ __device__ __forceinline__ u32 lz_block(const ZhBlockDesc *__restrict__ blocks, 
     }
     ZH_STAMP(st_E);
   }
-  if (dead && (((uintptr_t)d.src) & 15) == 0) {
-    // the probe found no match: no sequences, the whole block is literals, and they are the
-    // block's own bytes -- K2 reads them from the source (16-B aligned).  K1 leaves K2 the
-    // literal histogram instead: one 256-bin sub-histogram per worker wave, counted in LDS (the
-    // hash tables are dead) and stored after the first 64 KiB of the literal area (ZH_K1_HIST_OFF).
+  if (!dead) {
+    if (tid_ == 0) { meta[0] = nseq_tot; meta[1] = nlit_tot; meta[2] = 0; }
+#ifdef ZH_STAMPS
+    if (tid == 0) {
+      u32 *dbg = ws.dbg(b);
+      dbg[23] = (u32)rt0; dbg[24] = (u32)__builtin_amdgcn_s_memrealtime();
+      dbg[25] = __builtin_amdgcn_s_getreg((31 << 11) | 4);   // HW_ID
+      dbg[26] = __builtin_amdgcn_s_getreg((31 << 11) | 20);  // XCC_ID
+      dbg[27] = (u32)(__builtin_amdgcn_s_memtime() - mt0);
+      dbg[40] = st_Bmax; dbg[41] = st_Imax; dbg[55] = st_J1; dbg[56] = st_J2; dbg[57] = st_J3;
+      dbg[0] = st_stage; dbg[1] = st_A; dbg[2] = st_B; dbg[3] = st_J; dbg[4] = st_E; dbg[5] = st_rounds; dbg[20] = st_E2; dbg[21] = st_X; dbg[22] = st_E1;
+    }
+    if ((tid & 63) == 0 && tid < INS_TID) {  // each worker wave's length-phase cycles
+      u32 const w = tid >> 6;
+#ifdef ZH_EXP_PWAIT
+      ws.dbg(b)[w < 12 ? 28 + w : 53 + (w - 12)] = st_A;
+#else
+      ws.dbg(b)[w < 12 ? 28 + w : 53 + (w - 12)] = st_B;
+#endif
+    }
+#endif
+    return next_b;
+  }
+  }  // (worker waves)
+  // The probe ended the window loop (every wave left it at the same step): the repeat scan
+  // decides between the literal-only block and redoing the block from its staging without the
+  // probe (the oracle's parse simply goes on; lz_blocks calls lz_block again with `redo`).
+#ifdef ZH_NO_SCAN
+  if (false) return K1_REDO;  // (A/B variant: the probe alone decides, as in round 4)
+#else
+  if (repeat_scan(in32, (u32 *)TL, misc, pre, n, tid)) return K1_REDO;
+#endif
+  ZH_STAMP(st_E1);
+  if (tid >= INS_TID) return next_b;
+  u32 const wave = tid >> 6;
+  u32 bo;  // (opaque: the block's workspace offset is not kept live across the window loop)
+  __asm__ volatile("s_mov_b32 %0, %1" : "=s"(bo) : "s"((u32)__builtin_amdgcn_readfirstlane(b)));
+  u8 *const lit_out = ws.lits(bo);
+  if ((((uintptr_t)d.src) & 15) == 0) {
+    // no sequences, the whole block is literals, and they are the block's own bytes -- K2 reads
+    // them from the source (16-B aligned).  K1 leaves K2 the literal histogram instead: one
+    // 256-bin sub-histogram per worker wave, counted in LDS (the hash tables are dead) and stored
+    // after the first 64 KiB of the literal area (ZH_K1_HIST_OFF).
     u32 *const hw = (u32 *)(smem + OFF_TL) + 256u * wave;
     for (u32 i = lane; i < 256; i += 64) hw[i] = 0;
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -1226,7 +1439,7 @@ __device__ __forceinline__ u32 lz_block(const ZhBlockDesc *__restrict__ blocks, 
     __builtin_amdgcn_wave_barrier();
     u32 *const gh = (u32 *)(lit_out + ZH_K1_HIST_OFF) + 256u * wave;
     for (u32 i = lane; i < 256; i += 64) gh[i] = hw[i];
-    if (tid_ == 0) {
+    if (tid == 0) {
       u32 two;  // (opaque: a constant {0, n, 2} vector would be hoisted out of the block loop and spilled)
       __asm__ volatile("v_mov_b32 %0, 2" : "=v"(two));
       meta[0] = two - 2u; meta[1] = d.n; meta[2] = two;
@@ -1236,49 +1449,26 @@ __device__ __forceinline__ u32 lz_block(const ZhBlockDesc *__restrict__ blocks, 
     if (tid == 0) {
       u32 *dbg = ws.dbg(b);
       dbg[27] = (u32)(__builtin_amdgcn_s_memtime() - mt0);
-      dbg[0] = st_stage; dbg[1] = st_A; dbg[2] = st_B; dbg[3] = st_J; dbg[4] = st_E; dbg[5] = st_rounds;
+      dbg[0] = st_stage; dbg[1] = st_A; dbg[2] = st_B; dbg[3] = st_J; dbg[4] = st_E; dbg[5] = st_rounds; dbg[22] = st_E1;
     }
 #endif
     return next_b;
   }
-  if (dead) {
-    // (unaligned source) the block's bytes go out of LDS to the literal area in 16-B stores
-    u32 const nv = (d.n + 15) >> 4, sh = pre & 3;
-    const u32 *const src32 = in32 + (pre >> 2);
-    for (u32 i = tid_; i < nv; i += INS_TID) {
-      u32 w[5];
+  // (unaligned source) the block's bytes go out of LDS to the literal area in 16-B stores
+  u32 const nv = (d.n + 15) >> 4, sh = pre & 3;
+  const u32 *const src32 = in32 + (pre >> 2);
+  for (u32 i = tid; i < nv; i += INS_TID) {
+    u32 w[5];
 #pragma unroll
-      for (u32 k = 0; k < 5; k++) w[k] = src32[4 * i + k];
-      uint4 v;
-      v.x = __builtin_amdgcn_alignbyte(w[1], w[0], sh);
-      v.y = __builtin_amdgcn_alignbyte(w[2], w[1], sh);
-      v.z = __builtin_amdgcn_alignbyte(w[3], w[2], sh);
-      v.w = __builtin_amdgcn_alignbyte(w[4], w[3], sh);
-      ((uint4 *)lit_out)[i] = v;
-    }
-    nseq_tot = 0;
-    nlit_tot = d.n;
+    for (u32 k = 0; k < 5; k++) w[k] = src32[4 * i + k];
+    uint4 v;
+    v.x = __builtin_amdgcn_alignbyte(w[1], w[0], sh);
+    v.y = __builtin_amdgcn_alignbyte(w[2], w[1], sh);
+    v.z = __builtin_amdgcn_alignbyte(w[3], w[2], sh);
+    v.w = __builtin_amdgcn_alignbyte(w[4], w[3], sh);
+    ((uint4 *)lit_out)[i] = v;
   }
-  if (tid_ == 0) { meta[0] = nseq_tot; meta[1] = nlit_tot; meta[2] = 0; }
-#ifdef ZH_STAMPS
-  if (tid == 0) {
-    u32 *dbg = ws.dbg(b);
-    dbg[23] = (u32)rt0; dbg[24] = (u32)__builtin_amdgcn_s_memrealtime();
-    dbg[25] = __builtin_amdgcn_s_getreg((31 << 11) | 4);   // HW_ID
-    dbg[26] = __builtin_amdgcn_s_getreg((31 << 11) | 20);  // XCC_ID
-    dbg[27] = (u32)(__builtin_amdgcn_s_memtime() - mt0);
-    dbg[40] = st_Bmax; dbg[41] = st_Imax; dbg[55] = st_J1; dbg[56] = st_J2; dbg[57] = st_J3;
-    dbg[0] = st_stage; dbg[1] = st_A; dbg[2] = st_B; dbg[3] = st_J; dbg[4] = st_E; dbg[5] = st_rounds; dbg[20] = st_E2; dbg[21] = st_X; dbg[22] = st_E1;
-  }
-  if ((tid & 63) == 0 && tid < INS_TID) {  // each worker wave's length-phase cycles
-    u32 const w = tid >> 6;
-#ifdef ZH_EXP_PWAIT
-    ws.dbg(b)[w < 12 ? 28 + w : 53 + (w - 12)] = st_A;
-#else
-    ws.dbg(b)[w < 12 ? 28 + w : 53 + (w - 12)] = st_B;
-#endif
-  }
-#endif
+  if (tid == 0) { meta[0] = 0; meta[1] = d.n; meta[2] = 0; }
   return next_b;
 }
 
@@ -1298,9 +1488,12 @@ __device__ __forceinline__ void lz_blocks(const ZhBlockDesc *__restrict__ blocks
   Prefetch pf;
   u32 const wv = (u32)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   prefetch_block(blocks, b, nblocks, k1_tid(wv), pf);
+  bool redo = false;
   while (b < nblocks) {
-    b = lz_block<MODE>(blocks, ws, b, nblocks, &s_take, pf, wv);  // returns the next block taken
+    u32 const r = lz_block<MODE>(blocks, ws, b, nblocks, &s_take, pf, wv, redo);  // the next block taken, or K1_REDO
     __syncthreads();  // every wave is done with this block's LDS before the next is staged
+    redo = r == K1_REDO;
+    b = redo ? b : r;
   }
 }
 // one instantiation per parse mode (ZH_K1_MODE: levels 3-4 / 2 / 1)

@@ -101,10 +101,11 @@ int nvcomp_zstd_batch_compress_async_v5(nvcomp_zstd_batch_manager_t *mgr, const 
  * <= max_uncompressed_chunk_bytes and every output buffer must hold
  * nvcomp_zstd_batch_get_max_compressed_chunk_size_v5(max_uncompressed_chunk_bytes). */
 size_t nvcomp_zstd_batched_compress_get_temp_size_v5(size_t num_chunks, size_t max_uncompressed_chunk_bytes);
-/* The same for the handle's level and dictionary (levels >= 9 add the deep matcher's scratch
- * slots; a dictionary over 32 KiB chunks adds history blocks): what a handle at any level, with
- * or without a dictionary, needs for nvcomp_zstd_batched_compress_async_v5.  (The static size
- * above covers levels < 9 without a dictionary; a smaller workspace fails loudly with 7.) */
+/* The same for the handle's level and dictionary (levels >= 5, ZH_DEEP_LEVEL, add the deep
+ * matcher's scratch slots; a dictionary over 32 KiB chunks adds history blocks): what a handle at
+ * its level, with or without a dictionary, needs for nvcomp_zstd_batched_compress_async_v5.  (The
+ * static size above covers levels below 5 without a dictionary; at levels >= 5, or with a
+ * dictionary, a workspace of that size fails loudly with 7 and nothing is launched.) */
 size_t nvcomp_zstd_batch_get_batched_temp_size_v5(nvcomp_zstd_batch_manager_t *mgr, size_t num_chunks, size_t max_uncompressed_chunk_bytes);
 /* A dictionary for the batch handle's compress/decompress calls (the C++
  * manager's set_dictionary).  With a dictionary, chunks over 32 KiB take two history blocks:

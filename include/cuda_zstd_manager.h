@@ -12,23 +12,13 @@
 
 #include "cuda_zstd_types.h"
 #include "cuda_zstd_capi.h"
+#include "cuda_zstd_dictionary.h"
 
 #ifdef __cplusplus
 #include <memory>
 #include <vector>
 
 namespace cuda_zstd {
-
-namespace dictionary {
-// Dictionary bytes (reference include/cuda_zstd_dictionary.h): raw content or a formatted
-// RFC 8878 §5 dictionary.  dict_id is filled in by set_dictionary (the
-// formatted dictionary's ID; 0 for raw content).
-struct Dictionary {
-  std::vector<u8> raw_content;
-  u32 dict_id = 0;
-  size_t size() const { return raw_content.size(); }
-};
-}  // namespace dictionary
 
 class ZstdManager {
  public:
@@ -103,8 +93,9 @@ class ZstdBatchManager : public ZstdManager {
   Status compress_batch_device(const void *const *d_in_ptrs, const size_t *d_in_sizes, size_t max_chunk_bytes, size_t count,
                                void *const *d_out_ptrs, size_t *d_out_sizes, int *d_statuses, void *temp_workspace, size_t temp_size,
                                hipStream_t stream);
+  // levels below 5 (ZH_DEEP_LEVEL) without a dictionary; otherwise get_batch_device_temp_size_for
   static size_t get_batch_device_temp_size(size_t count, size_t max_chunk_bytes);
-  // the same for this manager's level and dictionary (levels >= 9 add the deep matcher's scratch
+  // the same for this manager's level and dictionary (levels >= 5 add the deep matcher's scratch
   // slots, ~1.2 MB per persistent workgroup; a dictionary over 32 KiB chunks adds history blocks)
   size_t get_batch_device_temp_size_for(size_t count, size_t max_chunk_bytes) const;
 

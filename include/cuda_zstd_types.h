@@ -7,6 +7,8 @@
 //   CompressionConfig           :196-232 (same fields; cpu_threshold default 0, see below)
 //   CompressionStats            :238-262
 //   BatchItem                   :268-274
+//   DictionaryContent           :280-284
+//   BatchRoutingResult          :430-437
 //   Hybrid enums / structs      :312-430
 // Streams are hipStream_t (same pointer ABI as cudaStream_t).
 #ifndef CUDA_ZSTD_TYPES_H_
@@ -35,13 +37,16 @@ enum class Status : u32 {
   ERROR_CUDA_ERROR = 4,  // HIP runtime error
   ERROR_INVALID_MAGIC = 5,
   ERROR_CORRUPT_DATA = 6,
+  ERROR_CORRUPTED_DATA [[deprecated("Use ERROR_CORRUPT_DATA instead")]] = 6,  // reference :101
   ERROR_BUFFER_TOO_SMALL = 7,
   ERROR_UNSUPPORTED_VERSION = 8,
   ERROR_DICTIONARY_MISMATCH = 9,
   ERROR_CHECKSUM_FAILED = 10,
   ERROR_IO = 11,
   ERROR_COMPRESSION = 12,
+  ERROR_COMPRESSION_FAILED [[deprecated("Use ERROR_COMPRESSION instead")]] = 12,  // reference :109
   ERROR_DECOMPRESSION = 13,
+  ERROR_DECOMPRESSION_FAILED [[deprecated("Use ERROR_DECOMPRESSION instead")]] = 13,  // reference :112
   ERROR_WORKSPACE_INVALID = 14,
   ERROR_STREAM_ERROR = 15,
   ERROR_ALLOCATION_FAILED = 16,
@@ -162,6 +167,13 @@ struct BatchItem {
   Status status = Status::SUCCESS;
 };
 
+// a dictionary's device-resident content (reference include/cuda_zstd_types.h:280-284)
+struct DictionaryContent {
+  const unsigned char *d_buffer = nullptr;
+  size_t size = 0;
+  u32 dict_id = 0;
+};
+
 // ---- hybrid CPU/GPU routing (reference include/cuda_zstd_types.h:312-430) ----
 enum class HybridMode : u32 { AUTO = 0, PREFER_CPU = 1, PREFER_GPU = 2, FORCE_CPU = 3, FORCE_GPU = 4, ADAPTIVE = 5 };
 enum class DataLocation : u32 { HOST = 0, DEVICE = 1, MANAGED = 2, UNKNOWN = 3 };
@@ -192,10 +204,14 @@ struct HybridResult {
   const char *routing_reason = nullptr;
 };
 
+// per-item result of HybridEngine's batch calls (reference include/cuda_zstd_types.h:430-437)
 struct BatchRoutingResult {
+  size_t item_index = 0;
   ExecutionBackend backend_used = ExecutionBackend::CPU_LIBZSTD;
   Status status = Status::SUCCESS;
-  size_t output_size = 0;
+  size_t input_bytes = 0;
+  size_t output_bytes = 0;
+  double compute_time_ms = 0.0;
 };
 
 inline bool is_valid_compression_level(int level) {

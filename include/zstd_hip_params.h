@@ -28,10 +28,25 @@
 #define ZH_FRAME_BLOCK(n, split_dict) ((n) <= ((split_dict) ? ZH_HIST_BLOCK : ZH_BLOCK_MAX) ? ZH_BLOCK_MAX : ZH_HIST_BLOCK)
 #define ZH_TILE 128                 /* hash insertion granularity (positions) */
 #define ZH_WINDOW 2048              /* parse window (positions); catch-up stays inside one */
-#define ZH_SKIP_TILES 2             /* tiles a window searches after a window without matches (miss skip) */
+#define ZH_SKIP_TILES 2             /* tiles a window searches after a window without matches (miss skip);
+                                       a match among them resumes the search of the whole window */
 #ifndef ZH_PROBE_WINDOWS
 #define ZH_PROBE_WINDOWS 1          /* a block whose parse takes no match in its first windows is all literals */
 #endif
+/* The probe applies only when its window holds at least ZH_WINDOW - ZH_PROBE_MAX_E0 block
+ * positions (a block whose `pre` sits late in its window is never probed). */
+#define ZH_PROBE_MAX_E0 (ZH_WINDOW / 2)
+/* Repeat scan: a block the probe finds no match in is all literals only when this whole-block
+ * test also finds (almost) no repeated 8-byte string.  Positions q = 0 mod ZH_SCAN_STRIDE of the
+ * staged buffer (history included) are entered into a 2^ZH_SCAN_LOG-slot table keyed by the long
+ * hash's top bits, each slot keeping the minimum of (16 more bits of the hash) << 16 | q; a block
+ * position p counts when its slot's entry carries p's 16 bits and a position below p.  The block is
+ * resurrected (parsed in full, no probe) when at least max(ZH_SCAN_MIN, block positions >>
+ * ZH_SCAN_SHIFT) positions count. */
+#define ZH_SCAN_LOG 14
+#define ZH_SCAN_STRIDE 4
+#define ZH_SCAN_SHIFT 10
+#define ZH_SCAN_MIN 8
 #define ZH_HASH_LOG_LONG 14         /* 8-byte hash table: 2^14 u16 entries */
 #define ZH_HASH_LOG_SHORT 14        /* 5-byte hash table: 2^14 u16 entries */
 #define ZH_HASH_READ 8              /* bytes read per hashed position */

@@ -815,7 +815,8 @@ static u32 common_prefix(const u8 *src, u32 a, u32 b, u32 n, u32 cap) {
  * len[p] (0 or >= ZH_MIN_MATCH_*), off[p].  Each tile's lookups see the tables after every
  * earlier tile's insertions (K1's inserter waves: zh_lz.hip insert_window).  `skip_from`:
  * tiles at or above it are neither looked up nor inserted (len 0), see orc_lz_parse_pre. */
-static u32 g_TL[1 << ZH_HASH_LOG_LONG], g_TS[1 << ZH_HASH_LOG_SHORT];
+/* per thread: oracle frames may run on a thread pool (test_c5_full_workload_vs_oracle's pattern) */
+static _Thread_local u32 g_TL[1 << ZH_HASH_LOG_LONG], g_TS[1 << ZH_HASH_LOG_SHORT];
 /* K1's parse mode of the level (ZH_K1_MODE): 0 = both tables, lazy-1 check (levels 3-4);
  * 1 = the short (5-byte) table only, lazy-1 (level 2); 2 = the short table only, greedy (level 1).
  * Set by orc_compress_frame_lv. */
@@ -930,6 +931,35 @@ size_t orc_lz_parse_deep(const u8 *buf, u32 pre, u32 n, u32 depth, orc_seq_t *se
  * finished when its insertion starts -- took no match (counted at the match position before
  * catch-up) searches and inserts only its first ZH_SKIP_TILES tiles; the rest of it has no
  * candidates.  Windows up to three past the one holding `pre` never skip. */
+/* Repeat scan (ZH_SCAN_*, include/zstd_hip_params.h; K1 zh_lz.hip repeat_scan): the number of
+ * block positions p in [pre, lim) whose 8 bytes repeat an earlier sampled position, as seen
+ * through a 2^ZH_SCAN_LOG-slot table of min(sig16 << 16 | q) over q = 0 mod ZH_SCAN_STRIDE in
+ * [0, lim) -- slot and sig16 from the long hash's sum (top 14 bits, the 16 below them). */
+static inline u32 scan_sum(u64 v) {
+  return mul24((u32)v, ZH_HK_L0) + mul24((u32)(v >> 24), ZH_HK_L1) + mul24((u32)(v >> 48), ZH_HK_L2);
+}
+u32 orc_repeat_scan(const u8 *src, u32 pre, u32 n) {
+  u32 const lim = n > ZH_HASH_READ ? n - ZH_HASH_READ : 0;
+  u32 *E = malloc(sizeof(u32) << ZH_SCAN_LOG);
+  memset(E, 0xFF, sizeof(u32) << ZH_SCAN_LOG);
+  for (u32 q = 0; q < lim; q += ZH_SCAN_STRIDE) {
+    u32 const t = scan_sum(rd64(src + q)), s = t >> (32 - ZH_SCAN_LOG), e = ((t << ZH_SCAN_LOG) & 0xFFFF0000u) | q;
+    if (e < E[s]) E[s] = e;
+  }
+  u32 c = 0;
+  for (u32 p = pre; p < lim; p++) {
+    u32 const t = scan_sum(rd64(src + p)), s = t >> (32 - ZH_SCAN_LOG);
+    c += E[s] - ((t << ZH_SCAN_LOG) & 0xFFFF0000u) < p;
+  }
+  free(E);
+  return c;
+}
+static int repeat_scan_alive(const u8 *src, u32 pre, u32 n) {
+  u32 const lim = n > ZH_HASH_READ ? n - ZH_HASH_READ : 0;
+  u32 const need = lim > pre ? (lim - pre) >> ZH_SCAN_SHIFT : 0;
+  return orc_repeat_scan(src, pre, n) >= (need > ZH_SCAN_MIN ? need : ZH_SCAN_MIN);
+}
+
 size_t orc_lz_parse_pre(const u8 *src, u32 pre, u32 n, orc_seq_t *seq, u32 *last_lits) {
   if (orc_parse_level >= ZH_DEEP_LEVEL) return orc_lz_parse_deep(src, pre, n, ZH_DEEP_DEPTH(orc_parse_level), seq, last_lits);
   u8 *len = malloc(n + 2);
@@ -944,16 +974,31 @@ size_t orc_lz_parse_pre(const u8 *src, u32 pre, u32 n, orc_seq_t *seq, u32 *last
     if (a < nwin) {
       u32 const t0 = a * ZH_WINDOW, t1 = (a + 1) * ZH_WINDOW;
       int const skip = a >= a0 + 3 && mcount[a - 3] == 0;
-      match_info_tiles(src, n, t0, t1, skip ? t0 + ZH_SKIP_TILES * ZH_TILE : 0xFFFFFFFFu, len, off);
+      if (skip) {
+        /* a miss-skip window searches its first ZH_SKIP_TILES tiles; a match among them (any
+         * position with a candidate of at least the minimum length) resumes the search of the
+         * rest of the window, as if it had not skipped (K1: the inserter waves check their
+         * candidates after the first batch of tiles) */
+        u32 const ts = t0 + ZH_SKIP_TILES * ZH_TILE;
+        match_info_tiles(src, n, t0, ts, 0xFFFFFFFFu, len, off);
+        int hit = 0;
+        for (u32 q = t0; q < ts && q < lim; q++) hit |= len[q] != 0;
+        if (hit) match_info_tiles(src, n, ts, t1, 0xFFFFFFFFu, len, off);
+      } else {
+        match_info_tiles(src, n, t0, t1, 0xFFFFFFFFu, len, off);
+      }
     }
     /* incompressibility probe: once the parse of the probe windows [a0, a0 + ZH_PROBE_WINDOWS)
      * is done (in the iteration after the one that inserted window a0 + ZH_PROBE_WINDOWS) and
-     * it took no match there, the block takes no sequences at all -- the whole block is
-     * literals (K1 stops; K2 reads them from the source, orc_compress_block_pre) */
-    if (a == a0 + ZH_PROBE_WINDOWS + 1 && a <= nwin) {
+     * it took no match there, and the repeat scan of the whole block finds (almost) no repeated
+     * 8-byte string, the block takes no sequences at all -- the whole block is literals (K1
+     * stops; K2 reads them from the source, orc_compress_block_pre).  Otherwise the parse goes
+     * on as if there were no probe (K1 restarts the block without it).  Blocks whose `pre` lies
+     * past ZH_PROBE_MAX_E0 in its window are not probed. */
+    if (a == a0 + ZH_PROBE_WINDOWS + 1 && a <= nwin && pre - a0 * ZH_WINDOW <= ZH_PROBE_MAX_E0) {
       u32 m = 0;
       for (u32 j = a0; j < a0 + ZH_PROBE_WINDOWS; j++) m += mcount[j];
-      if (m == 0) {
+      if (m == 0 && !repeat_scan_alive(src, pre, n)) {
         ns = 0;
         anchor = pre;
         break;

@@ -209,8 +209,12 @@ int main(int argc, char **argv) {
     if (argc < 4) return 1;
     bool const hist = std::stoul(argv[3]) != 0;
     std::vector<char> db = slurp(dir + "/dict.bin");
+    // the reference's caller shape (tests/test_dictionary_memory.cu:174-176): a view of the
+    // caller's bytes; the header's ID is the caller's (frames carry the content's RFC ID)
     dictionary::Dictionary dct;
-    dct.raw_content.assign(db.begin(), db.end());
+    dct.raw_content = (unsigned char *)db.data();
+    dct.raw_size = (u32)db.size();
+    dct.header.dictionary_id = 12345;
     ZstdStreamingManager sm(CompressionConfig::from_level(3));
     Status st = sm.set_dictionary(dct);
     if (st == Status::SUCCESS) st = hist ? sm.init_compression_with_history(0, 0) : sm.init_compression(0, 0);
@@ -232,6 +236,37 @@ int main(int argc, char **argv) {
       CK(hipMemcpy(back.data() + offs[i], d_o, sizes[i], hipMemcpyDeviceToHost));
     }
     dump(dir + "/back.bin", back.data(), back.size());
+  } else if (mode == "stream_ext") {
+    // frames made elsewhere with the dictionary (in.bin; e.g. libzstd with the
+    // Dictionary_ID left out, dictIDFlag 0) decode in a streaming manager that has the dictionary
+    // set and no history session: every frame against the dictionary, not the previous output.
+    // <dir>/usizes.bin = u64 decompressed sizes.  Writes back.bin.
+    std::vector<char> db = slurp(dir + "/dict.bin"), ub = slurp(dir + "/usizes.bin");
+    if (ub.size() != 8 * n) return 1;
+    std::vector<size_t> us(n);
+    memcpy(us.data(), ub.data(), 8 * n);
+    dictionary::Dictionary dct;
+    dct.raw_content = (unsigned char *)db.data();
+    dct.raw_size = (u32)db.size();
+    ZstdStreamingManager dec(CompressionConfig::from_level(3));
+    Status st = dec.set_dictionary(dct);
+    if (st == Status::SUCCESS) st = dec.init_decompression(0);
+    if (st != Status::SUCCESS) { fprintf(stderr, "init: %s\n", status_to_string(st)); return 3; }
+    size_t tot = 0;
+    for (size_t i = 0; i < n; i++) tot += us[i];
+    std::vector<char> back(tot);
+    void *d_o;
+    CK(hipMalloc(&d_o, std::max<size_t>(*std::max_element(us.begin(), us.end()), 1)));
+    size_t o = 0;
+    for (size_t i = 0; i < n; i++) {
+      size_t got = us[i];
+      bool last = false;
+      st = dec.decompress_chunk(d_in[i], sizes[i], d_o, &got, &last, 0);
+      if (st != Status::SUCCESS || got != us[i]) { fprintf(stderr, "decompress_chunk %zu: %s, %zu B\n", i, status_to_string(st), got); return 4; }
+      CK(hipMemcpy(back.data() + o, d_o, us[i], hipMemcpyDeviceToHost));
+      o += us[i];
+    }
+    dump(dir + "/back.bin", back.data(), back.size());  // (frames.bin stays empty: fsz 0)
   } else if (mode == "stream_split") {
     // advisor r3: frames from compress_chunk_with_history in one manager (dictionary set),
     // decoded by a SECOND, decode-only manager with the same dictionary set.  <flag> = 1: the
@@ -241,8 +276,12 @@ int main(int argc, char **argv) {
     if (argc < 4) return 1;
     bool const flag = std::stoul(argv[3]) != 0;
     std::vector<char> db = slurp(dir + "/dict.bin");
+    // the reference's caller shape (tests/test_dictionary_memory.cu:174-176): a view of the
+    // caller's bytes; the header's ID is the caller's (frames carry the content's RFC ID)
     dictionary::Dictionary dct;
-    dct.raw_content.assign(db.begin(), db.end());
+    dct.raw_content = (unsigned char *)db.data();
+    dct.raw_size = (u32)db.size();
+    dct.header.dictionary_id = 12345;
     ZstdStreamingManager enc(CompressionConfig::from_level(3)), dec(CompressionConfig::from_level(3));
     Status st = enc.set_dictionary(dct);
     if (st == Status::SUCCESS) st = dec.set_dictionary(dct);
@@ -276,8 +315,12 @@ int main(int argc, char **argv) {
     //  * HybridEngine move construction / assignment, decompress_batch, get_observed_throughput,
     //    reset_profiling, hybrid_decompress (include/cuda_zstd_hybrid.h:82-83,180-186,229-235,263-268)
     std::vector<char> db = slurp(dir + "/dict.bin");
+    // the reference's caller shape (tests/test_dictionary_memory.cu:174-176): a view of the
+    // caller's bytes; the header's ID is the caller's (frames carry the content's RFC ID)
     dictionary::Dictionary dct;
-    dct.raw_content.assign(db.begin(), db.end());
+    dct.raw_content = (unsigned char *)db.data();
+    dct.raw_size = (u32)db.size();
+    dct.header.dictionary_id = 12345;
     for (size_t i = 0; i < n; i++) {
       fsz[i] = cap;
       Status st = compress_with_dict(d_in[i], sizes[i], d_out[i], &fsz[i], dct, 3, 0);
@@ -294,6 +337,53 @@ int main(int argc, char **argv) {
       CK(hipMemcpy(back.data() + offs[i], d_o, sizes[i], hipMemcpyDeviceToHost));
     }
     dump(dir + "/back.bin", back.data(), back.size());
+    // the reference's dictionary API (include/cuda_zstd_dictionary.h:56-310, its manager's
+    // set/get/clear semantics src/cuda_zstd_manager.cu:3711-3868)
+    {
+      ZstdBatchManager dm(CompressionConfig::from_level(3));
+      dictionary::Dictionary got;
+      if (dm.get_dictionary(got) != Status::ERROR_INVALID_PARAMETER) { fprintf(stderr, "get_dictionary without one\n"); return 8; }
+      if (dm.set_dictionary(dct) != Status::SUCCESS) { fprintf(stderr, "set_dictionary\n"); return 8; }
+      if (dm.get_dictionary(got) != Status::SUCCESS || got.raw_size != db.size() || !got.raw_content ||
+          memcmp(got.raw_content, db.data(), db.size()) || got.raw_content == dct.raw_content) {
+        fprintf(stderr, "get_dictionary: not a deep copy of the content\n");
+        return 8;
+      }
+      dictionary::Dictionary cp = got;  // copy constructor: another malloc'd copy
+      if (!cp.raw_content || cp.raw_content == got.raw_content || memcmp(cp.raw_content, got.raw_content, got.raw_size)) return 8;
+      free(cp.raw_content);
+      free(got.raw_content);
+      if (dm.clear_dictionary() != Status::SUCCESS) return 8;
+      dictionary::Dictionary none;
+      if (dm.get_dictionary(none) != Status::ERROR_INVALID_PARAMETER) return 8;
+      dictionary::Dictionary bad;
+      bad.raw_content = (unsigned char *)db.data();
+      bad.raw_size = 100;  // below MIN_DICT_SIZE
+      if (dm.set_dictionary(bad) != Status::ERROR_INVALID_PARAMETER) { fprintf(stderr, "small dictionary accepted\n"); return 8; }
+      bad.raw_content = nullptr;
+      bad.raw_size = 4096;
+      if (dm.set_dictionary(bad) != Status::ERROR_INVALID_PARAMETER) return 8;
+      if (dictionary::get_optimal_dict_size(1000) != dictionary::MIN_DICT_SIZE || dictionary::get_optimal_dict_size(1u << 30) != dictionary::MAX_DICT_SIZE ||
+          dictionary::get_optimal_dict_size(1000000) != 10240 || !dictionary::is_valid_dictionary_size(4096) || dictionary::is_valid_dictionary_size(100)) {
+        fprintf(stderr, "dictionary size helpers\n");
+        return 8;
+      }
+      // training: the compat trainer (malloc'd content) and the buffer API over the inputs
+      std::vector<const void *> smp;
+      std::vector<size_t> ssz;
+      for (size_t i = 0; i < n; i++) { smp.push_back(in.data() + offs[i]); ssz.push_back(sizes[i]); }
+      dictionary::Dictionary tr;
+      Status st = dictionary::DictionaryTrainer::train_dictionary(smp, ssz, tr, 4096);
+      if (st != Status::SUCCESS || tr.raw_size != 4096 || !tr.raw_content) { fprintf(stderr, "DictionaryTrainer: %s\n", status_to_string(st)); return 8; }
+      std::vector<unsigned char> buf(4096);
+      if (dictionary::train_dictionary(smp, ssz, buf.data(), buf.size()) != Status::SUCCESS || memcmp(buf.data(), tr.raw_content, 4096)) return 8;
+      std::vector<size_t> so;
+      for (size_t i = 0; i < n; i++) so.push_back(offs[i]);
+      if (dictionary::create_dictionary_from_samples(in.data(), so.data(), n, buf.data(), 100) != Status::ERROR_INVALID_PARAMETER) return 8;
+      if (dm.set_dictionary(tr) != Status::SUCCESS) return 8;  // a trained dictionary is usable
+      dictionary::DictionaryManager::free_dictionary_gpu(tr);
+      if (tr.raw_content || tr.raw_size) return 8;
+    }
     // pre-sized workspace
     {
       CompressionConfig cfg = CompressionConfig::from_level(3);
@@ -378,7 +468,7 @@ int main(int argc, char **argv) {
         std::vector<char> g(sizes[i]);
         CK(hipMemcpy(g.data(), dop[i], sizes[i], hipMemcpyDeviceToHost));
         if (os[i] != sizes[i] || memcmp(hb[i].data(), in.data() + offs[i], sizes[i]) || rr[i].backend_used != ExecutionBackend::CPU_LIBZSTD ||
-            rr[i].output_size != sizes[i] || dos[i] != sizes[i] || memcmp(g.data(), in.data() + offs[i], sizes[i]) ||
+            rr[i].output_bytes != sizes[i] || rr[i].item_index != i || rr[i].input_bytes != is[i] || dr[i].output_bytes != sizes[i] || dos[i] != sizes[i] || memcmp(g.data(), in.data() + offs[i], sizes[i]) ||
             dr[i].backend_used != ExecutionBackend::GPU_KERNELS) {
           fprintf(stderr, "hybrid decompress_batch item %zu\n", i);
           return 7;

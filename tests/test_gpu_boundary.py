@@ -198,15 +198,95 @@ def test_cxx_extra_surface(tmp_path, libzstd, formatted):
         assert T.zstd_decompress(f, len(d), dictionary=dct) == d.tobytes()
 
 
-@pytest.mark.parametrize("formatted,flag", [(True, 0), (True, 1), (False, 1)])
+@pytest.mark.parametrize("formatted,flag", [(True, 1), (False, 1)])
 def test_streaming_history_second_manager(tmp_path, libzstd, formatted, flag):
     """Frames from compress_chunk_with_history (dictionary set) decode in a SECOND, decode-only
-    streaming manager with the same dictionary (advisor r3): a formatted dictionary's frames are
-    told from history frames by their Dictionary_ID; with a raw-content dictionary (ID 0 both ways)
-    the decoder is told by init_decompression_with_history."""
+    streaming manager with the same dictionary (advisor r3) once it is told the session has history
+    (init_decompression_with_history): history frames carry no Dictionary_ID, and neither does a
+    dictionary frame written without one (test_streaming_idless_dictionary_frames)."""
     recs = [T.gen(T.DG_JSON, 1, 0x5EED0005, 16384, first=i) for i in range(64)]
     dct = T.zdict_train(recs, 32768) if formatted else b"".join(r.tobytes() for r in recs[:2])
     datas = [T.gen(T.DG_JSON, 1, 0x5EED0005, n, first=300 + i) for i, n in enumerate([16384, 40000, 65536, 777, 30000])]
     (tmp_path / "dict.bin").write_bytes(dct)
     _run("stream_split", datas, tmp_path, str(flag))
+    assert (tmp_path / "back.bin").read_bytes() == b"".join(d.tobytes() for d in datas)
+
+
+@pytest.mark.parametrize("level", [3, 5])
+def test_static_batched_temp_size_levels(libzstd, level):
+    """nvcomp_zstd_batched_compress_get_temp_size_v5 (static) covers levels below 5
+    without a dictionary; at level 5 (the deep matcher's scratch slots) a workspace of that size
+    is refused with 7 before anything is launched, and the handle's own size
+    (nvcomp_zstd_batch_get_batched_temp_size_v5) works.  Frames equal the oracle's at that level."""
+    import torch
+
+    import cuda_zstd
+
+    L = cuda_zstd.lib()
+    datas = [T.gen(T.DG_MIX, 1, 0x5EED0003, 65536, first=i) for i in range(6)]
+    n, chunk = len(datas), 65536
+    c = cuda_zstd.BatchedCompressor(level, chunk)
+    static = L.nvcomp_zstd_batched_compress_get_temp_size_v5(n, chunk)
+    own = c.temp_size(n, chunk)
+    assert (own == static) if level < 5 else (own > static)
+    src = torch.from_numpy(np.concatenate(datas)).cuda()
+    cap = L.nvcomp_zstd_batch_get_max_compressed_chunk_size_v5(c._h, chunk)
+    out = torch.zeros(n * cap, dtype=torch.uint8, device="cuda")
+    ptrs = torch.tensor([src.data_ptr() + i * chunk for i in range(n)], dtype=torch.int64, device="cuda")
+    optr = torch.tensor([out.data_ptr() + i * cap for i in range(n)], dtype=torch.int64, device="cuda")
+    sizes = torch.full((n,), chunk, dtype=torch.int64, device="cuda")
+    osz = torch.zeros(n, dtype=torch.int64, device="cuda")
+    st = torch.zeros(n, dtype=torch.int32, device="cuda")
+    if level >= 5:
+        small = torch.zeros(static, dtype=torch.uint8, device="cuda")
+        with pytest.raises(cuda_zstd.ZstdError) as e:
+            c.compress_async(ptrs, sizes, chunk, optr, osz, st, small)
+        assert e.value.code == 7
+        assert int(osz.sum().item()) == 0  # nothing was launched
+    temp = torch.zeros(own, dtype=torch.uint8, device="cuda")
+    c.compress_async(ptrs, sizes, chunk, optr, osz, st, temp)
+    torch.cuda.synchronize()
+    o = out.cpu().numpy()
+    for i, d in enumerate(datas):
+        f = o[i * cap:i * cap + int(osz[i].item())].tobytes()
+        assert f == T.oracle_frame(d, level=level), f"item {i}"
+        assert T.zstd_decompress(f, len(d)) == d.tobytes()
+    c.close()
+
+
+def test_streaming_idless_dictionary_frames(tmp_path, libzstd):
+    """libzstd frames compressed with a formatted dictionary but without its ID in the
+    header (ZSTD_c_dictIDFlag = 0) decode, one after another, in a streaming manager with that
+    dictionary set and no history session -- each against the dictionary, not the previous output."""
+    import ctypes
+
+    z = libzstd
+    recs = [T.gen(T.DG_JSON, 1, 0x5EED0005, 16384, first=i) for i in range(64)]
+    dct = T.zdict_train(recs, 32768)
+    datas = [T.gen(T.DG_JSON, 1, 0x5EED0005, n, first=400 + i) for i, n in enumerate([16384, 9000, 30000, 16384])]
+    z.ZSTD_createCCtx.restype = ctypes.c_void_p
+    z.ZSTD_freeCCtx.argtypes = [ctypes.c_void_p]
+    z.ZSTD_CCtx_setParameter.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int]
+    z.ZSTD_CCtx_setParameter.restype = ctypes.c_size_t
+    z.ZSTD_CCtx_loadDictionary.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t]
+    z.ZSTD_CCtx_loadDictionary.restype = ctypes.c_size_t
+    z.ZSTD_compress2.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_size_t]
+    z.ZSTD_compress2.restype = ctypes.c_size_t
+    frames = []
+    db = np.frombuffer(dct, np.uint8).copy()
+    for d in datas:
+        cctx = z.ZSTD_createCCtx()
+        assert not z.ZSTD_isError(z.ZSTD_CCtx_setParameter(cctx, 100, 3))
+        assert not z.ZSTD_isError(z.ZSTD_CCtx_setParameter(cctx, 202, 0))  # ZSTD_c_dictIDFlag
+        assert not z.ZSTD_isError(z.ZSTD_CCtx_loadDictionary(cctx, db.ctypes.data, len(db)))
+        out = np.zeros(len(d) + 1024, np.uint8)
+        r = z.ZSTD_compress2(cctx, out.ctypes.data, len(out), d.ctypes.data, len(d))
+        z.ZSTD_freeCCtx(cctx)
+        assert not z.ZSTD_isError(r)
+        f = out[:r].copy()
+        assert f[4] & 3 == 0  # Frame_Header_Descriptor: no Dictionary_ID field
+        frames.append(f)
+    (tmp_path / "dict.bin").write_bytes(dct)
+    (tmp_path / "usizes.bin").write_bytes(np.array([len(d) for d in datas], np.uint64).tobytes())
+    _run("stream_ext", frames, tmp_path)
     assert (tmp_path / "back.bin").read_bytes() == b"".join(d.tobytes() for d in datas)

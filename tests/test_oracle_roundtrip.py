@@ -65,3 +65,80 @@ def test_lazy2_parse_roundtrip_and_gain(libzstd):
         l9 += len(f9)
         l3 += len(T.oracle_frame(c))
     assert l9 < l3
+
+
+def _prefixed(kind, pre, seed):
+    rng = np.random.default_rng(seed)
+    c = T.gen(T.KINDS[kind], 1, 200 + seed, 65536).copy()
+    c[:pre] = rng.integers(0, 256, pre, dtype=np.uint8)
+    return c
+
+
+@pytest.mark.parametrize("kind", ["text", "json", "mix"])
+def test_random_prefix_ratio_vs_libzstd(libzstd, kind):
+    """64 KiB chunks whose first 1-8 KiB are random (the incompressibility
+    probe used to leave them literal-only: JSON with a 2 KiB prefix 1.55 vs libzstd L3 5.39).  The
+    repeat scan resurrects them and the miss skip resumes at the first matching tiles: every chunk
+    within 5 % of libzstd level 3 (the GPU frames equal these, tests/test_gpu_probe.py)."""
+    for pre in (1024, 2048, 4096, 8192):
+        for i in range(2):
+            c = _prefixed(kind, pre, 31 * i + pre)
+            f = T.oracle_frame(c)
+            assert T.zstd_decompress(f, len(c)) == c.tobytes()
+            z = len(T.zstd_compress(c, 3))
+            assert len(f) * 0.95 <= z, (kind, pre, i, len(f), z)
+
+
+def test_repeat_scan_restatement():
+    """orc_repeat_scan against a direct Python statement of ZH_SCAN_* (include/zstd_hip_params.h)
+    on small buffers: random (no repeats), a copied stretch, a dictionary-like prefix."""
+    import ctypes
+    O = T.oracle()
+    O.orc_repeat_scan.restype = ctypes.c_uint32
+    O.orc_repeat_scan.argtypes = [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32]
+    m24 = lambda a, b: ((a & 0xFFFFFF) * (b & 0xFFFFFF)) & 0xFFFFFFFF
+
+    def ssum(v):
+        return (m24(v, 0x9E3779) + m24(v >> 24, 0x85EBCA) + m24(v >> 48, 0xC2B2AE)) & 0xFFFFFFFF
+
+    def py_scan(b, pre):
+        n = len(b)
+        lim = n - 8 if n > 8 else 0
+        E = {}
+        for q in range(0, lim, 4):
+            t = ssum(int.from_bytes(b[q:q + 8], "little"))
+            e = ((t << 14) & 0xFFFF0000) | q
+            s = t >> 18
+            E[s] = min(E.get(s, 0xFFFFFFFF), e)
+        c = 0
+        for p in range(pre, lim):
+            t = ssum(int.from_bytes(b[p:p + 8], "little"))
+            x = (E.get(t >> 18, 0xFFFFFFFF) - ((t << 14) & 0xFFFF0000)) & 0xFFFFFFFF
+            c += x < p
+        return c
+
+    rng = np.random.default_rng(3)
+    r = rng.integers(0, 256, 12000, dtype=np.uint8)
+    cp = r.copy()
+    cp[7000:9000] = cp[1001:3001]
+    txt = T.gen(T.DG_TEXT, 1, 9, 9000)
+    for b, pre in ((r, 0), (cp, 0), (cp, 5000), (txt, 0), (txt, 4321)):
+        b = np.ascontiguousarray(b)
+        assert O.orc_repeat_scan(b.ctypes.data, pre, len(b)) == py_scan(b.tobytes(), pre)
+    assert py_scan(r.tobytes(), 0) == 0 and py_scan(cp.tobytes(), 0) > 300
+
+
+def test_dictionary_unaligned_history_no_cliff(libzstd):
+    """one byte of dictionary size moved the probe window to a single block position and
+    made a 16 KiB JSON record with 4 random leading bytes 4.4x larger (10,071 vs 2,300 B)."""
+    rng = np.random.default_rng(23)
+    rec = T.gen(T.DG_JSON, 1, 0x5EED0105, 16384).copy()
+    rec[:4] = rng.integers(0, 256, 4, dtype=np.uint8)
+    content = T.gen(T.DG_JSON, 1, 0x5EED0106, 40000)
+    sizes = []
+    for dn in (32767, 32768):
+        dct = content[:dn].tobytes()
+        f = T.oracle_frame(rec, dictionary=dct)
+        assert T.zstd_decompress(f, len(rec), dictionary=dct) == rec.tobytes()
+        sizes.append(len(f))
+    assert max(sizes) <= 1.1 * min(sizes), sizes

@@ -58,13 +58,34 @@ def datagen():
     return _d
 
 
+# RTLD_DEEPBIND: the image's calls to its own exported functions bind inside that image.  A
+# process can hold two libzstd images -- this one (by path, 1.4.9) and the system's 1.4.8 in the
+# global scope when a preloaded tool links it (rocprofv3's libraries do) -- and without it the
+# library's PLT calls (ZSTD_freeCCtx's frees among them) resolved into the other image's 1.4.8
+# code and layouts: the r04f SIGSEGV in free <- ZSTD_freeCCtx under the profiler.
+LIBZSTD_MODE = os.RTLD_NOW | os.RTLD_LOCAL | getattr(os, "RTLD_DEEPBIND", 0)
+
+
 def find_libzstd():
     for p in ("/opt/conda/lib/libzstd.so.1", "libzstd.so.1", "/usr/lib/x86_64-linux-gnu/libzstd.so.1"):
         try:
-            return ctypes.CDLL(p)
+            return ctypes.CDLL(p, mode=LIBZSTD_MODE)
         except OSError:
             continue
     return None
+
+
+def libzstd_images():
+    """Paths of the libzstd images mapped into this process (/proc/self/maps)."""
+    out = []
+    try:
+        for line in open("/proc/self/maps"):
+            f = line.split()
+            if len(f) >= 6 and "libzstd" in f[5] and f[5] not in out:
+                out.append(f[5])
+    except OSError:
+        pass
+    return out
 
 
 def zstd():

@@ -14,6 +14,7 @@
 #define _GNU_SOURCE
 #include <dlfcn.h>
 #include <pthread.h>
+#include <sched.h>
 #include <stdatomic.h>
 #include <stddef.h>
 #include <stdint.h>
@@ -43,7 +44,7 @@ static int load(void) {
   if (Z.ok) return 0;
   const char *names[] = {"libzstd.so.1", "/opt/conda/lib/libzstd.so.1", "/usr/lib/x86_64-linux-gnu/libzstd.so.1", "libzstd.so"};
   for (unsigned i = 0; i < sizeof(names) / sizeof(names[0]); i++) {
-    void *h = dlopen(names[i], RTLD_NOW | RTLD_LOCAL);
+    void *h = dlopen(names[i], RTLD_NOW | RTLD_LOCAL | RTLD_DEEPBIND);  /* (one image, see tests/zh_testlib.py) */
     if (!h) continue;
     Z.create_c = (create_fn)dlsym(h, "ZSTD_createCCtx");
     Z.create_d = (create_fn)dlsym(h, "ZSTD_createDCtx");
@@ -109,8 +110,16 @@ static double now(void) {
 
 /* Returns 0 on success; secs[0..passes) = wall time of each pass, *out_bytes = bytes one
  * pass produced (compressed bytes for mode 0, decompressed bytes for mode 1). */
+/* cpus (optional, `threads` entries): thread t runs pinned to CPU cpus[t] (bench.py's SMT
+ * measurement: one core's two hardware threads against one thread alone). */
+int cpub_run_pinned(int mode, const uint8_t *data, const size_t *sizes, size_t nchunks, size_t chunk, size_t slot, int level, int threads,
+                    int passes, double *secs, size_t *out_bytes, const int *cpus);
 int cpub_run(int mode, const uint8_t *data, const size_t *sizes, size_t nchunks, size_t chunk, size_t slot, int level, int threads, int passes,
              double *secs, size_t *out_bytes) {
+  return cpub_run_pinned(mode, data, sizes, nchunks, chunk, slot, level, threads, passes, secs, out_bytes, NULL);
+}
+int cpub_run_pinned(int mode, const uint8_t *data, const size_t *sizes, size_t nchunks, size_t chunk, size_t slot, int level, int threads,
+                    int passes, double *secs, size_t *out_bytes, const int *cpus) {
   if (load() || threads < 1 || passes < 1 || (mode == 1 && !sizes)) return -1;
   pthread_t *th = (pthread_t *)calloc((size_t)threads, sizeof(pthread_t));
   if (!th) return -1;
@@ -127,8 +136,19 @@ int cpub_run(int mode, const uint8_t *data, const size_t *sizes, size_t nchunks,
     j.slot = slot;
     double const t0 = now();
     int started = 0;
-    for (int t = 0; t < threads; t++, started++)
-      if (pthread_create(&th[t], NULL, worker, &j)) { rc = -1; break; }
+    for (int t = 0; t < threads; t++, started++) {
+      pthread_attr_t at;
+      pthread_attr_init(&at);
+      if (cpus) {
+        cpu_set_t cs;
+        CPU_ZERO(&cs);
+        CPU_SET(cpus[t], &cs);
+        pthread_attr_setaffinity_np(&at, sizeof(cs), &cs);
+      }
+      int const e = pthread_create(&th[t], &at, worker, &j);
+      pthread_attr_destroy(&at);
+      if (e) { rc = -1; break; }
+    }
     for (int t = 0; t < started; t++) pthread_join(th[t], NULL);
     secs[p] = now() - t0;
     if (atomic_load(&j.err)) rc = -2;

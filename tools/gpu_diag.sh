@@ -37,10 +37,10 @@ for s in "$@"; do
     rstamps) timeout -k 10 200 python3 $R/tools/stamps.py random 4096 > $R/gpurun_out/${TAG}_rstamps.log 2>&1 ;;
     c5) C5_LEVEL=${C5_LEVEL:-9} timeout -k 10 300 python3 $R/tools/c5_dict.py > $R/gpurun_out/${TAG}_c5.json 2> $R/gpurun_out/${TAG}_c5.err; tail -c 400 $R/gpurun_out/${TAG}_c5.json ;;
     c5lds)
-      (cd /tmp && export TMPDIR=/tmp && C5_GPU_ONLY=1 C5_LEVEL=9 timeout -s KILL 200 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_INST_LDS SQ_ACTIVE_INST_LDS SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAIT_ANY SQ_INSTS_VALU GRBM_GUI_ACTIVE \
+      (cd /tmp && export TMPDIR=/tmp && C5_LEVEL=9 timeout -s KILL 200 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_INST_LDS SQ_ACTIVE_INST_LDS SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAIT_ANY SQ_INSTS_VALU GRBM_GUI_ACTIVE \
         --kernel-trace -d $R/gpurun_out/${TAG}_c5lds -o run --output-format csv -- python3 $R/tools/c5_dict.py > $R/gpurun_out/${TAG}_c5lds.log 2>&1) || { echo "c5lds failed"; exit 3; } ;;
     c5sq)
-      (cd /tmp && export TMPDIR=/tmp && C5_GPU_ONLY=1 C5_LEVEL=9 timeout -s KILL 200 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_ANY SQ_WAIT_INST_ANY GRBM_GUI_ACTIVE \
+      (cd /tmp && export TMPDIR=/tmp && C5_LEVEL=9 timeout -s KILL 200 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_ANY SQ_WAIT_INST_ANY GRBM_GUI_ACTIVE \
         --kernel-trace -d $R/gpurun_out/${TAG}_c5sq -o run --output-format csv -- python3 $R/tools/c5_dict.py > $R/gpurun_out/${TAG}_c5sq.log 2>&1) || { echo "c5sq failed"; exit 3; } ;;
     c5var)
       for v in B $VARIANTS; do
