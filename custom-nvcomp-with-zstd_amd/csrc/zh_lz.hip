@@ -219,22 +219,21 @@ __device__ __forceinline__ void insert_repair(u16 *T, u32 tb0, u32 lane, const u
 // slot verifies (insert_repair otherwise).  BT tiles are issued per LDS round trip together
 // with the next batch's input dwords and the workers' arrival counter.  Candidates
 // (position + 1, 0 = none) go to creg as u16 pairs.
-// Tiles [T0, NT) of the window (a window is inserted as tiles [0, NT) in one call, or -- a
-// miss-skip window whose first tiles found a match -- as [0, ZH_SKIP_TILES) and then the rest).
-// CHECK (a miss-skip window's single first batch): before the batch's between_tiles hook, on_check
-// gets whether any position of the batch has a candidate matching its first ZH_MIN_MATCH_LONG
-// (long table) / ZH_MIN_MATCH_SHORT (short) bytes -- the oracle's "a match among the searched
-// tiles" (orc_lz_parse_pre), which resumes the search of the whole window.
-template <bool LONG, u32 T0, u32 NT, bool CHECK, typename Hook, typename Check>
+// One instantiation per table serves every window (code size: K1's hot loops compete for the
+// instruction cache).  skip (a miss-skip window, orc_lz_parse_pre): after the first batch of
+// ZH_SKIP_TILES tiles, on_check gets whether any of its positions has a candidate matching its
+// first ZH_MIN_MATCH_LONG (long table) / ZH_MIN_MATCH_SHORT (short) bytes -- the oracle's "a match
+// among the searched tiles" -- and returns whether the window's search resumes; if not, the rest
+// of the window is neither looked up nor inserted and its candidates are never dumped.
+template <bool LONG, typename Hook, typename Check>
 __device__ __forceinline__ void insert_window(const u32 *in32, u16 *T, u32 wsb, u32 lim, u32 lane, u32 (&creg)[NCR], const u32 *arrivals,
-                                              Hook &&between_tiles, Check &&on_check, u32 pmin = 0) {
+                                              Hook &&between_tiles, Check &&on_check, bool skip, u32 pmin) {
   // positions below pmin are already in T (a dictionary's precomputed tables): treated like
-  // positions past lim (the junk slot, no candidate); tiles from NT on (a miss-skip window,
-  // orc_lz_parse_pre) are neither looked up nor inserted and their candidates never dumped
+  // positions past lim (the junk slot, no candidate)
   constexpr u32 JUNK = LONG ? HL_SIZE : HS_SIZE;
   constexpr u32 BT = 2;  // tiles per LDS round trip
-  static_assert(TILES % BT == 0 && ZH_SKIP_TILES % BT == 0 && T0 % BT == 0, "batches tile windows");
-  static_assert(!CHECK || (T0 == 0 && NT == BT), "the resume check covers the first batch only");
+  constexpr u32 T0 = 0, NT = TILES;
+  static_assert(TILES % BT == 0 && ZH_SKIP_TILES == BT, "batches tile windows; the resume check is the first batch");
   u32 wv[BT][TPL][3];
   auto load_in = [&](u32 tb0, u32 lim_t) {
 #pragma unroll
@@ -296,21 +295,25 @@ __device__ __forceinline__ void insert_window(const u32 *in32, u16 *T, u32 wsb, 
         // computation to the dump and keeps every tile's temporaries alive)
         __asm__ volatile("" : "+v"(creg[ri]) :: "memory");
       }
-    if constexpr (CHECK) {
+    if (t0 == 0 && skip) {
       bool v = false;
 #pragma unroll
       for (u32 b = 0; b < BT; b++)
 #pragma unroll
         for (u32 k = 0; k < TPL; k++) {
-          u32 const p = tb0 + b * ZH_TILE + 64 * k + lane, sh = min(p, lim_t) & 3u;
-          u32 const lo = __builtin_amdgcn_alignbyte(wv[b][k][1], wv[b][k][0], sh), hi = __builtin_amdgcn_alignbyte(wv[b][k][2], wv[b][k][1], sh);
+          // (the position's own bytes again from LDS: wv already holds the next batch's)
+          u32 const p = tb0 + b * ZH_TILE + 64 * k + lane;
           u32 const c = h[b][k] != JUNK ? e[b][k] : 0u;
-          u32 clo, chi;
+          u32 lo, hi, clo, chi;
+          ld64u(in32, min(p, lim_t), lo, hi);
           ld64u(in32, c ? c - 1u : 0u, clo, chi);
           u32 const dx = (lo ^ clo) | ((hi ^ chi) & (LONG ? ~0u : 0xFFu));
           v |= c != 0 && dx == 0;
         }
-      on_check(__ballot(v) != 0);
+      if (!on_check(__ballot(v) != 0)) {
+        between_tiles(arr);
+        break;
+      }
     }
     between_tiles(arr);
   }
@@ -330,7 +333,7 @@ __device__ __forceinline__ u32 lookahead(const u32 *in32, const u16 *T, u32 we, 
   return cwe;
 }
 struct NoCheck {
-  __device__ void operator()(bool) const {}
+  __device__ bool operator()(bool) const { return true; }
 };
 
 // Positions [s, e) into T in order (the latest position wins every slot), lookups discarded:
@@ -441,6 +444,13 @@ __device__ __forceinline__ void dump_window(u8 *ci8, u32 lane_, const u32 (&creg
   if (lane < 2) *(u16 *)(ci8 + 4 * cidx(ZH_WINDOW + lane) + (LONG ? 0 : 2)) = (u16)cwe;
 }
 
+// v_ffbl_b32 as the hardware computes it: the lowest set bit's index, 0xFFFFFFFF for 0 (ctz
+// builtins add a select for the zero case)
+__device__ __forceinline__ u32 ffbl_raw(u32 x) {
+  u32 r;
+  __asm__("v_ffbl_b32 %0, %1" : "=v"(r) : "v"(x));
+  return r;
+}
 // v from lane `src` (< 64) of the wave: ds_bpermute on a byte address, no lane-base math
 __device__ __forceinline__ u32 bperm(u32 v, u32 src) { return (u32)__builtin_amdgcn_ds_bpermute((int)(src << 2), (int)v); }
 __device__ __forceinline__ u32 ctz64(u64 v) { return (u32)__builtin_ctzll(v); }
@@ -531,8 +541,11 @@ __device__ __forceinline__ void span_lengths(const u32 *in32, u32 *ci, u64 *tm, 
     u32 const cw = hv ? cw0 : 0u;
     cwr[k] = cw;
     ld64u(in32, p, olo[k], ohi[k]);
-    u32 const cL = TWO ? cw & 0xFFFFu : 0u, cS = cw >> 16;
-    u32 const aL = (cL ? cL - 1u : 0u) >> 2, aS = (cS ? cS - 1u : 0u) >> 2;
+    // the candidates' positions (c - 1) mod 2^16, without a select: an empty candidate reads
+    // position 65535's bytes (inside the staging area and its pad), and its prefix is never used --
+    // a match needs a nonempty candidate, and no chain passes through an empty one (its successor
+    // would need candidate 0 + 1 to continue it ... from a candidate of -1)
+    u32 const aL = ((cw - 1u) & 0xFFFFu) >> 2, aS = ((cw >> 16) + 0xFFFFu) >> 2 & 0x3FFFu;
 #pragma unroll
     for (u32 t = 0; t < 3; t++) {
       if constexpr (TWO) Lw[k][t] = in32[aL + t];
@@ -549,11 +562,12 @@ __device__ __forceinline__ void span_lengths(const u32 *in32, u32 *ci, u64 *tm, 
     u32 const r = r_hi - 1 - k, i = 64 * r + lane;
     u32 const cw = cwr[k];
     u32 const cL = TWO ? cw & 0xFFFFu : 0u, cS = cw >> 16;
+    // common prefix (0..8) of the position's 8 bytes with the candidate's; for an empty candidate
+    // any value (see loadA): ctz64 of the difference as min(ffbl(x), min(ffbl(y), 32) + 32)
     auto pref = [&](u32 c, const u32 (&w)[3]) {
-      u32 const sh = (c ? c - 1u : 0u) & 3u;
+      u32 const sh = (c - 1u) & 3u;
       u32 const x = olo[k] ^ __builtin_amdgcn_alignbyte(w[1], w[0], sh), y = ohi[k] ^ __builtin_amdgcn_alignbyte(w[2], w[1], sh);
-      u32 const cx = __builtin_ctzg(x, 32), cy = __builtin_ctzg(y, 32);
-      return c ? (x ? cx : 32u + cy) >> 3 : 0u;
+      return min(ffbl_raw(x), min(ffbl_raw(y), 32u) + 32u) >> 3;
     };
     u32 const pL = TWO ? pref(cL, Lw[k]) : 0u, pS = pref(cS, Sw[k]);
     u32 cLn = wave_shl1(cL), cSn = wave_shl1(cS);
@@ -770,9 +784,9 @@ __device__ __forceinline__ bool inserter_loop(const u32 *in32, u16 *T, u8 *ci8, 
                                               u32 pmin, u32 span_s, u32 span_e, u32 kskip0, u32 kprobe, u32 e0p) {
   u32 creg[NCR];
   if (span_s < span_e) insert_span<LONG>(in32, T, span_s, span_e, lane);
-  u32 const we0 = min(wstart + (u32)ZH_WINDOW, n);
-  insert_window<LONG, 0, TILES, false>(in32, T, wstart, lim, lane, creg, &misc_[MISC_ARR], [](u32) {}, NoCheck{}, pmin);
-  u32 cwe = lookahead<LONG>(in32, T, we0, lim, lane);
+  // (the first window: its own instantiation, with pmin and no barriers to take)
+  insert_window<LONG>(in32, T, wstart, lim, lane, creg, &misc_[MISC_ARR], [](u32) {}, NoCheck{}, false, pmin);
+  u32 cwe = lookahead<LONG>(in32, T, min(wstart + (u32)ZH_WINDOW, n), lim, lane);
   bool skipc = false;  // the window whose candidates creg holds is a miss-skip window (not resumed)
 #ifdef ZH_STAMPS
   u32 st_ins = 0;
@@ -804,27 +818,18 @@ __device__ __forceinline__ bool inserter_loop(const u32 *in32, u16 *T, u8 *ci8, 
     u32 const nx = wsb + ZH_WINDOW;
     // window k + 1: the parse of window k - 2 ended in step k - 1 (before this step's P)
     skipc = skip_window(misc_, k + 1, kskip0);
-    // (a second, short instantiation for miss-skip windows: a runtime tile bound in the full one
-    // costs its unrolled batches more than the extra code does)
     if (k + 1 < nwin) {
 #ifdef ZH_NO_RESUME
-      if (skipc) {
-        insert_window<LONG, 0, ZH_SKIP_TILES, false>(in32, T, nx, lim, lane, creg, &misc_[MISC_ARR], take_ready, NoCheck{});
-      } else
+      bool const resumed = false;
+      insert_window<LONG>(in32, T, nx, lim, lane, creg, &misc_[MISC_ARR], take_ready, [](bool) { return false; }, skipc, 0u);
+#else
+      // a miss-skip window's first tiles, then the rest of it if any of them found a match (both
+      // inserters' checks combined before either takes a barrier)
+      bool resumed = false;
+      insert_window<LONG>(in32, T, nx, lim, lane, creg, &misc_[MISC_ARR], take_ready,
+                          [&](bool h) { return resumed = resume_exchange<LONG, TWO>(misc_, k + 1, h, lane); }, skipc, 0u);
 #endif
-      if (skipc) {
-        // the first tiles, then the rest of the window if any of them found a match (both
-        // inserters' checks combined before either takes a barrier)
-        bool hit = false;
-        insert_window<LONG, 0, ZH_SKIP_TILES, true>(in32, T, nx, lim, lane, creg, &misc_[MISC_ARR], take_ready,
-                                                    [&](bool h) { hit = resume_exchange<LONG, TWO>(misc_, k + 1, h, lane); });
-        if (hit) {
-          insert_window<LONG, ZH_SKIP_TILES, TILES, false>(in32, T, nx, lim, lane, creg, &misc_[MISC_ARR], take_ready, NoCheck{});
-          skipc = false;
-        }
-      } else {
-        insert_window<LONG, 0, TILES, false>(in32, T, nx, lim, lane, creg, &misc_[MISC_ARR], take_ready, NoCheck{});
-      }
+      if (resumed) skipc = false;
       cwe = lookahead<LONG>(in32, T, min(nx + ZH_WINDOW, n), lim, lane);
     }
 #ifdef ZH_STAMPS
@@ -949,46 +954,36 @@ __device__ __forceinline__ bool repeat_scan(const u32 *in32, u32 *E, u32 *misc, 
     }
   }
   __syncthreads();
-  // every block position p in [pre, lim) counts when E[slot] - key < p.  Groups of four
-  // positions (dwords j .. j + 2), two groups per lane in flight; only the first and last group
-  // of the range need the bounds (the others are checked by the unsigned range test alone)
+  // the sampled block positions p = pre + ZH_SCAN_STEP m < lim count when E[slot] - key < p; four
+  // per lane in flight (positions past lim load clamped bytes and are not counted)
+  static_assert(ZH_SCAN_STEP == 3, "strides coprime");
   u32 c = 0;
-  u32 const g0 = pre >> 2, g1 = (lim + 3) >> 2, span = lim > pre ? lim - pre : 0u;
-  for (u32 j0 = g0 + tid; j0 < g1; j0 += 2 * K1_THREADS) {
-    u32 w[2][3];
+  u32 const span = lim > pre ? lim - pre : 0u, nm = (span + ZH_SCAN_STEP - 1) / ZH_SCAN_STEP;
+  for (u32 m0 = tid; m0 < nm; m0 += 4 * K1_THREADS) {
+    u32 w[4][3], pp[4];
 #pragma unroll
-    for (u32 u = 0; u < 2; u++) {
-      u32 const j = min(j0 + u * K1_THREADS, g1 - 1u);
+    for (u32 u = 0; u < 4; u++) {
+      pp[u] = pre + ZH_SCAN_STEP * min(m0 + u * K1_THREADS, nm - 1u);
+      u32 const j = pp[u] >> 2;
       w[u][0] = in32[j];
       w[u][1] = in32[j + 1];
       w[u][2] = in32[j + 2];
     }
-    u32 t[2][4], e[2][4];
+    u32 t[4], e[4];
 #pragma unroll
-    for (u32 u = 0; u < 2; u++)
-#pragma unroll
-      for (u32 r = 0; r < 4; r++) {
-        u32 const lo = r ? __builtin_amdgcn_alignbyte(w[u][1], w[u][0], r) : w[u][0];
-        u32 const hi = r ? __builtin_amdgcn_alignbyte(w[u][2], w[u][1], r) : w[u][1];
-        t[u][r] = hash_long_sum(lo, hi);
-        e[u][r] = *slot(t[u][r]);
-      }
-#pragma unroll
-    for (u32 u = 0; u < 2; u++) {
-      u32 const j = j0 + u * K1_THREADS;
-#pragma unroll
-      for (u32 r = 0; r < 4; r++) {
-        u32 const p = 4 * j + r;
-        c += (e[u][r] - key(t[u][r]) < p && p - pre < span) ? 1u : 0u;
-      }
+    for (u32 u = 0; u < 4; u++) {
+      u32 const sh = pp[u] & 3u;
+      t[u] = hash_long_sum(__builtin_amdgcn_alignbyte(w[u][1], w[u][0], sh), __builtin_amdgcn_alignbyte(w[u][2], w[u][1], sh));
+      e[u] = *slot(t[u]);
     }
+#pragma unroll
+    for (u32 u = 0; u < 4; u++) c += (m0 + u * K1_THREADS < nm && e[u] - key(t[u]) < pp[u]) ? 1u : 0u;
   }
   u32 const wsum = lane_value(wave_scan_incl(c), 63);
   if ((tid & 63) == 0 && wsum) atomicAdd(&misc[MISC_SCAN], wsum);
   __syncthreads();
   u32 const total = (u32)__builtin_amdgcn_readfirstlane(__atomic_load_n(&misc[MISC_SCAN], __ATOMIC_RELAXED));
-  u32 const need = span >> ZH_SCAN_SHIFT;
-  return total >= max(need, (u32)ZH_SCAN_MIN);
+  return total >= max(span >> ZH_SCAN_SHIFT, (u32)ZH_SCAN_MIN);
 }
 
 template <u32 MODE>
@@ -1490,7 +1485,10 @@ __device__ __forceinline__ void lz_blocks(const ZhBlockDesc *__restrict__ blocks
   prefetch_block(blocks, b, nblocks, k1_tid(wv), pf);
   bool redo = false;
   while (b < nblocks) {
-    u32 const r = lz_block<MODE>(blocks, ws, b, nblocks, &s_take, pf, wv, redo);  // the next block taken, or K1_REDO
+    // the next block taken, or K1_REDO (the same in every wave; readfirstlane keeps it -- and the
+    // block index and descriptor fields derived from it -- in SGPRs: the function's return paths
+    // join under the inserter / worker split, which the compiler takes for divergence)
+    u32 const r = (u32)__builtin_amdgcn_readfirstlane(lz_block<MODE>(blocks, ws, b, nblocks, &s_take, pf, wv, redo));
     __syncthreads();  // every wave is done with this block's LDS before the next is staged
     redo = r == K1_REDO;
     b = redo ? b : r;

@@ -39,13 +39,15 @@
 /* Repeat scan: a block the probe finds no match in is all literals only when this whole-block
  * test also finds (almost) no repeated 8-byte string.  Positions q = 0 mod ZH_SCAN_STRIDE of the
  * staged buffer (history included) are entered into a 2^ZH_SCAN_LOG-slot table keyed by the long
- * hash's top bits, each slot keeping the minimum of (16 more bits of the hash) << 16 | q; a block
- * position p counts when its slot's entry carries p's 16 bits and a position below p.  The block is
- * resurrected (parsed in full, no probe) when at least max(ZH_SCAN_MIN, block positions >>
- * ZH_SCAN_SHIFT) positions count. */
+ * hash's top bits, each slot keeping the minimum of (16 more bits of the hash) << 16 | q; the block
+ * positions p = pre + ZH_SCAN_STEP m are looked up, and p counts when its slot's entry carries p's
+ * 16 bits and a position below p.  With the strides coprime, every repeat of at least 8 +
+ * ZH_SCAN_STRIDE x ZH_SCAN_STEP bytes has a sampled pair.  The block is resurrected (parsed in full,
+ * no probe) when at least max(ZH_SCAN_MIN, block positions >> ZH_SCAN_SHIFT) positions count. */
 #define ZH_SCAN_LOG 14
 #define ZH_SCAN_STRIDE 4
-#define ZH_SCAN_SHIFT 10
+#define ZH_SCAN_STEP 3
+#define ZH_SCAN_SHIFT 12
 #define ZH_SCAN_MIN 8
 #define ZH_HASH_LOG_LONG 14         /* 8-byte hash table: 2^14 u16 entries */
 #define ZH_HASH_LOG_SHORT 14        /* 5-byte hash table: 2^14 u16 entries */

@@ -932,7 +932,7 @@ size_t orc_lz_parse_deep(const u8 *buf, u32 pre, u32 n, u32 depth, orc_seq_t *se
  * catch-up) searches and inserts only its first ZH_SKIP_TILES tiles; the rest of it has no
  * candidates.  Windows up to three past the one holding `pre` never skip. */
 /* Repeat scan (ZH_SCAN_*, include/zstd_hip_params.h; K1 zh_lz.hip repeat_scan): the number of
- * block positions p in [pre, lim) whose 8 bytes repeat an earlier sampled position, as seen
+ * sampled block positions p = pre + ZH_SCAN_STEP m < lim whose 8 bytes repeat an earlier sampled position, as seen
  * through a 2^ZH_SCAN_LOG-slot table of min(sig16 << 16 | q) over q = 0 mod ZH_SCAN_STRIDE in
  * [0, lim) -- slot and sig16 from the long hash's sum (top 14 bits, the 16 below them). */
 static inline u32 scan_sum(u64 v) {
@@ -947,7 +947,7 @@ u32 orc_repeat_scan(const u8 *src, u32 pre, u32 n) {
     if (e < E[s]) E[s] = e;
   }
   u32 c = 0;
-  for (u32 p = pre; p < lim; p++) {
+  for (u32 p = pre; p < lim; p += ZH_SCAN_STEP) {
     u32 const t = scan_sum(rd64(src + p)), s = t >> (32 - ZH_SCAN_LOG);
     c += E[s] - ((t << ZH_SCAN_LOG) & 0xFFFF0000u) < p;
   }

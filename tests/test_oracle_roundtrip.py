@@ -111,7 +111,7 @@ def test_repeat_scan_restatement():
             s = t >> 18
             E[s] = min(E.get(s, 0xFFFFFFFF), e)
         c = 0
-        for p in range(pre, lim):
+        for p in range(pre, lim, 3):
             t = ssum(int.from_bytes(b[p:p + 8], "little"))
             x = (E.get(t >> 18, 0xFFFFFFFF) - ((t << 14) & 0xFFFF0000)) & 0xFFFFFFFF
             c += x < p
@@ -125,7 +125,7 @@ def test_repeat_scan_restatement():
     for b, pre in ((r, 0), (cp, 0), (cp, 5000), (txt, 0), (txt, 4321)):
         b = np.ascontiguousarray(b)
         assert O.orc_repeat_scan(b.ctypes.data, pre, len(b)) == py_scan(b.tobytes(), pre)
-    assert py_scan(r.tobytes(), 0) == 0 and py_scan(cp.tobytes(), 0) > 300
+    assert py_scan(r.tobytes(), 0) == 0 and py_scan(cp.tobytes(), 0) > 100
 
 
 def test_dictionary_unaligned_history_no_cliff(libzstd):
