@@ -108,6 +108,14 @@ static_assert(K1_LDS <= 163840 - 256, "K1 LDS budget");
 static_assert(OFF_TL % 16 == 0 && OFF_CI % 16 == 0 && OFF_HM % 16 == 0 && OFF_MISC % 4 == 0, "alignment");
 
 
+// v_ffbl_b32 as the hardware computes it: the lowest set bit's index, 0xFFFFFFFF for 0 (ctz
+// builtins add a select for the zero case)
+__device__ __forceinline__ u32 ffbl_raw(u32 x) {
+  u32 r;
+  __asm__("v_ffbl_b32 %0, %1" : "=v"(r) : "v"(x));
+  return r;
+}
+
 // 8 bytes at p from LDS as (lo, hi): three aligned dwords + v_alignbyte
 __device__ __forceinline__ void ld64u(const u32 *in32, u32 p, u32 &lo, u32 &hi) {
   u32 const w = p >> 2, sh = p & 3;
@@ -143,13 +151,17 @@ __device__ __forceinline__ u32 ext8(const u32 *in32, u32 p, u32 c, bool act) {
     u32 A[H + 1], B[H + 1];
 #pragma unroll
     for (u32 k = 0; k <= H; k++) { A[k] = in32[wp + k0 + k]; B[k] = in32[wq + k0 + k]; }
-    u32 lh = ZH_MAX_MATCH;
+    // the step's first differing bit: min over its dwords of ffbl(x) | 32 k (ffbl < 32 leaves the
+    // dword's bits free; an equal dword's ffbl is 0xFFFFFFFF and stays above every difference)
+    u32 const HK = NW - k0 < H ? NW - k0 : H;  // dwords compared in this step (constant once unrolled)
+    u32 m = ~0u;
 #pragma unroll
-    for (int k = (int)H - 1; k >= 0; k--) {
-      if (k0 + (u32)k >= NW) continue;
+    for (u32 k = 0; k < H; k++) {
+      if (k >= HK) continue;
       u32 const x = __builtin_amdgcn_alignbyte(A[k + 1], A[k], sp) ^ __builtin_amdgcn_alignbyte(B[k + 1], B[k], sq);
-      if (x) lh = 4 * (k0 + (u32)k) + (__builtin_ctz(x) >> 3);
+      m = min(m, ffbl_raw(x) | 32u * k);
     }
+    u32 const lh = m >= 32u * HK ? (u32)ZH_MAX_MATCH : 4u * k0 + (m >> 3);
     l = l == ZH_MAX_MATCH ? lh : l;
   }
   return l;
@@ -444,13 +456,6 @@ __device__ __forceinline__ void dump_window(u8 *ci8, u32 lane_, const u32 (&creg
   if (lane < 2) *(u16 *)(ci8 + 4 * cidx(ZH_WINDOW + lane) + (LONG ? 0 : 2)) = (u16)cwe;
 }
 
-// v_ffbl_b32 as the hardware computes it: the lowest set bit's index, 0xFFFFFFFF for 0 (ctz
-// builtins add a select for the zero case)
-__device__ __forceinline__ u32 ffbl_raw(u32 x) {
-  u32 r;
-  __asm__("v_ffbl_b32 %0, %1" : "=v"(r) : "v"(x));
-  return r;
-}
 // v from lane `src` (< 64) of the wave: ds_bpermute on a byte address, no lane-base math
 __device__ __forceinline__ u32 bperm(u32 v, u32 src) { return (u32)__builtin_amdgcn_ds_bpermute((int)(src << 2), (int)v); }
 __device__ __forceinline__ u32 ctz64(u64 v) { return (u32)__builtin_ctzll(v); }
