@@ -95,7 +95,7 @@ enum : u32 {
 // histogram as ZH_K1_HIST_WAVES 256-bin u32 sub-histograms at lits + ZH_K1_HIST_OFF
 #define ZH_META_K1HIST 2u
 #define ZH_K1_HIST_OFF 65536u
-#define ZH_K1_HIST_WAVES 14u
+#define ZH_K1_HIST_WAVES 16u
 static_assert(ZH_K1_HIST_OFF + ZH_K1_HIST_WAVES * 1024u <= ZH_LIT_BYTES, "K1 sub-histograms fit the literal area");
 
 struct ZhWorkspace {

@@ -928,64 +928,78 @@ __device__ __forceinline__ u32 k1_tid(u32 w) {
 
 // Repeat scan (ZH_SCAN_*, oracle orc_repeat_scan), all 1024 threads, after the probe found no
 // match: the hash tables' 64 KiB hold 2^ZH_SCAN_LOG u32 slots; positions q = 0 mod 4 below lim
-// enter min(sig16 << 16 | q) into the slot of their long hash (ds_min), then every block position
-// p counts when its slot holds its own sig16 with a position below p.  True: the block has enough
-// repeated 8-byte strings to be parsed after all.
-__device__ __forceinline__ bool repeat_scan(const u32 *in32, u32 *E, u32 *misc, u32 pre, u32 n, u32 tid) {
+// enter min(sig16 << 16 | q) into the slot of their long hash (ds_min), then every sampled block
+// position p counts when its slot holds its own sig16 with a position below p.  True: the block
+// has enough repeated 8-byte strings to be parsed after all.  The insert pass reads every dword
+// of the staging buffer once, so it also counts the block's bytes [pre, n) into one 256-bin
+// sub-histogram per wave at hw (16 x 256 u32): the literal histogram K2 needs when the block
+// stays literal-only.
+__device__ __forceinline__ bool repeat_scan(const u32 *in32, u32 *E, u32 *hw, u32 *misc, u32 pre, u32 n, u32 tid) {
   static_assert(ZH_SCAN_STRIDE == 4 && (4u << ZH_SCAN_LOG) <= 2 * (HL_SIZE + HS_SIZE + 2 * T_PAD), "scan table in the hash tables' space");
+  static_assert(K1_THREADS / 64 == ZH_K1_HIST_WAVES && 4 * 256 * ZH_K1_HIST_WAVES <= 2 * 4 * CI_WORDS, "sub-histograms in the cinfo space");
   constexpr u32 NS = 1u << ZH_SCAN_LOG;
-  u32 const lim = n > ZH_HASH_READ ? n - ZH_HASH_READ : 0u;
+  u32 const lim = n > ZH_HASH_READ ? n - ZH_HASH_READ : 0u, lane = tid & 63u, wave = tid >> 6;
   // slot and signature of a position's long-hash sum t: E[t >> 18], entry (t << 14) & ~0xFFFF | q
   auto slot = [&](u32 t) -> u32 * { return E + (t >> (32 - ZH_SCAN_LOG)); };
   auto key = [](u32 t) { return (t << ZH_SCAN_LOG) & 0xFFFF0000u; };
   for (u32 i = tid; i < NS / 4; i += K1_THREADS) ((uint4 *)E)[i] = make_uint4(~0u, ~0u, ~0u, ~0u);
+  ((uint4 *)hw)[tid] = make_uint4(0u, 0u, 0u, 0u);
   if (tid == 0) misc[MISC_SCAN] = 0;
   __syncthreads();
-  // positions q = 4j < lim: the 8 bytes at q are dwords j, j + 1; four per lane in flight
-  u32 const nq = (lim + 3) >> 2;
-  for (u32 j0 = tid; j0 < nq; j0 += 4 * K1_THREADS) {
-    u32 w[4][2];
+  // insert pass: a wave takes 256 consecutive dwords (4 per lane, 64 apart); the 8 bytes at q = 4j
+  // are dwords j and j + 1, the latter the next lane's (DPP), lane 63's from the next row
+  u32 *const hwv = hw + 256u * wave;
+  u32 const nq = (lim + 3) >> 2, nd = (n + 3) >> 2;
+  for (u32 base = 256u * wave; base < nd; base += 256u * (K1_THREADS / 64)) {
+    u32 w[5];
+#pragma unroll
+    for (u32 u = 0; u < 4; u++) w[u] = in32[base + 64u * u + lane];
+    w[4] = in32[base + 256u];  // (the buffer's zero pad at most)
 #pragma unroll
     for (u32 u = 0; u < 4; u++) {
-      u32 const j = min(j0 + u * K1_THREADS, nq - 1u);
-      w[u][0] = in32[j];
-      w[u][1] = in32[j + 1];
-    }
+      u32 const j = base + 64u * u + lane;
+      u32 const nx = u < 3 ? (u32)__builtin_amdgcn_readlane((int)w[u < 3 ? u + 1 : 0], 0) : w[4];
+      u32 const t = hash_long_sum(w[u], lane == 63u ? nx : wave_shl1(w[u]));
+      if (j < nq) atomicMin(slot(t), key(t) | (4u * j));
+      u32 const b0 = 4u * j;
+      if (b0 >= pre && b0 + 4u <= n) {
 #pragma unroll
-    for (u32 u = 0; u < 4; u++) {
-      u32 const j = j0 + u * K1_THREADS;
-      u32 const t = hash_long_sum(w[u][0], w[u][1]);
-      if (j < nq) atomicMin(slot(t), key(t) | (4 * j));
+        for (u32 i = 0; i < 4; i++) atomicAdd(&hwv[(w[u] >> (8 * i)) & 255u], 1u);
+      } else {
+#pragma unroll
+        for (u32 i = 0; i < 4; i++)
+          if (b0 + i >= pre && b0 + i < n) atomicAdd(&hwv[(w[u] >> (8 * i)) & 255u], 1u);
+      }
     }
   }
   __syncthreads();
-  // the sampled block positions p = pre + ZH_SCAN_STEP m < lim count when E[slot] - key < p; four
-  // per lane in flight (positions past lim load clamped bytes and are not counted)
-  static_assert(ZH_SCAN_STEP == 3, "strides coprime");
+  // lookup pass: the sampled block positions p = pre + ZH_SCAN_STEP m < lim count when
+  // E[slot] - key < p; a lane takes 4 consecutive samples (12 bytes apart between lanes: one
+  // shift for all, 6 dword loads for the 4, lanes 3 dwords apart hit distinct banks)
+  static_assert(ZH_SCAN_STEP == 3, "strides coprime; 4 samples are 12 bytes");
   u32 c = 0;
-  u32 const span = lim > pre ? lim - pre : 0u, nm = (span + ZH_SCAN_STEP - 1) / ZH_SCAN_STEP;
-  for (u32 m0 = tid; m0 < nm; m0 += 4 * K1_THREADS) {
-    u32 w[4][3], pp[4];
+  u32 const span = lim > pre ? lim - pre : 0u, nm = (span + ZH_SCAN_STEP - 1) / ZH_SCAN_STEP, sh = pre & 3u;
+  for (u32 g = tid; 4u * g < nm; g += K1_THREADS) {
+    u32 const p0 = pre + 12u * g, j0 = p0 >> 2;  // (a last group's unused samples may read past
+                                                 // the staging pad into the table: never counted)
+    u32 w[6], v[5];
 #pragma unroll
-    for (u32 u = 0; u < 4; u++) {
-      pp[u] = pre + ZH_SCAN_STEP * min(m0 + u * K1_THREADS, nm - 1u);
-      u32 const j = pp[u] >> 2;
-      w[u][0] = in32[j];
-      w[u][1] = in32[j + 1];
-      w[u][2] = in32[j + 2];
-    }
+    for (u32 k = 0; k < 6; k++) w[k] = in32[j0 + k];
+#pragma unroll
+    for (u32 k = 0; k < 5; k++) v[k] = __builtin_amdgcn_alignbyte(w[k + 1], w[k], sh);
+    u32 const lo[4] = {v[0], __builtin_amdgcn_alignbyte(v[1], v[0], 3), __builtin_amdgcn_alignbyte(v[2], v[1], 2), __builtin_amdgcn_alignbyte(v[3], v[2], 1)};
+    u32 const hi[4] = {v[1], __builtin_amdgcn_alignbyte(v[2], v[1], 3), __builtin_amdgcn_alignbyte(v[3], v[2], 2), __builtin_amdgcn_alignbyte(v[4], v[3], 1)};
     u32 t[4], e[4];
 #pragma unroll
     for (u32 u = 0; u < 4; u++) {
-      u32 const sh = pp[u] & 3u;
-      t[u] = hash_long_sum(__builtin_amdgcn_alignbyte(w[u][1], w[u][0], sh), __builtin_amdgcn_alignbyte(w[u][2], w[u][1], sh));
+      t[u] = hash_long_sum(lo[u], hi[u]);
       e[u] = *slot(t[u]);
     }
 #pragma unroll
-    for (u32 u = 0; u < 4; u++) c += (m0 + u * K1_THREADS < nm && e[u] - key(t[u]) < pp[u]) ? 1u : 0u;
+    for (u32 u = 0; u < 4; u++) c += (4u * g + u < nm && e[u] - key(t[u]) < p0 + 3u * u) ? 1u : 0u;
   }
   u32 const wsum = lane_value(wave_scan_incl(c), 63);
-  if ((tid & 63) == 0 && wsum) atomicAdd(&misc[MISC_SCAN], wsum);
+  if (lane == 0 && wsum) atomicAdd(&misc[MISC_SCAN], wsum);
   __syncthreads();
   u32 const total = (u32)__builtin_amdgcn_readfirstlane(__atomic_load_n(&misc[MISC_SCAN], __ATOMIC_RELAXED));
   return total >= max(span >> ZH_SCAN_SHIFT, (u32)ZH_SCAN_MIN);
@@ -1400,45 +1414,24 @@ __device__ __forceinline__ u32 lz_block(const ZhBlockDesc *__restrict__ blocks, 
   // The probe ended the window loop (every wave left it at the same step): the repeat scan
   // decides between the literal-only block and redoing the block from its staging without the
   // probe (the oracle's parse simply goes on; lz_blocks calls lz_block again with `redo`).
+  u32 *const hw = (u32 *)(smem + OFF_CI);  // the scan's per-wave literal sub-histograms
 #ifdef ZH_NO_SCAN
   if (false) return K1_REDO;  // (A/B variant: the probe alone decides, as in round 4)
 #else
-  if (repeat_scan(in32, (u32 *)TL, misc, pre, n, tid)) return K1_REDO;
+  if (repeat_scan(in32, (u32 *)TL, hw, misc, pre, n, tid)) return K1_REDO;
 #endif
   ZH_STAMP(st_E1);
-  if (tid >= INS_TID) return next_b;
   u32 const wave = tid >> 6;
   u32 bo;  // (opaque: the block's workspace offset is not kept live across the window loop)
   __asm__ volatile("s_mov_b32 %0, %1" : "=s"(bo) : "s"((u32)__builtin_amdgcn_readfirstlane(b)));
   u8 *const lit_out = ws.lits(bo);
   if ((((uintptr_t)d.src) & 15) == 0) {
     // no sequences, the whole block is literals, and they are the block's own bytes -- K2 reads
-    // them from the source (16-B aligned).  K1 leaves K2 the literal histogram instead: one
-    // 256-bin sub-histogram per worker wave, counted in LDS (the hash tables are dead) and stored
-    // after the first 64 KiB of the literal area (ZH_K1_HIST_OFF).
-    u32 *const hw = (u32 *)(smem + OFF_TL) + 256u * wave;
-    for (u32 i = lane; i < 256; i += 64) hw[i] = 0;
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    u32 const per = (((d.n + NWW - 1) / NWW) + 63) & ~63u;  // this wave's bytes: [per * wave, + per)
-    u32 const a = per * wave, e = min(a + per, d.n);
-    if (((pre + a) & 15u) == 0) {
-      // 16 bytes per lane per load, their 16 atomics issued back to back
-      for (u32 i = a + 16u * lane; i < e; i += 1024u) {
-        uint4 const v = *(const uint4 *)(in + pre + i);
-        u32 const cnt = min(16u, e - i);
-        u32 const w4[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-        for (u32 k = 0; k < 16; k++)
-          if (k < cnt) atomicAdd(&hw[(w4[k >> 2] >> (8 * (k & 3))) & 255u], 1u);
-      }
-    } else {
-      for (u32 i = a + lane; i < e; i += 64) atomicAdd(&hw[in[pre + i]], 1u);
-    }
-    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-    __builtin_amdgcn_wave_barrier();
+    // them from the source (16-B aligned).  K1 leaves K2 the literal histogram instead: the
+    // scan's 16 per-wave sub-histograms, stored after the first 64 KiB of the literal area
+    // (ZH_K1_HIST_OFF).
     u32 *const gh = (u32 *)(lit_out + ZH_K1_HIST_OFF) + 256u * wave;
-    for (u32 i = lane; i < 256; i += 64) gh[i] = hw[i];
+    for (u32 i = lane; i < 256; i += 64) gh[i] = hw[256u * wave + i];
     if (tid == 0) {
       u32 two;  // (opaque: a constant {0, n, 2} vector would be hoisted out of the block loop and spilled)
       __asm__ volatile("v_mov_b32 %0, 2" : "=v"(two));
@@ -1454,6 +1447,7 @@ __device__ __forceinline__ u32 lz_block(const ZhBlockDesc *__restrict__ blocks, 
 #endif
     return next_b;
   }
+  if (tid >= INS_TID) return next_b;
   // (unaligned source) the block's bytes go out of LDS to the literal area in 16-B stores
   u32 const nv = (d.n + 15) >> 4, sh = pre & 3;
   const u32 *const src32 = in32 + (pre >> 2);

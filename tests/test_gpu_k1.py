@@ -48,7 +48,7 @@ def k1_raw(datas):
         r = recs[i * SEQ_CAP:i * SEQ_CAP + ns]
         area = lits[i * LIT_AREA:(i + 1) * LIT_AREA]
         if rle == K1HIST:  # literals = the block itself; K1's sub-histograms after the first 64 KiB
-            out.append((r, area[K1_HIST_OFF:K1_HIST_OFF + 14 * 1024].view(np.uint32).reshape(14, 256).sum(0), rle))
+            out.append((r, area[K1_HIST_OFF:K1_HIST_OFF + 16 * 1024].view(np.uint32).reshape(16, 256).sum(0), rle))
         else:
             out.append((r, area[:nl].tobytes(), rle))
     k1_raw.area = lits
