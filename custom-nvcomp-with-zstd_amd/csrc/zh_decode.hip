@@ -1288,7 +1288,10 @@ extern "C" __global__ __launch_bounds__(DEC_THREADS) void zh_dec_exec_kernel(ZhD
 // ~180 dependent instructions a step.  Measured alternatives (profiles/r02m_dec_seq.json):
 // 4-32 buffers per wave with the tables staged in LDS (32- or 16-bit entries) were slower,
 // both isolated and pipelined -- LDS-limited occupancy, no shorter chain.
-constexpr u32 D2_BUF = 64;
+#ifndef ZH_D2_BUF
+#define ZH_D2_BUF 64
+#endif
+constexpr u32 D2_BUF = ZH_D2_BUF;
 // Decoded sequences go to an LDS ring and leave in 256-byte bursts every D2_RUN steps:
 // CDNA's vmcnt counts stores too and retires in order, so a per-step global store would
 // make every window load wait for the previous step's write acknowledgement.
@@ -1343,15 +1346,17 @@ __device__ __forceinline__ Win5 win_fetch(uintptr_t A) {
   return Win5{q[0], q[1], q[2], q[3], q[4]};
 }
 
-extern "C" __global__ __launch_bounds__(64) void zh_dec_seq_kernel(ZhDecArgs a, u32 nitems) {
+extern "C" __global__ __launch_bounds__(D2_BUF) void zh_dec_seq_kernel(ZhDecArgs a, u32 nitems) {
   // highest issue priority: the chains are issue-latency bound and share SIMDs with the
   // phase-1 / phase-3 waves of the other groups of the pipeline
   __builtin_amdgcn_s_setprio(3);
   __shared__ u32 info[2][64];
   __shared__ u64 ring[D2_BUF][D2_RUN];
   u32 const lane = lane_id();
-  if (lane < 36) info[0][lane] = c_LL_info[lane];
-  if (lane < 53) info[1][lane] = c_ML_info[lane];
+  for (u32 i = lane; i < 53; i += D2_BUF) {
+    if (i < 36) info[0][i] = c_LL_info[i];
+    info[1][i] = c_ML_info[i];
+  }
   u32 const it0 = a.item0 + blockIdx.x * D2_BUF, end = a.item0 + nitems;
   __syncthreads();
   u32 const it = it0 + lane;
@@ -1476,7 +1481,7 @@ hipError_t launch_decompress(const ZhDecArgs &a0, u32 nitems, hipStream_t stream
     hipLaunchKernelGGL(zh_decode_kernel, dim3(cnt), dim3(DEC_THREADS), 0, s, a);
     check("phase 1");
     if (after_p1) (void)hipEventRecord(after_p1, s);
-    hipLaunchKernelGGL(zh_dec_seq_kernel, dim3((cnt + D2_BUF - 1) / D2_BUF), dim3(64), 0, s, a, cnt);
+    hipLaunchKernelGGL(zh_dec_seq_kernel, dim3((cnt + D2_BUF - 1) / D2_BUF), dim3(D2_BUF), 0, s, a, cnt);
     check("sequences");
     hipLaunchKernelGGL(zh_dec_exec_kernel, dim3(cnt), dim3(DEC_THREADS), 0, s, a);
     check("phase 3");
