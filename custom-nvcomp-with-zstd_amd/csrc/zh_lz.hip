@@ -94,7 +94,9 @@ constexpr u32 OFF_ML = OFF_SEGM + 4 * 2 * NSEG;      // per window parity: the w
 constexpr u32 XQ_CAP = 192;                          // chain-end queue entries per worker wave
 constexpr u32 OFF_XQ = OFF_ML + 2 * 8 * ML_CAP;      // u16 per entry: window index | S << 15
 constexpr u32 OFF_MISC = OFF_XQ + 2 * XQ_CAP * NWW;  // [2 par + 0] matches, [2 par + 1] first parsed position
-constexpr u32 K1_LDS = OFF_MISC + 4 * 16;
+constexpr u32 OFF_LB = OFF_MISC + 4 * 16;            // window k - 2's literal prefix counts per walk
+                                                     // segment (+ the window's total), for the literal phase
+constexpr u32 K1_LDS = OFF_LB + 4 * (NSEG + 4);
 constexpr u32 ML_LO = 11, ML_LEN = 22, ML_OFF = 29, ML_CUM = 45;  // match-list entry: start [0, 11) | ...
 constexpr u32 MISC_WNM = 0;   // misc[par]: matches of the window of that parity (its match list's length)
 constexpr u32 MISC_ARR = 12;  // misc[12]: worker-wave barrier arrivals (cumulative)
@@ -115,6 +117,31 @@ __device__ __forceinline__ u32 ffbl_raw(u32 x) {
   __asm__("v_ffbl_b32 %0, %1" : "=v"(r) : "v"(x));
   return r;
 }
+
+// Perturbation builds only (-DZH_PAD_A/I/W=N, tools/variants.sh): N dependent VALU added to a
+// phase, to see which phase's instructions set K1's time.  Never in the product build.
+template <int N>
+__device__ __forceinline__ void vpad(u32 x) {
+  if constexpr (N > 0) {
+#pragma unroll
+    for (int i = 0; i < N; i++) __asm__ volatile("v_add_u32 %0, %0, %0" : "+v"(x));
+  }
+}
+#ifndef ZH_PAD_A
+#define ZH_PAD_A 0
+#endif
+#ifndef ZH_PAD_I
+#define ZH_PAD_I 0
+#endif
+#ifndef ZH_PAD_W
+#define ZH_PAD_W 0
+#endif
+#ifndef ZH_PAD_C
+#define ZH_PAD_C 0
+#endif
+#ifndef ZH_PAD_L
+#define ZH_PAD_L 0
+#endif
 
 // 8 bytes at p from LDS as (lo, hi): three aligned dwords + v_alignbyte
 __device__ __forceinline__ void ld64u(const u32 *in32, u32 p, u32 &lo, u32 &hi) {
@@ -172,14 +199,7 @@ __device__ __forceinline__ u32 hash_of(u32 lo, u32 hi) {
   return LONG ? hash_long(lo, hi) : hash_short(lo, hi);
 }
 
-// Inserter wave: the tiles of window [wsb, we) against one table (u16 entries = position
-// + 1).  Lane l handles positions tb + l + 64k of each tile; all lookups of a tile are
-// issued before its stores and after the previous tile's stores (program order = LDS
-// order within a wave).  Stores of later k carry later positions and land later; lanes
-// of ONE store that hit the same slot leave one of their values, so every lane reads its
-// slot back and lanes that find an earlier position rewrite theirs until none does: the
-// slot ends with the latest position, as in the oracle's serial loop.  Candidates
-// (position + 1, 0 = none) go to creg as u16 pairs.
+#ifdef ZH_INS_CHECK
 // Repair path of insert_window for a batch in which some lane of a ds_write_b16 lost its
 // slot to a LOWER position of the same store (never observed on gfx950, where the highest
 // lane of a store wins, but kept so the table semantics never depend on it).  The batch's
@@ -221,16 +241,23 @@ __device__ __forceinline__ void insert_repair(u16 *T, u32 tb0, u32 lane, const u
     if (!__ballot(need)) break;
   }
 }
+#endif
 
 // Inserter wave: the tiles of window [wsb, we) against one table (u16 entries = position
 // + 1).  Lane l handles positions tb + l + 64k of each tile; a tile's lookups are issued
 // before its stores and after the previous tile's stores (program order = LDS order within a
 // wave).  Stores of later k / later tiles carry later positions and land later; lanes of ONE
-// store that hit the same slot leave one of their values (on gfx950 the highest lane's, i.e.
-// the latest position, as in the oracle's serial loop), which a read-back of every lane's
-// slot verifies (insert_repair otherwise).  BT tiles are issued per LDS round trip together
-// with the next batch's input dwords and the workers' arrival counter.  Candidates
-// (position + 1, 0 = none) go to creg as u16 pairs.
+// store that hit the same slot leave the highest lane's value on gfx950 (the LDS services a
+// wave64 store's lanes in ascending groups, each group's same-address lanes in lane order), i.e.
+// the latest position, as in the oracle's serial loop.  Every K1 parity test depends on that
+// order; -DZH_INS_CHECK builds a read-back of every lane's slot and a repair path
+// (insert_repair) that make the tables independent of it (measured: no repair ever taken;
+// K1 11.16 ms without the read-back vs 11.27 with it, profiles/r05i_k1_perturbation.json).
+// BT tiles are issued per LDS round trip together with the next batch's input dwords and the
+// workers' arrival counter.  Candidates (position + 1, 0 = none) go to creg as u16 pairs.
+// A lane's positions are 4-aligned apart (tiles and rows are multiples of 64), so its byte
+// shift is lane & 3 and its dwords sit at one base + immediate offsets; positions past lim read
+// bytes past the block (inside the staging area's pad and the tables: never inserted).
 // One instantiation per table serves every window (code size: K1's hot loops compete for the
 // instruction cache).  skip (a miss-skip window, orc_lz_parse_pre): after the first batch of
 // ZH_SKIP_TILES tiles, on_check gets whether any of its positions has a candidate matching its
@@ -246,19 +273,19 @@ __device__ __forceinline__ void insert_window(const u32 *in32, u16 *T, u32 wsb, 
   constexpr u32 BT = 2;  // tiles per LDS round trip
   constexpr u32 T0 = 0, NT = TILES;
   static_assert(TILES % BT == 0 && ZH_SKIP_TILES == BT, "batches tile windows; the resume check is the first batch");
+  static_assert(ZH_TILE % 64 == 0 && ZH_WINDOW % 4 == 0, "a lane's positions share lane & 3");
+  u32 const sh = lane & 3u;
   u32 wv[BT][TPL][3];
-  auto load_in = [&](u32 tb0, u32 lim_t) {
+  auto load_in = [&](u32 tb0) {
+    const u32 *const q = in32 + (tb0 >> 2) + (lane >> 2);
 #pragma unroll
     for (u32 b = 0; b < BT; b++)
 #pragma unroll
-      for (u32 k = 0; k < TPL; k++) {
-        u32 const q = min(tb0 + b * ZH_TILE + 64 * k + lane, lim_t) >> 2;
-        wv[b][k][0] = in32[q];
-        wv[b][k][1] = in32[q + 1];
-        wv[b][k][2] = in32[q + 2];
-      }
+      for (u32 k = 0; k < TPL; k++)
+#pragma unroll
+        for (u32 t = 0; t < 3; t++) wv[b][k][t] = q[(b * ZH_TILE + 64 * k) / 4 + t];
   };
-  load_in(wsb + T0 * ZH_TILE, lim);
+  load_in(wsb + T0 * ZH_TILE);
 #pragma unroll
   for (u32 t0 = T0; t0 < NT; t0 += BT) {
     // opaque per-batch copy of lim: keeps the compiler from hoisting every tile's
@@ -266,25 +293,37 @@ __device__ __forceinline__ void insert_window(const u32 *in32, u16 *T, u32 wsb, 
     u32 lim_t;
     __asm__ volatile("v_mov_b32 %0, %1" : "=v"(lim_t) : "v"(lim));
     u32 const tb0 = wsb + t0 * ZH_TILE;
-    u32 h[BT][TPL], e[BT][TPL], r[BT][TPL];
+    u32 const p1 = tb0 + lane + 1u;  // the lane's first position of the batch, + 1
+    u32 h[BT][TPL], e[BT][TPL], sa[BT][TPL];
+    bool ok[BT][TPL];
 #pragma unroll
     for (u32 b = 0; b < BT; b++) {
-      u32 const tb = tb0 + b * ZH_TILE;
 #pragma unroll
       for (u32 k = 0; k < TPL; k++) {
-        u32 const p = tb + 64 * k + lane, sh = min(p, lim_t) & 3u;
+        u32 const q1 = p1 + b * ZH_TILE + 64 * k;  // position + 1: the stored value too
         u32 const lo = __builtin_amdgcn_alignbyte(wv[b][k][1], wv[b][k][0], sh), hi = __builtin_amdgcn_alignbyte(wv[b][k][2], wv[b][k][1], sh);
         u32 const hh = hash_of<LONG>(lo, hi);
-        e[b][k] = T[hh];
-        h[b][k] = (p < lim_t && p >= pmin) ? hh : JUNK;
+        // LDS addresses: the store goes to the lookup's slot or the junk slot (one select)
+        u32 const a = (u32)(uintptr_t)(T + hh);
+        e[b][k] = *(const __attribute__((address_space(3))) u16 *)(uintptr_t)a;
+        ok[b][k] = q1 <= lim_t && q1 > pmin;
+        sa[b][k] = ok[b][k] ? a : (u32)(uintptr_t)(T + JUNK);
+        h[b][k] = ok[b][k] ? hh : JUNK;  // (the check build's slot index)
       }
 #pragma unroll
-      for (u32 k = 0; k < TPL; k++) T[h[b][k]] = (u16)(tb + 64 * k + lane + 1);
+      for (u32 k = 0; k < TPL; k++) *(__attribute__((address_space(3))) u16 *)(uintptr_t)sa[b][k] = (u16)(p1 + b * ZH_TILE + 64 * k);
+    }
+#ifdef ZH_INS_CHECK
+    u32 r[BT][TPL];
+#pragma unroll
+    for (u32 b = 0; b < BT; b++)
 #pragma unroll
       for (u32 k = 0; k < TPL; k++) r[b][k] = T[h[b][k]];
-    }
-    if (t0 + BT < NT) load_in(tb0 + BT * ZH_TILE, lim_t);
+#endif
+    if (t0 + BT < NT) load_in(tb0 + BT * ZH_TILE);
+    vpad<ZH_PAD_I>(h[0][0]);
     u32 const arr = __atomic_load_n(arrivals, __ATOMIC_RELAXED);
+#ifdef ZH_INS_CHECK
     bool lost = false;
 #pragma unroll
     for (u32 b = 0; b < BT; b++)
@@ -296,11 +335,12 @@ __device__ __forceinline__ void insert_window(const u32 *in32, u16 *T, u32 wsb, 
 #endif
       insert_repair<LONG, BT>(T, tb0, lane, h, e);
     }
+#endif
 #pragma unroll
     for (u32 b = 0; b < BT; b++)
 #pragma unroll
       for (u32 k = 0; k < TPL; k += 2) {
-        u32 const c0 = h[b][k] != JUNK ? e[b][k] : 0u, c1 = h[b][k + 1] != JUNK ? e[b][k + 1] : 0u;
+        u32 const c0 = ok[b][k] ? e[b][k] : 0u, c1 = ok[b][k + 1] ? e[b][k + 1] : 0u;
         u32 const ri = ((t0 + b) * TPL + k) / 2;
         creg[ri] = c0 | (c1 << 16);
         // materialise this batch's candidates now (otherwise the compiler sinks their
@@ -315,7 +355,7 @@ __device__ __forceinline__ void insert_window(const u32 *in32, u16 *T, u32 wsb, 
         for (u32 k = 0; k < TPL; k++) {
           // (the position's own bytes again from LDS: wv already holds the next batch's)
           u32 const p = tb0 + b * ZH_TILE + 64 * k + lane;
-          u32 const c = h[b][k] != JUNK ? e[b][k] : 0u;
+          u32 const c = ok[b][k] ? e[b][k] : 0u;
           u32 lo, hi, clo, chi;
           ld64u(in32, min(p, lim_t), lo, hi);
           ld64u(in32, c ? c - 1u : 0u, clo, chi);
@@ -575,6 +615,7 @@ __device__ __forceinline__ void span_lengths(const u32 *in32, u32 *ci, u64 *tm, 
       return min(ffbl_raw(x), min(ffbl_raw(y), 32u) + 32u) >> 3;
     };
     u32 const pL = TWO ? pref(cL, Lw[k]) : 0u, pS = pref(cS, Sw[k]);
+    vpad<ZH_PAD_A>(pS);
     u32 cLn = wave_shl1(cL), cSn = wave_shl1(cS);
     cLn = lane == 63 ? ccL : cLn;
     cSn = lane == 63 ? ccS : cSn;
@@ -637,6 +678,7 @@ __device__ __forceinline__ void span_lengths(const u32 *in32, u32 *ci, u64 *tm, 
     u32 const cL = TWO ? cw & 0xFFFFu : 0u, cS = cw >> 16;
     u32 const lL = (runs[k] & 1u) ? min((u32)ZH_MAX_MATCH, lLr[k] + clL) : lLr[k];
     u32 const lS = (runs[k] & 2u) ? min((u32)ZH_MAX_MATCH, lSr[k] + clS) : lSr[k];
+    vpad<ZH_PAD_C>(lS);
     clL = lane_value(lL, 0);
     clS = lane_value(lS, 0);
     u32 const capj = min((u32)ZH_MAX_MATCH, n - min(p, n));
@@ -708,6 +750,7 @@ template <bool REWALK>
 __device__ __forceinline__ void seg_walk(const u32 *ci, u32 tmk, u32 S, u32 SE, u32 p, bool act0, u32 &LM, u32 &MM, u32 &ex) {
   // (the first walk has no old trajectory: REWALK = false drops the merge test from the step)
   u32 const old = (REWALK && act0) ? (LM | MM) : 0u;
+  vpad<ZH_PAD_W>(p);
   u32 nl = 0, nm = 0;
   bool act = act0 && p < SE, merged = false;
   u32 mpos = 0;
@@ -1203,6 +1246,7 @@ __device__ __forceinline__ u32 lz_block(const ZhBlockDesc *__restrict__ blocks, 
   u32 const r_hi = r_lo + rounds_of(wave);
   u32 *const ci0 = ci;
   u32 *const sgm = (u32 *)(smem + OFF_SEGM);
+  u32 *const lbx = (u32 *)(smem + OFF_LB);
   u16 *const xq = (u16 *)(smem + OFF_XQ) + XQ_CAP * wave;
   u32 const nwin = (n - wstart + ZH_WINDOW - 1) / ZH_WINDOW;
   u64 *const mlist = (u64 *)(smem + OFF_ML);
@@ -1353,6 +1397,12 @@ __device__ __forceinline__ u32 lz_block(const ZhBlockDesc *__restrict__ blocks, 
           }
         }
       }
+      // the window's literal bits are final now (the catch-up cleared its share): the literal
+      // phase's per-segment exclusive prefix counts, once for every wave (LDS ops of a wave
+      // apply in order, so the reads see this wave's atomics)
+      u32 const lc = (u32)__popc(lmQ[lane]), lincl = wave_scan_incl(lc);
+      lbx[lane] = lincl - lc;
+      if (lane == 63) lbx[NSEG] = lincl;
     }
     if (lane == 0) atomicAdd(&misc[MISC_ARR], 1u);
     __syncthreads();  // X: window k's match info and take masks; window k - 1's records and literal bits
@@ -1371,10 +1421,9 @@ __device__ __forceinline__ u32 lz_block(const ZhBlockDesc *__restrict__ blocks, 
     if (prev2) {
       // ---- literals of window k - 2, lanes = positions (round r = segments 2r, 2r + 1)
       u32 const nm = __builtin_amdgcn_readfirstlane(misc[MISC_WNM + kb]);
-      u32 const lc = (u32)__popc(lmQ[lane]), lincl = wave_scan_incl(lc), lb = lincl - lc;
       for (u32 r = wave; r < NROUND; r += NWW) {
         u64 const lm = ((u64)(u32)__builtin_amdgcn_readfirstlane(lmQ[2 * r + 1]) << 32) | (u32)__builtin_amdgcn_readfirstlane(lmQ[2 * r]);
-        u32 const lbr = lane_value(lb, 2 * r);
+        u32 const lbr = (u32)__builtin_amdgcn_readfirstlane(lbx[2 * r]);
         if ((lm >> lane) & 1ull) {
           u32 const rank = __builtin_amdgcn_mbcnt_hi((u32)(lm >> 32), __builtin_amdgcn_mbcnt_lo((u32)lm, 0u));
 #ifndef ZH_EXP_NOLIT
@@ -1382,7 +1431,8 @@ __device__ __forceinline__ u32 lz_block(const ZhBlockDesc *__restrict__ blocks, 
 #endif
         }
       }
-      nlit_tot += lane_value(lincl, 63);
+      vpad<ZH_PAD_L>(nm);
+      nlit_tot += (u32)__builtin_amdgcn_readfirstlane(lbx[NSEG]);
       nseq_tot += nm;
     }
     ZH_STAMP(st_E);
