@@ -1226,6 +1226,7 @@ __device__ __forceinline__ u32 lz_block(const ZhBlockDesc *__restrict__ blocks, 
     // issue arbitration to the 3 worker waves sharing their SIMD; the next window's tables
     // gate the workers' next window, so they take priority (MI355X_MICROARCH.md, "VALU issue
     // is arbitrated ... by priority, then age").
+    // (priority 0 or 1 measured the same, profiles/r05l_k1_priority_ab.json)
     __builtin_amdgcn_s_setprio(2);
     if (tid >= INS_TID + 64)
       dead = inserter_loop<false, two_tables<MODE>()>(in32, TS, ci8, misc, n, lim, lane, ws.dbg(b), wstart, pmin, span_s, span_e, kskip0, kprobe, e0p);
