@@ -118,6 +118,13 @@ __device__ __forceinline__ u32 ffbl_raw(u32 x) {
   return r;
 }
 
+// K1's LDS: the dynamic area, which starts at LDS address K1_DYN (after lz_blocks' one static
+// word; lz_blocks traps otherwise).  A constant base lets the compiler fold constant offsets into
+// the ds instructions' offset fields (through the extern symbol every address costs a v_add of
+// the symbol's link-time address).  (Address 0 is the LDS null pointer to the compiler.)
+constexpr u32 K1_DYN = 16;
+__device__ __forceinline__ u8 *k1_lds() { return (u8 *)(__attribute__((address_space(3))) u8 *)(uintptr_t)K1_DYN; }
+
 // Perturbation builds only (-DZH_PAD_A/I/W=N, tools/variants.sh): N dependent VALU added to a
 // phase, to see which phase's instructions set K1's time.  Never in the product build.
 template <int N>
@@ -467,7 +474,7 @@ static_assert(ZH_PROBE_WINDOWS >= 1 && ZH_PROBE_WINDOWS <= 3, "probe windows fit
 // inserters too -- tests them right after that P and leaves the window loop together.
 __device__ __forceinline__ bool probe_dead_tm(u32 k, u32 kprobe, u32 e0) {
   if (ZH_PROBE_WINDOWS != 1 || k + 1 != kprobe) return false;
-  extern __shared__ __attribute__((aligned(16))) u8 smem[];
+  u8 *const smem = k1_lds();
   u32 lane;
   __asm__ volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(lane));
   const u64 *const tmP = (const u64 *)(smem + OFF_HM) + ((k & 1u) ^ 1u) * NROUND;
@@ -1050,7 +1057,7 @@ __device__ __forceinline__ bool repeat_scan(const u32 *in32, u32 *E, u32 *hw, u3
 
 template <u32 MODE>
 __device__ __forceinline__ u32 lz_block(const ZhBlockDesc *__restrict__ blocks, ZhWorkspace ws, u32 b, u32 nblocks, u32 *s_take, Prefetch &pf, u32 wv, bool redo) {
-  extern __shared__ __attribute__((aligned(16))) u8 smem[];
+  u8 *const smem = k1_lds();
   u8 *in = smem + OFF_IN;
   u32 *in32 = (u32 *)in;
   u16 *TL = (u16 *)(smem + OFF_TL), *TS = (u16 *)(smem + OFF_TS);
@@ -1522,7 +1529,9 @@ __device__ __forceinline__ u32 lz_block(const ZhBlockDesc *__restrict__ blocks, 
 // one was processed, so the HBM latency of staging and the per-block launch gap overlap work.
 template <u32 MODE>
 __device__ __forceinline__ void lz_blocks(const ZhBlockDesc *__restrict__ blocks, u32 nblocks, ZhWorkspace ws) {
-  extern __shared__ __attribute__((aligned(16))) u8 smem[];
+  extern __shared__ __attribute__((aligned(16))) u8 smem_dyn[];
+  u8 *const smem = k1_lds();
+  if (threadIdx.x == 0 && (u32)(uintptr_t)smem_dyn != K1_DYN) __builtin_trap();  // (see k1_lds)
   __shared__ u32 s_take;  // block index taken from the counter, broadcast to the workgroup
   if (threadIdx.x == 0) {
     s_take = atomicAdd(ws.ctr, 1u);
