@@ -91,7 +91,8 @@ __device__ __forceinline__ u32 segm(u32 par) { return par * NSEG; }
 constexpr u32 ML_CAP = ((ZH_WINDOW + ZH_MIN_MATCH_SHORT - 1) / ZH_MIN_MATCH_SHORT + 12 + 3) & ~3u;  // matches per window
 constexpr u32 OFF_ML = OFF_SEGM + 4 * 2 * NSEG;      // per window parity: the window's matches in order (u64,
                                                      // ML_* fields) for the records one step later
-constexpr u32 XQ_CAP = 192;                          // chain-end queue entries per worker wave
+constexpr u32 XQ_CAP = 196;                          // chain-end queue entries per worker wave (<= 191
+                                                     // used: < 64 left + 2 x 64 per round; the last is a spare)
 constexpr u32 OFF_XQ = OFF_ML + 2 * 8 * ML_CAP;      // u16 per entry: window index | S << 15
 constexpr u32 OFF_MISC = OFF_XQ + 2 * XQ_CAP * NWW;  // [2 par + 0] matches, [2 par + 1] first parsed position
 constexpr u32 OFF_LB = OFF_MISC + 4 * 16;            // window k - 2's literal prefix counts per walk
@@ -638,9 +639,10 @@ __device__ __forceinline__ void span_lengths(const u32 *in32, u32 *ci, u64 *tm, 
     u32 const rL = __builtin_amdgcn_mbcnt_hi((u32)(bL >> 32), __builtin_amdgcn_mbcnt_lo((u32)bL, 0u));
     u32 const rS = __builtin_amdgcn_mbcnt_hi((u32)(bS >> 32), __builtin_amdgcn_mbcnt_lo((u32)bS, 0u));
     u32 const nL = (u32)__popcll(bL);
-    if (xL) xq[nq + rL] = (u16)i;
-    if (xS) xq[nq + nL + rS] = (u16)(i | 0x8000u);
-    nq += nL + (u32)__popcll(bS);
+    // branch-free stores: lanes without an entry write the wave's spare slot (never read)
+    xq[xL ? nq + rL : XQ_CAP - 1] = (u16)i;
+    xq[xS ? nq + nL + rS : XQ_CAP - 1] = (u16)(i | 0x8000u);
+    nq = (u32)__builtin_amdgcn_readfirstlane(nq + nL + (u32)__popcll(bS));
     while (nq >= 64) {
       nq -= 64;
       xq_flush(in32, ci, xq + nq, 64, wsb, lane);
