@@ -994,7 +994,9 @@ __device__ __forceinline__ bool repeat_scan(const u32 *in32, u32 *E, u32 *hw, u3
   // slot and signature of a position's long-hash sum t: E[t >> 18], entry (t << 14) & ~0xFFFF | q
   auto slot = [&](u32 t) -> u32 * { return E + (t >> (32 - ZH_SCAN_LOG)); };
   auto key = [](u32 t) { return (t << ZH_SCAN_LOG) & 0xFFFF0000u; };
-  for (u32 i = tid; i < NS / 4; i += K1_THREADS) ((uint4 *)E)[i] = make_uint4(~0u, ~0u, ~0u, ~0u);
+  u32 ones;  // (opaque: a constant vector would be hoisted out of the block loop and spilled)
+  __asm__ volatile("v_mov_b32 %0, -1" : "=v"(ones));
+  for (u32 i = tid; i < NS / 4; i += K1_THREADS) ((uint4 *)E)[i] = make_uint4(ones, ones, ones, ones);
   ((uint4 *)hw)[tid] = make_uint4(0u, 0u, 0u, 0u);
   if (tid == 0) misc[MISC_SCAN] = 0;
   __syncthreads();
@@ -1431,13 +1433,24 @@ __device__ __forceinline__ u32 lz_block(const ZhBlockDesc *__restrict__ blocks, 
     if (prev2) {
       // ---- literals of window k - 2, lanes = positions (round r = segments 2r, 2r + 1)
       u32 const nm = __builtin_amdgcn_readfirstlane(misc[MISC_WNM + kb]);
-      for (u32 r = wave; r < NROUND; r += NWW) {
-        u64 const lm = ((u64)(u32)__builtin_amdgcn_readfirstlane(lmQ[2 * r + 1]) << 32) | (u32)__builtin_amdgcn_readfirstlane(lmQ[2 * r]);
-        u32 const lbr = (u32)__builtin_amdgcn_readfirstlane(lbx[2 * r]);
+      // the wave's rounds r = wave + NWW j: every LDS read of them issued first (one round trip)
+      constexpr u32 LR = (NROUND + NWW - 1) / NWW;
+      u64 mw[LR];
+      u32 lbr[LR];
+#pragma unroll
+      for (u32 j = 0; j < LR; j++) {
+        u32 const r = min(wave + NWW * j, NROUND - 1u);
+        mw[j] = *(const u64 *)&lmQ[2 * r];
+        lbr[j] = lbx[2 * r];
+      }
+#pragma unroll
+      for (u32 j = 0; j < LR; j++) {
+        if (wave + NWW * j >= NROUND) continue;
+        u64 const lm = ((u64)(u32)__builtin_amdgcn_readfirstlane((u32)(mw[j] >> 32)) << 32) | (u32)__builtin_amdgcn_readfirstlane((u32)mw[j]);
         if ((lm >> lane) & 1ull) {
           u32 const rank = __builtin_amdgcn_mbcnt_hi((u32)(lm >> 32), __builtin_amdgcn_mbcnt_lo((u32)lm, 0u));
 #ifndef ZH_EXP_NOLIT
-          lit_out[nlit_tot + lbr + rank] = in[wsq + 64 * r + lane];
+          lit_out[nlit_tot + (u32)__builtin_amdgcn_readfirstlane(lbr[j]) + rank] = in[wsq + 64 * (wave + NWW * j) + lane];
 #endif
         }
       }
