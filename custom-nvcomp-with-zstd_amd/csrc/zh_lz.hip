@@ -589,9 +589,8 @@ __device__ __forceinline__ void span_lengths(const u32 *in32, u32 *ci, u64 *tm, 
   u32 olo[MAX_RW], ohi[MAX_RW], Lw[MAX_RW][3], Sw[MAX_RW][3];
   auto loadA = [&](u32 k) {
     u32 const r = r_hi - 1 - min(k, r_hi - 1 - r_lo), i = 64 * r + lane, p = wsb + i;  // (rounds past the span: repeat the last)
-    bool const hv = p < we && p < lim;
-    u32 const cw0 = ci[cidx(i)];
-    u32 const cw = hv ? cw0 : 0u;
+    // (positions at or past lim -- which covers we -- have no candidates: the inserters left 0)
+    u32 const cw = ci[cidx(i)];
     cwr[k] = cw;
     ld64u(in32, p, olo[k], ohi[k]);
     // the candidates' positions (c - 1) mod 2^16, without a select: an empty candidate reads
