@@ -1321,7 +1321,10 @@ extern "C" __global__ __launch_bounds__(K2_THREADS) void zh_entropy_kernel(const
       // Two chunks per iteration: the second chunk's run analysis, its permutes and both
       // chunks' code lookups depend only on records (not on the first chunk's results), so
       // their LDS round trips overlap; the open run and the repcodes pass on in order.
-      struct Chunk { u32 ll, off, runMl, incl, cum; u64 hm; bool head; };
+      // fast: every record of the chunk opens its own run (no same-offset continuation, the
+      // common case): the run sums, their scan and the permutes reduce to the records themselves
+      // and a shift by the open run (DPP)
+      struct Chunk { u32 ll, off, runMl, incl, cum; u64 hm; bool head, fast; };
       auto analyse = [&](u64 rec, u32 i, u32 pc0, u32 po0, Chunk &c) {
         bool const valid = i < nseq_raw;
         u32 const cum = (u32)(rec & 0x1FFFFu), ce = (u32)((rec >> 24) & 0xFFFu);
@@ -1333,15 +1336,28 @@ extern "C" __global__ __launch_bounds__(K2_THREADS) void zh_entropy_kernel(const
         bool const head = valid && !flag;
         u64 const hm = __ballot(head);
         u32 const mlv = valid ? ml : 0u;
-        u32 const incl = wave_scan_incl(mlv);
-        u64 const headBitsAfter = hm & ~((lane == 63) ? ~0ull : ((2ull << lane) - 1));
-        u32 const runEnd = headBitsAfter ? (u32)__builtin_ctzll(headBitsAfter) - 1u : 63u;
-        u32 const inclEnd = (u32)__builtin_amdgcn_ds_bpermute((int)(runEnd << 2), (int)incl);
-        c.runMl = inclEnd - (incl - mlv);
-        c.ll = ll; c.off = off; c.incl = incl; c.cum = cum; c.hm = hm; c.head = head;
+        c.fast = hm == __ballot(valid);
+        if (c.fast) {
+          c.runMl = mlv;
+          c.incl = 0;  // (advance reads it only before the first head: lane 0 is one)
+        } else {
+          u32 const incl = wave_scan_incl(mlv);
+          u64 const headBitsAfter = hm & ~((lane == 63) ? ~0ull : ((2ull << lane) - 1));
+          u32 const runEnd = headBitsAfter ? (u32)__builtin_ctzll(headBitsAfter) - 1u : 63u;
+          u32 const inclEnd = (u32)__builtin_amdgcn_ds_bpermute((int)(runEnd << 2), (int)incl);
+          c.runMl = inclEnd - (incl - mlv);
+          c.incl = incl;
+        }
+        c.ll = ll; c.off = off; c.cum = cum; c.hm = hm; c.head = head;
       };
       // the chunk's runs to lanes hp + rank (ds_permute, as in the single-chunk step below)
       auto gather = [&](const Chunk &c, u32 hp, u32 &sll, u32 &sml, u32 &soff) {
+        if (c.fast) {  // lane + hp (lane 0 takes the open run in advance)
+          sll = hp ? wave_shr1(c.ll) : c.ll;
+          sml = hp ? wave_shr1(c.runMl) : c.runMl;
+          soff = hp ? wave_shr1(c.off) : c.off;
+          return;
+        }
         u32 const hcount = (u32)__popcll(c.hm), rank = (u32)__popcll(c.hm & below);
         u32 const dest = c.head ? rank + hp : (hcount + hp + (lane - rank)) & 63u;
         sll = (u32)__builtin_amdgcn_ds_permute((int)(dest << 2), (int)c.ll);
