@@ -1937,7 +1937,10 @@ void entropy_launch(const ZhBlockDesc *d_descs, u32 nblocks, ZhWorkspace ws, u32
   // 3.04 -> 3.22 ms at 16,384 blocks, 0.75 -> 0.80 ms at 2,048)
   u32 const g3 = (nblocks + K3_BPW - 1) / K3_BPW, g4 = (nblocks + K4_WAVES - 1) / K4_WAVES;
   hipLaunchKernelGGL(zh_fse_chain_kernel, dim3(g3), dim3(64 * K3_WAVES), K3_LDS, stream, d_descs, nblocks, ws);
-  hipLaunchKernelGGL(zh_seq_pack_kernel, dim3(g4), dim3(64 * K4_WAVES), K4_WAVES * KP_LDS, stream, d_descs, nblocks, ws, d_item_size,
+#ifndef ZH_K4_LDS_PAD
+#define ZH_K4_LDS_PAD 0  // (occupancy experiments: LDS padding per K4 workgroup)
+#endif
+  hipLaunchKernelGGL(zh_seq_pack_kernel, dim3(g4), dim3(64 * K4_WAVES), K4_WAVES * KP_LDS + ZH_K4_LDS_PAD, stream, d_descs, nblocks, ws, d_item_size,
                      d_item_status, d_blk_size);
 }
 }  // namespace zh
