@@ -544,10 +544,13 @@ constexpr u32 MAX_RW = 3;   // rounds per worker wave
 // (wave 0 parses).  A CU's waves go to SIMDs by wave id mod 4 and the length phase saturates
 // VALU issue, so every SIMD gets 8 rounds -- SIMD 0 beside wave 0's parse, SIMD 1 beside wave
 // 1's records and wave 13's lookahead, SIMDs 2 and 3 beside an inserter each -- with the older
-// wave of a SIMD taking 3 (issue goes to the oldest ready wave).  Measured (C3 mix, K1 per
-// launch, one box): per-SIMD 9/11/6/6 rounds 12.30 ms, 9/9/7/7 11.86, 8/9/8/7 11.73,
-// 8/8/8/8 11.61, 8/7/8/9 12.29.
-constexpr u64 ROUND_TAB = 0xaabfbf8ull;  // 2 bits per wave: 0 2 3 3 3 2 3 3 3 2 2 2 2 2
+// wave of a SIMD taking 3 (issue goes to the oldest ready wave, so a SIMD's youngest wave
+// finishes last).  Measured (C3 mix, K1 per launch, one box): per-SIMD 9/11/6/6 rounds 12.30 ms,
+// 9/9/7/7 11.86, 8/9/8/7 11.73, 8/8/8/8 11.61, 8/7/8/9 12.29 (round 4).  Round 5, SIMD 1's waves
+// 1/5/9/13 (13 also computes the window's lookahead): 2/2/2/2 10.69 ms, 2/3/2/1 10.38, 1/3/3/1
+// 10.37, 2/2/3/1 10.37; moving rounds between SIMDs or 4-round waves (a larger unrolled span)
+// measured slower (`profiles/r05z_round_table_ab.json`).
+constexpr u64 ROUND_TAB = 0x6abfff8ull;  // 2 bits per wave: 0 2 3 3 3 3 3 3 3 2 2 2 2 1
 __device__ __forceinline__ u32 rounds_of(u32 w) {
 #ifdef ZH_RTAB
   return (u32)(((unsigned long long)(ZH_RTAB) >> (2 * w)) & 3u);
