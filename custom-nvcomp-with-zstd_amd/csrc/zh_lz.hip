@@ -151,6 +151,17 @@ __device__ __forceinline__ void vpad(u32 x) {
 #define ZH_PAD_L 0
 #endif
 
+// K1's workgroup barrier: LDS ordering only.  The waves exchange data through LDS alone; their
+// global writes (records, literals, the next block's prefetch loads in flight) need no ordering
+// inside the kernel, so the barrier does not wait for them (__syncthreads' workgroup fence waits
+// for every outstanding global access -- the literal stores' write acknowledgements and the
+// next block's prefetch -- before each barrier).
+__device__ __forceinline__ void k1_barrier() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
+
 // 8 bytes at p from LDS as (lo, hi): three aligned dwords + v_alignbyte
 __device__ __forceinline__ void ld64u(const u32 *in32, u32 p, u32 &lo, u32 &hi) {
   u32 const w = p >> 2, sh = p & 3;
@@ -832,9 +843,9 @@ __device__ __forceinline__ bool idle_inserter_loop(u32 *misc_, u32 n, u32 wstart
   u32 const nwin = (n - wstart + ZH_WINDOW - 1) / ZH_WINDOW;
   for (u32 k = 0; k < nwin + 2; k++) {
     if (probe_dead(misc_, k, kprobe)) return true;
-    __syncthreads();  // P
+    k1_barrier();  // P
     if (probe_dead_tm(k, kprobe, e0p)) return true;
-    __syncthreads();  // X
+    k1_barrier();  // X
   }
   return false;
 }
@@ -859,14 +870,14 @@ __device__ __forceinline__ bool inserter_loop(const u32 *in32, u16 *T, u8 *ci8, 
       if (skipc) dump_window<LONG, ZH_SKIP_TILES>(ci8 + (k & 1u) * 4 * CI_WORDS, lane, creg, cwe);
       else dump_window<LONG, TILES>(ci8 + (k & 1u) * 4 * CI_WORDS, lane, creg, cwe);
     }
-    __syncthreads();  // P: candidates of window k in buffer k & 1
+    k1_barrier();  // P: candidates of window k in buffer k & 1
     if (probe_dead_tm(k, kprobe, e0p)) return true;
     u32 const done = passed + WIN_BARRIERS;
     // arr: the arrival counter as read with the last tile's read-back; a barrier taken
     // here means the counter is re-read for the next one
     auto take_ready = [&](u32 arr) {
       while (passed < done && arr >= NWW * (passed + 1)) {
-        __syncthreads();
+        k1_barrier();
         passed++;
         arr = __atomic_load_n(&misc_[MISC_ARR], __ATOMIC_RELAXED);
       }
@@ -894,7 +905,7 @@ __device__ __forceinline__ bool inserter_loop(const u32 *in32, u16 *T, u8 *ci8, 
 #ifdef ZH_STAMPS
     st_ins += (u32)(__builtin_amdgcn_s_memtime() - ti0);
 #endif
-    while (passed < done) { __syncthreads(); passed++; }
+    while (passed < done) { k1_barrier(); passed++; }
   }
 #ifdef ZH_STAMPS
   if (LONG && lane == 0) dbg[16] = st_ins;
@@ -963,11 +974,11 @@ constexpr u64 K1_WAVE_MAP = ZH_K1_PERM ? 0xDBA9C876F543E210ull : 0xFEDCBA9876543
 // persistent block loop.)
 __device__ __forceinline__ bool block_any(bool v, u32 *flag, u32 tid) {
   if (__ballot(v) && (tid & 63) == 0) atomicOr(flag, 1u);
-  __syncthreads();
+  k1_barrier();
   bool const r = *flag != 0;
-  __syncthreads();
+  k1_barrier();
   if (tid == 0) *flag = 0;
-  __syncthreads();
+  k1_barrier();
   return r;
 }
 
@@ -999,9 +1010,10 @@ __device__ __forceinline__ bool repeat_scan(const u32 *in32, u32 *E, u32 *hw, u3
   u32 ones;  // (opaque: a constant vector would be hoisted out of the block loop and spilled)
   __asm__ volatile("v_mov_b32 %0, -1" : "=v"(ones));
   for (u32 i = tid; i < NS / 4; i += K1_THREADS) ((uint4 *)E)[i] = make_uint4(ones, ones, ones, ones);
-  ((uint4 *)hw)[tid] = make_uint4(0u, 0u, 0u, 0u);
+  u32 const zero = ones + 1u;  // (opaque as well)
+  ((uint4 *)hw)[tid] = make_uint4(zero, zero, zero, zero);
   if (tid == 0) misc[MISC_SCAN] = 0;
-  __syncthreads();
+  k1_barrier();
   // insert pass: a wave takes 256 consecutive dwords (4 per lane, 64 apart); the 8 bytes at q = 4j
   // are dwords j and j + 1, the latter the next lane's (DPP), lane 63's from the next row
   u32 *const hwv = hw + 256u * wave;
@@ -1028,7 +1040,7 @@ __device__ __forceinline__ bool repeat_scan(const u32 *in32, u32 *E, u32 *hw, u3
       }
     }
   }
-  __syncthreads();
+  k1_barrier();
   // lookup pass: the sampled block positions p = pre + ZH_SCAN_STEP m < lim count when
   // E[slot] - key < p; a lane takes 4 consecutive samples (12 bytes apart between lanes: one
   // shift for all, 6 dword loads for the 4, lanes 3 dwords apart hit distinct banks)
@@ -1056,7 +1068,7 @@ __device__ __forceinline__ bool repeat_scan(const u32 *in32, u32 *E, u32 *hw, u3
   }
   u32 const wsum = lane_value(wave_scan_incl(c), 63);
   if (lane == 0 && wsum) atomicAdd(&misc[MISC_SCAN], wsum);
-  __syncthreads();
+  k1_barrier();
   u32 const total = (u32)__builtin_amdgcn_readfirstlane(__atomic_load_n(&misc[MISC_SCAN], __ATOMIC_RELAXED));
   return total >= max(span >> ZH_SCAN_SHIFT, (u32)ZH_SCAN_MIN);
 }
@@ -1082,7 +1094,7 @@ __device__ __forceinline__ u32 lz_block(const ZhBlockDesc *__restrict__ blocks, 
   // taken once per block, not again when the block is redone without the probe)
   if (tid == 0 && !redo) *s_take = atomicAdd(ws.ctr, 1u);
   if (d.n == 0) {
-    __syncthreads();
+    k1_barrier();
     u32 const next_b = *s_take;
     prefetch_block(blocks, next_b, nblocks, tid, pf);
     return next_b;
@@ -1204,7 +1216,7 @@ __device__ __forceinline__ u32 lz_block(const ZhBlockDesc *__restrict__ blocks, 
     }
   } else {
     next_b = *s_take;
-    __syncthreads();  // the tables and counters
+    k1_barrier();  // the tables and counters
   }
   if (par_hist) {
     // store every position, then rounds of read-back: a slot holding an older position than
@@ -1224,7 +1236,7 @@ __device__ __forceinline__ u32 lz_block(const ZhBlockDesc *__restrict__ blocks, 
           if (TS[hs] < v) { TS[hs] = v; ch = true; }
         }
       }
-      if (round == 0) __syncthreads();
+      if (round == 0) k1_barrier();
       else if (!block_any(ch, &misc[MISC_ANY], tid)) break;
     }
   }
@@ -1294,7 +1306,7 @@ __device__ __forceinline__ u32 lz_block(const ZhBlockDesc *__restrict__ blocks, 
     u32 *const lmP = sgm + segm(kb ^ 1u);   // window k - 1's literal bits (the walk's)
     u32 *const lmQ = sgm + segm(kb);        // window k - 2's (after its catch-up)
     u64 *const mlP = mlist + (kb ^ 1u) * ML_CAP, *const mlQ = mlist + kb * ML_CAP;
-    __syncthreads();  // P: candidates of window k in buffer k & 1
+    k1_barrier();  // P: candidates of window k in buffer k & 1
     if (probe_dead_tm(k, kprobe, e0p)) {
       dead = true;
       break;
@@ -1419,7 +1431,7 @@ __device__ __forceinline__ u32 lz_block(const ZhBlockDesc *__restrict__ blocks, 
       if (lane == 63) lbx[NSEG] = lincl;
     }
     if (lane == 0) atomicAdd(&misc[MISC_ARR], 1u);
-    __syncthreads();  // X: window k's match info and take masks; window k - 1's records and literal bits
+    k1_barrier();  // X: window k's match info and take masks; window k - 1's records and literal bits
     ZH_STAMP(st_X);
     if (MODE != 2 && have && wave != 0 && wave < (skipk ? RS : NWW - 1)) {
       // ---- take decision at this wave's span top (the next position was the next wave's):
@@ -1435,16 +1447,23 @@ __device__ __forceinline__ u32 lz_block(const ZhBlockDesc *__restrict__ blocks, 
     if (prev2) {
       // ---- literals of window k - 2, lanes = positions (round r = segments 2r, 2r + 1)
       u32 const nm = __builtin_amdgcn_readfirstlane(misc[MISC_WNM + kb]);
+#ifdef ZH_EXP_NOLITPHASE
+      if (true) { nseq_tot += nm; } else  // (experiment: the literal phase's upper bound; output wrong)
+#endif
+      {
       // the wave's rounds r = wave + NWW j: every LDS read of them issued first (one round trip)
       constexpr u32 LR = (NROUND + NWW - 1) / NWW;
       u64 mw[LR];
-      u32 lbr[LR];
+      u32 lbr[LR], by[LR];
 #pragma unroll
       for (u32 j = 0; j < LR; j++) {
         u32 const r = min(wave + NWW * j, NROUND - 1u);
         mw[j] = *(const u64 *)&lmQ[2 * r];
-        lbr[j] = lbx[2 * r];
+        lbr[j] = (u32)__builtin_amdgcn_readfirstlane(lbx[2 * r]);
+        by[j] = in[wsq + 64 * r + lane];  // (every lane: the loads leave before the masks are tested)
       }
+#pragma unroll
+      for (u32 j = 0; j < LR; j++) __asm__ volatile("" : "+v"(by[j]));  // (not sunk into the branches)
 #pragma unroll
       for (u32 j = 0; j < LR; j++) {
         if (wave + NWW * j >= NROUND) continue;
@@ -1452,13 +1471,14 @@ __device__ __forceinline__ u32 lz_block(const ZhBlockDesc *__restrict__ blocks, 
         if ((lm >> lane) & 1ull) {
           u32 const rank = __builtin_amdgcn_mbcnt_hi((u32)(lm >> 32), __builtin_amdgcn_mbcnt_lo((u32)lm, 0u));
 #ifndef ZH_EXP_NOLIT
-          lit_out[nlit_tot + (u32)__builtin_amdgcn_readfirstlane(lbr[j]) + rank] = in[wsq + 64 * (wave + NWW * j) + lane];
+          lit_out[nlit_tot + lbr[j] + rank] = (u8)by[j];
 #endif
         }
       }
       vpad<ZH_PAD_L>(nm);
       nlit_tot += (u32)__builtin_amdgcn_readfirstlane(lbx[NSEG]);
       nseq_tot += nm;
+      }
     }
     ZH_STAMP(st_E);
   }
@@ -1554,7 +1574,7 @@ __device__ __forceinline__ void lz_blocks(const ZhBlockDesc *__restrict__ blocks
     s_take = atomicAdd(ws.ctr, 1u);
     ((u32 *)(smem + OFF_MISC))[MISC_ANY] = 0;
   }
-  __syncthreads();
+  k1_barrier();
   u32 b = s_take;
   Prefetch pf;
   u32 const wv = (u32)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -1565,7 +1585,7 @@ __device__ __forceinline__ void lz_blocks(const ZhBlockDesc *__restrict__ blocks
     // block index and descriptor fields derived from it -- in SGPRs: the function's return paths
     // join under the inserter / worker split, which the compiler takes for divergence)
     u32 const r = (u32)__builtin_amdgcn_readfirstlane(lz_block<MODE>(blocks, ws, b, nblocks, &s_take, pf, wv, redo));
-    __syncthreads();  // every wave is done with this block's LDS before the next is staged
+    k1_barrier();  // every wave is done with this block's LDS before the next is staged
     redo = r == K1_REDO;
     b = redo ? b : r;
   }
