@@ -48,7 +48,7 @@ enum : u32 {
 // FSE chain segments (zh_entropy.hip K3): each of the three tables' chains is cut into
 // ZH_K3_SEGS segments of L steps (L a multiple of ZH_K3_RUN); lane t * ZH_K3_SEGS + g of the
 // chain wave runs segment g of table t.  Step e of table t is element
-//   ((r / RUN) * ZH_K3_SLOTS + t * ZH_K3_SEGS + g) * RUN + r % RUN,   g = e / L, r = e % L
+//   ((r / RUN) * ZH_K3_SLOTS + ZH_K3_SLOT(t, g)) * RUN + r % RUN,   g = e / L, r = e % L
 // of the state (u16) and code (u8) arrays, RUN = ZH_K3_RUN: RUN consecutive steps of a
 // segment are contiguous (the packing kernel's 64-step chunks are whole lines) and the 63
 // segments' runs are adjacent.
@@ -60,7 +60,19 @@ enum : u32 {
 #define ZH_K3_SEGS (21u * ZH_K3_W)
 #define ZH_K3_SLOTS (64u * ZH_K3_W)
 #define ZH_K3_RUN 16u
-#define ZH_K3_TSTRIDE (ZH_K3_SEGS * ZH_K3_RUN)  // elements between a step's LL, OF and ML entries
+// Slot of (table t, segment g) in a batch row.  Segment-major (3 g + t, the default): a step's LL,
+// OF and ML runs are adjacent, so the packing kernel's loads of one segment's 16 steps touch one or
+// two 128-B lines instead of three (table-major t * SEGS + g: three lines, each used for 32 B)
+#ifndef ZH_K3_SEGMAJOR
+#define ZH_K3_SEGMAJOR 1
+#endif
+#if ZH_K3_SEGMAJOR
+#define ZH_K3_SLOT(t, g) (3u * (g) + (t))
+#define ZH_K3_TSTRIDE ZH_K3_RUN  // elements between a step's LL, OF and ML entries
+#else
+#define ZH_K3_SLOT(t, g) ((t) * ZH_K3_SEGS + (g))
+#define ZH_K3_TSTRIDE (ZH_K3_SEGS * ZH_K3_RUN)
+#endif
 #define ZH_K3_SEGLEN(nbseq) ((((nbseq) + ZH_K3_SEGS - 1u) / ZH_K3_SEGS + ZH_K3_RUN - 1u) & ~(ZH_K3_RUN - 1u))
 #define ZH_K3_CODES(L) (2u * ZH_K3_SLOTS * (L))  // byte offset of the codes (after the u16 states)
 #define ZH_K3_BYTES(nbseq) (3u * ZH_K3_SLOTS * ZH_K3_SEGLEN(nbseq))
@@ -131,7 +143,7 @@ struct ZhWorkspace {
 __host__ __device__ __forceinline__ u32 zh_k3_magic(u32 L) { return ((1u << 24) + L - 1u) / L; }
 __device__ __forceinline__ u32 zh_k3_index(u32 e, u32 t, u32 L, u32 m) {
   u32 const g = __umulhi(e << 8, m), r = e - g * L;
-  return ((r / ZH_K3_RUN) * ZH_K3_SLOTS + t * ZH_K3_SEGS + g) * ZH_K3_RUN + (r & (ZH_K3_RUN - 1u));
+  return ((r / ZH_K3_RUN) * ZH_K3_SLOTS + ZH_K3_SLOT(t, g)) * ZH_K3_RUN + (r & (ZH_K3_RUN - 1u));
 }
 
 // Status codes written per item (values of cuda_zstd::Status).

@@ -1683,11 +1683,13 @@ __device__ __forceinline__ void k3_chain(ZhWorkspace ws, u32 bb, u8 *smem, u32 l
   u32 const nbSeq = ff[ZH_FF_NBSEQ];
   const u16 *stT = (const u16 *)(smem + (t == 0 ? ZH_FT_STLL : t == 1 ? ZH_FT_STOF : ZH_FT_STML));
   const FseSym *syT = (const FseSym *)(smem + (t == 0 ? ZH_FT_SYLL : t == 1 ? ZH_FT_SYOF : ZH_FT_SYML));
-  // chain layout (zh_common.h): batch k of this lane's segment at element (SLOTS k + lane) * 16
+  // chain layout (zh_common.h): batch k of this lane's segment at element (SLOTS k + slot) * 16
   u32 const seglen = ZH_K3_SEGLEN(nbSeq), nk = seglen / K3_BATCH;
   u16 *const gst = (u16 *)ws.lits(bb);                          // states
   const u8 *const cbase = ws.lits(bb) + ZH_K3_CODES(seglen);    // codes
-  u32 const ln = lane;  // (slots past 3 K3_SEGS exist in the layout and are never read by the packing kernel)
+  // this lane's slot and the slot of the segment before (warm-up codes); slots past 3 K3_SEGS exist
+  // in the layout and are never read by the packing kernel
+  u32 const ln = lane < 3 * K3_SEGS ? ZH_K3_SLOT(t, g) : lane, lnp = ZH_K3_SLOT(t, g - 1u);
   // element of batch k (16 steps) of a slot's segment
   auto at = [&](u32 k, u32 slot) { return ((k * K3_BATCH / ZH_K3_RUN) * ZH_K3_SLOTS + slot) * ZH_K3_RUN + (k * K3_BATCH) % ZH_K3_RUN; };
   auto codes_at = [&](u32 k, u32 slot) { return *(const uint4 *)(cbase + at(k, slot)); };  // batch k's 16 codes
@@ -1719,7 +1721,7 @@ __device__ __forceinline__ void k3_chain(ZhWorkspace ws, u32 bb, u8 *smem, u32 l
     for (u32 j0 = 0; j0 < NW; j0 += CH) {
       uint4 cw[CH];
 #pragma unroll
-      for (u32 j = 0; j < CH; j++) cw[j] = kw + j0 + j < nk ? codes_at(kw + j0 + j, ln - 1) : make_uint4(0, 0, 0, 0);
+      for (u32 j = 0; j < CH; j++) cw[j] = kw + j0 + j < nk ? codes_at(kw + j0 + j, lnp) : make_uint4(0, 0, 0, 0);
 #pragma unroll
       for (u32 j = 0; j < CH; j++) {
         u32 const w[4] = {cw[j].x, cw[j].y, cw[j].z, cw[j].w};
