@@ -1656,6 +1656,8 @@ void lz_launch(const ZhBlockDesc *d_descs, u32 nblocks, ZhWorkspace ws, u32 mode
 // ZH_K1_MODE) over single-block items in[i * stride, + sizes[i]) (each <= ZH_BLOCK_MAX, no
 // dictionary), its raw output copied back: per item ZH_SEQ_CAP records, ZH_LIT_BYTES of the
 // literal area and meta {nseq, nlit, rle}.
+// The per-item sizes zh_test_lz copies back (the caller's buffers are sized from these).
+extern "C" void zh_test_lz_sizes(u32 *seq_cap, u32 *lit_bytes) { *seq_cap = ZH_SEQ_CAP; *lit_bytes = ZH_LIT_BYTES; }
 extern "C" int zh_test_lz(const u8 *d_in, u32 nitems, u32 stride, const u32 *h_sizes, int mode, u64 *h_recs, u8 *h_lits, u32 *h_meta) {
   if (!nitems) return 0;
   std::vector<ZhBlockDesc> descs(nitems);

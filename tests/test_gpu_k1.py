@@ -13,9 +13,7 @@ import zh_testlib as T
 
 pytestmark = pytest.mark.gpu
 
-SEQ_CAP = 13120
 BLOCK = 65536
-LIT_AREA = 122880  # ZH_LIT_BYTES
 K1HIST, K1_HIST_OFF = 2, 65536  # ZH_META_K1HIST, ZH_K1_HIST_OFF (zh_common.h)
 
 
@@ -32,6 +30,10 @@ def k1_raw(datas):
         buf[i * stride:i * stride + len(d)] = d
     dev = torch.from_numpy(buf).cuda()
     sizes = np.array([len(d) for d in datas], dtype=np.uint32)
+    # per-item sizes the hook copies back (ZH_SEQ_CAP, ZH_LIT_BYTES), from the library itself
+    cap, area_b = ctypes.c_uint32(), ctypes.c_uint32()
+    L.zh_test_lz_sizes(ctypes.byref(cap), ctypes.byref(area_b))
+    SEQ_CAP, LIT_AREA = cap.value, area_b.value
     recs = np.zeros(n * SEQ_CAP, dtype=np.uint64)
     lits = np.zeros(n * LIT_AREA, dtype=np.uint8)
     meta = np.zeros(n * 4, dtype=np.uint32)
