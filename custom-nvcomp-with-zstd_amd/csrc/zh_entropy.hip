@@ -149,6 +149,9 @@ struct BitSink {
   u32 pend;  // pending bits in sw[0] (0..7)
 };
 
+#ifndef ZH_SINK_BF
+#define ZH_SINK_BF 1
+#endif
 template <int K>
 __device__ __forceinline__ void sink_append(BitSink &bs, const Out &o, u32 *sw, const u32 (&val)[K], const u32 (&nb)[K]) {
   u32 const lane = lane_id();
@@ -161,6 +164,21 @@ __device__ __forceinline__ void sink_append(BitSink &bs, const Out &o, u32 *sw, 
   u32 const nwords = (end + 31) >> 5;
   for (u32 w = 1 + lane; w < nwords + 1; w += 64) sw[w] = 0;
   wave_sync();
+#if ZH_SINK_BF
+  // branch-free: every field ORs its low part into word bit >> 5 and its high part (0 unless it
+  // straddles) into the next word, which lies inside [1, nwords] (zeroed above) since bit < end;
+  // a field of 0 bits ORs 0.  Field widths are <= 31 (codes, states, extra bits), so v_bfe masks.
+  u32 *const swa = sw;
+#pragma unroll
+  for (int k = 0; k < K; k++) {
+    u32 const v = __builtin_amdgcn_ubfe(val[k], 0u, nb[k]);
+    u32 *const wp = swa + (bit >> 5);
+    u32 const sh = bit & 31u;
+    __hip_atomic_fetch_or(wp, v << sh, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    __hip_atomic_fetch_or(wp + 1, (v >> 1) >> (31u - sh), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    bit += nb[k];
+  }
+#else
 #pragma unroll
   for (int k = 0; k < K; k++) {
     if (nb[k]) {
@@ -171,6 +189,7 @@ __device__ __forceinline__ void sink_append(BitSink &bs, const Out &o, u32 *sw, 
       bit += nb[k];
     }
   }
+#endif
   wave_sync();
   u32 const full = end >> 3;
   const u8 *sb = (const u8 *)sw;
