@@ -543,9 +543,21 @@ def main():
                          "process may keep busy (affinity, capped by the cgroup quota and the pool share OMP_NUM_THREADS)")
     args = ap.parse_args()
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    from cuda_zstd import launch
+
+    if args.gpus < 1:
+        sys.exit(f"bench.py: --gpus must be >= 1 (got {args.gpus})")
+    if not launch.rank_env_present():
+        if args.gpus > 1:
+            # C4 without a launcher around us: start one rank per GPU as child processes (before
+            # any GPU call here, no exec) and pass rank 0's line through
+            ndev = launch.visible_gpus()
+            if args.gpus > ndev:
+                sys.exit(f"bench.py: --gpus {args.gpus} but only {ndev} GPU(s) are visible")
+            sys.exit(launch.spawn_ranks(args.gpus, os.path.abspath(__file__), sys.argv[1:]))
+    rank, local, world = launch.rank_env()
+    if world != args.gpus:
+        print(f"bench.py: WORLD_SIZE={world} from the launcher overrides --gpus {args.gpus}", file=sys.stderr)
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
     torch.cuda.set_device(local)

@@ -7,6 +7,18 @@
 // (src/cuda_zstd_manager.cu:2328-3112).
 #include <hip/hip_runtime.h>
 #include <dlfcn.h>
+// AddressSanitizer refuses RTLD_DEEPBIND dlopens: sanitizer builds of the host code
+// open libzstd without it
+#if defined(__SANITIZE_ADDRESS__)
+#define ZH_DLOPEN_DEEPBIND 0
+#elif defined(__has_feature)
+#if __has_feature(address_sanitizer)
+#define ZH_DLOPEN_DEEPBIND 0
+#endif
+#endif
+#ifndef ZH_DLOPEN_DEEPBIND
+#define ZH_DLOPEN_DEEPBIND RTLD_DEEPBIND
+#endif
 
 #include <algorithm>
 #include <chrono>
@@ -199,7 +211,7 @@ struct LibZstd {
     for (const char *nm : names) {
       // RTLD_DEEPBIND: a libzstd opened here binds its own calls inside itself even when another
       // libzstd image sits in the global scope (a preloaded tool's), never mixing two versions
-      void *h = dlopen(nm, RTLD_NOW | RTLD_LOCAL | RTLD_DEEPBIND);
+      void *h = dlopen(nm, RTLD_NOW | RTLD_LOCAL | ZH_DLOPEN_DEEPBIND);
       if (!h) continue;
       compress = (decltype(compress))dlsym(h, "ZSTD_compress");
       decompress = (decltype(decompress))dlsym(h, "ZSTD_decompress");
@@ -835,6 +847,7 @@ Status ZstdBatchManager::set_dictionary(const dictionary::Dictionary &d) {
 // reference :3858-3863: no dictionary -> ERROR_INVALID_PARAMETER; else a deep copy (the caller
 // frees dict.raw_content with free(), Dictionary's copy semantics)
 Status ZstdBatchManager::get_dictionary(dictionary::Dictionary &d) const {
+  std::lock_guard<std::mutex> lock(pimpl_->api_mutex);  // set_dictionary swaps mgr_dict under it
   if (!pimpl_->has_dict) return Status::ERROR_INVALID_PARAMETER;
   dictionary::Dictionary view;
   view.header = pimpl_->dict_hdr;
@@ -1236,15 +1249,25 @@ Status ZstdStreamingManager::decompress_chunk(const void *in, size_t n, void *ou
   // in this manager, or init_decompression_with_history) has history frames, and those carry no
   // Dictionary_ID: a frame naming the dictionary, or any frame outside a history session -- a
   // formatted dictionary's frame written without its ID (libzstd dictIDFlag 0) included -- decodes
-  // with the dictionary.
-  bool hist_frame = true;
+  // with the dictionary.  History frames therefore need init_decompression_with_history (ADVICE
+  // r5): outside a history session an ID-less frame with a content checksum that fails against the
+  // dictionary is decoded once more against the window, and kept if its checksum holds there; an
+  // ID-less frame without a checksum cannot be told apart and decodes with the dictionary.
+  bool hist_frame = true, retry_hist = false;
   if (pimpl_->has_dict) {
     FrameProbe fp;
-    hist_frame = pimpl_->hist_mode && probe_frame(in, n, fp) == Status::SUCCESS && fp.dict_id == 0;
+    bool const probed = probe_frame(in, n, fp) == Status::SUCCESS;
+    hist_frame = pimpl_->hist_mode && probed && fp.dict_id == 0;
+    retry_hist = !pimpl_->hist_mode && probed && fp.dict_id == 0 && fp.checksum && pimpl_->dhist.n;
   }
   bool const use_hist = pimpl_->dhist.n && hist_frame;
+  size_t const cap = *out_size;
   s = pimpl_->mgr.decompress_with_history(in, n, out, out_size, pimpl_->ws, pimpl_->ws_size, use_hist ? pimpl_->dhist.data() : nullptr,
                                           use_hist ? pimpl_->dhist.n : 0, stream);
+  if (s == Status::ERROR_CHECKSUM_FAILED && retry_hist) {
+    *out_size = cap;
+    s = pimpl_->mgr.decompress_with_history(in, n, out, out_size, pimpl_->ws, pimpl_->ws_size, pimpl_->dhist.data(), pimpl_->dhist.n, stream);
+  }
   if (s == Status::SUCCESS) s = pimpl_->dhist.append(out, *out_size, stream);
   return s;
 }
@@ -2011,7 +2034,7 @@ cuda_zstd_dict_t *cuda_zstd_train_dictionary(const void **samples, const size_t 
       s.emplace_back((const u8 *)samples[i], sizes[i]);
     }
     std::vector<u8> c = zh::cover_train(s, std::min(dict_size, zh::kDictMaxBytes));
-    if (c.empty()) return nullptr;
+    if (c.size() < dictionary::MIN_DICT_SIZE) return nullptr;  // (set_dictionary would refuse it)
     auto *d = new cuda_zstd_dict_t;
     d->set(std::move(c), 0);
     return d;
@@ -2023,7 +2046,9 @@ void cuda_zstd_destroy_dictionary(cuda_zstd_dict_t *d) { delete d; }
 // reference DictionaryManager::load_dictionary (include/cuda_zstd_dictionary.h:292-310): a host
 // buffer with raw content or a formatted dictionary (e.g. ZDICT_trainFromBuffer's)
 cuda_zstd_dict_t *cuda_zstd_load_dictionary(const void *buffer, size_t size) {
-  if (!buffer || size == 0 || size > zh::kDictMaxBytes) return nullptr;
+  // the managers' set_dictionary limits (MIN_DICT_SIZE .. MAX_DICT_SIZE, reference
+  // src/cuda_zstd_manager.cu:3711-3736) apply here already, so a handle is always settable
+  if (!buffer || size < dictionary::MIN_DICT_SIZE || size > zh::kDictMaxBytes) return nullptr;
   u32 id = 0;
   size_t off = 0;
   if (!zh::dict_layout((const u8 *)buffer, size, id, off)) return nullptr;

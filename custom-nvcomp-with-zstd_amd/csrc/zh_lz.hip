@@ -41,8 +41,8 @@
 #include <algorithm>
 #include <vector>
 
-#ifdef ZH_STAMPS
-__device__ u32 g_fixups;  // diagnostic: inserter read-back fix-up rounds (all blocks)
+#if defined(ZH_STAMPS) || defined(ZH_INS_CHECK)
+__device__ u32 g_fixups;  // diagnostic: inserter read-back repairs (all blocks; tests/test_gpu_k1.py)
 extern "C" __global__ void zh_read_fixups(u32 *out) { *out = g_fixups; g_fixups = 0; }
 extern "C" u32 zh_fixups_host() {
   u32 *d = nullptr, h = 0;
@@ -349,9 +349,7 @@ __device__ __forceinline__ void insert_window(const u32 *in32, u16 *T, u32 wsb, 
 #pragma unroll
       for (u32 k = 0; k < TPL; k++) lost |= h[b][k] != JUNK && r[b][k] < tb0 + b * ZH_TILE + 64 * k + lane + 1;
     if (__ballot(lost)) {
-#ifdef ZH_STAMPS
       if (lane == 0) atomicAdd(&g_fixups, 1u);
-#endif
       insert_repair<LONG, BT>(T, tb0, lane, h, e);
     }
 #endif
@@ -1002,6 +1000,10 @@ __device__ __forceinline__ u32 k1_tid(u32 w) {
 __device__ __forceinline__ bool repeat_scan(const u32 *in32, u32 *E, u32 *hw, u32 *misc, u32 pre, u32 n, u32 tid) {
   static_assert(ZH_SCAN_STRIDE == 4 && (4u << ZH_SCAN_LOG) <= 2 * (HL_SIZE + HS_SIZE + 2 * T_PAD), "scan table in the hash tables' space");
   static_assert(K1_THREADS / 64 == ZH_K1_HIST_WAVES && 4 * 256 * ZH_K1_HIST_WAVES <= 2 * 4 * CI_WORDS, "sub-histograms in the cinfo space");
+  // the clears below take no barrier first: with one probe window the window loop is left right
+  // after barrier P, when no inserter is inside a window (with 2-3, probe_dead fires at a step's
+  // top while an inserter that took X in take_ready may still write TL) -- ADVICE r5
+  static_assert(ZH_PROBE_WINDOWS == 1, "repeat_scan reuses the hash tables without a barrier");
   constexpr u32 NS = 1u << ZH_SCAN_LOG;
   u32 const lim = n > ZH_HASH_READ ? n - ZH_HASH_READ : 0u, lane = tid & 63u, wave = tid >> 6;
   // slot and signature of a position's long-hash sum t: E[t >> 18], entry (t << 14) & ~0xFFFF | q

@@ -52,13 +52,14 @@ class ShardPlan:
             self._keep[device] = k
         return k
 
-    def gather_offsets(self, local_sizes, group=None):
+    def gather_offsets(self, local_sizes, group=None, force_collective=False):
         """All-gather this rank's per-chunk sizes (padded to q) -> (all_sizes[n_total],
-        exclusive offsets[n_total]) in global chunk order."""
+        exclusive offsets[n_total]) in global chunk order.  A one-rank plan skips the
+        collective unless force_collective (the RCCL test drives the gather at world 1)."""
         import torch
         import torch.distributed as dist
 
-        if self.world == 1:
+        if self.world == 1 and not force_collective:
             all_sizes = local_sizes.clone()
         else:
             n = local_sizes.numel()

@@ -45,7 +45,9 @@ int cuda_zstd_set_dictionary(cuda_zstd_manager_t *manager, cuda_zstd_dict_t *dic
 /* dictionaries: cuda_zstd_train_dictionary is COVER training (raw content);
  * load = raw content or a formatted RFC 8878 §5 dictionary from a host buffer (reference
  * DictionaryManager::load_dictionary, include/cuda_zstd_dictionary.h:292); content copies the
- * bytes out (returns the size); layout gives the Dictionary_ID and content offset (0, 0 for raw) */
+ * bytes out (returns the size); layout gives the Dictionary_ID and content offset (0, 0 for raw).
+ * Both return NULL for a dictionary outside 256 B .. 128 KiB (MIN/MAX_DICT_SIZE, the limits
+ * cuda_zstd_set_dictionary enforces), so every handle they return can be set on a manager */
 cuda_zstd_dict_t *cuda_zstd_load_dictionary(const void *buffer, size_t size);
 size_t cuda_zstd_get_dictionary_content(const cuda_zstd_dict_t *dict, void *out, size_t capacity);
 int cuda_zstd_get_dictionary_layout(const cuda_zstd_dict_t *dict, unsigned int *dict_id, size_t *content_offset);

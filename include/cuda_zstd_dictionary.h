@@ -104,7 +104,8 @@ struct Dictionary {
 Status train_dictionary(const std::vector<const void *> &samples, const std::vector<size_t> &sample_sizes, void *dict_buffer,
                         size_t dict_size, const DictionaryTrainingParams *params = nullptr, hipStream_t stream = 0);
 // samples as one buffer with start offsets; sample i ends where i + 1 starts, the last one after
-// 8 KiB (reference src/cuda_zstd_dictionary.cu:475-503)
+// 8 KiB (reference src/cuda_zstd_dictionary.cu:475-503): the caller's buffer must hold at least
+// sample_offsets[num_samples - 1] + 8192 bytes, whatever the last sample's real length
 Status create_dictionary_from_samples(const void *samples_buffer, const size_t *sample_offsets, size_t num_samples, void *dict_buffer,
                                       size_t dict_size, const DictionaryTrainingParams *params = nullptr, hipStream_t stream = 0);
 // ~1 % of the data, clamped to [MIN_DICT_SIZE, MAX_DICT_SIZE], rounded up to a KiB

@@ -269,12 +269,15 @@ int main(int argc, char **argv) {
     dump(dir + "/back.bin", back.data(), back.size());  // (frames.bin stays empty: fsz 0)
   } else if (mode == "stream_split") {
     // advisor r3: frames from compress_chunk_with_history in one manager (dictionary set),
-    // decoded by a SECOND, decode-only manager with the same dictionary set.  <flag> = 1: the
-    // decoder calls init_decompression_with_history (needed for a raw-content dictionary, whose
-    // frames carry Dictionary_ID 0 like history frames); 0: a formatted dictionary's frames are
-    // told apart by their header alone.
+    // decoded by a SECOND, decode-only manager with the same dictionary set.  History frames carry
+    // no Dictionary_ID, like a raw-content dictionary's frames or a formatted one's written without
+    // its ID, so the decoder must be told the session has history.  <flag> = 1: the decoder calls
+    // init_decompression_with_history; 2: it does not (plain init_decompression), and the frames
+    // carry a content checksum: each ID-less frame fails its checksum against the dictionary and
+    // is decoded again against the window (an explicit outcome, never silent bytes).
     if (argc < 4) return 1;
-    bool const flag = std::stoul(argv[3]) != 0;
+    unsigned const mode_f = (unsigned)std::stoul(argv[3]);
+    bool const flag = mode_f == 1;
     std::vector<char> db = slurp(dir + "/dict.bin");
     // the reference's caller shape (tests/test_dictionary_memory.cu:174-176): a view of the
     // caller's bytes; the header's ID is the caller's (frames carry the content's RFC ID)
@@ -282,7 +285,9 @@ int main(int argc, char **argv) {
     dct.raw_content = (unsigned char *)db.data();
     dct.raw_size = (u32)db.size();
     dct.header.dictionary_id = 12345;
-    ZstdStreamingManager enc(CompressionConfig::from_level(3)), dec(CompressionConfig::from_level(3));
+    CompressionConfig ecfg = CompressionConfig::from_level(3);
+    if (mode_f == 2) ecfg.checksum = ChecksumPolicy::COMPUTE_AND_VERIFY;
+    ZstdStreamingManager enc(ecfg), dec(CompressionConfig::from_level(3));
     Status st = enc.set_dictionary(dct);
     if (st == Status::SUCCESS) st = dec.set_dictionary(dct);
     if (st == Status::SUCCESS) st = enc.init_compression_with_history(0, 0);

@@ -198,12 +198,15 @@ def test_cxx_extra_surface(tmp_path, libzstd, formatted):
         assert T.zstd_decompress(f, len(d), dictionary=dct) == d.tobytes()
 
 
-@pytest.mark.parametrize("formatted,flag", [(True, 1), (False, 1)])
+@pytest.mark.parametrize("formatted,flag", [(True, 1), (False, 1), (True, 2), (False, 2)])
 def test_streaming_history_second_manager(tmp_path, libzstd, formatted, flag):
     """Frames from compress_chunk_with_history (dictionary set) decode in a SECOND, decode-only
     streaming manager with the same dictionary (advisor r3) once it is told the session has history
-    (init_decompression_with_history): history frames carry no Dictionary_ID, and neither does a
-    dictionary frame written without one (test_streaming_idless_dictionary_frames)."""
+    (init_decompression_with_history, flag 1): history frames carry no Dictionary_ID, and neither
+    does a dictionary frame written without one (test_streaming_idless_dictionary_frames).
+    flag 2: the decoder is NOT told (plain init_decompression) and the frames carry a
+    content checksum; each fails it against the dictionary and is decoded again against the decoded
+    window, so the bytes come back right instead of silently wrong."""
     recs = [T.gen(T.DG_JSON, 1, 0x5EED0005, 16384, first=i) for i in range(64)]
     dct = T.zdict_train(recs, 32768) if formatted else b"".join(r.tobytes() for r in recs[:2])
     datas = [T.gen(T.DG_JSON, 1, 0x5EED0005, n, first=300 + i) for i, n in enumerate([16384, 40000, 65536, 777, 30000])]

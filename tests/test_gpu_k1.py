@@ -192,3 +192,30 @@ def test_k1_special_and_ragged_vs_oracle():
         names.append(f"text{n}")
         datas.append(T.gen(T.DG_TEXT, 1, int(rng.integers(1 << 30)), 65536)[:n].copy())
     _compare(datas, names)
+
+
+def test_ins_check_variant_never_repairs(tmp_path):
+    """The determinism guard (DESIGN §2 K1 inserters): K1's hash tables rely on
+    gfx950 leaving the highest lane's value when lanes of one ds_write_b16 hit the same slot.  The
+    -DZH_INS_CHECK build reads every slot back and repairs a lost store.  Run the C3 sample and the
+    corpora batch through that build (child process, CUDA_ZSTD_HIP_LIB): the repair path must fire 0
+    times and its frames must equal this (default) build's."""
+    import os
+    import subprocess
+    import sys
+
+    import ins_check_data as D
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    so = os.path.join(root, "custom-nvcomp-with-zstd_amd", "libcuda_zstd_hip_inscheck.so")
+    assert os.path.exists(so), "build() makes the check variant"
+    env = dict(os.environ, CUDA_ZSTD_HIP_LIB=so)
+    out = tmp_path / "ic.npz"
+    subprocess.run([sys.executable, os.path.join(root, "tests", "ins_check_worker.py"), str(out)], env=env, check=True, timeout=300)
+    r = np.load(out)
+    assert int(r["repairs"][0]) == 0, "the inserter repair path fired: same-slot lane order differs from the oracle's"
+    for level in D.LEVELS:
+        want = D.compress(level)
+        sizes = r[f"sizes{level}"]
+        assert sizes.tolist() == [len(f) for f in want], level
+        assert r[f"frames{level}"].tobytes() == b"".join(want), level

@@ -63,7 +63,8 @@ def datagen():
 # global scope when a preloaded tool links it (rocprofv3's libraries do) -- and without it the
 # library's PLT calls (ZSTD_freeCCtx's frees among them) resolved into the other image's 1.4.8
 # code and layouts: the r04f SIGSEGV in free <- ZSTD_freeCCtx under the profiler.
-LIBZSTD_MODE = os.RTLD_NOW | os.RTLD_LOCAL | getattr(os, "RTLD_DEEPBIND", 0)
+# AddressSanitizer refuses RTLD_DEEPBIND dlopens: a sanitizer run sets ZH_NO_DEEPBIND=1.
+LIBZSTD_MODE = os.RTLD_NOW | os.RTLD_LOCAL | (0 if os.environ.get("ZH_NO_DEEPBIND") else getattr(os, "RTLD_DEEPBIND", 0))
 
 
 def find_libzstd():

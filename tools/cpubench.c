@@ -13,6 +13,17 @@
  */
 #define _GNU_SOURCE
 #include <dlfcn.h>
+/* AddressSanitizer refuses RTLD_DEEPBIND dlopens: sanitizer builds open libzstd without it */
+#if defined(__SANITIZE_ADDRESS__)
+#define CPB_DEEPBIND 0
+#elif defined(__has_feature)
+#if __has_feature(address_sanitizer)
+#define CPB_DEEPBIND 0
+#endif
+#endif
+#ifndef CPB_DEEPBIND
+#define CPB_DEEPBIND RTLD_DEEPBIND
+#endif
 #include <pthread.h>
 #include <sched.h>
 #include <stdatomic.h>
@@ -44,7 +55,7 @@ static int load(void) {
   if (Z.ok) return 0;
   const char *names[] = {"libzstd.so.1", "/opt/conda/lib/libzstd.so.1", "/usr/lib/x86_64-linux-gnu/libzstd.so.1", "libzstd.so"};
   for (unsigned i = 0; i < sizeof(names) / sizeof(names[0]); i++) {
-    void *h = dlopen(names[i], RTLD_NOW | RTLD_LOCAL | RTLD_DEEPBIND);  /* (one image, see tests/zh_testlib.py) */
+    void *h = dlopen(names[i], RTLD_NOW | RTLD_LOCAL | CPB_DEEPBIND);  /* (one image, see tests/zh_testlib.py) */
     if (!h) continue;
     Z.create_c = (create_fn)dlsym(h, "ZSTD_createCCtx");
     Z.create_d = (create_fn)dlsym(h, "ZSTD_createDCtx");
