@@ -1250,21 +1250,21 @@ Status ZstdStreamingManager::decompress_chunk(const void *in, size_t n, void *ou
   // Dictionary_ID: a frame naming the dictionary, or any frame outside a history session -- a
   // formatted dictionary's frame written without its ID (libzstd dictIDFlag 0) included -- decodes
   // with the dictionary.  History frames therefore need init_decompression_with_history (ADVICE
-  // r5): outside a history session an ID-less frame with a content checksum that fails against the
-  // dictionary is decoded once more against the window, and kept if its checksum holds there; an
-  // ID-less frame without a checksum cannot be told apart and decodes with the dictionary.
+  // r5): outside a history session an ID-less frame that fails against the dictionary (corrupt, or
+  // its content checksum does not hold) is decoded once more against the window; an ID-less frame
+  // without a checksum that decodes against the dictionary cannot be told apart and is kept.
   bool hist_frame = true, retry_hist = false;
   if (pimpl_->has_dict) {
     FrameProbe fp;
     bool const probed = probe_frame(in, n, fp) == Status::SUCCESS;
     hist_frame = pimpl_->hist_mode && probed && fp.dict_id == 0;
-    retry_hist = !pimpl_->hist_mode && probed && fp.dict_id == 0 && fp.checksum && pimpl_->dhist.n;
+    retry_hist = !pimpl_->hist_mode && probed && fp.dict_id == 0 && pimpl_->dhist.n;
   }
   bool const use_hist = pimpl_->dhist.n && hist_frame;
   size_t const cap = *out_size;
   s = pimpl_->mgr.decompress_with_history(in, n, out, out_size, pimpl_->ws, pimpl_->ws_size, use_hist ? pimpl_->dhist.data() : nullptr,
                                           use_hist ? pimpl_->dhist.n : 0, stream);
-  if (s == Status::ERROR_CHECKSUM_FAILED && retry_hist) {
+  if ((s == Status::ERROR_CHECKSUM_FAILED || s == Status::ERROR_CORRUPT_DATA) && retry_hist) {
     *out_size = cap;
     s = pimpl_->mgr.decompress_with_history(in, n, out, out_size, pimpl_->ws, pimpl_->ws_size, pimpl_->dhist.data(), pimpl_->dhist.n, stream);
   }

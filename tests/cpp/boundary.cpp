@@ -273,8 +273,8 @@ int main(int argc, char **argv) {
     // no Dictionary_ID, like a raw-content dictionary's frames or a formatted one's written without
     // its ID, so the decoder must be told the session has history.  <flag> = 1: the decoder calls
     // init_decompression_with_history; 2: it does not (plain init_decompression), and the frames
-    // carry a content checksum: each ID-less frame fails its checksum against the dictionary and
-    // is decoded again against the window (an explicit outcome, never silent bytes).
+    // carry a content checksum: each ID-less frame fails against the dictionary (corrupt or a
+    // wrong checksum) and is decoded again against the window (an explicit outcome, never silent bytes).
     if (argc < 4) return 1;
     unsigned const mode_f = (unsigned)std::stoul(argv[3]);
     bool const flag = mode_f == 1;

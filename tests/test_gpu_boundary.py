@@ -205,8 +205,8 @@ def test_streaming_history_second_manager(tmp_path, libzstd, formatted, flag):
     (init_decompression_with_history, flag 1): history frames carry no Dictionary_ID, and neither
     does a dictionary frame written without one (test_streaming_idless_dictionary_frames).
     flag 2: the decoder is NOT told (plain init_decompression) and the frames carry a
-    content checksum; each fails it against the dictionary and is decoded again against the decoded
-    window, so the bytes come back right instead of silently wrong."""
+    content checksum; each fails against the dictionary (corrupt, or a wrong checksum) and is decoded
+    again against the decoded window, so the bytes come back right instead of silently wrong."""
     recs = [T.gen(T.DG_JSON, 1, 0x5EED0005, 16384, first=i) for i in range(64)]
     dct = T.zdict_train(recs, 32768) if formatted else b"".join(r.tobytes() for r in recs[:2])
     datas = [T.gen(T.DG_JSON, 1, 0x5EED0005, n, first=300 + i) for i, n in enumerate([16384, 40000, 65536, 777, 30000])]
