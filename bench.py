@@ -344,7 +344,11 @@ def level_leg(host, dev, level, steps, threads):
     ok = int((b.status != 0).sum().item()) == 0
     comp = int(b.out_sizes.sum().item())
     gbs = b.n * CHUNK / (ms / 1e3) / 1e9
+    n1k = min(b.n, 1024)
+    comp1k = int(b.out_sizes[:n1k].sum().item())
     res = {"value": round(gbs, 3), "unit": "GB/s", "ms_per_step": round(ms, 3), "ratio": round(b.n * CHUNK / comp, 4), "status_ok": ok,
+           # (on the chunks libzstd's line below compresses: the like-for-like ratio)
+           "ratio_first_1024": round(n1k * CHUNK / comp1k, 4) if comp1k else None,
            "workload": f"C3 mix: {b.n} x 64 KiB chunks, level {level}", "roofline": leg_roofline(b.n * CHUNK + comp, kms, launches)}
     res["libzstd_verified"] = libzstd_roundtrip(b.d_out.cpu().numpy(), b.out_sizes.cpu().numpy(), b.slot, host)
     del b

@@ -719,6 +719,125 @@ __device__ __forceinline__ void span_lengths(const u32 *in32, u32 *ci, u64 *tm, 
   }
 }
 
+// ---- level 1 (mode 2): lengths at every ZH_L1_STRIDE-th position ------------------------------
+// Oracle orc_lz_parse_pre with orc_lz_mode 2: only positions p = 0 mod S of the staged buffer take
+// a match (the short table still holds every position).  Round r of a window covers positions
+// 64 S r + S lane; along same-offset chains (the candidate of p + S is the candidate of p plus S)
+// lcp(p) = S + lcp(p + S), so pass C's chain distance counts S bytes per lane.  Greedy: the take
+// mask is the nonzero match info, spread to every S-th bit of the window's 64-position mask words.
+constexpr u32 L1_S = ZH_L1_STRIDE;
+constexpr u32 NROUND1 = NROUND / L1_S;  // length rounds per window
+static_assert(L1_S == 1 || L1_S == 2 || L1_S == 4, "level-1 stride");
+// 64-bit take ballot of a round -> the S mask words of its 64 S positions (bit j -> bit S j)
+__device__ __forceinline__ u64 spread_bits(u64 v, u32 s) {
+  if (s == 2) {
+    v = (v | (v << 16)) & 0x0000FFFF0000FFFFull;
+    v = (v | (v << 8)) & 0x00FF00FF00FF00FFull;
+    v = (v | (v << 4)) & 0x0F0F0F0F0F0F0F0Full;
+    v = (v | (v << 2)) & 0x3333333333333333ull;
+    v = (v | (v << 1)) & 0x5555555555555555ull;
+  } else if (s == 4) {
+    v = (v | (v << 24)) & 0x000000FF000000FFull;
+    v = (v | (v << 12)) & 0x000F000F000F000Full;
+    v = (v | (v << 6)) & 0x0303030303030303ull;
+    v = (v | (v << 3)) & 0x1111111111111111ull;
+  }
+  return v;
+}
+__device__ __forceinline__ void span_lengths_l1(const u32 *in32, u32 *ci, u64 *tm, u16 *xq, u32 r_lo, u32 r_hi, u32 wsb, u32 n, u32 lane) {
+  constexpr u32 S = L1_S;
+  u32 cwr[MAX_RW], flg[MAX_RW], olo[MAX_RW], ohi[MAX_RW], Sw[MAX_RW][3];
+  auto loadA = [&](u32 k) {
+    u32 const r = r_hi - 1 - min(k, r_hi - 1 - r_lo), i = 64 * S * r + S * lane, p = wsb + i;
+    u32 const cw = ci[cidx(i)];
+    cwr[k] = cw;
+    ld64u(in32, p, olo[k], ohi[k]);
+    u32 const aS = ((cw >> 16) + 0xFFFFu) >> 2 & 0x3FFFu;  // (an empty candidate: see span_lengths)
+#pragma unroll
+    for (u32 t = 0; t < 3; t++) Sw[k][t] = in32[aS + t];
+  };
+  u32 ccS = 0, nq = 0;
+#pragma unroll
+  for (u32 k = 0; k < MAX_RW; k++) {
+    flg[k] = 0;
+    if (r_lo + k >= r_hi) { cwr[k] = 0; continue; }
+    loadA(k);
+    u32 const r = r_hi - 1 - k, i = 64 * S * r + S * lane;
+    u32 const cS = cwr[k] >> 16;
+    u32 const sh = (cS - 1u) & 3u;
+    u32 const x = olo[k] ^ __builtin_amdgcn_alignbyte(Sw[k][1], Sw[k][0], sh), y = ohi[k] ^ __builtin_amdgcn_alignbyte(Sw[k][2], Sw[k][1], sh);
+    u32 const pS = min(ffbl_raw(x), min(ffbl_raw(y), 32u) + 32u) >> 3;
+    u32 cSn = wave_shl1(cS);
+    cSn = lane == 63 ? ccS : cSn;
+    bool const fS = pS == 8 && cSn == cS + S;
+    bool const xS = pS == 8 && !fS;
+    flg[k] = (pS << 4) | (fS ? LF_FS : 0u) | (xS ? LF_XS : 0u);
+    ccS = lane_value(cS, 0);
+    u64 const bS = __ballot(xS);
+    u32 const rS = __builtin_amdgcn_mbcnt_hi((u32)(bS >> 32), __builtin_amdgcn_mbcnt_lo((u32)bS, 0u));
+    xq[xS ? nq + rS : XQ_CAP - 1] = (u16)(i | 0x8000u);
+    nq = (u32)__builtin_amdgcn_readfirstlane(nq + (u32)__popcll(bS));
+    while (nq >= 64) {
+      nq -= 64;
+      xq_flush(in32, ci, xq + nq, 64, wsb, lane);
+    }
+  }
+  if (nq) xq_flush(in32, ci, xq, nq, wsb, lane);
+  u32 lSr[MAX_RW], runs[MAX_RW];
+#pragma unroll
+  for (u32 k = 0; k < MAX_RW; k++) {
+    u32 const r = r_hi - 1 - min(k, r_hi - 1 - r_lo), i = 64 * S * r + S * lane;
+    u32 const f = flg[k];
+    u32 const ce = ci[cidx(i)];
+    u32 const eS = (f & LF_XS) ? ((ce >> 16) & 255u) : ((f >> 4) & 15u);
+    u64 const RS = __ballot(!(f & LF_FS)) >> lane;
+    u32 const qS = RS ? ctz64(RS) : 64u - lane;
+    u32 const vS = bperm(eS, min(lane + qS, 63u));
+    lSr[k] = RS ? min((u32)ZH_MAX_MATCH, S * qS + vS) : S * qS;
+    runs[k] = RS ? 0u : 2u;
+  }
+  u32 clS = 0;
+#pragma unroll
+  for (u32 k = 0; k < MAX_RW; k++) {
+    if (r_lo + k >= r_hi) continue;
+    u32 const r = r_hi - 1 - k, i = 64 * S * r + S * lane, p = wsb + i;
+    u32 const cS = cwr[k] >> 16;
+    u32 const lS = (runs[k] & 2u) ? min((u32)ZH_MAX_MATCH, lSr[k] + clS) : lSr[k];
+    clS = lane_value(lS, 0);
+    u32 const capj = min((u32)ZH_MAX_MATCH, n - min(p, n));
+    u32 const rS = min(lS, capj);
+    u32 const mS = (cS && rS >= ZH_MIN_MATCH_SHORT) ? rS : 0u;
+    u32 const v = mS ? ((p - (cS - 1u)) << 8) | mS : 0u;
+    ci[cidx(i)] = v;
+    u64 const tb = __ballot(v != 0);
+    if (lane == 0) {
+#pragma unroll
+      for (u32 s = 0; s < S; s++) tm[S * r + s] = S == 1 ? tb : spread_bits((tb >> (64 / S * s)) & ((1ull << (64 / S)) - 1ull), S);
+    }
+  }
+}
+// Rounds of worker wave w in a level-1 window (NROUND1 = 16 over waves 1..13; SIMDs 2 and 0,
+// whose fourth wave is the idle long-table inserter / the parse, take the extra rounds)
+constexpr u64 ROUND_TAB1 = 0x5556664ull;  // 2 bits per wave: 0 1 2 1 2 1 2 1 1 1 1 1 1 1
+static_assert(L1_S != 2 || (((ROUND_TAB1 >> 2) & 3) + ((ROUND_TAB1 >> 4) & 3) + ((ROUND_TAB1 >> 6) & 3) + ((ROUND_TAB1 >> 8) & 3) +
+                            ((ROUND_TAB1 >> 10) & 3) + ((ROUND_TAB1 >> 12) & 3) + ((ROUND_TAB1 >> 14) & 3) + ((ROUND_TAB1 >> 16) & 3) +
+                            ((ROUND_TAB1 >> 18) & 3) + ((ROUND_TAB1 >> 20) & 3) + ((ROUND_TAB1 >> 22) & 3) + ((ROUND_TAB1 >> 24) & 3) +
+                            ((ROUND_TAB1 >> 26) & 3)) == NROUND1, "level-1 round table covers the window");
+template <u32 MODE>
+__device__ __forceinline__ u32 rounds_of_mode(u32 w) {
+  if constexpr (MODE == 2 && L1_S == 2) {
+#ifdef ZH_RTAB1
+    return (u32)(((unsigned long long)(ZH_RTAB1) >> (2 * w)) & 3u);
+#else
+    return (u32)((ROUND_TAB1 >> (2 * w)) & 3u);
+#endif
+  } else if constexpr (MODE == 2 && L1_S == 4) {
+    return w >= 1 && w <= 8 ? 1u : 0u;
+  } else {
+    return rounds_of(w);
+  }
+}
+
 // Match info of one position from scratch (the lookahead positions `we`, `we + 1` of the
 // next window, which the next window's rounds compute again): c = candidate word.
 template <u32 MODE>
@@ -1270,8 +1389,8 @@ __device__ __forceinline__ u32 lz_block(const ZhBlockDesc *__restrict__ blocks, 
   u32 const tid_ = tid;
   u32 const wave = tid >> 6;
   u32 r_lo = 0;
-  for (u32 w = 0; w < wave; w++) r_lo += rounds_of(w);
-  u32 const r_hi = r_lo + rounds_of(wave);
+  for (u32 w = 0; w < wave; w++) r_lo += rounds_of_mode<MODE>(w);
+  u32 const r_hi = r_lo + rounds_of_mode<MODE>(wave);
   u32 *const ci0 = ci;
   u32 *const sgm = (u32 *)(smem + OFF_SEGM);
   u32 *const lbx = (u32 *)(smem + OFF_LB);
@@ -1321,11 +1440,18 @@ __device__ __forceinline__ u32 lz_block(const ZhBlockDesc *__restrict__ blocks, 
     static_assert(RS < NWW && (RS & 1) == 0, "miss-skip rounds");
     bool const skipk = have && skip_window_eff(misc, k, kskip0);
     if (skipk && wave != 0) {
-      if (wave <= RS) span_lengths<MODE>(in32, ciK, tmK, xq, wave - 1, wave, wsb, we, n, lim, lane, wave == RS, 0u);
+      if constexpr (MODE == 2) {
+        if (wave <= RS / L1_S) span_lengths_l1(in32, ciK, tmK, xq, wave - 1, wave, wsb, n, lane);
+      } else {
+        if (wave <= RS) span_lengths<MODE>(in32, ciK, tmK, xq, wave - 1, wave, wsb, we, n, lim, lane, wave == RS, 0u);
+      }
       for (u32 r = RS + wave - 1; r < NROUND; r += NWW - 1) {
         ciK[cidx(64 * r + lane)] = 0;
         if (lane == 0) tmK[r] = 0;
       }
+      ZH_STAMP(st_B);
+    } else if (MODE == 2 && have && wave != 0) {
+      if (r_lo < r_hi) span_lengths_l1(in32, ciK, tmK, xq, r_lo, r_hi, wsb, n, lane);
       ZH_STAMP(st_B);
     } else if (have && wave != 0) {
       // the window's top span (wave 13) first takes the lookahead position `we`: the take

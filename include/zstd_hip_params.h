@@ -58,6 +58,16 @@
  * mix (256 chunks; libzstd at that level): mode 2 2.647 (L1 2.534), mode 1 2.682 (L2 2.673),
  * mode 0 2.796 (L3 2.791). */
 #define ZH_K1_MODE(level) ((level) <= 1 ? 2 : (level) == 2 ? 1 : 0)
+/* Level 1's search stride (mode 2; libzstd fast's idea of not searching every
+ * position): every position is still inserted into the short table, but only positions
+ * p = 0 mod ZH_L1_STRIDE of the staged buffer look a match up -- a repeat is found at most
+ * ZH_L1_STRIDE - 1 bytes late and the catch-up takes those bytes back -- so K1's length phase
+ * runs NROUND / ZH_L1_STRIDE rounds per window.  Measured (C3 mix, 16,384 chunks, round 6,
+ * profiles/r06b_level1_stride.json): stride 1 K1 9.51 ms, 84.0 GB/s, ratio 2.622; stride 2 8.05 ms,
+ * 96.3 GB/s, 2.477 (libzstd L1 2.477); stride 4 7.42 ms, 102.7 GB/s, 2.271. */
+#ifndef ZH_L1_STRIDE
+#define ZH_L1_STRIDE 2
+#endif
 #define ZH_MIN_MATCH_LONG 8
 #define ZH_MIN_MATCH_SHORT 5
 #define ZH_MAX_MATCH 64             /* per-position length cap; continuations are merged */

@@ -1008,7 +1008,10 @@ size_t orc_lz_parse_pre(const u8 *src, u32 pre, u32 n, orc_seq_t *seq, u32 *last
     u32 const pe = a < nwin ? a * ZH_WINDOW : lim;
     while (p < lim && p < pe) {
       int defer;
-      if (len[p] == 0) defer = 1;
+      /* level 1 (mode 2) looks matches up at positions p = 0 mod ZH_L1_STRIDE only (K1
+       * span_lengths_l1); the skip windows' resume check above still sees every position's
+       * candidate, as K1's inserter waves do */
+      if (len[p] == 0 || (orc_lz_mode == 2 && p % ZH_L1_STRIDE)) defer = 1;
       else if (orc_parse_lazy2) {
         int const g0 = match_gain(len, off, p);
         defer = match_gain(len, off, p + 1) > g0 + 4 || match_gain(len, off, p + 2) > g0 + 7;

@@ -8,7 +8,7 @@ import numpy as np
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 PKG = os.path.join(ROOT, "custom-nvcomp-with-zstd_amd")
-ORACLE_SO = os.path.join(ROOT, "oracle", "liboracle.so")
+ORACLE_SO = os.environ.get("ZH_ORACLE_SO") or os.path.join(ROOT, "oracle", "liboracle.so")
 DATAGEN_SO = os.path.join(ROOT, "tools", "libdatagen.so")
 GOLDEN = os.path.join(ROOT, "tests", "golden")
 

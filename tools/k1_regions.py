@@ -29,7 +29,7 @@ reps = [
  ('      seg_walk<false>(ciP, tmk, S, SE, entry, true, LM, MM, ex);\n', '      ' + M('walk') + '\n      seg_walk<false>(ciP, tmk, S, SE, entry, true, LM, MM, ex);\n'),
  ('      e_in = wsp + lane_value(ex, 63);\n', '      e_in = wsp + lane_value(ex, 63);\n      ' + M('mlist') + '\n'),
  ('    if (wave == REC_WAVE && prev2) {\n', '    ' + M('rec') + '\n    if (wave == REC_WAVE && prev2) {\n'),
- ('    if (lane == 0) atomicAdd(&misc[MISC_ARR], 1u);\n    __syncthreads();  // X', '    ' + M('X') + '\n    if (lane == 0) atomicAdd(&misc[MISC_ARR], 1u);\n    __syncthreads();  // X'),
+ ('    if (lane == 0) atomicAdd(&misc[MISC_ARR], 1u);\n    k1_barrier();  // X', '    ' + M('X') + '\n    if (lane == 0) atomicAdd(&misc[MISC_ARR], 1u);\n    k1_barrier();  // X'),
  ('    if (prev2) {\n      // ---- literals of window k - 2', '    ' + M('lits') + '\n    if (prev2) {\n      // ---- literals of window k - 2'),
  ('    ZH_STAMP(st_E);\n  }\n  if (!dead) {', '    ZH_STAMP(st_E);\n    ' + M('loop') + '\n  }\n  if (!dead) {'),
  ('    bool const skipk = have && skip_window_eff(misc, k, kskip0);\n', '    ' + M('steptop') + '\n    bool const skipk = have && skip_window_eff(misc, k, kskip0);\n'),

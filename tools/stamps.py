@@ -17,7 +17,7 @@ kind = sys.argv[1] if len(sys.argv) > 1 else "mix"
 n, cs = (int(sys.argv[2]) if len(sys.argv) > 2 else 2048), 65536
 data = T.gen(T.KINDS[kind], n, 0x5EED0003, cs)
 dev = torch.from_numpy(data).cuda()
-bc = cuda_zstd.BatchedCompressor(3, cs)
+bc = cuda_zstd.BatchedCompressor(int(os.environ.get("STAMPS_LEVEL", "3")), cs)
 slot = (bc.max_out(cs) + 255) // 256 * 256
 out = torch.empty(n * slot, dtype=torch.uint8, device="cuda")
 ar = torch.arange(n, dtype=torch.int64, device="cuda")
