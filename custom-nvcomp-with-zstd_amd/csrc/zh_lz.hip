@@ -53,6 +53,34 @@ extern "C" u32 zh_fixups_host() {
   return h;
 }
 #endif
+// Diagnostic build only (-DZH_TIMELINE, tools/timeline.py): per K1 wave and step phase, the
+// s_memtime cycles summed over every step of every block (VERDICT r5 item 2's executed per-phase
+// breakdown of the window pipeline).  Worker waves: 0 P wait, 1 lengths, 2 parse / records,
+// 3 X wait, 4 span tops + literals; inserter waves: 0 P wait, 1 insertion of the next window (the X
+// barrier taken between its tiles included), 3 barriers left after it, 4 candidate dump; [5] steps.
+#ifdef ZH_TIMELINE
+__device__ unsigned long long g_tl[16 * 8];
+extern "C" __global__ void zh_read_timeline(unsigned long long *out) {
+  for (u32 i = threadIdx.x; i < 16 * 8; i += blockDim.x) { out[i] = g_tl[i]; g_tl[i] = 0; }
+}
+extern "C" int zh_timeline_host(unsigned long long *out128) {
+  unsigned long long *d = nullptr;
+  if (hipMalloc(&d, 16 * 8 * 8) != hipSuccess) return 1;
+  hipLaunchKernelGGL(zh_read_timeline, dim3(1), dim3(128), 0, 0, d);
+  hipError_t e = hipMemcpy(out128, d, 16 * 8 * 8, hipMemcpyDeviceToHost);
+  (void)hipFree(d);
+  return e == hipSuccess ? 0 : 1;
+}
+#define TL_DECL u64 tl_[6] = {0, 0, 0, 0, 0, 0}; u64 tl_prev = __builtin_amdgcn_s_memtime()
+#define TL_MARK(ph) do { u64 const _t = __builtin_amdgcn_s_memtime(); tl_[ph] += _t - tl_prev; tl_prev = _t; } while (0)
+#define TL_STEP() (tl_[5]++)
+#define TL_FLUSH(w, lane) do { if ((lane) == 0) for (u32 _i = 0; _i < 6; _i++) atomicAdd(&g_tl[(w) * 8 + _i], (unsigned long long)tl_[_i]); } while (0)
+#else
+#define TL_DECL do { } while (0)
+#define TL_MARK(ph) do { } while (0)
+#define TL_STEP() do { } while (0)
+#define TL_FLUSH(w, lane) do { } while (0)
+#endif
 namespace {
 
 #ifndef ZH_K1_PMAX
@@ -980,6 +1008,7 @@ __device__ __forceinline__ bool inserter_loop(const u32 *in32, u16 *T, u8 *ci8, 
 #endif
   u32 const nwin = (n - wstart + ZH_WINDOW - 1) / ZH_WINDOW;
   u32 passed = 0;  // X barriers taken so far
+  TL_DECL;
   for (u32 k = 0; k < nwin + 2; k++) {
     if (probe_dead(misc_, k, kprobe)) return true;
     u32 const wsb = wstart + k * ZH_WINDOW;
@@ -987,7 +1016,10 @@ __device__ __forceinline__ bool inserter_loop(const u32 *in32, u16 *T, u8 *ci8, 
       if (skipc) dump_window<LONG, ZH_SKIP_TILES>(ci8 + (k & 1u) * 4 * CI_WORDS, lane, creg, cwe);
       else dump_window<LONG, TILES>(ci8 + (k & 1u) * 4 * CI_WORDS, lane, creg, cwe);
     }
+    TL_MARK(4);
     k1_barrier();  // P: candidates of window k in buffer k & 1
+    TL_MARK(0);
+    TL_STEP();
     if (probe_dead_tm(k, kprobe, e0p)) return true;
     u32 const done = passed + WIN_BARRIERS;
     // arr: the arrival counter as read with the last tile's read-back; a barrier taken
@@ -1022,8 +1054,11 @@ __device__ __forceinline__ bool inserter_loop(const u32 *in32, u16 *T, u8 *ci8, 
 #ifdef ZH_STAMPS
     st_ins += (u32)(__builtin_amdgcn_s_memtime() - ti0);
 #endif
+    TL_MARK(1);
     while (passed < done) { k1_barrier(); passed++; }
+    TL_MARK(3);
   }
+  TL_FLUSH(LONG ? 14u : 15u, lane);
 #ifdef ZH_STAMPS
   if (LONG && lane == 0) dbg[16] = st_ins;
 #endif
@@ -1398,6 +1433,7 @@ __device__ __forceinline__ u32 lz_block(const ZhBlockDesc *__restrict__ blocks, 
   u32 const nwin = (n - wstart + ZH_WINDOW - 1) / ZH_WINDOW;
   u64 *const mlist = (u64 *)(smem + OFF_ML);
   u32 nwalk_tot = 0;  // the walk's literal count before the parsed window (records carry it)
+  TL_DECL;
   // Step k (window j at wstart + j * ZH_WINDOW, parity j & 1):
   //   phase A  lengths of window k (waves 1..13) | parse, catch-up and sequence records of
   //            window k - 1 (wave 0)
@@ -1428,6 +1464,8 @@ __device__ __forceinline__ u32 lz_block(const ZhBlockDesc *__restrict__ blocks, 
     u32 *const lmQ = sgm + segm(kb);        // window k - 2's (after its catch-up)
     u64 *const mlP = mlist + (kb ^ 1u) * ML_CAP, *const mlQ = mlist + kb * ML_CAP;
     k1_barrier();  // P: candidates of window k in buffer k & 1
+    TL_MARK(0);
+    TL_STEP();
     if (probe_dead_tm(k, kprobe, e0p)) {
       dead = true;
       break;
@@ -1467,6 +1505,7 @@ __device__ __forceinline__ u32 lz_block(const ZhBlockDesc *__restrict__ blocks, 
       span_lengths<MODE>(in32, ciK, tmK, xq, r_lo, r_hi, wsb, we, n, lim, lane, wave == NWW - 1, la1);
       ZH_STAMP(st_B);
     }
+    TL_MARK(1);
     if (wave == 0 && prev) {
       // ---- the parse of window k - 1, lanes = 32-position segments
       u32 const wn = wep - wsp;
@@ -1558,8 +1597,10 @@ __device__ __forceinline__ u32 lz_block(const ZhBlockDesc *__restrict__ blocks, 
       lbx[lane] = lincl - lc;
       if (lane == 63) lbx[NSEG] = lincl;
     }
+    TL_MARK(2);
     if (lane == 0) atomicAdd(&misc[MISC_ARR], 1u);
     k1_barrier();  // X: window k's match info and take masks; window k - 1's records and literal bits
+    TL_MARK(3);
     ZH_STAMP(st_X);
     if (MODE != 2 && have && wave != 0 && wave < (skipk ? RS : NWW - 1)) {
       // ---- take decision at this wave's span top (the next position was the next wave's):
@@ -1609,7 +1650,9 @@ __device__ __forceinline__ u32 lz_block(const ZhBlockDesc *__restrict__ blocks, 
       }
     }
     ZH_STAMP(st_E);
+    TL_MARK(4);
   }
+  TL_FLUSH(wave, lane);
   if (!dead) {
     if (tid_ == 0) { meta[0] = nseq_tot; meta[1] = nlit_tot; meta[2] = 0; }
 #ifdef ZH_STAMPS
