@@ -913,8 +913,8 @@ __device__ __forceinline__ u32 catch_up(const u32 *in32, u32 P, u32 off, u32 lo,
 // segment's literal and match-start bits, ex: the exit (first position >= SE).  With old
 // visited bits (a Jacobi re-walk from a new entry), the walk stops where it meets a position
 // the old walk visited -- from there on both are the same -- and keeps the old bits above it.
-template <bool REWALK>
-__device__ __forceinline__ void seg_walk(const u32 *ci, u32 tmk, u32 S, u32 SE, u32 p, bool act0, u32 &LM, u32 &MM, u32 &ex) {
+template <bool REWALK, typename LenQ>
+__device__ __forceinline__ void seg_walk(LenQ &&lenq, u32 tmk, u32 S, u32 SE, u32 p, bool act0, u32 &LM, u32 &MM, u32 &ex) {
   // (the first walk has no old trajectory: REWALK = false drops the merge test from the step)
   u32 const old = (REWALK && act0) ? (LM | MM) : 0u;
   vpad<ZH_PAD_W>(p);
@@ -930,7 +930,7 @@ __device__ __forceinline__ void seg_walk(const u32 *ci, u32 tmk, u32 S, u32 SE, 
       u32 const o = p - S;                          // (< 32 on active lanes)
       u32 const q = p + __builtin_ctzg(tmk >> o, 32);  // next take position (>= SE: none)
       bool const st = act && q < SE;
-      u32 const len = ci[cidx(q)] & 255u;           // (q <= S + 63: inside the cinfo buffers)
+      u32 const len = lenq(q);                      // (q <= S + 63; used only when q < SE)
       nl |= act ? bit_range32(o, min(q, SE) - S) : 0u;
       nm |= st ? 1u << (q - S) : 0u;
       p = act ? (st ? q + len : SE) : p;
@@ -954,7 +954,7 @@ __device__ __forceinline__ void seg_walk(const u32 *ci, u32 tmk, u32 S, u32 SE, 
     bool const st = act && !mg && q < SE;
     u32 const re = mg ? x : min(q, SE);
     nl |= act ? bit_range32(o, re - S) : 0u;
-    u32 const len = ci[cidx(q)] & 255u;
+    u32 const len = lenq(q);
     nm |= st ? 1u << (q - S) : 0u;
     mpos = mg ? x - S : mpos;
     merged = merged || mg;
@@ -1514,7 +1514,11 @@ __device__ __forceinline__ u32 lz_block(const ZhBlockDesc *__restrict__ blocks, 
       u32 const e0 = e_in - wsp;  // first parsed position (< 64 except in the window holding `pre`)
       u32 entry = lane == 0 ? e0 : max(S, e0), ex = entry;
       u32 LM = 0, MM = 0;
-      seg_walk<false>(ciP, tmk, S, SE, entry, true, LM, MM, ex);
+      // (round 6: the segment's lengths packed into 8 VGPRs, a select tree + v_perm per step instead
+      // of this LDS read, measured slower: K1 10.43 -> 10.86 ms, the parse wave 6.6 k -> 7.8 k cycles
+      // per step, profiles/r06d_walk_reg_ab.json)
+      auto lenq = [&](u32 q) { return ciP[cidx(q)] & 255u; };
+      seg_walk<false>(lenq, tmk, S, SE, entry, true, LM, MM, ex);
       // Jacobi rounds: a segment's entry is its predecessor's exit
       for (;;) {
 #if ZH_K1_PMAX
@@ -1530,7 +1534,7 @@ __device__ __forceinline__ u32 lz_block(const ZhBlockDesc *__restrict__ blocks, 
         st_rounds++;
 #endif
         if (!__ballot(ch)) break;
-        seg_walk<true>(ciP, tmk, S, SE, ne, ch, LM, MM, ex);
+        seg_walk<true>(lenq, tmk, S, SE, ne, ch, LM, MM, ex);
         entry = ne;
       }
       e_in = wsp + lane_value(ex, 63);
