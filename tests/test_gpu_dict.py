@@ -200,3 +200,19 @@ def test_dictionary_tables_ragged_sizes(torch_cuda):
             f = m.compress(_dev(torch_cuda, data)).cpu().numpy().tobytes()
             assert f == T.oracle_frame(data, dictionary=d, level=level), (level, n)
             assert T.zstd_decompress(f, n, dictionary=d) == data.tobytes(), (level, n)
+
+
+@pytest.mark.parametrize("level", [1, 2])
+@pytest.mark.parametrize("kind", ["zdict", "cover"])
+def test_dictionary_low_levels_match_oracle(torch_cuda, dicts, kind, level):
+    """Levels 1 and 2 with a dictionary (K1's short-table modes behind the dictionary's precomputed
+    tables; level 1 searches every ZH_L1_STRIDE-th position): frames equal the oracle's at that
+    level, decode with libzstd and the dictionary, ragged sizes included."""
+    d = dicts[kind]
+    m = _mgr(level, d)
+    src = T.gen(T.DG_JSON, 1, 0x5EED0405 + level, 200000)
+    for n in SIZES:
+        data = src[:n]
+        f = m.compress(_dev(torch_cuda, data)).cpu().numpy().tobytes()
+        assert f == T.oracle_frame(data, dictionary=d, level=level), (kind, level, n)
+        assert T.zstd_decompress(f, n, dictionary=d) == data.tobytes(), (kind, level, n)
