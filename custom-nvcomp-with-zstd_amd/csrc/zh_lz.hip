@@ -113,11 +113,22 @@ __device__ __forceinline__ u32 cidx(u32 i) { return i; }
 // two cinfo buffers: window k's candidates / match info in buffer k & 1 (the parse of window k
 // overlaps the lengths of window k + 1)
 constexpr u32 OFF_HM = OFF_CI + 2 * 4 * CI_WORDS;    // per buffer u64 per round: take masks (see span_lengths)
-constexpr u32 OFF_SEGM = OFF_HM + 2 * 8 * NROUND;    // per window parity, per walk segment (u32 each):
+// The literal bytes of a window are extracted (ZH_LIT_INS = 0) by the worker waves after barrier X
+// of the step that wrote its records, or (1) one step later by the inserter waves, before X, once
+// they have built the next window's tables (the step's post-X phase shrinks to the span tops).
+// Round 6 (profiles/r06i_lit_ins_ab.json): level 3 K1 10.36 -> 10.12 ms, level 1 8.02 -> 7.52 ms;
+// the step 11.66 k -> 10.95 k cycles (tools/timeline.py).
+#ifndef ZH_LIT_INS
+#define ZH_LIT_INS 1
+#endif
+constexpr u32 LM_BUFS = ZH_LIT_INS ? 3 : 2;         // windows whose literal bits are alive at once
+constexpr u32 LB_BUFS = ZH_LIT_INS ? 2 : 1;         // literal prefix-count buffers
+constexpr u32 STEPS_EXTRA = ZH_LIT_INS ? 3 : 2;     // loop steps per block: windows + STEPS_EXTRA
+constexpr u32 OFF_SEGM = OFF_HM + 2 * 8 * NROUND;    // per window (mod LM_BUFS), per walk segment (u32 each):
 // the literal bits left after catch-up
 __device__ __forceinline__ u32 segm(u32 par) { return par * NSEG; }
 constexpr u32 ML_CAP = ((ZH_WINDOW + ZH_MIN_MATCH_SHORT - 1) / ZH_MIN_MATCH_SHORT + 12 + 3) & ~3u;  // matches per window
-constexpr u32 OFF_ML = OFF_SEGM + 4 * 2 * NSEG;      // per window parity: the window's matches in order (u64,
+constexpr u32 OFF_ML = OFF_SEGM + 4 * LM_BUFS * NSEG;  // per window parity: the window's matches in order (u64,
                                                      // ML_* fields) for the records one step later
 constexpr u32 XQ_CAP = 196;                          // chain-end queue entries per worker wave (<= 191
                                                      // used: < 64 left + 2 x 64 per round; the last is a spare)
@@ -125,7 +136,8 @@ constexpr u32 OFF_XQ = OFF_ML + 2 * 8 * ML_CAP;      // u16 per entry: window in
 constexpr u32 OFF_MISC = OFF_XQ + 2 * XQ_CAP * NWW;  // [2 par + 0] matches, [2 par + 1] first parsed position
 constexpr u32 OFF_LB = OFF_MISC + 4 * 16;            // window k - 2's literal prefix counts per walk
                                                      // segment (+ the window's total), for the literal phase
-constexpr u32 K1_LDS = OFF_LB + 4 * (NSEG + 4);
+constexpr u32 LB_WORDS = NSEG + 4;
+constexpr u32 K1_LDS = OFF_LB + 4 * LB_WORDS * LB_BUFS;
 constexpr u32 ML_LO = 11, ML_LEN = 22, ML_OFF = 29, ML_CUM = 45;  // match-list entry: start [0, 11) | ...
 constexpr u32 MISC_WNM = 0;   // misc[par]: matches of the window of that parity (its match list's length)
 constexpr u32 MISC_ARR = 12;  // misc[12]: worker-wave barrier arrivals (cumulative)
@@ -984,19 +996,68 @@ constexpr u32 WIN_BARRIERS = 1;  // X
 // The long table's wave in modes 1, 2 (the short table only): no insertion, only the step's two
 // barriers (P, X) and the probe exit, so the workgroup's barrier sequence stays the same.
 // Returns whether the loop ended at the incompressibility probe.
-__device__ __forceinline__ bool idle_inserter_loop(u32 *misc_, u32 n, u32 wstart, u32 kprobe, u32 e0p) {
+// Literal bytes of the window at staged position wsj (ZH_LIT_INS): rounds r = r0, r0 + rs, ... of
+// 64 positions; lm = its literal bits per walk segment, lb = their exclusive prefix counts (+ the
+// window's total at lb[NSEG]); nlit = the literals before the window.  Four rounds' LDS reads per
+// round trip.
+__device__ __forceinline__ void lit_rounds(const u8 *in, const u32 *lm, const u32 *lb, u8 *lit_out, u32 nlit, u32 wsj, u32 r0, u32 rs, u32 lane) {
+  constexpr u32 B = 4;
+  for (u32 rb = r0; rb < NROUND; rb += B * rs) {
+    u64 mw[B];
+    u32 lbr[B], by[B];
+#pragma unroll
+    for (u32 j = 0; j < B; j++) {
+      u32 const r = min(rb + rs * j, NROUND - 1u);
+      mw[j] = *(const u64 *)&lm[2 * r];
+      lbr[j] = (u32)__builtin_amdgcn_readfirstlane(lb[2 * r]);
+      by[j] = in[wsj + 64 * r + lane];
+    }
+#pragma unroll
+    for (u32 j = 0; j < B; j++) __asm__ volatile("" : "+v"(by[j]));
+#pragma unroll
+    for (u32 j = 0; j < B; j++) {
+      if (rb + rs * j >= NROUND) continue;
+      u64 const m = ((u64)(u32)__builtin_amdgcn_readfirstlane((u32)(mw[j] >> 32)) << 32) | (u32)__builtin_amdgcn_readfirstlane((u32)mw[j]);
+      if ((m >> lane) & 1ull) {
+        u32 const rank = __builtin_amdgcn_mbcnt_hi((u32)(m >> 32), __builtin_amdgcn_mbcnt_lo((u32)m, 0u));
+        lit_out[nlit + lbr[j] + rank] = (u8)by[j];
+      }
+    }
+  }
+}
+// The literal work of an inserter wave in step k (ZH_LIT_INS): window k - 3's rounds r0, r0 + rs, ...
+struct LitJob {
+  const u8 *in;
+  u32 *sgm, *lbx;
+  u8 *lit_out;
+  u32 wstart, n, pre, r0, rs;
+  u32 nlit;  // literals of the windows before the next one (running; every inserter keeps the total)
+  __device__ __forceinline__ void step(u32 k, u32 lane) {
+    if constexpr (ZH_LIT_INS) {
+      if (k < 3) return;
+      u32 const j = k - 3, wsj = wstart + j * ZH_WINDOW;
+      if (wsj >= n || min(wsj + ZH_WINDOW, n) <= pre) return;
+      const u32 *const lm = sgm + segm(j % LM_BUFS);
+      const u32 *const lb = lbx + (j & 1u) * LB_WORDS;
+      if (rs) lit_rounds(in, lm, lb, lit_out, nlit, wsj, r0, rs, lane);
+      nlit += (u32)__builtin_amdgcn_readfirstlane(lb[NSEG]);
+    }
+  }
+};
+__device__ __forceinline__ bool idle_inserter_loop(u32 *misc_, u32 n, u32 wstart, u32 kprobe, u32 e0p, LitJob &lj, u32 lane) {
   u32 const nwin = (n - wstart + ZH_WINDOW - 1) / ZH_WINDOW;
-  for (u32 k = 0; k < nwin + 2; k++) {
+  for (u32 k = 0; k < nwin + STEPS_EXTRA; k++) {
     if (probe_dead(misc_, k, kprobe)) return true;
     k1_barrier();  // P
     if (probe_dead_tm(k, kprobe, e0p)) return true;
+    lj.step(k, lane);
     k1_barrier();  // X
   }
   return false;
 }
 template <bool LONG, bool TWO>
 __device__ __forceinline__ bool inserter_loop(const u32 *in32, u16 *T, u8 *ci8, u32 *misc_, u32 n, u32 lim, u32 lane, u32 *dbg, u32 wstart,
-                                              u32 pmin, u32 span_s, u32 span_e, u32 kskip0, u32 kprobe, u32 e0p) {
+                                              u32 pmin, u32 span_s, u32 span_e, u32 kskip0, u32 kprobe, u32 e0p, LitJob &lj) {
   u32 creg[NCR];
   if (span_s < span_e) insert_span<LONG>(in32, T, span_s, span_e, lane);
   // (the first window: its own instantiation, with pmin and no barriers to take)
@@ -1009,7 +1070,7 @@ __device__ __forceinline__ bool inserter_loop(const u32 *in32, u16 *T, u8 *ci8, 
   u32 const nwin = (n - wstart + ZH_WINDOW - 1) / ZH_WINDOW;
   u32 passed = 0;  // X barriers taken so far
   TL_DECL;
-  for (u32 k = 0; k < nwin + 2; k++) {
+  for (u32 k = 0; k < nwin + STEPS_EXTRA; k++) {
     if (probe_dead(misc_, k, kprobe)) return true;
     u32 const wsb = wstart + k * ZH_WINDOW;
     if (k < nwin) {
@@ -1055,6 +1116,10 @@ __device__ __forceinline__ bool inserter_loop(const u32 *in32, u16 *T, u8 *ci8, 
     st_ins += (u32)(__builtin_amdgcn_s_memtime() - ti0);
 #endif
     TL_MARK(1);
+    // window k - 3's literal bytes (their bits and prefix counts were final at X of step k - 1;
+    // the next writes to those buffers come after P of step k + 1)
+    lj.step(k, lane);
+    TL_MARK(2);
     while (passed < done) { k1_barrier(); passed++; }
     TL_MARK(3);
   }
@@ -1409,12 +1474,16 @@ __device__ __forceinline__ u32 lz_block(const ZhBlockDesc *__restrict__ blocks, 
     // is arbitrated ... by priority, then age").
     // (priority 0 or 1 measured the same, profiles/r05l_k1_priority_ab.json)
     __builtin_amdgcn_s_setprio(2);
+    // literal rounds (ZH_LIT_INS): both inserters half each in mode 0, else the idle long-table wave all
+    bool const lw = tid < INS_TID + 64;
+    LitJob lj{in, (u32 *)(smem + OFF_SEGM), (u32 *)(smem + OFF_LB), ws.lits(b), wstart, n, pre,
+              two_tables<MODE>() ? (lw ? 0u : 1u) : 0u, two_tables<MODE>() ? 2u : (lw ? 1u : 0u), 0u};
     if (tid >= INS_TID + 64)
-      dead = inserter_loop<false, two_tables<MODE>()>(in32, TS, ci8, misc, n, lim, lane, ws.dbg(b), wstart, pmin, span_s, span_e, kskip0, kprobe, e0p);
+      dead = inserter_loop<false, two_tables<MODE>()>(in32, TS, ci8, misc, n, lim, lane, ws.dbg(b), wstart, pmin, span_s, span_e, kskip0, kprobe, e0p, lj);
     else if (two_tables<MODE>())
-      dead = inserter_loop<true, true>(in32, TL, ci8, misc, n, lim, lane, ws.dbg(b), wstart, pmin, span_s, span_e, kskip0, kprobe, e0p);
+      dead = inserter_loop<true, true>(in32, TL, ci8, misc, n, lim, lane, ws.dbg(b), wstart, pmin, span_s, span_e, kskip0, kprobe, e0p, lj);
     else
-      dead = idle_inserter_loop(misc, n, wstart, kprobe, e0p);
+      dead = idle_inserter_loop(misc, n, wstart, kprobe, e0p, lj, lane);
     __builtin_amdgcn_s_setprio(0);
     if (!dead) return next_b;
   } else {
@@ -1440,7 +1509,8 @@ __device__ __forceinline__ u32 lz_block(const ZhBlockDesc *__restrict__ blocks, 
   //   X
   //   phase B  take decisions at window k's span tops (each wave its own), the literals of
   //            window k - 1 (lanes = positions, all worker waves)
-  for (u32 k = 0; k < nwin + 2; k++) {
+  u32 m3 = 0;  // k mod LM_BUFS
+  for (u32 k = 0; k < nwin + STEPS_EXTRA; k++, m3 = m3 + 1 == LM_BUFS ? 0u : m3 + 1) {
     if (probe_dead(misc, k, kprobe)) {
       dead = true;
       break;
@@ -1452,7 +1522,7 @@ __device__ __forceinline__ u32 lz_block(const ZhBlockDesc *__restrict__ blocks, 
     u32 const wsp = wsb - ZH_WINDOW, wep = min(wsp + ZH_WINDOW, n);
     bool const prev = k >= 1 && k <= nwin && wep > pre;        // window k - 1: parse, match list
     u32 const wsq = wsb - 2 * ZH_WINDOW;
-    bool const prev2 = k >= 2 && min(wsq + ZH_WINDOW, n) > pre;  // window k - 2: records, literals
+    bool const prev2 = k >= 2 && k - 2 < nwin && min(wsq + ZH_WINDOW, n) > pre;  // window k - 2: records, literals
     // opaque per-step thread index: keeps the compiler from hoisting every LDS address
     // derived from it out of the loop (they would be spilled to scratch)
     u32 tid;
@@ -1460,8 +1530,10 @@ __device__ __forceinline__ u32 lz_block(const ZhBlockDesc *__restrict__ blocks, 
     u32 const lane = tid & 63;
     u32 *const ciK = ci0 + kb * CI_WORDS, *const ciP = ci0 + (kb ^ 1u) * CI_WORDS;
     u64 *const tmK = hm + kb * NROUND, *const tmP = hm + (kb ^ 1u) * NROUND;
-    u32 *const lmP = sgm + segm(kb ^ 1u);   // window k - 1's literal bits (the walk's)
-    u32 *const lmQ = sgm + segm(kb);        // window k - 2's (after its catch-up)
+    // window k - 1's literal bits (the walk's), window k - 2's (after its catch-up)
+    u32 *const lmP = sgm + segm(LM_BUFS == 2 ? (kb ^ 1u) : (m3 == 0 ? 2u : m3 - 1u));
+    u32 *const lmQ = sgm + segm(LM_BUFS == 2 ? kb : (m3 == 0 ? 1u : m3 == 1 ? 2u : 0u));
+    u32 *const lbxq = lbx + (LB_BUFS == 2 ? kb : 0u) * LB_WORDS;  // window k - 2's prefix counts
     u64 *const mlP = mlist + (kb ^ 1u) * ML_CAP, *const mlQ = mlist + kb * ML_CAP;
     k1_barrier();  // P: candidates of window k in buffer k & 1
     TL_MARK(0);
@@ -1598,8 +1670,8 @@ __device__ __forceinline__ u32 lz_block(const ZhBlockDesc *__restrict__ blocks, 
       // phase's per-segment exclusive prefix counts, once for every wave (LDS ops of a wave
       // apply in order, so the reads see this wave's atomics)
       u32 const lc = (u32)__popc(lmQ[lane]), lincl = wave_scan_incl(lc);
-      lbx[lane] = lincl - lc;
-      if (lane == 63) lbx[NSEG] = lincl;
+      lbxq[lane] = lincl - lc;
+      if (lane == 63) lbxq[NSEG] = lincl;
     }
     TL_MARK(2);
     if (lane == 0) atomicAdd(&misc[MISC_ARR], 1u);
@@ -1617,7 +1689,11 @@ __device__ __forceinline__ u32 lz_block(const ZhBlockDesc *__restrict__ blocks, 
         if (i < we - wsb && (inf & 255u) && take_rule<MODE>(inf, inf1)) atomicOr((u32 *)&tmK[i >> 6] + ((i >> 5) & 1u), 1u << (i & 31));
       }
     }
-    if (prev2) {
+    if (ZH_LIT_INS && prev2) {
+      // (the inserters extract window k - 2's literals in step k + 1)
+      nlit_tot += (u32)__builtin_amdgcn_readfirstlane(lbxq[NSEG]);
+      nseq_tot += __builtin_amdgcn_readfirstlane(misc[MISC_WNM + kb]);
+    } else if (prev2) {
       // ---- literals of window k - 2, lanes = positions (round r = segments 2r, 2r + 1)
       u32 const nm = __builtin_amdgcn_readfirstlane(misc[MISC_WNM + kb]);
 #ifdef ZH_EXP_NOLITPHASE

@@ -2,7 +2,7 @@
 `bash tools/variants.sh build tl -DZH_TIMELINE`): s_memtime cycles per step in each phase, averaged
 over every step of every block of one C3-style batch.  Worker waves 0..13: P wait | lengths |
 parse/records | X wait | span tops + literals; inserter waves 14 (long) / 15 (short): P wait |
-insertion (X taken between tiles included) | length rounds (ZH_INS_ROUNDS) | barriers after them | dump.
+insertion (X taken between tiles included) | literal rounds (ZH_LIT_INS) | barriers after them | dump.
 usage: CUDA_ZSTD_HIP_LIB=tools/libV_tl.so python3 tools/timeline.py [LEVEL] [CHUNKS] [KIND]"""
 import ctypes
 import json
@@ -42,7 +42,7 @@ torch.cuda.synchronize()
 assert L.zh_timeline_host(buf) == 0
 a = np.array(buf[:], dtype=np.float64).reshape(16, 8)
 names_w = ["P_wait", "lengths", "parse_rec", "X_wait", "lits"]
-names_i = ["P_wait", "insert", "rounds", "X_after", "dump"]
+names_i = ["P_wait", "insert", "lits", "X_after", "dump"]
 res = {"level": level, "chunks": n, "kind": kind, "waves": {}}
 for w in range(16):
     steps = a[w, 5]
