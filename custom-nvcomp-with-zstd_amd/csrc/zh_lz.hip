@@ -92,6 +92,8 @@ constexpr u32 NROUND = ZH_WINDOW / 64;      // 64-position length rounds per win
 constexpr u32 SEGP = 32;                    // positions per walk segment (one lane of wave 0)
 constexpr u32 NSEG = ZH_WINDOW / SEGP;      // walk segments per window
 constexpr u32 INS_TID = 896;                // first inserter thread (waves 14, 15)
+// worker rounds per wave (rounds_of below): 2 bits per wave, 0 2 3 3 3 3 3 3 3 2 2 2 2 1
+constexpr u64 ROUND_TAB = 0x6abfff8ull;
 constexpr u32 NWW = INS_TID / 64;           // worker waves
 constexpr u32 TILES = ZH_WINDOW / ZH_TILE;  // 16 tiles per window
 constexpr u32 TPL = ZH_TILE / 64;           // positions per inserter lane per tile
@@ -137,10 +139,22 @@ constexpr u32 OFF_MISC = OFF_XQ + 2 * XQ_CAP * NWW;  // [2 par + 0] matches, [2 
 constexpr u32 OFF_LB = OFF_MISC + 4 * 16;            // window k - 2's literal prefix counts per walk
                                                      // segment (+ the window's total), for the literal phase
 constexpr u32 LB_WORDS = NSEG + 4;
+// One barrier per window step (ZH_ONE_BARRIER, needs ZH_LIT_INS): the take bits at the worker
+// waves' span tops (lazy rule: they need the next span's first info) are decided by wave 0 at the
+// start of the window's parse in the next step (and by every wave in the probe step), and the
+// inserters dump the next window's candidates once wave 0 has read the previous window's match info
+// (an LDS flag, MISC_PF) -- so nothing needs barrier X.  Measured K1 10.12 -> 9.70 ms at level 3,
+// 7.52 -> 7.21 ms at level 1 (profiles/r06k_one_barrier_ab.json; the first version, every wave
+// deciding its own top from an extra info, was slower: 10.50 ms)
+#ifndef ZH_ONE_BARRIER
+#define ZH_ONE_BARRIER 1
+#endif
+static_assert(!ZH_ONE_BARRIER || ZH_LIT_INS, "one barrier per step needs the literals on the inserters");
 constexpr u32 K1_LDS = OFF_LB + 4 * LB_WORDS * LB_BUFS;
 constexpr u32 ML_LO = 11, ML_LEN = 22, ML_OFF = 29, ML_CUM = 45;  // match-list entry: start [0, 11) | ...
 constexpr u32 MISC_WNM = 0;   // misc[par]: matches of the window of that parity (its match list's length)
 constexpr u32 MISC_ARR = 12;  // misc[12]: worker-wave barrier arrivals (cumulative)
+constexpr u32 MISC_PF = 12;   // (ZH_ONE_BARRIER, no arrivals) misc[12]: k + 1 once wave 0 has read window k - 1's match info
 constexpr u32 MISC_NM = 4;    // misc[4 + (j & 3)]: matches the parse took in window j (miss skip)
 constexpr u32 MISC_ANY = 13;  // misc[13]: block_any's flag (0 between calls)
 constexpr u32 MISC_SCAN = 2;  // misc[2]: the repeat scan's count
@@ -517,19 +531,44 @@ __device__ __forceinline__ bool probe_dead(const u32 *misc, u32 k, u32 kprobe) {
   return (u32)__builtin_amdgcn_readfirstlane(m) == 0;
 }
 static_assert(ZH_PROBE_WINDOWS >= 1 && ZH_PROBE_WINDOWS <= 3, "probe windows fit the match-count ring");
+// Span tops of a window's worker waves (ZH_ONE_BARRIER, modes 0-1): the last position 64 hi - 1 of
+// a span whose next position belongs to another wave -- hi = r_hi of waves 1..NWW-2, or 1..RS-1 in
+// a miss-skip window -- takes its match under the lazy rule only with the next position's info,
+// which its own wave never sees.  Lane L (< 32) decides the top at hi = L + 1 from the window's
+// match info ci (length wn).
+constexpr u32 span_top_mask(u64 tab) {
+  u32 m = 0, hi = 0;
+  for (u32 w = 1; w + 1 < INS_TID / 64; w++) {
+    hi += (u32)((tab >> (2 * w)) & 3u);
+    m |= 1u << hi;
+  }
+  return m;
+}
+__device__ __forceinline__ bool span_top_dec(const u32 *ci, u32 wn, bool skip, u32 L, bool act) {
+  constexpr u32 TOPS_FULL = span_top_mask(ROUND_TAB), TOPS_SKIP = ((1u << (2 * ZH_SKIP_TILES)) - 1u) & ~1u;
+  u32 const hi = L + 1, i = 64 * hi - 1;
+  bool const top = act && L < NROUND && (((skip ? TOPS_SKIP : TOPS_FULL) >> hi) & 1u) && i < wn;
+  u32 const inf = top ? ci[cidx(i)] : 0u, inf1 = top ? ci[cidx(i + 1)] : 0u;
+  return top && (inf & 255u) && (inf1 & 255u) <= (inf & 255u);  // (take_rule of modes 0-1)
+}
 // The one-window probe from the take masks: before any match the parse visits every position,
 // so it takes a match in the probe window exactly when the window has a take bit at or after
 // its first parsed position e0.  Window k - 1's masks (and their span-top bits, set after
 // barrier X of step k - 1) are final at barrier P of step k = kprobe - 1, so every wave --
 // inserters too -- tests them right after that P and leaves the window loop together.
-__device__ __forceinline__ bool probe_dead_tm(u32 k, u32 kprobe, u32 e0) {
+__device__ __forceinline__ bool probe_dead_tm(u32 k, u32 kprobe, u32 e0, bool lazy = false, u32 wnp = 0) {
   if (ZH_PROBE_WINDOWS != 1 || k + 1 != kprobe) return false;
   u8 *const smem = k1_lds();
   u32 lane;
   __asm__ volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(lane));
   const u64 *const tmP = (const u64 *)(smem + OFF_HM) + ((k & 1u) ^ 1u) * NROUND;
   u32 const r = lane & (NROUND - 1);
-  u64 const m = tmP[r];
+  u64 m = tmP[r];
+  if (ZH_ONE_BARRIER && lazy) {
+    // (the span tops of the probe window, never a miss-skip window: decided here by every wave)
+    const u32 *const ciP = (const u32 *)(smem + OFF_CI) + ((k & 1u) ^ 1u) * CI_WORDS;
+    m |= span_top_dec(ciP, wnp, false, r, lane < NROUND) ? 1ull << 63 : 0ull;
+  }
   u32 const lo = 64 * r;
   u64 const keep = e0 <= lo ? ~0ull : e0 >= lo + 64 ? 0ull : ~0ull << (e0 - lo);
   return __ballot(lane < NROUND && (m & keep) != 0) == 0;
@@ -599,7 +638,6 @@ constexpr u32 MAX_RW = 3;   // rounds per worker wave
 // 1/5/9/13 (13 also computes the window's lookahead): 2/2/2/2 10.69 ms, 2/3/2/1 10.38, 1/3/3/1
 // 10.37, 2/2/3/1 10.37; moving rounds between SIMDs or 4-round waves (a larger unrolled span)
 // measured slower (`profiles/r05z_round_table_ab.json`).
-constexpr u64 ROUND_TAB = 0x6abfff8ull;  // 2 bits per wave: 0 2 3 3 3 3 3 3 3 2 2 2 2 1
 __device__ __forceinline__ u32 rounds_of(u32 w) {
 #ifdef ZH_RTAB
   return (u32)(((unsigned long long)(ZH_RTAB) >> (2 * w)) & 3u);
@@ -1044,20 +1082,21 @@ struct LitJob {
     }
   }
 };
-__device__ __forceinline__ bool idle_inserter_loop(u32 *misc_, u32 n, u32 wstart, u32 kprobe, u32 e0p, LitJob &lj, u32 lane) {
+__device__ __forceinline__ bool idle_inserter_loop(u32 *misc_, u32 n, u32 wstart, u32 kprobe, u32 e0p, LitJob &lj, u32 lane, bool lazy) {
   u32 const nwin = (n - wstart + ZH_WINDOW - 1) / ZH_WINDOW;
   for (u32 k = 0; k < nwin + STEPS_EXTRA; k++) {
     if (probe_dead(misc_, k, kprobe)) return true;
     k1_barrier();  // P
-    if (probe_dead_tm(k, kprobe, e0p)) return true;
+    u32 const wsb = wstart + k * ZH_WINDOW;
+    if (probe_dead_tm(k, kprobe, e0p, lazy, min(wsb, n) - (wsb - ZH_WINDOW))) return true;
     lj.step(k, lane);
-    k1_barrier();  // X
+    if (!ZH_ONE_BARRIER) k1_barrier();  // X
   }
   return false;
 }
 template <bool LONG, bool TWO>
 __device__ __forceinline__ bool inserter_loop(const u32 *in32, u16 *T, u8 *ci8, u32 *misc_, u32 n, u32 lim, u32 lane, u32 *dbg, u32 wstart,
-                                              u32 pmin, u32 span_s, u32 span_e, u32 kskip0, u32 kprobe, u32 e0p, LitJob &lj) {
+                                              u32 pmin, u32 span_s, u32 span_e, u32 kskip0, u32 kprobe, u32 e0p, LitJob &lj, bool lazy) {
   u32 creg[NCR];
   if (span_s < span_e) insert_span<LONG>(in32, T, span_s, span_e, lane);
   // (the first window: its own instantiation, with pmin and no barriers to take)
@@ -1074,6 +1113,12 @@ __device__ __forceinline__ bool inserter_loop(const u32 *in32, u16 *T, u8 *ci8, 
     if (probe_dead(misc_, k, kprobe)) return true;
     u32 const wsb = wstart + k * ZH_WINDOW;
     if (k < nwin) {
+      if (ZH_ONE_BARRIER) {
+        // buffer k & 1 held window k - 2's match info, which wave 0 read in step k - 1
+        // (bounded: wave 0 sets the flag every step; the bound only keeps a bug from hanging the GPU)
+        for (u32 it = 0; it < (1u << 22) && (u32)__builtin_amdgcn_readfirstlane(__atomic_load_n(&misc_[MISC_PF], __ATOMIC_RELAXED)) < k; it++)
+          __builtin_amdgcn_s_sleep(1);
+      }
       if (skipc) dump_window<LONG, ZH_SKIP_TILES>(ci8 + (k & 1u) * 4 * CI_WORDS, lane, creg, cwe);
       else dump_window<LONG, TILES>(ci8 + (k & 1u) * 4 * CI_WORDS, lane, creg, cwe);
     }
@@ -1081,12 +1126,12 @@ __device__ __forceinline__ bool inserter_loop(const u32 *in32, u16 *T, u8 *ci8, 
     k1_barrier();  // P: candidates of window k in buffer k & 1
     TL_MARK(0);
     TL_STEP();
-    if (probe_dead_tm(k, kprobe, e0p)) return true;
+    if (probe_dead_tm(k, kprobe, e0p, lazy, min(wsb, n) - (wsb - ZH_WINDOW))) return true;
     u32 const done = passed + WIN_BARRIERS;
     // arr: the arrival counter as read with the last tile's read-back; a barrier taken
     // here means the counter is re-read for the next one
     auto take_ready = [&](u32 arr) {
-      while (passed < done && arr >= NWW * (passed + 1)) {
+      while (!ZH_ONE_BARRIER && passed < done && arr >= NWW * (passed + 1)) {
         k1_barrier();
         passed++;
         arr = __atomic_load_n(&misc_[MISC_ARR], __ATOMIC_RELAXED);
@@ -1120,7 +1165,7 @@ __device__ __forceinline__ bool inserter_loop(const u32 *in32, u16 *T, u8 *ci8, 
     // the next writes to those buffers come after P of step k + 1)
     lj.step(k, lane);
     TL_MARK(2);
-    while (passed < done) { k1_barrier(); passed++; }
+    while (!ZH_ONE_BARRIER && passed < done) { k1_barrier(); passed++; }
     TL_MARK(3);
   }
   TL_FLUSH(LONG ? 14u : 15u, lane);
@@ -1479,11 +1524,12 @@ __device__ __forceinline__ u32 lz_block(const ZhBlockDesc *__restrict__ blocks, 
     LitJob lj{in, (u32 *)(smem + OFF_SEGM), (u32 *)(smem + OFF_LB), ws.lits(b), wstart, n, pre,
               two_tables<MODE>() ? (lw ? 0u : 1u) : 0u, two_tables<MODE>() ? 2u : (lw ? 1u : 0u), 0u};
     if (tid >= INS_TID + 64)
-      dead = inserter_loop<false, two_tables<MODE>()>(in32, TS, ci8, misc, n, lim, lane, ws.dbg(b), wstart, pmin, span_s, span_e, kskip0, kprobe, e0p, lj);
+      dead = inserter_loop<false, two_tables<MODE>()>(in32, TS, ci8, misc, n, lim, lane, ws.dbg(b), wstart, pmin, span_s, span_e, kskip0, kprobe, e0p, lj,
+                                                      MODE != 2);
     else if (two_tables<MODE>())
-      dead = inserter_loop<true, true>(in32, TL, ci8, misc, n, lim, lane, ws.dbg(b), wstart, pmin, span_s, span_e, kskip0, kprobe, e0p, lj);
+      dead = inserter_loop<true, true>(in32, TL, ci8, misc, n, lim, lane, ws.dbg(b), wstart, pmin, span_s, span_e, kskip0, kprobe, e0p, lj, MODE != 2);
     else
-      dead = idle_inserter_loop(misc, n, wstart, kprobe, e0p, lj, lane);
+      dead = idle_inserter_loop(misc, n, wstart, kprobe, e0p, lj, lane, MODE != 2);
     __builtin_amdgcn_s_setprio(0);
     if (!dead) return next_b;
   } else {
@@ -1504,12 +1550,12 @@ __device__ __forceinline__ u32 lz_block(const ZhBlockDesc *__restrict__ blocks, 
   u32 nwalk_tot = 0;  // the walk's literal count before the parsed window (records carry it)
   TL_DECL;
   // Step k (window j at wstart + j * ZH_WINDOW, parity j & 1):
-  //   phase A  lengths of window k (waves 1..13) | parse, catch-up and sequence records of
-  //            window k - 1 (wave 0)
-  //   X
-  //   phase B  take decisions at window k's span tops (each wave its own), the literals of
-  //            window k - 1 (lanes = positions, all worker waves)
+  //   phase A  lengths of window k (waves 1..13) | span-top take decisions and parse of window
+  //            k - 1 (wave 0) | catch-up and sequence records of window k - 2 (REC_WAVE)
+  //   (ZH_ONE_BARRIER=0 only: X, then the take decisions at window k's span tops, each wave its
+  //   own, and without ZH_LIT_INS the literals of window k - 2, lanes = positions)
   u32 m3 = 0;  // k mod LM_BUFS
+  bool skp_prev = false;  // (ZH_ONE_BARRIER) window k - 1 was a miss-skip window (its span tops)
   for (u32 k = 0; k < nwin + STEPS_EXTRA; k++, m3 = m3 + 1 == LM_BUFS ? 0u : m3 + 1) {
     if (probe_dead(misc, k, kprobe)) {
       dead = true;
@@ -1538,7 +1584,7 @@ __device__ __forceinline__ u32 lz_block(const ZhBlockDesc *__restrict__ blocks, 
     k1_barrier();  // P: candidates of window k in buffer k & 1
     TL_MARK(0);
     TL_STEP();
-    if (probe_dead_tm(k, kprobe, e0p)) {
+    if (probe_dead_tm(k, kprobe, e0p, MODE != 2, wep - wsp)) {
       dead = true;
       break;
     }
@@ -1582,7 +1628,14 @@ __device__ __forceinline__ u32 lz_block(const ZhBlockDesc *__restrict__ blocks, 
       // ---- the parse of window k - 1, lanes = 32-position segments
       u32 const wn = wep - wsp;
       u32 const S = SEGP * lane, SE = min(S + SEGP, wn);
-      u32 const tmk = (u32)(tmP[lane >> 1] >> (32 * (lane & 1)));
+      u32 tmk = (u32)(tmP[lane >> 1] >> (32 * (lane & 1)));
+      if constexpr (ZH_ONE_BARRIER && MODE != 2) {
+        // the worker waves' span tops of window k - 1 (lane L: the top ending round L): a top
+        // ends the odd segment 2 hi - 1, at its bit 31
+        bool const dt = span_top_dec(ciP, wn, skp_prev, lane, lane < NROUND);
+        u32 const d = bperm(dt ? 1u : 0u, (lane - 1u) >> 1);
+        tmk |= ((lane & 1u) && d) ? 1u << 31 : 0u;
+      }
       u32 const e0 = e_in - wsp;  // first parsed position (< 64 except in the window holding `pre`)
       u32 entry = lane == 0 ? e0 : max(S, e0), ex = entry;
       u32 LM = 0, MM = 0;
@@ -1645,6 +1698,9 @@ __device__ __forceinline__ u32 lz_block(const ZhBlockDesc *__restrict__ blocks, 
       if (lane == 0) { misc[MISC_WNM + (kb ^ 1u)] = nm; misc[MISC_NM + ((k - 1) & 3)] = nm; }
       ZH_STAMP(st_J);
     }
+    // (ZH_ONE_BARRIER) wave 0 is done with window k - 1's match info: the inserters may dump
+    // window k + 1's candidates into that buffer
+    if (ZH_ONE_BARRIER && wave == 0 && lane == 0) __atomic_store_n(&misc[MISC_PF], k + 1, __ATOMIC_RELAXED);
     if (wave == REC_WAVE && prev2) {
       // ---- catch-up and sequence records of window k - 2, lanes = matches.  A match grows
       // back over the literals down to the end of the match before it; it takes back e bytes of
@@ -1672,13 +1728,19 @@ __device__ __forceinline__ u32 lz_block(const ZhBlockDesc *__restrict__ blocks, 
       u32 const lc = (u32)__popc(lmQ[lane]), lincl = wave_scan_incl(lc);
       lbxq[lane] = lincl - lc;
       if (lane == 63) lbxq[NSEG] = lincl;
+      if (ZH_ONE_BARRIER) {  // (this wave keeps the block's totals: no barrier before the others could read them)
+        nlit_tot += lane_value(lincl, 63);
+        nseq_tot += nm;
+      }
     }
     TL_MARK(2);
-    if (lane == 0) atomicAdd(&misc[MISC_ARR], 1u);
-    k1_barrier();  // X: window k's match info and take masks; window k - 1's records and literal bits
+    if (!ZH_ONE_BARRIER) {
+      if (lane == 0) atomicAdd(&misc[MISC_ARR], 1u);
+      k1_barrier();  // X: window k's match info and take masks; window k - 1's records and literal bits
+    }
     TL_MARK(3);
     ZH_STAMP(st_X);
-    if (MODE != 2 && have && wave != 0 && wave < (skipk ? RS : NWW - 1)) {
+    if (!ZH_ONE_BARRIER && MODE != 2 && have && wave != 0 && wave < (skipk ? RS : NWW - 1)) {
       // ---- take decision at this wave's span top (the next position was the next wave's):
       // every wave but the window's top one, its last position
       u32 const hi = skipk ? wave : r_hi;
@@ -1689,7 +1751,9 @@ __device__ __forceinline__ u32 lz_block(const ZhBlockDesc *__restrict__ blocks, 
         if (i < we - wsb && (inf & 255u) && take_rule<MODE>(inf, inf1)) atomicOr((u32 *)&tmK[i >> 6] + ((i >> 5) & 1u), 1u << (i & 31));
       }
     }
-    if (ZH_LIT_INS && prev2) {
+    if (ZH_ONE_BARRIER) {
+      // (the records wave keeps the totals)
+    } else if (ZH_LIT_INS && prev2) {
       // (the inserters extract window k - 2's literals in step k + 1)
       nlit_tot += (u32)__builtin_amdgcn_readfirstlane(lbxq[NSEG]);
       nseq_tot += __builtin_amdgcn_readfirstlane(misc[MISC_WNM + kb]);
@@ -1731,10 +1795,11 @@ __device__ __forceinline__ u32 lz_block(const ZhBlockDesc *__restrict__ blocks, 
     }
     ZH_STAMP(st_E);
     TL_MARK(4);
+    skp_prev = skipk;
   }
   TL_FLUSH(wave, lane);
   if (!dead) {
-    if (tid_ == 0) { meta[0] = nseq_tot; meta[1] = nlit_tot; meta[2] = 0; }
+    if (tid_ == (ZH_ONE_BARRIER ? 64u * REC_WAVE : 0u)) { meta[0] = nseq_tot; meta[1] = nlit_tot; meta[2] = 0; }
 #ifdef ZH_STAMPS
     if (tid == 0) {
       u32 *dbg = ws.dbg(b);
