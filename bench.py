@@ -140,14 +140,22 @@ def cpu_run(mode, data, nchunks, threads, passes=5, sizes=None, slot=0, chunk=CH
     return {"seconds": t, "out_bytes": outb.value, "version": L.cpub_zstd_version()}
 
 
-def smt_yield(host, mode=0, sizes=None, slot=0):
+def smt_yield(host, mode=0, sizes=None, slot=0, ref_g1=None):
     """libzstd throughput (mode 0: level-3 compression of the chunks in `host`; mode 1:
     decompression of the frames in `host`, `sizes` bytes at `slot` strides) of one core's two
     hardware threads over one thread alone, both pinned (the hardware threads the affinity holds
-    beyond the physical cores are worth this much each, not a whole core).  None when the
-    affinity holds no sibling pair."""
+    beyond the physical cores are worth this much each, not a whole core).  The box shares its
+    host: a core whose pinned thread runs below 0.8 x `ref_g1` (the unpinned 1-thread rate) is
+    busy with someone else's work, so up to 4 cores spread over the affinity are tried and the
+    median yield of the uncontended ones is reported (round 6: a contended cpu 0 ran at a third
+    of the unpinned rate and reported a yield above 4).  None when no sibling pair was usable."""
     aff = sorted(os.sched_getaffinity(0))
-    for a in aff:
+    pairs, seen = [], set()
+    # candidate cores spread over the affinity list, cpu 0 last (it takes the host's interrupts)
+    order = [aff[(len(aff) * j) // 8] for j in (1, 3, 5, 7, 2, 6)] + aff
+    for a in order:
+        if a in seen:
+            continue
         try:
             sib = open(f"/sys/devices/system/cpu/cpu{a}/topology/thread_siblings_list").read().strip()
         except OSError:
@@ -156,20 +164,33 @@ def smt_yield(host, mode=0, sizes=None, slot=0):
         for part in sib.split(","):
             lo, _, hi = part.partition("-")
             ids.update(range(int(lo), int(hi or lo) + 1))
+        seen.update(ids)
         b = next((x for x in sorted(ids) if x != a and x in aff), None)
-        if b is None:
-            continue
-        avail = len(sizes) if sizes is not None else len(host) // CHUNK
-        n = min(avail, 512)
-        n2 = 2 * n if avail >= 2 * n else n
+        if b is not None and a != 0:
+            pairs.append((a, b))
+        if len(pairs) == 4:
+            break
+    avail = len(sizes) if sizes is not None else len(host) // CHUNK
+    n = min(avail, 512)
+    n2 = 2 * n if avail >= 2 * n else n
+    tried = []
+    for a, b in pairs:
         r1 = cpu_run(mode, host, n, 1, passes=3, cpus=[a], sizes=sizes, slot=slot)
         r2 = cpu_run(mode, host, n2, 2, passes=3, cpus=[a, b], sizes=sizes, slot=slot)
         if not r1 or not r2:
-            return None
+            continue
         g1 = n * CHUNK / r1["seconds"]
         g2 = n2 * CHUNK / r2["seconds"]
-        return {"value": round(g2 / g1, 3), "cpus": [a, b], "one_thread_GBps": round(g1 / 1e9, 4), "two_siblings_GBps": round(g2 / 1e9, 4)}
-    return None
+        ok = ref_g1 is None or g1 >= 0.8 * ref_g1 * 1e9
+        tried.append({"cpus": [a, b], "one_thread_GBps": round(g1 / 1e9, 4), "two_siblings_GBps": round(g2 / 1e9, 4),
+                      "yield": round(g2 / g1, 3), "uncontended": ok})
+        if sum(t["uncontended"] for t in tried) >= 2:
+            break
+    good = sorted(t["yield"] for t in tried if t["uncontended"])
+    if not good:
+        return None
+    return {"value": good[len(good) // 2], "pairs": tried,
+            "rule": "median over pinned sibling pairs whose 1-thread rate is >= 0.8 x the unpinned 1-thread rate"}
 
 
 def cpu_baseline(host, threads, gpu_gbs):
@@ -203,7 +224,7 @@ def cpu_baseline(host, threads, gpu_gbs):
     # threads (the affinity holds 2 threads per core); the denominator of
     # gpu_speedup.vs_all_core
     hw = info["affinity_threads"] or threads
-    smt = smt_yield(host) if (hw > cores and not measured_all) else None
+    smt = smt_yield(host, ref_g1=g1) if (hw > cores and not measured_all) else None
     smt_f = min(smt["value"], 2.0) if smt else (hw / cores if hw > cores else 1.0)
     base_all = gm if measured_all else max(gm, all_core)
     all_hw = base_all * (smt_f if hw > cores and not measured_all else 1.0)
@@ -511,7 +532,7 @@ def cpu_decompress_baseline(b, threads, gpu_gbs=None):
     if g1:
         eff = gm / (threads * g1)
         base_all = gm if measured_all else max(gm, g1 * cores * min(1.0, eff))
-        smt = smt_yield(frames, mode=1, sizes=sizes, slot=b.slot) if (hw > cores and not measured_all) else None
+        smt = smt_yield(frames, mode=1, sizes=sizes, slot=b.slot, ref_g1=g1) if (hw > cores and not measured_all) else None
         smt_f = min(smt["value"], 2.0) if smt else (hw / cores if hw > cores else 1.0)
         all_hw = base_all * (smt_f if hw > cores and not measured_all else 1.0)
         res["single_thread"] = {"value": round(g1, 4), "unit": "GB/s (decompressed bytes)", "sample": f"the first {n1} frames, median of 3 sweeps"}
