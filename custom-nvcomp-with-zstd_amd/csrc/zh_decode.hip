@@ -42,6 +42,11 @@
 
 typedef int64_t s64;
 
+// 1: the quad sequence kernel (four lanes per buffer); 0: the one-lane-per-buffer kernel
+#ifndef ZH_DEC_QUAD
+#define ZH_DEC_QUAD 1
+#endif
+
 namespace {
 
 constexpr u32 DEC_THREADS = 64;
@@ -1109,7 +1114,17 @@ extern "C" __global__ __launch_bounds__(DEC_THREADS) void zh_decode_kernel(ZhDec
           if (a.phase == 1 && produced == 0 && last && ip + bsz + (chk ? 4ull : 0ull) == srcn) {
             // the buffer's only block: hand the sequence bitstream to zh_dec_seq_kernel
             DecHandoff *const ho = handoff(a, item);
+#if ZH_DEC_QUAD
+            // the quad sequence kernel's entries: newState | symbol << 9 | extra bits << 16 |
+            // state bits << 24 (the extra bits of a code: LL / ML from the code tables, OF = code)
+            for (u32 w = lane; w < 1280; w += 64) {
+              u32 const e = L.fse[w], sym = e & 0x3Fu;
+              u32 const xb = w < 512 ? L.info[0][sym] >> 24 : w < 768 ? sym : L.info[1][sym] >> 24;
+              ho->tabs[w] = (e >> 16) | sym << 9 | xb << 16 | ((e >> 8) & 0xFFu) << 24;
+            }
+#else
             for (u32 w = lane; w < 1280; w += 64) ho->tabs[w] = L.fse[w];
+#endif
             if (lane == 0) {
               ho->sp = (u64)sp;
               ho->rem = rem;
@@ -1291,11 +1306,11 @@ extern "C" __global__ __launch_bounds__(DEC_THREADS) void zh_dec_exec_kernel(ZhD
 #ifndef ZH_D2_BUF
 #define ZH_D2_BUF 64
 #endif
-constexpr u32 D2_BUF = ZH_D2_BUF;
+[[maybe_unused]] constexpr u32 D2_BUF = ZH_D2_BUF;
 // Decoded sequences go to an LDS ring and leave in 256-byte bursts every D2_RUN steps:
 // CDNA's vmcnt counts stores too and retires in order, so a per-step global store would
 // make every window load wait for the previous step's write acknowledgement.
-constexpr u32 D2_RUN = 32;
+[[maybe_unused]] constexpr u32 D2_RUN = 32;
 
 // the top k (<= 31) bits of T; T <<= k
 __device__ __forceinline__ u32 take(u64 &T, u32 k) {
@@ -1346,6 +1361,147 @@ __device__ __forceinline__ Win5 win_fetch(uintptr_t A) {
   return Win5{q[0], q[1], q[2], q[3], q[4]};
 }
 
+#if ZH_DEC_QUAD
+// Quad sequence kernel: FOUR lanes per buffer, 16 buffers per wave.  A block's FSE chain is
+// serial (decoding from a guessed entry never rejoins the true trajectory: tools/seq_sync.py
+// measured 0 of 240 guesses synchronising over whole C3 blocks), so the step itself is what
+// has to get shorter.  Lane q of a quad owns one table: 0 = offsets, 1 = match lengths,
+// 2 = literal lengths, 3 = the record (repcodes, ring).  A step is the same instruction stream
+// for all of them: one table read each (entries repacked by phase 1 as newState | symbol << 9
+// | extra bits << 16 | state bits << 24), three quad broadcasts (DPP) give every lane the
+// bit offsets of its two fields (extra bits in the order OF, ML, LL from the top, then the
+// states LL, ML, OF), two 64-bit reads of a 32-byte window the previous step staged in LDS
+// by an LDS-DMA load, and three broadcasts more hand the values to lane 3.  About half the
+// instructions of the one-lane step, and four times as many waves to share the SIMDs the
+// 64-buffer waves left idle.
+constexpr u32 DQ_BUF = 16;  // buffers per wave
+constexpr u32 DQ_RUN = 32;  // records per ring run (256 bytes per buffer)
+
+// resolve_off_bf with the repeat candidates picked by masks: the nested selects of the
+// one-lane kernel compile to exec-mask branches here
+__device__ __forceinline__ u32 resolve_off_masks(u32 ofv, u32 ll, u32 &r0, u32 &r1, u32 &r2) {
+  bool const lit = ofv > 3;
+  u32 const idx = ofv - 1 + (ll == 0 ? 1u : 0u);  // repeat index when !lit: 0..3
+  u32 const m1 = 0u - (u32)(idx == 1), m2 = 0u - (u32)(idx == 2), m3 = 0u - (u32)(idx == 3);
+  u32 rs = (r1 & m1) | (r2 & m2) | ((r0 - 1) & m3);
+  rs += rs == 0 ? 1u : 0u;
+  u32 const off = lit ? ofv - 3 : idx == 0 ? r0 : rs;
+  bool const upd = lit || idx != 0;
+  u32 const n2 = (r2 & m1) | (r1 & ~m1);  // (a literal offset has m1 = 0)
+  r2 = upd ? n2 : r2;
+  r1 = upd ? r0 : r1;
+  r0 = upd ? off : r0;
+  return off;
+}
+
+template <u32 L>
+__device__ __forceinline__ u32 quad_bcast(u32 v) {
+  return ZH_DPP(v, L * 0x55u, 0xf);  // quad_perm [L, L, L, L]
+}
+
+typedef const __attribute__((address_space(1))) void *gvoid;
+typedef __attribute__((address_space(3))) void *lvoid;
+
+extern "C" __global__ __launch_bounds__(64) void zh_dec_seq_kernel(ZhDecArgs a, u32 nitems) {
+  __builtin_amdgcn_s_setprio(3);
+  __shared__ u32 info[4][64];  // baselines by code: OF (1 << code), ML, LL, none
+  __shared__ __attribute__((aligned(16))) u32 win[2][DQ_BUF][16];  // stream windows, 64 B per quad
+  __shared__ __attribute__((aligned(16))) u64 ring[DQ_BUF][DQ_RUN];
+  u32 const lane = lane_id(), q = lane & 3u, b = lane >> 2;
+  info[0][lane] = lane < 32 ? 1u << lane : 0u;
+  info[1][lane] = lane < 53 ? c_ML_info[lane] & 0xFFFFFFu : 0u;
+  info[2][lane] = lane < 36 ? c_LL_info[lane] & 0xFFFFFFu : 0u;
+  info[3][lane] = 0u;
+  __syncthreads();
+  u32 const it = a.item0 + blockIdx.x * DQ_BUF + b, end = a.item0 + nitems;
+  if (it >= end) return;  // (quad-uniform from here on: the four lanes read the same buffer)
+  DecHandoff *const ho = handoff(a, it);
+  if (ho->flag != 1) return;
+  const u32 *const tq = ho->tabs + (q == 0 ? 512u : q == 1 ? 768u : 0u);
+  const u8 *const sp = (const u8 *)ho->sp;
+  u32 const nseq = ho->nseq, lg = ho->lg;
+  s32 const n = (s32)ho->rem;
+  u64 *const seq = (u64 *)(a.ws + (size_t)it * a.slot_bytes + a.lit_bytes);
+  u32 const lastb = n > 0 ? sp[n - 1] : 0u;
+  bool const bad = lastb == 0;
+  s32 pos = bad ? 0 : 8 * (n - 1) + (s32)hb32(lastb);
+  u32 rep0 = ho->rep[0], rep1 = ho->rep[1], rep2 = ho->rep[2];
+  bool big = false;
+  u64 acc = 0;  // lane 1: sum of match lengths, lane 2: of literal lengths
+  if (!bad) {
+    // The window of a step holds the 32 stream bytes from A = (the byte of bit pos - 89) & ~15
+    // (a step reads at most 89 bits below pos): lanes 0 and 1 load its two 16-byte pieces, lanes
+    // 2 and 3 the lines 128 and 256 bytes further down (a prefetch; their LDS pieces are never
+    // read).  Pieces are clamped to the 16-byte chunks holding the stream's first and last byte,
+    // so no load leaves the pages the stream touches; the bits a valid stream reads always lie in
+    // the first 32 bytes of the window (bits below the stream start are the frame's own bytes and
+    // are only read by corrupt streams, which end with pos != 0).
+    uintptr_t const base = (uintptr_t)sp, wlo = base & ~(uintptr_t)15;
+    s32 const bofs = (s32)(base - wlo), wspan = (s32)(((base + (u32)n - 1) & ~(uintptr_t)15) - wlo);
+    s32 const qoff = q == 0 ? 0 : q == 1 ? 16 : q == 2 ? -128 : -256;
+    auto fetch = [&](s32 p, u32 buf) -> s32 {  // -> the window's first stream bit
+      s32 const A = max(((p - 89) >> 3) + bofs, 0) & ~15;  // byte offsets from wlo
+      s32 const P = min(max(A + qoff, 0), wspan);
+      __builtin_amdgcn_global_load_lds((gvoid)(wlo + (u32)P), (lvoid)&win[buf][0][0], 16, 0, 0);
+      return 8 * (A - bofs);
+    };
+    // k bits whose lowest is window bit lo (lo within [0, 224) for valid streams)
+    auto field = [&](u32 buf, s32 lo, u32 k) -> u32 {
+      u32 const d = min((u32)(lo >> 5), 6u);
+      u32 const w0 = win[buf][b][d], w1 = win[buf][b][d + 1];
+      return __builtin_amdgcn_ubfe(__builtin_amdgcn_alignbit(w1, w0, (u32)lo & 31u), 0u, k);
+    };
+    s32 wb = fetch(pos, 0);
+    u32 s;
+    {  // initial states, from the top: LL, OF, ML
+      u32 const kL = lg & 0xFFu, kO = (lg >> 8) & 0xFFu, kM = lg >> 16;
+      u32 const k = q == 0 ? kO : q == 1 ? kM : q == 2 ? kL : 0u;
+      u32 const off = q == 0 ? kL : q == 1 ? kL + kO : 0u;
+      s = field(0, pos - (s32)(off + k) - wb, k);
+      pos -= (s32)(kL + kO + kM);
+    }
+    // software-pipelined: the table read of step i + 1 is issued as soon as its state is
+    // known, before step i's record work, which then covers its latency
+    u32 e = tq[s];
+    for (u32 i = 0; i < nseq; i++) {
+      u32 const cur = i & 1u;
+      u32 const v = q == 3 ? 0u : e >> 16;  // extra bits | state bits << 8
+      u32 const v0 = quad_bcast<0>(v), v1 = quad_bcast<1>(v), v2 = quad_bcast<2>(v);
+      u32 const s01 = v0 + v1, S = s01 + v2;
+      u32 const pre = q == 0 ? 0u : q == 1 ? v0 : s01;  // the fields of the lanes before this one
+      bool const more = i + 1 < nseq;                    // the last sequence reads no states
+      u32 const X = S & 0xFFu, NB = more ? S >> 8 : 0u;
+      u32 const xb = v & 0xFFu, nb = more ? v >> 8 : 0u;
+      u32 const xv = field(cur, pos - (s32)((pre & 0xFFu) + xb) - wb, xb);
+      u32 const sv = field(cur, pos - (s32)(X + NB) + (s32)(pre >> 8) - wb, nb);
+      pos -= (s32)(X + NB);
+      s = q == 3 ? 0u : (e & 0x1FFu) + sv;
+      u32 const en = tq[s];       // step i + 1 (after the last step: a harmless read)
+      wb = fetch(pos, cur ^ 1u);  // (after the last step too: no branch; drained below)
+      u32 const val = info[q][(e >> 9) & 0x3Fu] + xv;
+      acc += val;
+      // the record (every lane of the quad computes it; lane 3 keeps it)
+      u32 const ofv = quad_bcast<0>(val), ml = quad_bcast<1>(val), ll = quad_bcast<2>(val);
+      u32 const off = resolve_off_masks(ofv, ll, rep0, rep1, rep2);
+      big |= off >= OFF_LIMIT;
+      u32 const r = i & (DQ_RUN - 1);
+      if (q == 3) ring[b][r] = (u64)ll | (u64)(ml - 3) << 17 | (u64)off << 34;
+      if (r == DQ_RUN - 1) {  // a full run: 256 bytes, 64 from each lane of the quad
+        uint4 *const dst = (uint4 *)(seq + (i + 1 - DQ_RUN)) + 4 * q;
+        const uint4 *const srcr = (const uint4 *)ring[b] + 4 * q;
+#pragma unroll
+        for (u32 k = 0; k < 4; k++) dst[k] = srcr[k];
+      }
+      e = en;
+    }
+    for (u32 k = (nseq & ~(DQ_RUN - 1)) + q; k < nseq; k += 4) seq[k] = ring[b][k & (DQ_RUN - 1)];  // the partial last run
+    __builtin_amdgcn_s_waitcnt(0);  // the last window load lands before the workgroup's LDS is released
+  }
+  if (q == 1) ho->sumML = acc;
+  if (q == 2) ho->sumLL = acc;
+  if (q == 3) ho->sbad = (bad || pos != 0 || big) ? 1u : 0u;
+}
+#else
 extern "C" __global__ __launch_bounds__(D2_BUF) void zh_dec_seq_kernel(ZhDecArgs a, u32 nitems) {
   // highest issue priority: the chains are issue-latency bound and share SIMDs with the
   // phase-1 / phase-3 waves of the other groups of the pipeline
@@ -1456,6 +1612,7 @@ extern "C" __global__ __launch_bounds__(D2_BUF) void zh_dec_seq_kernel(ZhDecArgs
   ho->sumML = sumML;
   ho->sbad = (bad || pos != 0 || big) ? 1u : 0u;
 }
+#endif  // ZH_DEC_QUAD
 
 namespace {
 struct DecPipeTag {};
@@ -1481,7 +1638,11 @@ hipError_t launch_decompress(const ZhDecArgs &a0, u32 nitems, hipStream_t stream
     hipLaunchKernelGGL(zh_decode_kernel, dim3(cnt), dim3(DEC_THREADS), 0, s, a);
     check("phase 1");
     if (after_p1) (void)hipEventRecord(after_p1, s);
+#if ZH_DEC_QUAD
+    hipLaunchKernelGGL(zh_dec_seq_kernel, dim3((cnt + DQ_BUF - 1) / DQ_BUF), dim3(64), 0, s, a, cnt);
+#else
     hipLaunchKernelGGL(zh_dec_seq_kernel, dim3((cnt + D2_BUF - 1) / D2_BUF), dim3(D2_BUF), 0, s, a, cnt);
+#endif
     check("sequences");
     hipLaunchKernelGGL(zh_dec_exec_kernel, dim3(cnt), dim3(DEC_THREADS), 0, s, a);
     check("phase 3");
