@@ -43,6 +43,9 @@
 typedef int64_t s64;
 
 // 1: the quad sequence kernel (four lanes per buffer); 0: the one-lane-per-buffer kernel
+#ifndef ZH_DEC_HUFPAR
+#define ZH_DEC_HUFPAR 1  // segment-parallel Huffman literal streams (0: one lane per stream)
+#endif
 #ifndef ZH_DEC_QUAD
 #define ZH_DEC_QUAD 1
 #endif
@@ -559,6 +562,160 @@ __device__ void wave_fill(u8 *dst, u32 v, u32 n) {
 }
 
 // Literals section (RFC 8878 §3.1.1.3.1).  Returns section bytes, 0 on error (status in st).
+#if ZH_DEC_HUFPAR
+// ---- segment-parallel Huffman streams --------------------------------------------------------
+// One lane per stream (the libzstd decoder's shape) makes a block's literals a chain of
+// n / 4 dependent table reads.  A Huffman code resynchronises within a few symbols when
+// decoding starts at an arbitrary bit, so each stream is cut into S = 64 / streams segments of
+// L bits, lane j of a stream decoding the symbols that start in (top - (j+1) L, top - j L]:
+//   pass A: lane j decodes from its segment's first bit (a guess for j > 0), recording the first
+//           HP_TRAJ positions of its trajectory, its symbol count and its exit (the first
+//           position at or below its segment's end);
+//   fix-up: while a lane's entry differs from its left neighbour's exit, it decodes again from
+//           that exit until it lands on a recorded position of its pass-A trajectory (from there
+//           on the two coincide: count = new steps + pass-A steps after that point) or leaves
+//           its segment (Jacobi rounds: lane 0 is exact, lane j after at most j rounds);
+//   pass B: each lane decodes its count of symbols from its exact entry and writes them at the
+//           prefix sum of the counts before it.
+// The symbols and the stream verdict equal the serial decode's: a stream is valid when the
+// counts add up to its symbol count and the last segment ends exactly at bit 0.
+constexpr u32 HP_TRAJ = 32;
+
+// A lane's reader over one stream: dwords from the 4-aligned base ab (dwords holding no stream
+// byte read as 0, so no load leaves the pages the stream touches), a 4-dword window w0..w3 at
+// dword index wi and the two dwords below it prefetched.  Bits below the stream's bit 0 read
+// as zeros (the serial reader's rule).
+struct HufReader {
+  const u32 *ab;
+  s32 da8, lastw, wi, p;
+  u32 w0, w1, w2, w3, q0, q1;
+  __device__ __forceinline__ u32 ld(s32 i) const { return (i >= 0 && i <= lastw) ? ab[i] : 0u; }
+  __device__ __forceinline__ void init(const u8 *sp, u32 n) {
+    ab = (const u32 *)((uintptr_t)sp & ~(uintptr_t)3);
+    da8 = 8 * (s32)((uintptr_t)sp & 3u);
+    lastw = (s32)(((uintptr_t)sp + n - 1 - (uintptr_t)ab) >> 2);
+  }
+  __device__ __forceinline__ void seek(s32 pos) {
+    p = pos;
+    wi = ((pos + da8 + 31) >> 5) - 4;  // bit pos lies in (96, 128] of the window
+    w0 = ld(wi); w1 = ld(wi + 1); w2 = ld(wi + 2); w3 = ld(wi + 3);
+    q0 = ld(wi - 2); q1 = ld(wi - 1);
+  }
+  // decode one symbol: sym | nbBits << 8
+  __device__ __forceinline__ u32 next(const u16 *dt, u32 tlog) {
+    s32 v = p + da8 - 32 * wi - (s32)tlog;  // window bit of the peek's lowest bit
+    if (v < 32) {  // slide down two dwords (v >= 21: a step consumes <= 11 bits)
+      w3 = w1; w2 = w0; w1 = q1; w0 = q0;
+      wi -= 2;
+      v += 64;
+      q0 = ld(wi - 2);
+      q1 = ld(wi - 1);
+    }
+    u32 const k = (u32)v >> 5;  // 1..3
+    // (mask selects: the compiler turns a select chain on k into a scratch-indexed array)
+    u32 const m2 = 0u - ((k >> 1) & 1u), m1 = 0u - (k & 1u);
+    u32 const lo = (w1 & ~m2) | (((w2 & ~m1) | (w3 & m1)) & m2), hi = (w2 & ~m2) | (w3 & ~m1 & m2);
+    u32 x = __builtin_amdgcn_alignbit(hi, lo, (u32)v & 31u) & ((1u << tlog) - 1u);
+    if (p < (s32)tlog) x &= (p <= 0) ? 0u : ~0u << (tlog - (u32)p);  // bits below the stream
+    u32 const e = dt[x];
+    p -= (s32)max(e >> 8, 1u);  // (>= 1 in any table huf_build_dtable makes; a loop bound)
+    return e;
+  }
+};
+
+// Decodes the ns (1 or 4) streams into o + off[k]; false = corrupt.  Every lane calls it.
+// (msp, mn, mc, mo: this lane's stream -- bytes, size, symbols, output offset)
+__device__ __forceinline__ bool huf_streams_par(DecLds &L, u32 ns, const u8 *msp, u32 mn, u32 mc, u32 mo, u8 *o, u32 tlog) {
+  u32 const lane = lane_id();
+  u32 const S = 64u / ns, k = lane / S, j = lane % S;
+  u32 const last = mn ? msp[mn - 1] : 0u;
+  bool bad = last == 0;
+  s32 const top = bad ? 0 : 8 * (s32)(mn - 1) + (s32)hb32(last);
+  s32 const Lb = max((top + (s32)S - 1) / (s32)S, 1);
+  s32 const hiB = top - (s32)j * Lb, lo = max(top - (s32)(j + 1) * Lb, 0);
+  const u16 *const dt = L.u.h.dt;
+  u16 *const traj = (u16 *)&L.u.h.hs[0][0];  // [HP_TRAJ][64]
+  HufReader r;
+  r.init(msp, mn);
+  // pass A
+  s32 const gA = max(hiB, 0);
+  u32 cA = 0;
+  r.seek(gA);
+  if (!bad) {
+    while (r.p > lo) {
+      if (cA < HP_TRAJ) traj[cA * 64 + lane] = (u16)(gA - r.p);
+      r.next(dt, tlog);
+      cA++;
+    }
+  }
+  s32 const xA = r.p;
+  // fix-up rounds
+  auto shr = [&](s32 v) -> s32 {  // the value of lane j - 1 of this stream (lane j = 0: top)
+    s32 const u = ns == 1 ? (s32)wave_shr1((u32)v) : (s32)ZH_DPP((u32)v, 0x111, 0xf);
+    return j == 0 ? top : u;
+  };
+  s32 entry = gA, x = xA;
+  u32 c = cA;
+  for (;;) {
+    s32 const px = shr(x);
+    bool const need = !bad && entry != px;
+    if (!__ballot(need)) break;
+    if (need) {
+      r.seek(px);
+      u32 n = 0, t = 0;
+      u32 const tmax = min(cA, HP_TRAJ);
+      s32 nx = 0;
+      u32 nc = 0;
+      for (;;) {
+        s32 const pn = r.p;
+        while (t < tmax && gA - (s32)traj[t * 64 + lane] > pn) t++;
+        if (t < tmax && gA - (s32)traj[t * 64 + lane] == pn) { nc = n + (cA - t); nx = xA; break; }
+        if (pn <= lo) { nc = n; nx = pn; break; }
+        r.next(dt, tlog);
+        n++;
+      }
+      entry = px;
+      c = nc;
+      x = nx;
+    }
+  }
+  // counts -> output offsets; the stream's verdict
+  u32 incl = c;
+  if (ns == 1) {
+    incl = wave_scan_incl(c);
+  } else {
+    incl += ZH_DPP(incl, 0x111, 0xf);
+    incl += ZH_DPP(incl, 0x112, 0xf);
+    incl += ZH_DPP(incl, 0x114, 0xf);
+    incl += ZH_DPP(incl, 0x118, 0xf);
+  }
+  int const src = (int)((k * S + S - 1) << 2);  // the stream's last lane (a per-lane index)
+  u32 const total = (u32)__builtin_amdgcn_ds_bpermute(src, (int)incl);
+  s32 const fin = __builtin_amdgcn_ds_bpermute(src, x);
+  bad |= total != mc || fin != 0;
+  if (__ballot(bad)) return false;
+  // pass B: c symbols from entry to o + mo + (incl - c); bytes until the dword boundary, packed
+  // dwords inside, bytes for the tail
+  u32 const o0 = mo + incl - c, o1 = mo + incl;
+  u32 const a0 = (o0 + 3u) & ~3u, a1 = o1 & ~3u;
+  r.seek(entry);
+  u32 acc = 0;
+  for (u32 i = o0; i < o1; i++) {
+    u32 const sym = r.next(dt, tlog) & 0xFFu;
+    if (i < a0 || i >= a1) {
+      o[i] = (u8)sym;
+    } else {
+      acc |= sym << (8 * (i & 3u));
+      if ((i & 3u) == 3u) {
+        *(u32 *)(o + i - 3) = acc;
+        acc = 0;
+      }
+    }
+  }
+  return true;
+}
+#endif
+
 __device__ u32 decode_literals(DecLds &L, const u8 *bp, u32 bsz, const Slot &sl, LitSrc &lits, u32 &st) {
   u32 const lane = lane_id();
   if (bsz < 1) { st = ST_CORRUPT; return 0; }
@@ -658,6 +815,16 @@ __device__ u32 decode_literals(DecLds &L, const u8 *bp, u32 bsz, const Slot &sl,
       off[k] = k * seg;
     }
   }
+#if ZH_DEC_HUFPAR
+  {
+    u32 const k = lane / (64u / ns);
+    const u8 *msp = sp[0];
+    u32 mn = ssz[0], mc = cnt[0], mo = off[0];
+    for (u32 t = 1; t < 4; t++)
+      if (k == t) { msp = sp[t]; mn = ssz[t]; mc = cnt[t]; mo = off[t]; }
+    if (!huf_streams_par(L, ns, msp, mn, mc, mo, sl.lit, tlog)) { st = ST_CORRUPT; return 0; }
+  }
+#else
   // lanes 0..ns-1 decode one stream each, reading it from an LDS stage; a lane whose
   // stage runs out stops, and the wave restages every such stream in one burst per round
   const u8 *mp = sp[0];
@@ -698,6 +865,7 @@ __device__ u32 decode_literals(DecLds &L, const u8 *bp, u32 bsz, const Slot &sl,
   }
   bad |= act && r.pos != 0;
   if (__ballot(bad)) { st = ST_CORRUPT; return 0; }
+#endif
   lits.g = sl.lit;
   lits.rle = 0;
   lits.n = n;
@@ -783,11 +951,29 @@ __device__ __forceinline__ u32 to_nvcomp(u32 s) {
 // Returns false when an offset reaches before the frame start and the dictionary content
 // (dlen bytes ending at dend) that precedes it.
 template <class LDS>
-__device__ bool execute_block(LDS &L, const Slot &sl, u8 *ob, s64 fpos, const LitSrc &lits, u32 nseq, u32 tl, const u8 *dend, s64 dlen) {
+__device__ bool execute_block(LDS &L, const Slot &sl, u8 *ob, s64 fpos, const LitSrc &lits, u32 nseq, u32 tl, const u8 *dend, s64 dlen,
+                              u64 *xs = nullptr) {
   u32 const lane = lane_id();
   u32 q = 0, qd = 0, opos = 0, lcur = 0;
   bool bad = false;
+#ifdef ZH_STAMPS
+  // (-DZH_STAMPS, phase 3: xs[1] windows, xs[2] records + scan, [3] pass A, [4] pass B, [5] flush)
+  u64 xp = __builtin_amdgcn_s_memtime();
+#define XSTAMP(k)                                   \
+  do {                                              \
+    if (xs) {                                       \
+      u64 const _t = __builtin_amdgcn_s_memtime();  \
+      xs[k] += _t - xp;                             \
+      xp = _t;                                      \
+    }                                               \
+  } while (0)
+#else
+#define XSTAMP(k) do { } while (0)
+#endif
   while (q <= nseq) {
+#ifdef ZH_STAMPS
+    if (xs) xs[1]++;
+#endif
     u32 const gs = opos;
     u32 const idx = q + lane;
     bool const valid = idx <= nseq;
@@ -816,6 +1002,7 @@ __device__ bool execute_block(LDS &L, const Slot &sl, u8 *ob, s64 fpos, const Li
     L.wlit[lane] = lit0;
     L.woff[lane] = off;
     __syncthreads();
+    XSTAMP(2);
     // pass A
     constexpr u32 UA = 8;
     for (u32 x0 = 0; x0 < wlen; x0 += 64 * UA) {
@@ -847,6 +1034,7 @@ __device__ bool execute_block(LDS &L, const Slot &sl, u8 *ob, s64 fpos, const Li
       for (u32 t = 0; t < UA; t++)
         if (w[t]) L.u.out[x0 + 64 * t + lane] = v[t];
     }
+    XSTAMP(3);
     // pass B: matches with a source inside the window, in order
     s32 const mlo = ms < 0 ? -ms : 0;
     s32 const mhi = min((s32)ml, (s32)wlen - ms);
@@ -862,6 +1050,7 @@ __device__ bool execute_block(LDS &L, const Slot &sl, u8 *ob, s64 fpos, const Li
         if (sw >= 0) L.u.out[msj + m] = L.u.out[sw];
       }
     }
+    XSTAMP(4);
     // flush the window: head bytes to a 4-B aligned destination, then dwords
     {
       u8 *const d = ob + gs;
@@ -878,6 +1067,7 @@ __device__ bool execute_block(LDS &L, const Slot &sl, u8 *ob, s64 fpos, const Li
     }
     __threadfence_block();  // later windows read this one back from HBM
     __syncthreads();
+    XSTAMP(5);
     // advance: sequences that ended inside the window are done
     u32 const k = (u32)__popcll(__ballot(valid && ve <= (s32)wlen));
     if (k < 64) {
@@ -1272,13 +1462,19 @@ extern "C" __global__ __launch_bounds__(DEC_THREADS) void zh_dec_exec_kernel(ZhD
   lits.n = uni(ho->litn);
   u32 const nseq = uni(ho->nseq);
   u64 const sumLL = uni64(ho->sumLL), sumML = uni64(ho->sumML), fcs = uni64(ho->fcs), ipc = uni64(ho->ipc);
+#ifdef ZH_STAMPS
+  u64 xs[8] = {};
+  u64 const xt0 = __builtin_amdgcn_s_memtime();
+#else
+  u64 *const xs = nullptr;
+#endif
   u32 st = ST_OK;
   u64 produced = 0;
   if (uni(ho->sbad) || sumLL > lits.n || lits.n + sumML > BLOCKSIZE_MAX) {
     st = ST_CORRUPT;
   } else if (lits.n + sumML > cap) {
     st = ST_SMALL;
-  } else if (!execute_block(L, sl, dst, 0, lits, nseq, lits.n - (u32)sumLL, dend, dlen)) {
+  } else if (!execute_block(L, sl, dst, 0, lits, nseq, lits.n - (u32)sumLL, dend, dlen, xs)) {
     st = ST_CORRUPT;
   } else {
     produced = lits.n + sumML;
@@ -1288,6 +1484,12 @@ extern "C" __global__ __launch_bounds__(DEC_THREADS) void zh_dec_exec_kernel(ZhD
     __threadfence_block();
     if ((u32)zh_xxh64(dst, produced) != rd32(src + ipc)) st = ST_CHECKSUM;
   }
+#ifdef ZH_STAMPS
+  xs[0] = __builtin_amdgcn_s_memtime() - xt0;
+  xs[6] = nseq;
+  xs[7] = produced;
+  if (lane < 8) ((u64 *)sl.lit)[lane] = xs[lane];
+#endif
   if (lane == 0) {
     a.out_sizes[item] = st == ST_OK ? produced : 0ull;
     if (a.statuses) a.statuses[item] = a.nvcomp_codes ? to_nvcomp(st) : st;
@@ -1374,6 +1576,12 @@ __device__ __forceinline__ Win5 win_fetch(uintptr_t A) {
 // by an LDS-DMA load, and three broadcasts more hand the values to lane 3.  About half the
 // instructions of the one-lane step, and four times as many waves to share the SIMDs the
 // 64-buffer waves left idle.
+#ifndef ZH_DQ_XCD
+#define ZH_DQ_XCD 0
+#endif
+#ifndef ZH_DQ_PF
+#define ZH_DQ_PF 0
+#endif
 constexpr u32 DQ_BUF = 16;  // buffers per wave
 constexpr u32 DQ_RUN = 32;  // records per ring run (256 bytes per buffer)
 
@@ -1407,13 +1615,22 @@ extern "C" __global__ __launch_bounds__(64) void zh_dec_seq_kernel(ZhDecArgs a, 
   __shared__ u32 info[4][64];  // baselines by code: OF (1 << code), ML, LL, none
   __shared__ __attribute__((aligned(16))) u32 win[2][DQ_BUF][16];  // stream windows, 64 B per quad
   __shared__ __attribute__((aligned(16))) u64 ring[DQ_BUF][DQ_RUN];
+#if ZH_DQ_PF
+  __shared__ u32 pfd[64];  // (the prefetch's landing words, never read)
+#endif
   u32 const lane = lane_id(), q = lane & 3u, b = lane >> 2;
   info[0][lane] = lane < 32 ? 1u << lane : 0u;
   info[1][lane] = lane < 53 ? c_ML_info[lane] & 0xFFFFFFu : 0u;
   info[2][lane] = lane < 36 ? c_LL_info[lane] & 0xFFFFFFu : 0u;
   info[3][lane] = 0u;
   __syncthreads();
+#if ZH_DQ_XCD
+  // the items phase 1 ran on this workgroup's XCD (blocks b and b + 8 share one): workgroup w
+  // takes items w % 8 + 8 (16 (w / 8) + b), so their tables are in the local L2 (speed only)
+  u32 const it = a.item0 + (blockIdx.x & 7u) + 8u * (DQ_BUF * (blockIdx.x >> 3) + b), end = a.item0 + nitems;
+#else
   u32 const it = a.item0 + blockIdx.x * DQ_BUF + b, end = a.item0 + nitems;
+#endif
   if (it >= end) return;  // (quad-uniform from here on: the four lanes read the same buffer)
   DecHandoff *const ho = handoff(a, it);
   if (ho->flag != 1) return;
@@ -1475,6 +1692,12 @@ extern "C" __global__ __launch_bounds__(64) void zh_dec_seq_kernel(ZhDecArgs a, 
       u32 const xv = field(cur, pos - (s32)((pre & 0xFFu) + xb) - wb, xb);
       u32 const sv = field(cur, pos - (s32)(X + NB) + (s32)(pre >> 8) - wb, nb);
       pos -= (s32)(X + NB);
+#if ZH_DQ_PF
+      // the next entry lies in [newState, newState + 2^nb): one 128-byte line when nb <= 5;
+      // touch it before the window read that finishes the state (an LDS-DMA load, so no
+      // register waits for it)
+      __builtin_amdgcn_global_load_lds((gvoid)(tq + (e & 0x1FFu)), (lvoid)&pfd[0], 4, 0, 0);
+#endif
       s = q == 3 ? 0u : (e & 0x1FFu) + sv;
       u32 const en = tq[s];       // step i + 1 (after the last step: a harmless read)
       wb = fetch(pos, cur ^ 1u);  // (after the last step too: no branch; drained below)
@@ -1639,7 +1862,11 @@ hipError_t launch_decompress(const ZhDecArgs &a0, u32 nitems, hipStream_t stream
     check("phase 1");
     if (after_p1) (void)hipEventRecord(after_p1, s);
 #if ZH_DEC_QUAD
+#if ZH_DQ_XCD
+    hipLaunchKernelGGL(zh_dec_seq_kernel, dim3(((cnt + 8 * DQ_BUF - 1) / (8 * DQ_BUF)) * 8), dim3(64), 0, s, a, cnt);
+#else
     hipLaunchKernelGGL(zh_dec_seq_kernel, dim3((cnt + DQ_BUF - 1) / DQ_BUF), dim3(64), 0, s, a, cnt);
+#endif
 #else
     hipLaunchKernelGGL(zh_dec_seq_kernel, dim3((cnt + D2_BUF - 1) / D2_BUF), dim3(D2_BUF), 0, s, a, cnt);
 #endif
@@ -1656,11 +1883,14 @@ hipError_t launch_decompress(const ZhDecArgs &a0, u32 nitems, hipStream_t stream
   // 56.0 / 56.2 / 36.6 GB/s, 2 : 1 and 3 : 1 splits 59.3 / 59.7.  Re-measured in round 4 with
   // the current kernels (tools/dec_ab.sh, profiles/r04zd_decode_groups_ab.json): G = 1 / 2 / 3
   // -> 57.6 / 60.6 / 59.1 GB/s; two groups 1 : 1 / 2 : 1 / 3 : 1 -> 60.6 / 60.6 / 60.5.
+  // Round 6 (quad sequence kernel ~4.3 ms, segment-parallel literals: phase 1 4.5 -> 2.5 ms;
+  // profiles/r06n_dec_hufpar_ab.json): two groups 1 : 1 / 2 : 1 / 3 : 1 -> 87.9 / 85.3 / 85.7
+  // GB/s, three groups 2 : 1 : 1 / 1 : 1 : 1 -> 86.9 / 81.0, four 1 : 1 : 1 : 1 80.5.
 #ifndef ZH_DEC_G
 #define ZH_DEC_G 2
 #endif
 #ifndef ZH_DEC_W0
-#define ZH_DEC_W0 2
+#define ZH_DEC_W0 1
 #endif
   constexpr u32 G = ZH_DEC_G, W0 = ZH_DEC_W0, MIN_GROUP = 1024;
   StreamPipe<G> *p = (!dbg && nitems >= G * MIN_GROUP) ? stream_pipe<DecPipeTag, G>(stream) : nullptr;
