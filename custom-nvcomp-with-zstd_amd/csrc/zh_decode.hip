@@ -89,6 +89,7 @@ constexpr u32 TAB_NONE = 0xFFFFu, TAB_PREDEF = 0xFFFEu;  // tkind; else RLE symb
 // The union's three views are used one after the other inside a block: Huffman decode,
 // sequence bitstream, execution window.
 struct DecLds {
+  static constexpr bool kLitStage = false;
   u32 fse[1280];  // LL [0,512) OF [512,768) ML [768,1280): sym | nbBits << 8 | newState << 16
   union {
     struct {
@@ -716,6 +717,39 @@ __device__ __forceinline__ bool huf_streams_par(DecLds &L, u32 ns, const u8 *msp
 }
 #endif
 
+// The literals section's size without decoding it (the split pipeline's tables pass); 0 when
+// its header is corrupt -- the literals pass then finds and reports the same error.
+__device__ u32 skip_literals(const u8 *bp, u32 bsz) {
+  if (bsz < 1) return 0;
+  u32 const h0 = ub(bp);
+  u32 const lt = h0 & 3u, sf = (h0 >> 2) & 3u;
+  if (lt <= 1) {
+    u32 hs, n;
+    if (sf == 1) {
+      if (bsz < 2) return 0;
+      hs = 2;
+      n = rd16(bp) >> 4;
+    } else if (sf == 3) {
+      if (bsz < 3) return 0;
+      hs = 3;
+      n = rd24(bp) >> 4;
+    } else {
+      hs = 1;
+      n = h0 >> 3;
+    }
+    if (n > BLOCKSIZE_MAX) return 0;
+    u32 const t = hs + (lt == 0 ? n : 1u);
+    return t <= bsz ? t : 0u;
+  }
+  u32 const hs = sf <= 1 ? 3u : sf == 2 ? 4u : 5u;
+  if (bsz < hs) return 0;
+  u64 const hv = sf <= 1 ? (u64)rd24(bp) : sf == 2 ? (u64)rd32(bp) : ((u64)rd32(bp) | (u64)ub(bp + 4) << 32);
+  u32 const n = sf <= 1 ? (u32)(hv >> 4) & 0x3FFu : sf == 2 ? (u32)(hv >> 4) & 0x3FFFu : (u32)(hv >> 4) & 0x3FFFFu;
+  u32 const cs = sf <= 1 ? (u32)(hv >> 14) & 0x3FFu : sf == 2 ? (u32)(hv >> 18) & 0x3FFFu : (u32)(hv >> 22) & 0x3FFFFu;
+  if (n > BLOCKSIZE_MAX || hs + cs > bsz) return 0;
+  return hs + cs;
+}
+
 __device__ u32 decode_literals(DecLds &L, const u8 *bp, u32 bsz, const Slot &sl, LitSrc &lits, u32 &st) {
   u32 const lane = lane_id();
   if (bsz < 1) { st = ST_CORRUPT; return 0; }
@@ -992,7 +1026,7 @@ __device__ bool execute_block(LDS &L, const Slot &sl, u8 *ob, s64 fpos, const Li
     s32 const ve = (s32)incl - (s32)qd;
     u32 const lit0 = lcur + linc - ll;
     u32 const tot = __builtin_amdgcn_readlane(incl, 63) - qd;
-    u32 const wlen = min((u32)DEC_STAGE, tot);
+    u32 const wlen = min((u32)sizeof(L.u.out) - 16u, tot);
     s32 const ms = vs + (s32)ll;  // window-relative match start
     // an offset reaching before the frame start is corrupt (checked before any read)
     bool const obad = valid && ml && vs < (s32)wlen && fpos + (s64)gs + ms - (s64)off < -dlen;
@@ -1001,13 +1035,35 @@ __device__ bool execute_block(LDS &L, const Slot &sl, u8 *ob, s64 fpos, const Li
     L.wll[lane] = ll;
     L.wlit[lane] = lit0;
     L.woff[lane] = off;
+    // the window's literal bytes, lits [lfirst, lfirst + wlen), staged with 16-byte loads
+    u32 lbase = 0, lfirst = 0;
+    if constexpr (LDS::kLitStage) {
+      if (lits.g) {
+        lfirst = lcur + min(qd, (u32)__builtin_amdgcn_readlane(ll, 0));
+        u32 const nlw = lits.n > lfirst ? min(wlen, lits.n - lfirst) : 0u;
+        if (nlw) {
+          uintptr_t const s0 = (uintptr_t)lits.g + lfirst, a0 = s0 & ~(uintptr_t)15;
+          uintptr_t const alast = ((uintptr_t)lits.g + lits.n - 1) & ~(uintptr_t)15;  // (no chunk past the literals)
+          u32 const nch = (u32)((s0 + nlw - 1 - a0) >> 4) + 1u;
+          for (u32 c = lane; c < nch; c += 64) {
+            uintptr_t const a = min(a0 + 16u * c, alast);
+            *(uint4 *)(L.lst + 16 * c) = *(const uint4 *)a;
+          }
+          lbase = (u32)(s0 - a0);
+        }
+      }
+    }
     __syncthreads();
     XSTAMP(2);
     // pass A
-    constexpr u32 UA = 8;
+#ifndef ZH_EXEC_UA
+#define ZH_EXEC_UA 4  // bytes per lane per pass-A round (8: 92.8, 16: 89.2, 4: 93.6 GB/s)
+#endif
+    constexpr u32 UA = ZH_EXEC_UA;
     for (u32 x0 = 0; x0 < wlen; x0 += 64 * UA) {
       const u8 *ad[UA];
       bool w[UA];
+      u32 li[UA];  // (staged literals: the byte's stage index, else ~0)
 #pragma unroll
       for (u32 t = 0; t < UA; t++) {
         u32 const x = x0 + 64 * t + lane;
@@ -1016,8 +1072,14 @@ __device__ bool execute_block(LDS &L, const Slot &sl, u8 *ob, s64 fpos, const Li
         for (u32 stp = 32; stp; stp >>= 1) j += L.wvs[j + stp] <= (s32)x ? stp : 0u;
         u32 const d = (u32)((s32)x - L.wvs[j]);
         u32 const llj = L.wll[j];
+        li[t] = ~0u;
         if (d < llj) {
-          ad[t] = lits.g ? lits.g + L.wlit[j] + d : nullptr;
+          if (LDS::kLitStage && lits.g) {
+            li[t] = lbase + L.wlit[j] + d - lfirst;
+            ad[t] = nullptr;
+          } else {
+            ad[t] = lits.g ? lits.g + L.wlit[j] + d : nullptr;
+          }
           w[t] = x < wlen;
         } else {
           u32 const m = d - llj, offj = L.woff[j];
@@ -1029,7 +1091,13 @@ __device__ bool execute_block(LDS &L, const Slot &sl, u8 *ob, s64 fpos, const Li
       }
       u8 v[UA];
 #pragma unroll
-      for (u32 t = 0; t < UA; t++) v[t] = w[t] ? (ad[t] ? *ad[t] : (u8)lits.rle) : (u8)0;
+      for (u32 t = 0; t < UA; t++) {
+        if constexpr (LDS::kLitStage) {
+          v[t] = !w[t] ? (u8)0 : li[t] != ~0u ? L.lst[min(li[t], (u32)sizeof(L.lst) - 1u)] : ad[t] ? *ad[t] : (u8)lits.rle;
+        } else {
+          v[t] = w[t] ? (ad[t] ? *ad[t] : (u8)lits.rle) : (u8)0;
+        }
+      }
 #pragma unroll
       for (u32 t = 0; t < UA; t++)
         if (w[t]) L.u.out[x0 + 64 * t + lane] = v[t];
@@ -1164,7 +1232,10 @@ extern "C" __global__ __launch_bounds__(DEC_THREADS) void zh_decode_kernel(ZhDec
   if (lane < 53) L.info[1][lane] = c_ML_info[lane];
   __syncthreads();
 
-  if (a.phase == 1 && lane == 0) handoff(a, item)->flag = 0;
+  // split pipeline (launch_decompress): phase 4 = the sequence tables of deferrable buffers
+  // only (no literals, no status), phase 5 = everything else (the literals of the deferred
+  // buffers, whole decodes of the others)
+  if ((a.phase == 1 || a.phase == 4) && lane == 0) handoff(a, item)->flag = 0;
 
   u32 st = ST_OK;
   u64 produced = 0, ip = 0;
@@ -1233,6 +1304,7 @@ extern "C" __global__ __launch_bounds__(DEC_THREADS) void zh_decode_kernel(ZhDec
       u32 const last = bh & 1u, bt = (bh >> 1) & 3u, bsz = bh >> 3;
       ip += 3;
       u8 *const ob = dst + produced;  // this block's first output byte
+      if (a.phase == 4 && !(bt == 2 && produced == 0 && last)) return;  // not deferrable
       if (bt == 0) {
         if (srcn - ip < bsz) { st = ST_CORRUPT; break; }
         if (bsz > cap - produced) { st = ST_SMALL; break; }
@@ -1250,9 +1322,27 @@ extern "C" __global__ __launch_bounds__(DEC_THREADS) void zh_decode_kernel(ZhDec
         const u8 *const bp = src + ip;
         LitSrc lits;
         DSTAMP(0);
-        u32 const ls = decode_literals(L, bp, bsz, sl, lits, st);
+        u32 const ls = a.phase == 4 ? skip_literals(bp, bsz) : decode_literals(L, bp, bsz, sl, lits, st);
         DSTAMP(1);
-        if (!ls) break;
+        if (a.phase == 5 && produced == 0 && uni(handoff(a, item)->flag) == 1) {
+          // deferred by phase 4: the literals are all this pass owes it (a corrupt literals
+          // section takes it back: the status is written below, phase 3 skips it)
+          DecHandoff *const ho = handoff(a, item);
+          if (!ls) {
+            if (lane == 0) ho->flag = 0;
+            break;
+          }
+          if (lane == 0) {
+            ho->litg = (u64)lits.g;
+            ho->litrle = lits.rle;
+            ho->litn = lits.n;
+          }
+          return;  // phase 3 writes the size and status
+        }
+        if (!ls) {
+          if (a.phase == 4) return;
+          break;
+        }
         // ---- sequences section header (RFC 8878 §3.1.1.3.2.1)
         const u8 *sp = bp + ls;
         u32 rem = bsz - ls;
@@ -1301,7 +1391,7 @@ extern "C" __global__ __launch_bounds__(DEC_THREADS) void zh_decode_kernel(ZhDec
           u32 const tused = uni(L.used);
           sp += tused;
           rem -= tused;
-          if (a.phase == 1 && produced == 0 && last && ip + bsz + (chk ? 4ull : 0ull) == srcn) {
+          if ((a.phase == 1 || a.phase == 4) && produced == 0 && last && ip + bsz + (chk ? 4ull : 0ull) == srcn) {
             // the buffer's only block: hand the sequence bitstream to zh_dec_seq_kernel
             DecHandoff *const ho = handoff(a, item);
 #if ZH_DEC_QUAD
@@ -1320,9 +1410,11 @@ extern "C" __global__ __launch_bounds__(DEC_THREADS) void zh_decode_kernel(ZhDec
               ho->rem = rem;
               ho->nseq = nseq;
               ho->lg = L.tlog[TAB_LL] | L.tlog[TAB_OF] << 8 | L.tlog[TAB_ML] << 16;
-              ho->litg = (u64)lits.g;
-              ho->litrle = lits.rle;
-              ho->litn = lits.n;
+              if (a.phase == 1) {
+                ho->litg = (u64)lits.g;
+                ho->litrle = lits.rle;
+                ho->litn = lits.n;
+              }
               ho->fcs = fcs;
               ho->ipc = chk ? ip + bsz : ~0ull;
               ho->rep[0] = rep0;
@@ -1332,6 +1424,7 @@ extern "C" __global__ __launch_bounds__(DEC_THREADS) void zh_decode_kernel(ZhDec
             }
             return;  // phase 3 writes the size and status
           }
+          if (a.phase == 4) return;
           // ---- sequence bitstream (RFC 8878 §3.1.1.3.2.2): every lane decodes redundantly
           // (uniform control flow, no exec-mask work); lane j keeps record j of each 64
           BitRevS r;
@@ -1387,6 +1480,7 @@ extern "C" __global__ __launch_bounds__(DEC_THREADS) void zh_decode_kernel(ZhDec
           st = ST_CORRUPT;
           break;
         }
+        if (a.phase == 4) return;  // (no sequences: nothing deferred)
         if (sumLL > lits.n) { st = ST_CORRUPT; break; }
         u64 const total = lits.n + sumML;
         // RFC 8878 §3.1.1.2.4: a block regenerates at most Block_Maximum_Size (128 KiB), which
@@ -1422,6 +1516,7 @@ extern "C" __global__ __launch_bounds__(DEC_THREADS) void zh_decode_kernel(ZhDec
   DSTAMP(5);
   if (lane < 8) ((u64 *)sl.lit)[lane] = stv[lane];
 #endif
+  if (a.phase == 4) return;  // (an error met here is reported by phase 5)
   if (lane == 0) {
     a.out_sizes[item] = st == ST_OK ? produced : 0ull;
     if (a.statuses) a.statuses[item] = a.nvcomp_codes ? to_nvcomp(st) : st;
@@ -1431,12 +1526,22 @@ extern "C" __global__ __launch_bounds__(DEC_THREADS) void zh_decode_kernel(ZhDec
 // Phase 3: execute the block of a buffer deferred by phase 1 (its sequence records are in
 // the slot) and finish the frame.  Its own kernel with only the execution window in LDS
 // (ExecLds, ~9 KB against DecLds' ~16 KB), so twice as many buffers execute per CU.
+#ifndef ZH_EXEC_STAGE
+#define ZH_EXEC_STAGE 2048  // (8192: 87.8 GB/s, 1024: 92.9, 2048: 92.8, 3072: 92.4; profiles/r06o_dec_exec_ab.json)
+#endif
+#ifndef ZH_EXEC_LSTAGE
+#define ZH_EXEC_LSTAGE 0
+#endif
 struct ExecLds {
+  static constexpr bool kLitStage = ZH_EXEC_LSTAGE != 0;
   union {
-    u8 out[DEC_STAGE + 16];
+    u8 out[ZH_EXEC_STAGE + 16];
   } u;
   s32 wvs[68];
   u32 wll[64], wlit[64], woff[64];
+#if ZH_EXEC_LSTAGE
+  __attribute__((aligned(16))) u8 lst[ZH_EXEC_STAGE + 32];  // the window's literal bytes
+#endif
 };
 
 extern "C" __global__ __launch_bounds__(DEC_THREADS) void zh_dec_exec_kernel(ZhDecArgs a) {
@@ -1891,6 +1996,33 @@ hipError_t launch_decompress(const ZhDecArgs &a0, u32 nitems, hipStream_t stream
 #endif
 #ifndef ZH_DEC_W0
 #define ZH_DEC_W0 1
+#endif
+#ifndef ZH_DEC_SPLIT
+#define ZH_DEC_SPLIT 1
+#endif
+#if ZH_DEC_SPLIT
+  // Split pipeline: phase 4 (headers + sequence tables of the deferrable buffers, no literals)
+  // gates the sequence kernel, which then runs every chain at once beside phase 5 (the
+  // literals, and whole decodes of the other buffers) on the side stream; phase 3 waits for
+  // both.  The chains no longer wait for the Huffman literals.
+  if (StreamPipe<2> *const sp2 = (!dbg && nitems >= 2048) ? stream_pipe<DecPipeTag, 2>(stream) : nullptr) {
+    std::lock_guard<std::mutex> lk(sp2->mu);
+    hipStream_t const side = sp2->side[0];
+    ZhDecArgs a = a0;
+    a.item0 = 0;
+    a.phase = 4;
+    hipLaunchKernelGGL(zh_decode_kernel, dim3(nitems), dim3(DEC_THREADS), 0, stream, a);
+    (void)hipEventRecord(sp2->first_done[0], stream);
+    (void)hipStreamWaitEvent(side, sp2->first_done[0], 0);
+    a.phase = 5;
+    hipLaunchKernelGGL(zh_decode_kernel, dim3(nitems), dim3(DEC_THREADS), 0, side, a);
+    (void)hipEventRecord(sp2->done[0], side);
+    hipLaunchKernelGGL(zh_dec_seq_kernel, dim3((nitems + DQ_BUF - 1) / DQ_BUF), dim3(64), 0, stream, a, nitems);
+    (void)hipStreamWaitEvent(stream, sp2->done[0], 0);
+    a.phase = 3;
+    hipLaunchKernelGGL(zh_dec_exec_kernel, dim3(nitems), dim3(DEC_THREADS), 0, stream, a);
+    return hipGetLastError();
+  }
 #endif
   constexpr u32 G = ZH_DEC_G, W0 = ZH_DEC_W0, MIN_GROUP = 1024;
   StreamPipe<G> *p = (!dbg && nitems >= G * MIN_GROUP) ? stream_pipe<DecPipeTag, G>(stream) : nullptr;
