@@ -109,6 +109,7 @@ struct DecLds {
   u8 hufw[256];     // Huffman weights of the last table (treeless literals rebuild from them)
   u32 tlog[3];      // table logs
   u32 tkind[3];     // TAB_NONE / TAB_PREDEF / RLE symbol | 0x100 / 0 = FSE
+  u32 bld[3];       // sequence tables whose build is left to build_dtable_wave (norm in norm + 64 t)
   u32 hlog, hnsym, hvalid;
   u32 err;   // serial-section status (lane 0 writes)
   u32 used;  // serial-section byte count (lane 0 writes)
@@ -908,16 +909,79 @@ __device__ u32 decode_literals(DecLds &L, const u8 *bp, u32 bsz, const Slot &sl,
 
 // One sequence table (mode 0 predefined, 1 RLE, 2 FSE, 3 repeat) on lane 0.
 // Returns bytes consumed (>= 0) or -1 on error.
-__device__ __noinline__ s32 seq_table(DecLds &L, u32 t, u32 mode, const u8 *p, u32 avail) {
+// FSE_buildDTable with the whole wave (same table as build_dtable): lanes = symbols for the
+// counts, then lanes = cells.  The spread visits position k * step mod size at step k, so the
+// cell placed at position u <= high is number k(u) = u * step^-1 mod size less the high
+// (low-probability) positions reached before it; its symbol is the one whose range of cells
+// holds that number.  A cell's state counter (symbolNext) is its symbol's count plus the cells
+// of that symbol at lower positions: counted chunk by chunk with one ballot per distinct
+// symbol, the running counts held by the symbols' lanes.  All lanes call it; false = invalid.
+__device__ bool build_dtable_wave(u32 *T, const s16 *norm, u32 maxSV, u32 tlog) {
+  u32 const lane = lane_id(), size = 1u << tlog, mask = size - 1u;
+  u64 const below = (1ull << lane) - 1ull;
+  s32 const c = lane <= maxSV ? (s32)norm[lane] : 0;
+  u64 const lowm = __ballot(c == -1);
+  u32 const nlow = (u32)__popcll(lowm), high = size - 1u - nlow;
+  u32 const cp = c > 0 ? (u32)c : 0u;
+  u32 const incl = wave_scan_incl(cp);
+  if (lane_value(incl, 63) != high + 1u || nlow > size) return false;
+  if (c == -1) T[size - 1u - (u32)__popcll(lowm & below)] = lane;  // low-probability symbols at the top
+  u32 const step = (size >> 1) + (size >> 3) + 3u;
+  u32 inv = step;  // step^-1 mod 2^32 (Newton: each round doubles the correct low bits)
+#pragma unroll
+  for (u32 r = 0; r < 5; r++) inv *= 2u - step * inv;
+  u32 const kh = lane < nlow ? ((high + 1u + lane) * inv) & mask : 0xFFFFFFFFu;  // steps of the high positions
+  for (u32 u = lane; u <= high; u += 64) {
+    u32 const k = (u * inv) & mask;
+    u32 skip = 0;
+    for (u32 l = 0; l < nlow; l++) skip += lane_value(kh, l) < k ? 1u : 0u;
+    u32 const r = k - skip;
+    // the symbol s with incl[s - 1] <= r < incl[s]: count the symbols whose range ends at or below r
+    u32 s = 0;
+    for (u32 t = 0; t <= maxSV; t++) s += lane_value(incl, t) <= r ? 1u : 0u;
+    T[u] = s;
+  }
+  __builtin_amdgcn_s_waitcnt(0xC07F);  // (lgkmcnt(0): the wave's LDS stores are done before the reads below)
+  __builtin_amdgcn_wave_barrier();
+  u32 cnt = c == -1 ? 1u : cp;  // symbolNext of symbol `lane`
+  for (u32 c0 = 0; c0 < size; c0 += 64) {
+    u32 const u = c0 + lane;
+    bool const valid = u < size;
+    u32 const s = valid ? T[u] & 0xFFu : 0xFFu;
+    u64 pending = __ballot(valid);
+    u32 ns = 0;
+    while (pending) {
+      u32 const s0 = (u32)__builtin_amdgcn_readlane((int)s, (int)__builtin_ctzll(pending));
+      u64 const m = __ballot(valid && s == s0);
+      u32 const base = lane_value(cnt, s0);
+      if (s == s0) ns = base + (u32)__popcll(m & below);
+      if (lane == s0) cnt += (u32)__popcll(m);
+      pending &= ~m;
+    }
+    if (valid) {
+      u32 const nb = tlog - hb32(ns);
+      T[u] = s | nb << 8 | ((ns << nb) - size) << 16;
+    }
+  }
+  __builtin_amdgcn_s_waitcnt(0xC07F);
+  __builtin_amdgcn_wave_barrier();
+  return true;
+}
+
+// defer: leave the table build to build_dtable_wave (the normalised counts go to norm + 64 t,
+// bld[t] is set); else build it here, serially.
+__device__ __noinline__ s32 seq_table(DecLds &L, u32 t, u32 mode, const u8 *p, u32 avail, bool defer = false) {
   u32 *T = L.fse + tab_off(t);
   u32 const maxSV = tab_maxsv(t);
+  s16 *const nrm = defer ? L.norm + 64 * t : L.norm;
   if (mode == 0) {
     if (L.tkind[t] == TAB_PREDEF) return 0;
     u32 const nsym = t == TAB_LL ? 36u : t == TAB_ML ? 53u : 29u;
     const s16 *src = t == TAB_LL ? c_LL_norm : t == TAB_ML ? c_ML_norm : c_OF_norm;
-    for (u32 s = 0; s <= maxSV; s++) L.norm[s] = s < nsym ? src[s] : (s16)0;
+    for (u32 s = 0; s <= maxSV; s++) nrm[s] = s < nsym ? src[s] : (s16)0;
     u32 const lg = t == TAB_OF ? 5u : 6u;
-    if (!build_dtable(T, L.norm, maxSV, lg, L.next)) return -1;
+    if (defer) L.bld[t] = 1;
+    else if (!build_dtable(T, nrm, maxSV, lg, L.next)) return -1;
     L.tlog[t] = lg;
     L.tkind[t] = TAB_PREDEF;
     return 0;
@@ -933,9 +997,10 @@ __device__ __noinline__ s32 seq_table(DecLds &L, u32 t, u32 mode, const u8 *p, u
   }
   if (mode == 2) {
     u32 lg;
-    u32 const used = read_ncount(p, avail, L.norm, maxSV, tab_maxlog(t), lg);
+    u32 const used = read_ncount(p, avail, nrm, maxSV, tab_maxlog(t), lg);
     if (!used) return -1;
-    if (!build_dtable(T, L.norm, maxSV, lg, L.next)) return -1;
+    if (defer) L.bld[t] = 1;
+    else if (!build_dtable(T, nrm, maxSV, lg, L.next)) return -1;
     L.tlog[t] = lg;
     L.tkind[t] = 0;
     return (s32)used;
@@ -1377,8 +1442,9 @@ extern "C" __global__ __launch_bounds__(DEC_THREADS) void zh_decode_kernel(ZhDec
           if (lane == 0) {
             u32 e = 0, used = 0;
             u32 const md[3] = {modes >> 6, (modes >> 4) & 3u, (modes >> 2) & 3u};
+            L.bld[0] = L.bld[1] = L.bld[2] = 0;
             for (u32 t = 0; t < 3 && !e; t++) {
-              s32 const u = seq_table(L, t, md[t], sp + used, rem - used);
+              s32 const u = seq_table(L, t, md[t], sp + used, rem - used, true);
               if (u < 0) e = 1;
               else used += (u32)u;
             }
@@ -1387,6 +1453,17 @@ extern "C" __global__ __launch_bounds__(DEC_THREADS) void zh_decode_kernel(ZhDec
           }
           __syncthreads();
           if (uni(L.err)) { st = ST_CORRUPT; break; }
+          {
+            bool ok = true;
+            for (u32 t = 0; t < 3; t++)
+              if (uni(L.bld[t])) ok = ok && build_dtable_wave(L.fse + tab_off(t), L.norm + 64 * t, tab_maxsv(t), uni(L.tlog[t]));
+            __syncthreads();
+            if (!ok) {
+              if (lane == 0) L.tkind[0] = L.tkind[1] = L.tkind[2] = TAB_NONE;  // (as the serial build left them unusable)
+              st = ST_CORRUPT;
+              break;
+            }
+          }
           DSTAMP(2);
           u32 const tused = uni(L.used);
           sp += tused;
