@@ -90,6 +90,7 @@ constexpr u32 TAB_NONE = 0xFFFFu, TAB_PREDEF = 0xFFFEu;  // tkind; else RLE symb
 // sequence bitstream, execution window.
 struct DecLds {
   static constexpr bool kLitStage = false;
+  static constexpr bool kStartMap = false;
   u32 fse[1280];  // LL [0,512) OF [512,768) ML [768,1280): sym | nbBits << 8 | newState << 16
   union {
     struct {
@@ -1118,6 +1119,21 @@ __device__ bool execute_block(LDS &L, const Slot &sl, u8 *ob, s64 fpos, const Li
         }
       }
     }
+    if constexpr (LDS::kStartMap) {
+      // the sequence of window byte x is the number of sequence starts at or below x, less one:
+      // a start bitmap (lane 0's sequence starts at 0 or before) and its per-word prefix counts
+      // (barriers between the lanes' LDS accesses: a one-wave workgroup, so an s_barrier
+      // costs little, and without them the compiler may move a lane's read above the others' ORs)
+      L.bm[2 * lane] = 0;
+      __syncthreads();
+      if (valid && vs < (s32)wlen) {
+        u32 const p = vs > 0 ? (u32)vs : 0u;
+        atomicOr(&L.bm[2 * (p >> 5)], 1u << (p & 31u));
+      }
+      __syncthreads();
+      u32 const c = (u32)__popc(L.bm[2 * lane]);
+      L.bm[2 * lane + 1] = wave_scan_incl(c) - c;
+    }
     __syncthreads();
     XSTAMP(2);
     // pass A
@@ -1133,8 +1149,14 @@ __device__ bool execute_block(LDS &L, const Slot &sl, u8 *ob, s64 fpos, const Li
       for (u32 t = 0; t < UA; t++) {
         u32 const x = x0 + 64 * t + lane;
         u32 j = 0;
+        if constexpr (LDS::kStartMap) {
+          u64 const e = ((const u64 *)L.bm)[min(x >> 5, 63u)];
+          u32 const m = (u32)e & (0xFFFFFFFFu >> (31u - (x & 31u)));
+          j = min((u32)(e >> 32) + (u32)__popc(m) - 1u, 63u);  // (bytes past wlen: any j, unused)
+        } else {
 #pragma unroll
-        for (u32 stp = 32; stp; stp >>= 1) j += L.wvs[j + stp] <= (s32)x ? stp : 0u;
+          for (u32 stp = 32; stp; stp >>= 1) j += L.wvs[j + stp] <= (s32)x ? stp : 0u;
+        }
         u32 const d = (u32)((s32)x - L.wvs[j]);
         u32 const llj = L.wll[j];
         li[t] = ~0u;
@@ -1609,13 +1631,21 @@ extern "C" __global__ __launch_bounds__(DEC_THREADS) void zh_decode_kernel(ZhDec
 #ifndef ZH_EXEC_LSTAGE
 #define ZH_EXEC_LSTAGE 0
 #endif
+#ifndef ZH_EXEC_BM
+#define ZH_EXEC_BM 1
+#endif
 struct ExecLds {
   static constexpr bool kLitStage = ZH_EXEC_LSTAGE != 0;
+  static constexpr bool kStartMap = ZH_EXEC_BM != 0;
   union {
     u8 out[ZH_EXEC_STAGE + 16];
   } u;
   s32 wvs[68];
   u32 wll[64], wlit[64], woff[64];
+#if ZH_EXEC_BM
+  static_assert(ZH_EXEC_STAGE <= 2048, "one start-map word per lane");
+  alignas(8) u32 bm[128];  // word 2 w: the window bytes [32 w, 32 w + 32) where a sequence starts; 2 w + 1: starts before them
+#endif
 #if ZH_EXEC_LSTAGE
   __attribute__((aligned(16))) u8 lst[ZH_EXEC_STAGE + 32];  // the window's literal bytes
 #endif
