@@ -43,6 +43,9 @@
 typedef int64_t s64;
 
 // 1: the quad sequence kernel (four lanes per buffer); 0: the one-lane-per-buffer kernel
+#ifndef ZH_EXEC_CHASE
+#define ZH_EXEC_CHASE 1  // (with the start bitmap) in-window sources followed in pass A; no pass B
+#endif
 #ifndef ZH_DEC_HUFPAR
 #define ZH_DEC_HUFPAR 1  // segment-parallel Huffman literal streams (0: one lane per stream)
 #endif
@@ -1148,6 +1151,42 @@ __device__ bool execute_block(LDS &L, const Slot &sl, u8 *ob, s64 fpos, const Li
 #pragma unroll
       for (u32 t = 0; t < UA; t++) {
         u32 const x = x0 + 64 * t + lane;
+        if constexpr (LDS::kStartMap && ZH_EXEC_CHASE) {
+          // every byte here: an in-window source is followed back (sequence by sequence, each
+          // step to an earlier one or into a literal run) to a literal or a byte already in HBM
+          u32 y = x < wlen ? x : 0u;
+          bool lit = false;
+          s32 swf = 0;
+          u32 litidx = 0;
+          for (;;) {
+            u64 const e = ((const u64 *)L.bm)[y >> 5];
+            u32 const m32 = (u32)e & (0xFFFFFFFFu >> (31u - (y & 31u)));
+            u32 const j = min((u32)(e >> 32) + (u32)__popc(m32) - 1u, 63u);
+            u32 const d = (u32)((s32)y - L.wvs[j]);
+            u32 const llj = L.wll[j];
+            if (d < llj) {
+              lit = true;
+              litidx = L.wlit[j] + d;
+              break;
+            }
+            u32 const m = d - llj, offj = L.woff[j];
+            s32 const sw = L.wvs[j] + (s32)llj - (s32)offj + (s32)(m < offj ? m : umod(m, offj));
+            if (sw < 0) {
+              swf = sw;
+              break;
+            }
+            y = (u32)sw;
+          }
+          li[t] = ~0u;
+          w[t] = x < wlen;
+          if (lit) {
+            ad[t] = lits.g ? lits.g + litidx : nullptr;
+          } else {
+            s64 const fa = fpos + (s64)gs + swf;  // frame position of the source (< 0: dictionary)
+            ad[t] = fa >= 0 ? ob + (s64)gs + swf : dend + fa;
+          }
+          continue;
+        }
         u32 j = 0;
         if constexpr (LDS::kStartMap) {
           u64 const e = ((const u64 *)L.bm)[min(x >> 5, 63u)];
@@ -1193,7 +1232,7 @@ __device__ bool execute_block(LDS &L, const Slot &sl, u8 *ob, s64 fpos, const Li
     // pass B: matches with a source inside the window, in order
     s32 const mlo = ms < 0 ? -ms : 0;
     s32 const mhi = min((s32)ml, (s32)wlen - ms);
-    bool const nearp = valid && mhi > mlo && ms - (s32)off + (s32)min(off, (u32)mhi) - 1 >= 0;
+    bool const nearp = !(LDS::kStartMap && ZH_EXEC_CHASE) && valid && mhi > mlo && ms - (s32)off + (s32)min(off, (u32)mhi) - 1 >= 0;
     u64 nm = __ballot(nearp);
     while (nm) {
       u32 const j = (u32)__builtin_ctzll(nm);
