@@ -263,3 +263,53 @@ def test_c3_full_batch_decode(torch_cuda):
     torch_cuda.cuda.synchronize()
     assert (status == 0).all().item() and (dsizes == cs).all().item()
     assert torch_cuda.equal(back, dev)
+
+
+def test_split_pipeline_mixed_batch_matches_small_batches(torch_cuda, mgr, libzstd):
+    """Batches of >= 2048 buffers take the split pipeline (zh_decode.hip launch_decompress:
+    a tables-only pass, the sequence kernel beside the literals pass, execution); smaller ones
+    the one-pass phase 1.  A 2,304-buffer batch mixing deferrable frames (this library's and
+    libzstd's), raw / RLE / multi-block frames, damaged frames (some fail only in the literals
+    pass, after the tables pass deferred them) and truncated ones must give every buffer the
+    same status and bytes as the same frames decoded 576 at a time, and agree with libzstd."""
+    rng = np.random.default_rng(2304)
+    frames = []
+    own = [T.gen(T.DG_MIX, 1, 900 + i, 65536) for i in range(6)]
+    own_frames = [bytes(f.cpu().numpy().tobytes()) for f in mgr.compress_batch([torch_cuda.from_numpy(np.ascontiguousarray(d)).cuda() for d in own])]
+    z_frames = [T.zstd_compress(T.gen(k, 1, 950 + j, s), level=lv)
+                for j, (k, s, lv) in enumerate([(T.DG_TEXT, 30000, 1), (T.DG_JSON, 65536, 3), (T.DG_SOURCE, 50000, 9),
+                                                 (T.DG_CSV, 40000, 19), (T.DG_RANDOM, 20000, 3), (T.DG_TEXT, 200000, 3)])]
+    z_frames.append(T.zstd_compress(np.zeros(60000, np.uint8), level=3))
+    pool = own_frames + z_frames
+    for i in range(2304):
+        f = bytearray(pool[i % len(pool)])
+        kind = i % 7
+        if kind == 5:  # damaged: a few byte flips past the frame header
+            for _ in range(1 + i % 3):
+                f[int(rng.integers(6, len(f)))] ^= int(rng.integers(1, 256))
+        elif kind == 6 and i % 14 == 6:  # truncated
+            f = f[: int(rng.integers(1, len(f)))]
+        frames.append(bytes(f))
+    caps = [262144] * len(frames)
+    outs, st = _decode(torch_cuda, mgr, frames, caps)
+    small_o, small_s = [], []
+    for k in range(0, len(frames), 576):
+        o, s = _decode(torch_cuda, mgr, frames[k:k + 576], caps[k:k + 576])
+        small_o += o
+        small_s += s
+    assert st == small_s
+    for k, (a, b, s) in enumerate(zip(outs, small_o, st)):
+        if s == 0:
+            assert a == b, f"item {k}"
+    z = T.zstd()
+    agree = 0
+    for f, o, s in zip(frames, outs, st):
+        src = np.frombuffer(f, np.uint8).copy()
+        dst = np.zeros(262144, np.uint8)
+        r = z.ZSTD_decompress(dst.ctypes.data_as(ctypes.c_void_p), ctypes.c_size_t(262144), src.ctypes.data_as(ctypes.c_void_p), ctypes.c_size_t(len(src)))
+        ok_ref = not z.ZSTD_isError(r)
+        if s == 0 and ok_ref:
+            assert o == dst[:r].tobytes()
+        agree += (s == 0) == ok_ref
+    assert agree >= len(frames) - 40, agree
+    assert sum(1 for s in st if s == 0) >= 1900
