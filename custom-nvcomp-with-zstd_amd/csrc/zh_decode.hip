@@ -1500,12 +1500,25 @@ extern "C" __global__ __launch_bounds__(DEC_THREADS) void zh_decode_kernel(ZhDec
           sp += 1;
           rem -= 1;
           if (modes & 3u) { st = ST_CORRUPT; break; }
+          // the table descriptions staged in LDS with one wave load: lane 0's NCount parse was a
+          // chain of dependent global byte loads (three descriptions take <= ~240 bytes)
+#ifndef ZH_DEC_TSTAGE
+#define ZH_DEC_TSTAGE 320u
+#endif
+          u32 const tb = min(rem, (u32)ZH_DEC_TSTAGE);
+          const u8 *tsrc = sp;
+          if (ZH_DEC_TSTAGE) {
+            for (u32 k = lane; k < tb; k += 64) L.u.sstage[k] = sp[k];
+            __syncthreads();
+            tsrc = L.u.sstage;
+          }
+          u32 const tavail = ZH_DEC_TSTAGE ? tb : rem;
           if (lane == 0) {
             u32 e = 0, used = 0;
             u32 const md[3] = {modes >> 6, (modes >> 4) & 3u, (modes >> 2) & 3u};
             L.bld[0] = L.bld[1] = L.bld[2] = 0;
             for (u32 t = 0; t < 3 && !e; t++) {
-              s32 const u = seq_table(L, t, md[t], sp + used, rem - used, true);
+              s32 const u = seq_table(L, t, md[t], tsrc + used, tavail - used, true);
               if (u < 0) e = 1;
               else used += (u32)u;
             }
