@@ -2174,8 +2174,14 @@ hipError_t launch_decompress(const ZhDecArgs &a0, u32 nitems, hipStream_t stream
     (void)hipEventRecord(sp2->first_done[0], stream);
     (void)hipStreamWaitEvent(side, sp2->first_done[0], 0);
     a.phase = 5;
-    hipLaunchKernelGGL(zh_decode_kernel, dim3(nitems), dim3(DEC_THREADS), 0, side, a);
+#ifndef ZH_DEC_P5_PAD
+#define ZH_DEC_P5_PAD 0  // (occupancy experiments: dynamic LDS added to phase 5's workgroups)
+#endif
+    hipLaunchKernelGGL(zh_decode_kernel, dim3(nitems), dim3(DEC_THREADS), ZH_DEC_P5_PAD, side, a);
     (void)hipEventRecord(sp2->done[0], side);
+#ifdef ZH_DEC_SERIAL_P5
+    (void)hipStreamWaitEvent(stream, sp2->done[0], 0);  // (diagnostic: phase 5 and the chains one after the other)
+#endif
     hipLaunchKernelGGL(zh_dec_seq_kernel, dim3((nitems + DQ_BUF - 1) / DQ_BUF), dim3(64), 0, stream, a, nitems);
     (void)hipStreamWaitEvent(stream, sp2->done[0], 0);
     a.phase = 3;
