@@ -113,6 +113,9 @@ struct DecLds {
   u8 hufw[256];     // Huffman weights of the last table (treeless literals rebuild from them)
   u32 tlog[3];      // table logs
   u32 tkind[3];     // TAB_NONE / TAB_PREDEF / RLE symbol | 0x100 / 0 = FSE
+#ifdef ZH_STAMPS
+  u64 lst_t[4];     // (-DZH_STAMPS) decode_literals: s_memtime after the header, weights, table, streams
+#endif
   u32 bld[3];       // sequence tables whose build is left to build_dtable_wave (norm in norm + 64 t)
   u32 hlog, hnsym, hvalid;
   u32 err;   // serial-section status (lane 0 writes)
@@ -591,10 +594,22 @@ constexpr u32 HP_TRAJ = 32;
 // byte read as 0, so no load leaves the pages the stream touches), a 4-dword window w0..w3 at
 // dword index wi and the two dwords below it prefetched.  Bits below the stream's bit 0 read
 // as zeros (the serial reader's rule).
+#ifndef ZH_HUF_PF2
+#define ZH_HUF_PF2 1  // prefetch two slides ahead (4 dwords) instead of one
+#endif
+#ifndef ZH_HUF_PF3
+#define ZH_HUF_PF3 0  // (with PF2) three slides ahead
+#endif
 struct HufReader {
   const u32 *ab;
   s32 da8, lastw, wi, p;
   u32 w0, w1, w2, w3, q0, q1;
+#if ZH_HUF_PF2
+  u32 q2, q3;  // dwords wi-2, wi-1 (q0, q1: wi-4, wi-3)
+#endif
+#if ZH_HUF_PF3
+  u32 r0, r1;  // dwords wi-6, wi-5 (a third slide ahead)
+#endif
   __device__ __forceinline__ u32 ld(s32 i) const { return (i >= 0 && i <= lastw) ? ab[i] : 0u; }
   __device__ __forceinline__ void init(const u8 *sp, u32 n) {
     ab = (const u32 *)((uintptr_t)sp & ~(uintptr_t)3);
@@ -605,17 +620,40 @@ struct HufReader {
     p = pos;
     wi = ((pos + da8 + 31) >> 5) - 4;  // bit pos lies in (96, 128] of the window
     w0 = ld(wi); w1 = ld(wi + 1); w2 = ld(wi + 2); w3 = ld(wi + 3);
+#if ZH_HUF_PF2
+    q2 = ld(wi - 2); q3 = ld(wi - 1);
+    q0 = ld(wi - 4); q1 = ld(wi - 3);
+#if ZH_HUF_PF3
+    r0 = ld(wi - 6); r1 = ld(wi - 5);
+#endif
+#else
     q0 = ld(wi - 2); q1 = ld(wi - 1);
+#endif
   }
   // decode one symbol: sym | nbBits << 8
   __device__ __forceinline__ u32 next(const u16 *dt, u32 tlog) {
     s32 v = p + da8 - 32 * wi - (s32)tlog;  // window bit of the peek's lowest bit
     if (v < 32) {  // slide down two dwords (v >= 21: a step consumes <= 11 bits)
+#if ZH_HUF_PF2
+      w3 = w1; w2 = w0; w1 = q3; w0 = q2;
+      q3 = q1; q2 = q0;
+      wi -= 2;
+      v += 64;
+#if ZH_HUF_PF3
+      q1 = r1; q0 = r0;
+      r0 = ld(wi - 6);
+      r1 = ld(wi - 5);
+#else
+      q0 = ld(wi - 4);
+      q1 = ld(wi - 3);
+#endif
+#else
       w3 = w1; w2 = w0; w1 = q1; w0 = q0;
       wi -= 2;
       v += 64;
       q0 = ld(wi - 2);
       q1 = ld(wi - 1);
+#endif
     }
     u32 const k = (u32)v >> 5;  // 1..3
     // (mask selects: the compiler turns a select chain on k into a scratch-indexed array)
@@ -807,9 +845,25 @@ __device__ u32 decode_literals(DecLds &L, const u8 *bp, u32 bsz, const Slot &sl,
   if (n > sl.lit_cap) { st = ST_SMALL; return 0; }
   const u8 *p = bp + hs;
   u32 rem = cs;
+#ifdef ZH_STAMPS
+  if (lane == 0) L.lst_t[0] = __builtin_amdgcn_s_memtime();
+#endif
   if (lt == 2) {
+    // the tree description (<= 128 bytes) staged in LDS first: lane 0's weight decode is a
+    // serial FSE chain whose every byte read was a dependent global load
+#ifndef ZH_DEC_WSTAGE
+#define ZH_DEC_WSTAGE 0  // (1: 117.7 GB/s vs 119.1 without; profiles/r06u_dec_p5_reader_ab.json)
+#endif
+    const u8 *wp = p;
+    if (ZH_DEC_WSTAGE) {
+      u32 const wn = min(rem, 128u);
+      u8 *const ws = L.u.h.hs[0];
+      for (u32 k = lane; k < wn; k += 64) ws[k] = p[k];
+      __syncthreads();
+      wp = ws;
+    }
     if (lane == 0) {
-      u32 const used = huf_read_weights(L, p, rem);
+      u32 const used = huf_read_weights(L, wp, ZH_DEC_WSTAGE ? min(rem, 128u) : rem);
       L.err = used ? 0u : 1u;
       L.hvalid = used ? 1u : 0u;
       L.used = used;
@@ -823,7 +877,13 @@ __device__ u32 decode_literals(DecLds &L, const u8 *bp, u32 bsz, const Slot &sl,
     st = ST_CORRUPT;
     return 0;
   }
+#ifdef ZH_STAMPS
+  if (lane == 0) L.lst_t[1] = __builtin_amdgcn_s_memtime();
+#endif
   huf_build_dtable(L);
+#ifdef ZH_STAMPS
+  if (lane == 0) L.lst_t[2] = __builtin_amdgcn_s_memtime();
+#endif
   u32 const tlog = uni(L.hlog);
   // streams
   const u8 *sp[4];
@@ -1463,6 +1523,18 @@ extern "C" __global__ __launch_bounds__(DEC_THREADS) void zh_decode_kernel(ZhDec
             ho->litrle = lits.rle;
             ho->litn = lits.n;
           }
+#ifdef ZH_STAMPS
+          // (-DZH_STAMPS: phase 5's split into the record's spare bytes, tools/p5_stamps.py)
+          if (lane == 0) {
+            u64 *const xs5 = (u64 *)((u8 *)ho + 5248);
+            xs5[0] = stv[0];
+            xs5[1] = L.lst_t[0] - (stp - stv[1]);
+            xs5[2] = L.lst_t[1] - L.lst_t[0];
+            xs5[3] = L.lst_t[2] - L.lst_t[1];
+            xs5[4] = stp - L.lst_t[2];
+            xs5[5] = lits.n;
+          }
+#endif
           return;  // phase 3 writes the size and status
         }
         if (!ls) {
