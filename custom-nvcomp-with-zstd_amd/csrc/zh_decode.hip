@@ -90,23 +90,28 @@ __device__ __forceinline__ u32 tab_maxlog(u32 t) { return t == 1 ? 8u : 9u; }
 constexpr u32 TAB_NONE = 0xFFFFu, TAB_PREDEF = 0xFFFEu;  // tkind; else RLE symbol | 0x100, or 0 = FSE
 
 // The union's three views are used one after the other inside a block: Huffman decode,
-// sequence bitstream, execution window.
-struct DecLds {
+// sequence bitstream, execution window.  TAB = the split pipeline's tables-only pass
+// (zh_dec_tables_kernel): no literals, no execution, so the union shrinks to the 320-byte stage
+// of the table descriptions and the window arrays to stubs (8.5 KB instead of 16.8: twice the
+// workgroups per CU).
+template <bool TAB>
+struct DecLdsT {
   static constexpr bool kLitStage = false;
   static constexpr bool kStartMap = false;
+  static constexpr bool kTablesOnly = TAB;
   u32 fse[1280];  // LL [0,512) OF [512,768) ML [768,1280): sym | nbBits << 8 | newState << 16
   union {
     struct {
-      u16 dt[1 << HUF_LOG_MAX];  // Huffman decode table: sym | nbBits << 8
-      u8 hs[4][HSTAGE + 16];     // staged bytes of the 4 streams
+      u16 dt[TAB ? 2 : (1 << HUF_LOG_MAX)];  // Huffman decode table: sym | nbBits << 8
+      u8 hs[4][TAB ? 4 : HSTAGE + 16];       // staged bytes of the 4 streams
     } h;
-    u8 sstage[SSTAGE + 16];      // staged bytes of the sequence bitstream
-    u8 out[DEC_STAGE + 16];      // execution window
+    u8 sstage[TAB ? 336 : SSTAGE + 16];      // staged bytes of the sequence bitstream (TAB: table descriptions)
+    u8 out[TAB ? 16 : DEC_STAGE + 16];       // execution window
   } u;
   u32 wt[64];       // FSE table of the Huffman weights (log <= 6)
   u8 symlist[256];  // Huffman build: symbols grouped by weight
-  s32 wvs[68];      // execution window: virtual start of each sequence (binary search keys)
-  u32 wll[64], wlit[64], woff[64];  // execution window: literal length, first literal, offset
+  s32 wvs[TAB ? 4 : 68];  // execution window: virtual start of each sequence (binary search keys)
+  u32 wll[TAB ? 1 : 64], wlit[TAB ? 1 : 64], woff[TAB ? 1 : 64];  // execution window: literal length, first literal, offset
   u32 info[2][64];  // LL / ML code info (baseline | bits << 24), copied from constants
   s16 norm[256];    // NCount scratch
   u16 next[256];    // FSE build scratch (symbolNext)
@@ -121,6 +126,8 @@ struct DecLds {
   u32 err;   // serial-section status (lane 0 writes)
   u32 used;  // serial-section byte count (lane 0 writes)
 };
+using DecLds = DecLdsT<false>;
+using DecLdsTab = DecLdsT<true>;
 
 __device__ __forceinline__ u32 hb32(u32 v) { return 31u - (u32)__builtin_clz(v); }
 __device__ __forceinline__ u32 lane_id() { return threadIdx.x; }
@@ -403,7 +410,8 @@ __device__ __forceinline__ u32 umod(u32 m, u32 d) {
 // ---- Huffman ------------------------------------------------------------------------------
 // HUF_readStats (libzstd lib/common/entropy_common.c) on lane 0: weights -> L.hufw, L.hlog,
 // L.hnsym.  Returns the header bytes consumed, 0 on error.
-__device__ __noinline__ u32 huf_read_weights(DecLds &L, const u8 *p, u32 avail) {
+template <class LDS>
+__device__ __noinline__ u32 huf_read_weights(LDS &L, const u8 *p, u32 avail) {
   if (avail < 1) return 0;
   u32 const hb = p[0];
   u32 nw = 0, used;
@@ -1034,7 +1042,8 @@ __device__ bool build_dtable_wave(u32 *T, const s16 *norm, u32 maxSV, u32 tlog) 
 
 // defer: leave the table build to build_dtable_wave (the normalised counts go to norm + 64 t,
 // bld[t] is set); else build it here, serially.
-__device__ __noinline__ s32 seq_table(DecLds &L, u32 t, u32 mode, const u8 *p, u32 avail, bool defer = false) {
+template <class LDS>
+__device__ __noinline__ s32 seq_table(LDS &L, u32 t, u32 mode, const u8 *p, u32 avail, bool defer = false) {
   u32 *T = L.fse + tab_off(t);
   u32 const maxSV = tab_maxsv(t);
   s16 *const nrm = defer ? L.norm + 64 * t : L.norm;
@@ -1075,7 +1084,8 @@ __device__ __noinline__ s32 seq_table(DecLds &L, u32 t, u32 mode, const u8 *p, u
 // Formatted dictionary (RFC 8878 §5): its Huffman table and OF / ML / LL FSE tables become
 // the frame's previous tables (treeless literals and repeat modes use them).  Lane 0; false
 // when they do not parse.  d = the dictionary, off = its content offset.
-__device__ __forceinline__ bool load_dict_entropy(DecLds &L, const u8 *d, u32 off) {
+template <class LDS>
+__device__ __forceinline__ bool load_dict_entropy(LDS &L, const u8 *d, u32 off) {
   if (off < 8 + 12) return false;
   const u8 *const p = d + 8;
   u32 const avail = off - 8 - 12;
@@ -1398,8 +1408,8 @@ __device__ __forceinline__ u32 resolve_off(u32 ofv, u32 ll, u32 &rep0, u32 &rep1
 #endif
 
 // One workgroup (one wave) per input buffer.
-extern "C" __global__ __launch_bounds__(DEC_THREADS) void zh_decode_kernel(ZhDecArgs a) {
-  __shared__ DecLds L;
+template <class LDS>
+__device__ __forceinline__ void decode_body(LDS &L, ZhDecArgs a) {
   u32 const item = a.item0 + blockIdx.x, lane = lane_id();
   const u8 *const src = (const u8 *)(a.in_ptrs ? a.in_ptrs[item] : a.one_in);
   u64 const srcn = a.in_ptrs ? (u64)a.in_sizes[item] : a.one_in_size;
@@ -1413,7 +1423,9 @@ extern "C" __global__ __launch_bounds__(DEC_THREADS) void zh_decode_kernel(ZhDec
   // dictionary content precedes every frame: match sources before the frame start
   const u8 *const dend = a.dict ? a.dict + a.dict_n : nullptr;
   s64 const dlen = a.dict ? (s64)(a.dict_n - a.dict_off) : 0;
-  if (lane < 4) L.wvs[64 + lane] = 0x7FFFFFFF;
+  if constexpr (!LDS::kTablesOnly) {
+    if (lane < 4) L.wvs[64 + lane] = 0x7FFFFFFF;
+  }
   if (lane < 36) L.info[0][lane] = c_LL_info[lane];
   if (lane < 53) L.info[1][lane] = c_ML_info[lane];
   __syncthreads();
@@ -1508,7 +1520,9 @@ extern "C" __global__ __launch_bounds__(DEC_THREADS) void zh_decode_kernel(ZhDec
         const u8 *const bp = src + ip;
         LitSrc lits;
         DSTAMP(0);
-        u32 const ls = a.phase == 4 ? skip_literals(bp, bsz) : decode_literals(L, bp, bsz, sl, lits, st);
+        u32 ls;
+        if constexpr (LDS::kTablesOnly) ls = skip_literals(bp, bsz);
+        else ls = a.phase == 4 ? skip_literals(bp, bsz) : decode_literals(L, bp, bsz, sl, lits, st);
         DSTAMP(1);
         if (a.phase == 5 && produced == 0 && uni(handoff(a, item)->flag) == 1) {
           // deferred by phase 4: the literals are all this pass owes it (a corrupt literals
@@ -1647,7 +1661,8 @@ extern "C" __global__ __launch_bounds__(DEC_THREADS) void zh_decode_kernel(ZhDec
             }
             return;  // phase 3 writes the size and status
           }
-          if (a.phase == 4) return;
+          if (LDS::kTablesOnly || a.phase == 4) return;
+          if constexpr (!LDS::kTablesOnly) {
           // ---- sequence bitstream (RFC 8878 §3.1.1.3.2.2): every lane decodes redundantly
           // (uniform control flow, no exec-mask work); lane j keeps record j of each 64
           BitRevS r;
@@ -1699,11 +1714,13 @@ extern "C" __global__ __launch_bounds__(DEC_THREADS) void zh_decode_kernel(ZhDec
           }
           if (r.pos > 0 || big) { st = ST_CORRUPT; break; }
           DSTAMP(3);
+          }  // !kTablesOnly
         } else if (rem != 0) {
           st = ST_CORRUPT;
           break;
         }
-        if (a.phase == 4) return;  // (no sequences: nothing deferred)
+        if (LDS::kTablesOnly || a.phase == 4) return;  // (no sequences: nothing deferred)
+        if constexpr (!LDS::kTablesOnly) {
         if (sumLL > lits.n) { st = ST_CORRUPT; break; }
         u64 const total = lits.n + sumML;
         // RFC 8878 §3.1.1.2.4: a block regenerates at most Block_Maximum_Size (128 KiB), which
@@ -1719,6 +1736,7 @@ extern "C" __global__ __launch_bounds__(DEC_THREADS) void zh_decode_kernel(ZhDec
         if (bad) { st = ST_CORRUPT; break; }
         produced += total;
         ip += bsz;
+        }  // !kTablesOnly
       } else {
         st = ST_CORRUPT;
         break;
@@ -1744,6 +1762,17 @@ extern "C" __global__ __launch_bounds__(DEC_THREADS) void zh_decode_kernel(ZhDec
     a.out_sizes[item] = st == ST_OK ? produced : 0ull;
     if (a.statuses) a.statuses[item] = a.nvcomp_codes ? to_nvcomp(st) : st;
   }
+}
+
+extern "C" __global__ __launch_bounds__(DEC_THREADS) void zh_decode_kernel(ZhDecArgs a) {
+  __shared__ DecLds L;
+  decode_body(L, a);
+}
+
+// The split pipeline's phase 4 with the small LDS layout (a.phase == 4)
+extern "C" __global__ __launch_bounds__(DEC_THREADS) void zh_dec_tables_kernel(ZhDecArgs a) {
+  __shared__ DecLdsTab L;
+  decode_body(L, a);
 }
 
 // Phase 3: execute the block of a buffer deferred by phase 1 (its sequence records are in
@@ -2242,7 +2271,11 @@ hipError_t launch_decompress(const ZhDecArgs &a0, u32 nitems, hipStream_t stream
     ZhDecArgs a = a0;
     a.item0 = 0;
     a.phase = 4;
-    hipLaunchKernelGGL(zh_decode_kernel, dim3(nitems), dim3(DEC_THREADS), 0, stream, a);
+#ifndef ZH_DEC_TABK
+#define ZH_DEC_TABK 1
+#endif
+    if (ZH_DEC_TABK) hipLaunchKernelGGL(zh_dec_tables_kernel, dim3(nitems), dim3(DEC_THREADS), 0, stream, a);
+    else hipLaunchKernelGGL(zh_decode_kernel, dim3(nitems), dim3(DEC_THREADS), 0, stream, a);
     (void)hipEventRecord(sp2->first_done[0], stream);
     (void)hipStreamWaitEvent(side, sp2->first_done[0], 0);
     a.phase = 5;
