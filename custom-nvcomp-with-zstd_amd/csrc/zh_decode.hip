@@ -684,6 +684,10 @@ __device__ __forceinline__ bool huf_streams_par(DecLds &L, u32 ns, const u8 *msp
   bool bad = last == 0;
   s32 const top = bad ? 0 : 8 * (s32)(mn - 1) + (s32)hb32(last);
   s32 const Lb = max((top + (s32)S - 1) / (s32)S, 1);
+  // trajectory positions are kept as u16 offsets into a segment: a stream with 2^16 bits or more
+  // per segment (> 1 M bits for 4 streams) holds more bits than its <= 32 K symbols of <= 11 bits
+  // can consume, so it is corrupt
+  bad |= Lb >= 65536;
   s32 const hiB = top - (s32)j * Lb, lo = max(top - (s32)(j + 1) * Lb, 0);
   const u16 *const dt = L.u.h.dt;
   u16 *const traj = (u16 *)&L.u.h.hs[0][0];  // [HP_TRAJ][64]
