@@ -56,8 +56,14 @@ typedef int64_t s64;
 namespace {
 
 constexpr u32 DEC_THREADS = 64;
-constexpr u32 DEC_STAGE = 8192;   // output window (LDS)
-constexpr u32 HSTAGE = 1024;      // per-stream LDS stage of a Huffman stream
+#ifndef ZH_DEC_STAGE
+#define ZH_DEC_STAGE 8192
+#endif
+#ifndef ZH_HSTAGE
+#define ZH_HSTAGE 1024
+#endif
+constexpr u32 DEC_STAGE = ZH_DEC_STAGE;  // output window (LDS)
+constexpr u32 HSTAGE = ZH_HSTAGE;        // per-stream LDS stage of a Huffman stream
 constexpr u32 SSTAGE = 4096;      // LDS stage of the sequence bitstream
 constexpr u32 HUF_LOG_MAX = 11;   // RFC 8878 §4.2.1: Max_Number_of_Bits <= 11
 constexpr u32 BLOCKSIZE_MAX = 128u * 1024u;
@@ -596,7 +602,11 @@ __device__ void wave_fill(u8 *dst, u32 v, u32 n) {
 //           prefix sum of the counts before it.
 // The symbols and the stream verdict equal the serial decode's: a stream is valid when the
 // counts add up to its symbol count and the last segment ends exactly at bit 0.
-constexpr u32 HP_TRAJ = 32;
+#ifndef ZH_HP_TRAJ
+#define ZH_HP_TRAJ 32
+#endif
+constexpr u32 HP_TRAJ = ZH_HP_TRAJ;
+static_assert(HP_TRAJ * 64 * 2 <= 4 * (HSTAGE + 16), "trajectory records fit the stream stages");
 
 // A lane's reader over one stream: dwords from the 4-aligned base ab (dwords holding no stream
 // byte read as 0, so no load leaves the pages the stream touches), a 4-dword window w0..w3 at
