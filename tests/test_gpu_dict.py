@@ -216,3 +216,27 @@ def test_dictionary_low_levels_match_oracle(torch_cuda, dicts, kind, level):
         f = m.compress(_dev(torch_cuda, data)).cpu().numpy().tobytes()
         assert f == T.oracle_frame(data, dictionary=d, level=level), (kind, level, n)
         assert T.zstd_decompress(f, n, dictionary=d) == data.tobytes(), (kind, level, n)
+
+
+@pytest.mark.parametrize("level", [1, 3, 19])
+def test_split_pipeline_decodes_dictionary_frames(torch_cuda, dicts, level):
+    """>= 2048 dictionary frames take the decoder's split pipeline: its tables-only pass
+    (zh_dec_tables_kernel, small LDS layout) loads the formatted dictionary's entropy tables
+    for repeat-mode sequence tables and treeless literals, as the literals pass does.  libzstd
+    frames with each dictionary plus this library's, 2,176 buffers, every one byte-exact."""
+    a = T.gen(T.DG_JSON, 34, 0x5EED0605, 16384)
+    recs = [a[i:i + 16384][: 2000 + 431 * i] for i in range(34)]
+    for kind in ("zdict", "cover"):
+        d = dicts[kind]
+        m = _mgr(3, d)
+        z_frames = [T.zstd_compress_dict(r, d, level) for r in recs]
+        own = [f.cpu().numpy().tobytes() for f in m.compress_batch([_dev(torch_cuda, r) for r in recs])]
+        frames, want = [], []
+        for k in range(2176):
+            i = k % len(recs)
+            frames.append(z_frames[i] if (k // len(recs)) % 2 == 0 else own[i])
+            want.append(recs[i].tobytes())
+        outs, st = m.decompress_batch([_dev(torch_cuda, f) for f in frames], [len(w) for w in want], raise_on_error=False)
+        assert st == [0] * len(frames), (kind, level)
+        for k, (o, w) in enumerate(zip(outs, want)):
+            assert o.cpu().numpy().tobytes() == w, (kind, level, k)
